@@ -1,0 +1,337 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by RUNNING the reference.
+
+This script is the only thing in the repository that touches /root/reference,
+and it only runs in the build container (the GPU box never sees the reference).
+It produces data only: inputs and the reference's outputs, as .npz files.
+
+Two harnesses:
+
+* ``_extract(path)``: AST-extract the ``def``/``class`` nodes (plus the literal
+  module constants) of a reference script and exec them in a fresh namespace
+  with numpy / scipy KDTree / matplotlib.tri injected.  Used for the per-kernel
+  fixtures (assembly, div/grad, BCs, semi-Lagrangian advection, mixing index).
+* ``_run_script(path, ...)``: exec the WHOLE script text headless (jax stubbed
+  with numpy -- jax is absent here and only ``poisson.py:283-287`` uses it;
+  pyplot replaced by an inert stub; the mesh paths and STEPS text-substituted)
+  and snapshot the module globals every time the script prints its per-step
+  line.  Used for Poisson / heat / Stokes end-to-end fixtures.
+
+Run:  python tests/golden/gen_golden.py            (per-kernel + short runs, ~1 min)
+      python tests/golden/gen_golden.py --long     (adds 6000-step mesh.1 traces, ~15 min)
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import io
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = os.environ.get("PUCFEM_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+MESHES = {
+    # name: (node, ele, poly) relative to REF
+    "mesh1": ("code/mesh/mesh.1.node", "code/mesh/mesh.1.ele", "code/mesh/mesh.1.poly"),
+    "mesh21": ("resources/mesh2.1.node", "resources/mesh2.1.ele", "resources/mesh2.1.poly"),
+    "fine": ("resources/mesh_fine.1.node", "resources/mesh_fine.1.ele", "resources/mesh_fine.1.poly"),
+}
+
+
+# ----------------------------------------------------------------------------- stubs
+class _Inert:
+    """Accepts any attribute access / call and returns itself (headless pyplot)."""
+
+    def __getattr__(self, name):
+        return self
+
+    def __call__(self, *a, **k):
+        return self
+
+    def __iter__(self):
+        return iter((self, self))
+
+    def __bool__(self):
+        return True
+
+
+def _install_stubs():
+    import matplotlib
+
+    matplotlib.use("Agg")
+    jax = types.ModuleType("jax")
+    jax.config = types.SimpleNamespace(update=lambda *a, **k: None)
+    jnp = types.ModuleType("jax.numpy")
+    jnp.array = np.array
+    jnp.allclose = np.allclose
+    jnp.linalg = types.SimpleNamespace(solve=np.linalg.solve)
+    exp = types.ModuleType("jax.experimental")
+    exp.sparse = types.ModuleType("jax.experimental.sparse")
+    jax.numpy = jnp
+    jax.experimental = exp
+    sys.modules.update({"jax": jax, "jax.numpy": jnp, "jax.experimental": exp,
+                        "jax.experimental.sparse": exp.sparse})
+    plt = types.ModuleType("matplotlib.pyplot")
+    inert = _Inert()
+    plt.__getattr__ = lambda name: inert  # module-level __getattr__ (PEP 562)
+    sys.modules["matplotlib.pyplot"] = plt
+    import matplotlib as _m
+    _m.pyplot = plt
+
+
+# ----------------------------------------------------------------------------- harness 1
+def _extract(relpath, extra_globals=None):
+    src = open(os.path.join(REF, relpath)).read()
+    tree = ast.parse(src)
+    keep = []
+    for node in tree.body:
+        if isinstance(node, (ast.FunctionDef, ast.ClassDef, ast.Import, ast.ImportFrom)):
+            keep.append(node)
+        elif isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
+            # literal module constants only (B1, DT, SQUIRMER_CENTER, ...)
+            names = {n.id for n in ast.walk(node.value) if isinstance(n, ast.Name)}
+            if names <= {"np", "SQUIRMER_RADIUS"}:
+                keep.append(node)
+    mod = ast.Module(body=keep, type_ignores=[])
+    ns = {"__name__": "ref_extract"}
+    exec(compile(mod, relpath, "exec"), ns)
+    if extra_globals:
+        ns.update(extra_globals)
+    return ns
+
+
+# ----------------------------------------------------------------------------- harness 2
+def _run_script(relpath, mesh, steps_var, steps, subs=(), snap_prefix="Step:", snap_vars=()):
+    """exec the whole reference script; snapshot ``snap_vars`` at each per-step print."""
+    src = open(os.path.join(REF, relpath)).read()
+    node, ele, poly = (os.path.join(REF, p) for p in MESHES[mesh])
+    src = src.replace('"./mesh/mesh.1.node"', repr(node)).replace('"./mesh/mesh.1.ele"', repr(ele))
+    src = src.replace('"./mesh/mesh.1.poly"', repr(poly))
+    line = f"{steps_var} = "
+    i = src.index("\n" + line) + 1
+    j = src.index("\n", i)
+    src = src[:i] + f"{steps_var} = {steps}" + src[j:]
+    for a, b in subs:
+        assert a in src, a
+        src = src.replace(a, b)
+    snaps = []
+    logs = []
+    g = {"__name__": "ref_script"}
+
+    def _print(*args, **kw):
+        s = " ".join(str(a) for a in args)
+        logs.append(s)
+        if s.startswith(snap_prefix):
+            snaps.append({k: np.array(g[k], copy=True) for k in snap_vars})
+
+    g["print"] = _print
+    exec(compile(src, relpath, "exec"), g)
+    return g, snaps, logs
+
+
+def _coo(A):
+    r, c = np.nonzero(A)
+    return np.stack([r, c]).astype(np.int32), A[r, c]
+
+
+# ----------------------------------------------------------------------------- fixtures
+def gen_kernels(name):
+    node, ele, poly = (os.path.join(REF, p) for p in MESHES[name])
+    C = _extract("code/StokesColor.py")
+    P = _extract("code/poisson.py")
+    out = {}
+    X, mk = C["readNode"](node)
+    X32, mk32 = P["readNode"](node)
+    T = C["readEle"](ele)
+    assert np.array_equal(mk, mk32)
+    out.update(coords64=X, coords32=X32, markers=mk, tris=T)
+    try:
+        seg, segm = P["readPoly"](poly)
+        out.update(poly_segments=seg, poly_markers=segm)
+    except Exception as e:  # readPoly expects a Triangle *output* .poly
+        print("readPoly failed on", poly, type(e).__name__, e)
+    N = X.shape[0]
+    pairs_all = np.array(C["find_boundary_pairs"](X, L=1.0), dtype=np.int64).reshape(-1, 2)
+    tol, H = 1e-6, 1.0
+    keep = [not (abs(X[m, 1]) < tol or abs(X[m, 1] - H) < tol) for m, s in pairs_all]
+    pairs = pairs_all[np.array(keep, dtype=bool)] if len(pairs_all) else pairs_all
+    out.update(pairs_all=pairs_all, pairs=pairs)
+    # fp32-coordinate pairs (poisson/heat read fp32 coordinates)
+    pairs32_all = np.array(P["find_boundary_pairs"](X32, L=1.0), dtype=np.int64).reshape(-1, 2)
+    out.update(pairs32_all=pairs32_all)
+
+    K, _ = C["buildStiffnessMatrix"](X, T, g_source=0.0)
+    out["K_ij"], out["K_v"] = _coo(K)
+    M = C["buildLumpedMassMatrix"](X, T)
+    out["M"] = M
+
+    # Poisson assembly in the reference's own fp32 arithmetic (poisson.py:100-146, :235-236)
+    Ap, bp = P["buildFemSystem"](X32, T, g_source=lambda x, y: 50 * np.sin(3 * y))
+    out["Apois_ij"], out["Apois_v"] = _coo(Ap)
+    out["bpois"] = bp
+
+    rng = np.random.default_rng(0)
+    u_rand = rng.standard_normal((N, 2))
+    p_rand = rng.standard_normal(N)
+    out.update(u_rand=u_rand, p_rand=p_rand)
+    out["div_rand"] = C["calculate_divergence"](X, T, u_rand)
+    gx, gy = C["calculate_gradiant"](X, T, p_rand)
+    out["grad_rand"] = np.stack([gx, gy], 1)
+    u_lin = np.stack([2 * X[:, 0], 3 * X[:, 1]], 1)
+    out["div_lin"] = C["calculate_divergence"](X, T, u_lin)
+    gx, gy = C["calculate_gradiant"](X, T, 2 * X[:, 0] + 3 * X[:, 1])
+    out["grad_lin"] = np.stack([gx, gy], 1)
+
+    wall = np.where(np.isclose(X[:, 1], 0.0, atol=tol) | np.isclose(X[:, 1], H, atol=tol))[0]
+    inner = np.where(mk == 2)[0]
+    dirichlet = np.union1d(wall, inner)
+    interior = np.setdiff1d(np.arange(N), dirichlet)
+    out.update(wall=wall, inner_bc=inner, dirichlet=dirichlet, interior=interior)
+
+    # squirmer Dirichlet BC values (StokesColor.py:405-427) for neutral / pusher / puller
+    for tag, B2 in (("neutral", 0.0), ("pusher", -5.0), ("puller", 5.0)):
+        u = np.full((N, 2), 7.0)
+        C.update(wall_node_indices=wall, inner_boundary_indices=inner, nodes_coords=X, B1=-2.0, B2=B2)
+        C["makeDirBCU"](u)
+        out[f"dirbc_{tag}"] = u
+
+    # one viscous solve per parameter set (StokesColor.py:471-475, :544)
+    for tag, dt, nu in (("color", 0.05, 0.1), ("food", 0.01, 1.0)):
+        A = np.eye(N) + dt * nu * K
+        A[dirichlet, :] = 0.0
+        A[:, dirichlet] = 0.0
+        A[dirichlet, dirichlet] = 1.0
+        rhs = u_rand[:, 0].copy()
+        out[f"visc_{tag}_x"] = np.linalg.solve(A, rhs)
+
+    # semi-Lagrangian advection (StokesColor.py:314-389) from a synthetic swirl, two DTs
+    c0 = np.zeros(N)
+    c0[X[:, 0] < 0.5] = 1.0
+    out["c0"] = c0
+    r = X - 0.5
+    u_sw = np.stack([-r[:, 1], r[:, 0]], 1) * 3.0 + np.array([0.7, 0.0])
+    out["u_swirl"] = u_sw
+    PL = C["PointLocator"](X, T)
+    C.update(N=N, nodes_coords=X, triangles=T, point_locator=PL)
+    for tag, dt in (("small", 0.05), ("large", 0.2)):
+        c = c0.copy()
+        C["advect_semilagrange"](c, u_sw, dt)
+        out[f"sl_{tag}"] = c
+        # which nodes took the "not found -> keep c[n]" branch
+        nf = []
+        for n in range(N):
+            xb = (X[n, 0] - dt * u_sw[n, 0] * 1.0) % 1.0
+            yb = X[n, 1] - dt * u_sw[n, 1] * 1.0
+            if yb < 0.0:
+                yb = 1e-12
+            if yb > 1.0:
+                yb = 1.0 - 1e-12
+            nf.append(PL.find(xb, yb) is None)
+        out[f"sl_{tag}_notfound"] = np.array(nf)
+    # mixing index (StokesColor.py:391-403)
+    Imix, mu, var = C["mixing_index"](out["sl_small"], M, mask=np.where(mk == 0)[0])
+    out["mixing_sl_small"] = np.array([Imix, mu, var])
+
+    # tracer step (StokesFood.py:420-436, :482-499), 10 steps on the fixed swirl field
+    F = _extract("code/StokesFood.py")
+    import matplotlib.tri as mtri
+
+    tri = mtri.Triangulation(X[:, 0], X[:, 1], T)
+    xx = np.linspace(0.05, 0.95, 25)
+    gx_, gy_ = np.meshgrid(xx, xx)
+    pts = np.vstack([gx_.ravel(), gy_.ravel()]).T
+    pts = pts[np.linalg.norm(pts - F["SQUIRMER_CENTER"], axis=1) > F["SQUIRMER_RADIUS"]]
+    out["tracer0"] = pts.copy()
+    status = np.zeros(len(pts), dtype=int)
+    ix = mtri.LinearTriInterpolator(tri, u_sw[:, 0])
+    iy = mtri.LinearTriInterpolator(tri, u_sw[:, 1])
+    for _ in range(10):
+        ux = ix(pts[:, 0], pts[:, 1])
+        uy = iy(pts[:, 0], pts[:, 1])
+        pts[:, 0] += ux * 0.01
+        pts[:, 1] += uy * 0.01
+        pts[:, 0] = np.mod(pts[:, 0], 1.0)
+        d = np.linalg.norm(pts - F["SQUIRMER_CENTER"], axis=1)
+        status[np.where(d <= F["CAPTURE_RADIUS"])[0]] = 1
+    out["tracer10"] = pts
+    out["tracer10_status"] = status
+    return out
+
+
+def gen_scripts(name, stokes_steps=3, heat_steps=(1, 10, 600)):
+    out = {}
+    # --- poisson.py end to end (f = solution) ---
+    g, _, logs = _run_script("code/poisson.py", name, "WALL_VALUE", 0.0, snap_prefix="\0")
+    out["poisson_f"] = np.asarray(g["f"])
+    out["poisson_pairs_filtered"] = np.array(g["filtered_pairs"], dtype=np.int64).reshape(-1, 2)
+    # --- heatEq.py: u after each step ---
+    nmax = max(heat_steps)
+    g, snaps, _ = _run_script("code/heatEq.py", name, "steps", nmax, snap_prefix="Completed step",
+                              snap_vars=("u",))
+    for k in heat_steps:
+        out[f"heat_u{k}"] = snaps[k - 1]["u"]
+    out["heat_pairs_unfiltered"] = np.array(g["pairs"], dtype=np.int64).reshape(-1, 2)
+    if name == "mesh21":
+        return out
+    # --- StokesColor.py: literal first steps (dense LU pressure, SURVEY §0 finding 1) ---
+    vars_ = ("u_star", "div_u_star", "p", "u", "p2", "final_div", "c")
+    g, snaps, logs = _run_script("code/StokesColor.py", name, "STEPS", stokes_steps, snap_vars=vars_)
+    for k, s in enumerate(snaps):
+        for v in vars_:
+            out[f"color_s{k}_{v}"] = s[v]
+    out["color_log"] = np.array([l for l in logs if l.startswith("Step:")])
+    # --- StokesFood.py pusher: literal first steps incl. tracers ---
+    vars_ = ("u_star", "div_u_star", "p", "u", "p2", "final_div", "tracer_points", "tracer_status")
+    g, snaps, logs = _run_script("code/StokesFood.py", name, "STEPS", stokes_steps,
+                                 subs=(("B2 = 0.0", "B2 = -5.0"),), snap_vars=vars_)
+    for k, s in enumerate(snaps):
+        for v in vars_:
+            out[f"food_s{k}_{v}"] = s[v]
+    out["food_log"] = np.array([l for l in logs if l.startswith("Step:")])
+    return out
+
+
+def gen_long():
+    """6000-step mesh.1 traces: mixing progress (Color) and eaten counts (Food x3)."""
+    import re
+
+    out = {}
+    _, _, logs = _run_script("code/StokesColor.py", "mesh1", "STEPS", 6000)
+    prog = [float(re.search(r"progress=([-0-9.e]+)", l).group(1)) for l in logs if l.startswith("Step:")]
+    divs = [float(re.search(r"Div\(u\*\): ([-0-9.e+]+)", l).group(1)) for l in logs if l.startswith("Step:")]
+    out["color_mesh1_progress"] = np.array(prog)
+    out["color_mesh1_divstar"] = np.array(divs)
+    print("color done", prog[-1])
+    for tag, B2 in (("neutral", "0.0"), ("pusher", "-5.0"), ("puller", "5.0")):
+        _, _, logs = _run_script("code/StokesFood.py", "mesh1", "STEPS", 6000,
+                                 subs=(("B2 = 0.0", f"B2 = {B2}"),))
+        eaten = [int(re.search(r"Eaten \(Red\): (\d+)", l).group(1)) for l in logs if l.startswith("Step:")]
+        out[f"food_mesh1_{tag}_eaten"] = np.array(eaten)
+        print("food", tag, eaten[-1])
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--long", action="store_true")
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    _install_stubs()
+    if a.long:
+        np.savez_compressed(os.path.join(OUT, "long_mesh1.npz"), **gen_long())
+        return
+    for name in MESHES:
+        if a.only and name != a.only:
+            continue
+        d = gen_kernels(name)
+        d.update(gen_scripts(name))
+        np.savez_compressed(os.path.join(OUT, f"golden_{name}.npz"), **d)
+        print(name, "->", len(d), "arrays")
+
+
+if __name__ == "__main__":
+    main()
