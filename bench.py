@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: Stokes timesteps/s (and CG iterations/s) of the StokesColor operator-split step.
+
+Workload (BASELINE.json configs[4], the metric's ~10M-node case; it fits one GPU, so N=1 runs it
+too): the neutral-squirmer StokesColor step (B1=-2, B2=0, nu=0.1, DT=0.05, StokesColor.py:32-44)
+on mesh_fine red-refined 7 times (L7 = 14,230,528 nodes, 28,409,856 triangles), synthetic but
+deterministic (no RNG: initial state is the reference's u=0+squirmer BC, c=1[x<0.5]).  A "step"
+is one full pass of StokesColor.py:537-586: 2-RHS viscous CG, two periodic-merged pressure CGs
+(rtol --rtol-pres), three divergences, two gradient projections, BCs, semi-Lagrangian dye
+advection and the mixing index.  Strong scaling: the mesh is fixed and partitioned into y-slabs.
+
+  python bench.py [--gpus N --steps K --warmup W --level 7]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
+    ap.add_argument("--rtol-pres", type=float, default=1e-8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--fine-steps", type=int, default=200)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        # control plane only (rendezvous, barriers, max-over-ranks timing); the data path uses RCCL
+        # from libpucfem on the GPU stream.  torch is imported BEFORE libpucfem is loaded so the
+        # process has a single HIP runtime.
+        import torch
+        import torch.distributed as td
+
+        td.init_process_group("gloo", rank=rank, world_size=world)
+    pf = importlib.import_module("puc-fluidsimulation-project_amd")
+    L = importlib.import_module("puc-fluidsimulation-project_amd._lib")
+    if world > 1:
+        import ctypes as ct
+
+        uid = (ct.c_uint8 * 128)()
+        if rank == 0:
+            L.check(L.lib().pucfem_rccl_unique_id(uid))
+        obj = [bytes(uid)]
+        td.broadcast_object_list(obj, src=0)
+        dist = (rank, world, obj[0])
+
+    def barrier():
+        if world > 1:
+            td.barrier()
+
+    def allmax(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        return float(t.item())
+
+    t_setup = time.time()
+    mesh = pf.load_mesh("fine", refine=a.level)
+    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres)
+    sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
+    info = sim.ctx.info()
+    t_setup = time.time() - t_setup
+    if a.warmup:
+        sim.step(a.warmup)
+    sim.ctx.timing(True)
+    barrier()
+    sim.ctx.sync()
+    t0 = time.perf_counter()
+    stats = sim.step(a.steps)
+    sim.ctx.sync()
+    barrier()
+    dt_local = time.perf_counter() - t0
+    elapsed = allmax(dt_local)
+    ms_dir, n_dir, bytes_dir = sim.ctx.timing_get(0)
+    ms_upd, n_upd, bytes_upd = sim.ctx.timing_get(1)
+    sim.ctx.timing(False)
+    cg_iters = sum(2 * s.it_visc + s.it_p + s.it_p2 for s in stats)  # viscous CG is 2-RHS
+    cg_iter_launches = sum(s.it_visc + s.it_p + s.it_p2 for s in stats)
+    steps_per_s = a.steps / elapsed
+    rec = {
+        "metric": "Stokes timesteps/sec (and CG iters/sec) on mesh_fine & 10M-node mesh, 1/2/4/8 GPU",
+        "value": steps_per_s,
+        "unit": "timesteps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic red-refined mesh_fine, reference initial state)",
+        "config": {
+            "workload": f"StokesColor neutral squirmer step, mesh_fine refined x{a.level}",
+            "nodes": info["N"] if world == 1 else mesh.N, "triangles": mesh.T,
+            "dt": 0.05, "nu": 0.1, "B1": -2.0, "B2": 0.0,
+            "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
+        },
+        "cg_iters_per_s": cg_iters / elapsed,
+        "cg_iters_per_step": {"visc_2rhs": [s.it_visc for s in stats], "p": [s.it_p for s in stats],
+                              "p2": [s.it_p2 for s in stats]},
+        "diagnostics": {"max_div_star": stats[-1].max_div_star, "max_final_div": stats[-1].max_final_div,
+                        "mix_var": stats[-1].mix_var},
+        "setup_s": t_setup,
+    }
+    # roofline of the dominant kernel: k_cg_dir (SpMV + direction update of the Jacobi-CG),
+    # algorithmic bytes 12*nnz + 32*NRHS*n per launch, timed with HIP events on the library stream
+    if n_dir:
+        avg_ms = ms_dir / n_dir
+        ach = bytes_dir / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                key = f"L{a.level}_n{world}"
+                traffic = d.get(key, {}).get("k_cg_dir_hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        rec["roofline"] = {"bound": "hbm", "kernel": "k_cg_dir", "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                           "bytes_per_launch": bytes_dir, "avg_launch_ms": avg_ms, "launches": n_dir,
+                           "k_cg_upd": {"avg_launch_ms": ms_upd / max(n_upd, 1),
+                                        "achieved": bytes_upd / max(ms_upd / max(n_upd, 1), 1e-9) / 1e6}}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats)
+    if rank == 0 and world == 1 and not a.no_secondary:
+        rec["mesh_fine"] = secondary_fine(pf, a.fine_steps)
+    sim.close()
+    if rank == 0:
+        print(json.dumps(rec))
+    if world > 1:
+        td.destroy_process_group()
+
+
+def cpu_baseline(pf, level, stats):
+    """The oracle (numpy/scipy restatement, oracle/) timed on a bounded sample on this host.
+
+    Sample: mesh_fine refined min(level, 5) times (L5 = 894,208 nodes).  Timed pieces: Jacobi-PCG
+    iterations on the merged pressure operator and on A_visc (the HIP solver's algorithm),
+    divergence + gradient (reference-order element loops), one semi-Lagrangian step (KDTree k=10).
+    CPU seconds per step = (measured pieces) x (nnz ratio to the benchmarked level) with the GPU
+    run's own CG iteration counts."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    import numpy as np
+
+    import oracle as O
+
+    lv = min(level, 5)
+    m = pf.load_mesh("fine", refine=lv)
+    X, mk, T = m.coords, m.markers, m.triangles
+    pairs = O.filter_wall_pairs(X, O.find_boundary_pairs(X))
+    wall, inner, dirichlet, interior = O.boundary_sets(X, mk)
+    K = O.stiffness(X, T)
+    Ap = O.pressure_operator(K, pairs)
+    Av = O.visc_matrix(K, 0.05, 0.1, dirichlet)
+    rng = np.random.default_rng(0)
+    b = rng.standard_normal(m.N)
+    b -= b.mean()
+    it_s = 20
+    t = time.perf_counter()
+    O.jacobi_pcg(Ap, b, np.zeros(m.N), it_s)
+    t_pcg = (time.perf_counter() - t) / it_s
+    t = time.perf_counter()
+    O.jacobi_pcg(Av, b, np.zeros(m.N), it_s)
+    t_vcg = (time.perf_counter() - t) / it_s
+    u = rng.standard_normal((m.N, 2))
+    t = time.perf_counter()
+    O.divergence(X, T, u)
+    O.gradient(X, T, u[:, 0])
+    t_dg = (time.perf_counter() - t) / 2
+    c0 = (X[:, 0] < 0.5).astype(float)
+    t = time.perf_counter()
+    O.sl_advect(c0, 0.02 * u, 0.05, X, T)
+    t_sl = time.perf_counter() - t
+    scale = 4.0 ** (level - lv)  # nnz / nodes / triangles all grow 4x per red refinement
+    it_p = np.mean([s.it_p + s.it_p2 for s in stats])
+    it_v = np.mean([s.it_visc for s in stats])
+    sec_step = scale * (it_p * t_pcg + 2 * it_v * t_vcg + 5 * t_dg + t_sl)
+    return {"value": 1.0 / sec_step, "unit": "timesteps/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle (numpy/scipy, 1 thread) on mesh_fine x{lv} ({m.N} nodes): "
+                       f"{it_s} Jacobi-PCG iters each of the pressure and viscous operators, div+grad, one SL "
+                       f"step; scaled x{scale:g} to x{level} with the GPU run's CG iterations/step "
+                       f"(p+p2 {it_p:.0f}, visc {it_v:.0f})"),
+            "sample_seconds": {"pcg_iter": t_pcg, "visc_iter": t_vcg, "div_or_grad": t_dg, "sl": t_sl}}
+
+
+def secondary_fine(pf, steps):
+    """mesh_fine itself (BASELINE configs[2]): GPU steps/s vs the oracle's full step on this host.
+    The literal reference measured 173 ms/step (8 threads) / 203 ms/step (1 thread) in BASELINE.md."""
+    import numpy as np
+
+    import oracle as O
+
+    mesh = pf.load_mesh("fine")
+    sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", tol=pf.Tolerances(rtol_pres=1e-12))
+    sim.step(20)
+    sim.ctx.sync()
+    t = time.perf_counter()
+    st = sim.step(steps)
+    sim.ctx.sync()
+    gpu = steps / (time.perf_counter() - t)
+    sim.close()
+    ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.05, 0.1, -2.0, 0.0, "color")
+    u, c = ref.initial()
+    for _ in range(3):
+        out = ref.step(u, c)
+        u, c = out["u"], out["c"]
+    n = 20
+    t = time.perf_counter()
+    for _ in range(n):
+        out = ref.step(u, c)
+        u, c = out["u"], out["c"]
+    cpu = n / (time.perf_counter() - t)
+    return {"workload": "StokesColor neutral squirmer, mesh_fine (1,067 nodes), rtol_pres 1e-12",
+            "gpu_steps_per_s": gpu, "cpu_oracle_steps_per_s": cpu, "cpu_oracle_kind": "port (scipy splu per step)",
+            "ratio_vs_oracle": gpu / cpu, "reference_literal_steps_per_s_baseline_md": 5.8,
+            "ratio_vs_reference_literal": gpu / 5.8,
+            "cg_iters_last_step": [st[-1].it_visc, st[-1].it_p, st[-1].it_p2]}
+
+
+if __name__ == "__main__":
+    main()

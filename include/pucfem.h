@@ -1,0 +1,190 @@
+/*
+ * pucfem.h -- C ABI of libpucfem.so, the MI355X (gfx950) hot path of the
+ * PUC-Fluidsimulation-Project Stokes/squirmer time-stepping core.
+ *
+ * The reference (TobiasHoffmannP/PUC-Fluidsimulation-Project, pure Python/NumPy)
+ * has no FFI layer: its de-facto interface is a set of module-level functions plus
+ * the np.linalg.solve call sites.  Each entry point below names the
+ * reference code it replaces (file:line into /root/reference).  The Python host
+ * (puc-fluidsimulation-project_amd/_lib.py) binds these with ctypes; INTEGRATION.md
+ * shows the binding.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = ok, < 0 = error (PUCFEM_E*); the message is in
+ *     pucfem_last_error(ctx) (or pucfem_last_error(NULL) for context-free calls).
+ *   - Plain pointers and sizes only.  The library COPIES every input buffer; the caller
+ *     keeps ownership.  Output buffers are caller-allocated.
+ *   - Node / triangle numbering at the ABI is always the CALLER's (reference) numbering,
+ *     0-based.  The library renumbers internally for locality and partitioning.
+ *   - A context is bound to one HIP device (or none: device = PUCFEM_HOST_ONLY builds the
+ *     host-side operators only, for CPU tests) and is NOT thread-safe.  Calls are
+ *     synchronous at the ABI level; device streams are internal.
+ *   - fp64 throughout, except the fp32-coordinate assembly of poisson.py / heatEq.py
+ *     (poisson.py:40, :100-146), reproduced bit-for-bit on the host.
+ */
+#ifndef PUCFEM_H
+#define PUCFEM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PUCFEM_ABI_VERSION 1
+#define PUCFEM_HOST_ONLY (-1)
+#define PUCFEM_UNIQUE_ID_BYTES 128
+
+enum pucfem_status {
+  PUCFEM_OK = 0,
+  PUCFEM_EINVAL = -1,   /* bad argument / shape */
+  PUCFEM_EHIP = -2,     /* HIP runtime error (no device, launch failure, ...) */
+  PUCFEM_ENOCONV = -3,  /* iterative solver hit maxit without reaching rtol */
+  PUCFEM_ESTATE = -4,   /* call out of order (e.g. step before build) */
+  PUCFEM_ENCCL = -5,    /* RCCL error */
+  PUCFEM_ENOMEM = -6,
+  PUCFEM_ENODEV = -7    /* compute call on a host-only context */
+};
+
+/* which reference script's step loop the context runs */
+enum pucfem_scheme {
+  PUCFEM_STOKES_COLOR = 0, /* StokesColor.py:537-586  (Stokes + semi-Lagrangian dye) */
+  PUCFEM_STOKES_FOOD = 1,  /* StokesFood.py:441-505   (Stokes + tracer capture)     */
+  PUCFEM_HEAT = 2,         /* heatEq.py:304-325       (backward-Euler diffusion)    */
+  PUCFEM_POISSON = 3       /* poisson.py:218-285      (steady Poisson)              */
+};
+
+typedef struct pucfem_params {
+  int32_t scheme;      /* enum pucfem_scheme */
+  int32_t nstrips;     /* y-strips of the node ordering / partition; 0 = auto */
+  double dt;           /* DT  (StokesColor.py:43, StokesFood.py:42, heatEq.py:304) */
+  double nu;           /* v   (kinematic viscosity, StokesColor.py:39) */
+  double rtol_visc;    /* CG rtol, viscous solve  (replaces LU at StokesColor.py:544-545) */
+  double rtol_pres;    /* CG rtol, pressure solve (replaces LU at StokesColor.py:555,569) */
+  double rtol_lin;     /* BiCGStab rtol, heat / Poisson literal operators */
+  int32_t maxit_visc, maxit_pres, maxit_lin;
+  int32_t warm_start;  /* 1: start each solve from the previous step's solution */
+  int32_t sl_k;        /* PointLocator k (StokesColor.py:324), 10 */
+  double capture_radius; /* StokesFood.py:50-51, 0.28 */
+  double center_x, center_y; /* squirmer centre (0.5, 0.5) */
+} pucfem_params;
+
+/* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
+typedef struct pucfem_step_stats {
+  double max_div_star;   /* max |div u*|          */
+  double max_final_div;  /* max |div u^{n+1}|     */
+  double mix_I, mix_mu, mix_var; /* mixing_index (StokesColor.py:391-403) over marker==0 */
+  int64_t eaten;         /* StokesFood: sum(tracer_status) */
+  int32_t it_visc, it_p, it_p2; /* CG iterations of the three solves */
+  int32_t sl_notfound;   /* nodes that kept c[n] because PointLocator.find returned None */
+} pucfem_step_stats;
+
+/* fields exchanged with pucfem_set_field / pucfem_get_field (reference numbering) */
+enum pucfem_field {
+  PUCFEM_F_U = 0,         /* u      (N,2) row-major */
+  PUCFEM_F_USTAR = 1,     /* u_star (N,2) */
+  PUCFEM_F_P = 2,         /* p      (N)   zero-mean gauge */
+  PUCFEM_F_P2 = 3,        /* p2     (N) */
+  PUCFEM_F_DIV_STAR = 4,  /* div_u_star (N) */
+  PUCFEM_F_DIV_U = 5,     /* div_u      (N) (before the 2nd projection) */
+  PUCFEM_F_FINAL_DIV = 6, /* final_div  (N) */
+  PUCFEM_F_C = 7,         /* dye c  (N) */
+  PUCFEM_F_SCALAR = 8,    /* heat u / Poisson f (N) */
+  PUCFEM_F_TRACERS = 9,   /* tracer_points (n_tr,2); set_field defines n_tr */
+  PUCFEM_F_STATUS = 10    /* tracer_status (n_tr) as 0.0 / 1.0 */
+};
+
+/* operators for pucfem_apply / pucfem_solve / pucfem_host_get_csr */
+enum pucfem_op {
+  PUCFEM_OP_K = 0,      /* stiffness K (StokesColor.py:98-128), y = K x */
+  PUCFEM_OP_VISC = 1,   /* A_visc (StokesColor.py:471-475) */
+  PUCFEM_OP_PRES = 2,   /* periodic-merged pressure operator P^T K P (+ identity slave rows) */
+  PUCFEM_OP_GX = 3,     /* lumped gradient coefficients (StokesColor.py:224-263), x-part */
+  PUCFEM_OP_GY = 4,
+  PUCFEM_OP_DIV = 5,    /* calculate_divergence (StokesColor.py:130-165): x = u (N,2), y = div (N) */
+  PUCFEM_OP_GRAD = 6,   /* calculate_gradiant  (StokesColor.py:224-263): x = p (N), y = (N,2) */
+  PUCFEM_OP_LIT = 7     /* literal heat operator I + DT*A (heatEq.py:305) or Poisson A (poisson.py:253-278) */
+};
+
+/* ---- library / context ---------------------------------------------------------- */
+int pucfem_abi_version(void);
+const char* pucfem_last_error(const void* ctx);
+int pucfem_device_count(int32_t* n);
+int pucfem_ctx_create(int32_t device, void** out_ctx);
+/* multi-GPU: one process per GPU; rank/world from torch.distributed, unique id from
+   rank 0's pucfem_rccl_unique_id broadcast over the control plane. */
+int pucfem_rccl_unique_id(uint8_t* out_id /* PUCFEM_UNIQUE_ID_BYTES */);
+int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const uint8_t* unique_id,
+                           void** out_ctx);
+int pucfem_ctx_destroy(void* ctx);
+
+/* ---- mesh + boundary conditions (replaces readNode/readEle globals, StokesColor.py:437-464) */
+int pucfem_mesh_upload(void* ctx, int64_t n_nodes, const double* xy /* N x 2 */,
+                       const int32_t* markers, int64_t n_tris, const int32_t* tris /* T x 3 */,
+                       int32_t coord_fp32 /* 1: poisson/heat fp32 coordinates (poisson.py:40) */);
+/* periodic pairs (master, slave):
+   kind 0 = operator pairs: filtered pairs of StokesColor.py:449-457 / poisson.py:242-253
+   kind 1 = BC-copy pairs: makePerBCU (StokesColor.py:429-431) / reapply_periodic_u (heatEq.py:298-301,
+            UNFILTERED).  Sequential semantics (u[s] = u[m] in list order) are preserved. */
+int pucfem_set_pairs(void* ctx, int32_t kind, int64_t n_pairs, const int64_t* pairs /* P x 2 */);
+/* Dirichlet nodes and values, applied in list order (makeDirBCU StokesColor.py:405-427,
+   reapply_dirchlect_u heatEq.py:282-295, Dirichlet rows poisson.py:258-278). ncomp = 2 (Stokes) or 1. */
+int pucfem_set_dirichlet(void* ctx, int64_t n, const int32_t* nodes, const double* values, int32_t ncomp);
+/* Poisson load g(centroid) per triangle, evaluated by the host in the reference's dtype
+   (poisson.py:135-144, g = 50 sin(3y) in fp32). */
+int pucfem_set_source(void* ctx, int64_t n_tris, const float* g_tri);
+int pucfem_build_operators(void* ctx, const pucfem_params* params);
+
+/* ---- fields ---------------------------------------------------------------------- */
+int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count);
+int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count);
+
+/* ---- time stepping: nsteps iterations of the scheme's loop body ------------------- */
+int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats /* nsteps entries or NULL */);
+
+/* ---- unit operations (reference-named shims and parity tests) --------------------- */
+int pucfem_apply(void* ctx, int32_t op, const double* x, double* y);
+/* op VISC: b,x are (N,2) (both velocity components, StokesColor.py:544-545);
+   op PRES: b = b_p (N) as formed at StokesColor.py:554, x = zero-mean p;
+   op LIT : heat / Poisson literal system. */
+int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol, int32_t maxit,
+                 int32_t* iters);
+/* advect_semilagrange (StokesColor.py:347-389): c_out = SL(c, u, dt); notfound may be NULL */
+int pucfem_sl_advect(void* ctx, const double* c, const double* u, double dt, double* c_out,
+                     int32_t* notfound);
+/* tracer step (StokesFood.py:482-499) on the tracers held in the context, with u given */
+int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps);
+/* mixing_index (StokesColor.py:391-403) over marker==0 nodes: out = (I, mu, var) */
+int pucfem_mixing_index(void* ctx, const double* c, double* out3);
+
+/* ---- measurement ------------------------------------------------------------------ */
+/* HIP-event timing of each kernel class on the context's stream (bench.py roofline). */
+int pucfem_timing_enable(void* ctx, int32_t on);
+/* kernel classes: 0 = CG SpMV+direction (dominant), 1 = CG update, 2 = div/grad, 3 = SL, 4 = other */
+int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
+                      double* bytes_per_launch);
+int pucfem_sync(void* ctx);
+/* sizes of the internal operators: out[0]=N, [1]=T, [2]=nnz(P), [3]=nnz(Pp), [4]=n_own,
+   [5]=n_ghost, [6]=padded SELL entries (P), [7]=padded SELL entries (Pp), [8]=n_pairs, [9]=n_dirichlet */
+int pucfem_info(void* ctx, int64_t* out10);
+
+/* ---- host-only (no device needed) ---------------------------------------------------- */
+/* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */
+int pucfem_refine(int64_t n_nodes, const double* xy, const int32_t* markers, int64_t n_tris,
+                  const int32_t* tris, int32_t levels, int64_t* n_nodes_out, int64_t* n_tris_out,
+                  double* xy_out, int32_t* markers_out, int32_t* tris_out);
+/* The host-assembled operator of this rank in the CALLER's numbering (rows owned by this rank,
+   global column ids).  Call with col == NULL to get nnz.  For CPU tests of the assembly. */
+int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, int64_t* rowptr,
+                        int64_t* col, double* val);
+/* Partition plan for (rank, world) computed on a host-only context (pucfem_ctx_create(-1)):
+   owned rows (caller numbering) in internal order, then the ghost ids; send lists per peer.
+   Sizes first (arrays NULL), then contents. */
+int pucfem_host_partition(void* ctx, int32_t rank, int32_t world, int64_t* n_own, int64_t* n_ghost,
+                          int64_t* owned, int64_t* ghosts, int32_t* ghost_owner,
+                          int64_t* n_send, int64_t* send_ids, int32_t* send_peer);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PUCFEM_H */

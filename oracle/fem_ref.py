@@ -19,7 +19,7 @@ __all__ = [
     "boundary_sets", "squirmer_bc", "make_dir_bcu", "make_per_bcu",
     "visc_matrix", "PressureSolver", "centroids", "sl_advect", "mixing_index",
     "plane_coefficients", "locate_bary", "tracer_init", "tracer_step",
-    "poisson_literal", "HeatLiteral", "StokesRef",
+    "poisson_literal", "HeatLiteral", "StokesRef", "pressure_operator", "jacobi_pcg",
 ]
 
 TOL = 1e-6
@@ -554,3 +554,35 @@ class StokesRef:
         if tracers is not None:
             out["tracers"], out["status"] = tracer_step(tracers, status, un, dt, X, T)
         return out
+
+
+# ----------------------------------------------------------------------------- CPU baseline helpers
+def pressure_operator(K, pairs):
+    """P^T K P of PressureSolver without the factorisation (node numbering, slave rows identity)."""
+    N = K.shape[0]
+    dof = np.arange(N)
+    dof[pairs[:, 1]] = pairs[:, 0]
+    P = sp.csr_matrix((np.ones(N), (np.arange(N), dof)), shape=(N, N))
+    A = (P.T @ K @ P).tolil()
+    A[pairs[:, 1], pairs[:, 1]] = 1.0
+    return A.tocsr()
+
+
+def jacobi_pcg(A, b, x0, iters):
+    """`iters` iterations of Jacobi-preconditioned CG (the algorithm of the HIP solver), scipy CSR."""
+    dinv = 1.0 / A.diagonal()
+    x = x0.copy()
+    r = b - A @ x
+    z = dinv * r
+    p = z.copy()
+    rz = r @ z
+    for _ in range(iters):
+        q = A @ p
+        a = rz / (p @ q)
+        x += a * p
+        r -= a * q
+        z = dinv * r
+        rz2 = r @ z
+        p = z + (rz2 / rz) * p
+        rz = rz2
+    return x, float(np.sqrt(r @ r))

@@ -1,0 +1,1575 @@
+// libpucfem C ABI (include/pucfem.h): context, device memory, solver orchestration, RCCL halo /
+// all-reduce, and the Stokes / heat / Poisson step loops.  One HIP stream per context; every
+// kernel of a step is enqueued back to back and the host synchronises only to poll CG
+// convergence (once per chunk of iterations) and to return results.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "pucfem.h"
+#include "pucfem_host.hpp"
+#include "pucfem_kernels.hpp"
+#include "pucfem_kernels_impl.hpp"
+
+using namespace pucfem;
+using namespace pucfem::dev;
+
+namespace {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                 \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess)                                                                         \
+      throw Error(PUCFEM_EHIP, std::string(#x) + ": " + hipGetErrorString(e_));                   \
+  } while (0)
+#define NCCLCHK(x)                                                                                \
+  do {                                                                                            \
+    ncclResult_t r_ = (x);                                                                        \
+    if (r_ != ncclSuccess) throw Error(PUCFEM_ENCCL, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+#define KCHK() HIPCHK(hipGetLastError())
+
+std::string g_err;  // errors of context-free calls
+
+struct DevSell {
+  int64_t* off = nullptr;
+  int32_t* w = nullptr;
+  int32_t* col = nullptr;
+  int64_t nslices = 0, nrows = 0, nnz = 0, padded = 0;
+  SellDev view() const { return SellDev{off, w, col, nslices, nrows}; }
+};
+
+struct Red {  // a (possibly globally reduced) partial array
+  const double* p;
+  int nb;
+  int stride;
+};
+
+struct Timer {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  struct Pend { int cls; hipEvent_t a, b; double bytes; };
+  std::vector<Pend> pend;
+  double ms[5] = {0, 0, 0, 0, 0};
+  double bytes[5] = {0, 0, 0, 0, 0};
+  int64_t n[5] = {0, 0, 0, 0, 0};
+  hipEvent_t get() {
+    if (pool.empty()) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      return e;
+    }
+    hipEvent_t e = pool.back();
+    pool.pop_back();
+    return e;
+  }
+  void flush() {
+    for (auto& p : pend) {
+      float t = 0;
+      HIPCHK(hipEventSynchronize(p.b));
+      HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
+      ms[p.cls] += t;
+      bytes[p.cls] += p.bytes;
+      n[p.cls]++;
+      pool.push_back(p.a);
+      pool.push_back(p.b);
+    }
+    pend.clear();
+  }
+  ~Timer() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+    for (auto& p : pend) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+  }
+};
+
+struct Ctx {
+  std::string err;
+  int device = -1;
+  bool host_only = true;
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  hipStream_t st = nullptr;
+  std::vector<void*> allocs;
+  Timer timer;
+
+  // ---- inputs
+  HostMesh mesh;
+  bool has_mesh = false;
+  std::vector<std::pair<i64, i64>> op_pairs, bc_pairs;
+  std::vector<i32> dir_nodes;
+  std::vector<double> dir_vals;
+  int dir_ncomp = 0;
+  std::vector<float> g_tri;
+  pucfem_params prm{};
+  bool built = false;
+
+  // ---- host structures (internal numbering)
+  Ordering ord;
+  Csr P, Pp, Lit;
+  Assembly as;
+  std::vector<double> litb, Kv;
+  std::vector<i64> row_start;
+  LocalPlan lp;
+  Sell sP, sPp, sLit;
+  std::vector<i32> dof, slave_of, master_of;  // global internal ids
+  i64 n_free = 0;
+  int scheme = 0;
+
+  // ---- device operators
+  DevSell dP, dPp, dLit;
+  double *dK = nullptr, *dGx = nullptr, *dGy = nullptr, *dKv = nullptr, *dKp = nullptr, *dLitv = nullptr;
+  double *dsv = nullptr, *dsqv = nullptr, *dsp = nullptr, *dsqp = nullptr, *dlit_dinv = nullptr;
+  double *das1 = nullptr, *dmp = nullptr, *dwmix = nullptr;
+  uint8_t* ddir = nullptr;
+  int32_t *dslave_of = nullptr, *dmaster_of = nullptr;
+  int32_t *dcdst = nullptr, *dcsrc = nullptr, *ddnode = nullptr;
+  double *ddval = nullptr, *dbctmp = nullptr;
+  int ncopy = 0, ndir = 0;
+  int32_t* dsend = nullptr;
+  double* dsendbuf = nullptr;
+  i64 nsend = 0;
+
+  // ---- device fields (local: n_own + n_ghost)
+  i64 nloc = 0;
+  double *ux = nullptr, *uy = nullptr, *usx = nullptr, *usy = nullptr, *p = nullptr, *p2 = nullptr;
+  double *yp = nullptr, *yp2 = nullptr, *yvx = nullptr, *yvy = nullptr;
+  double *div_star = nullptr, *div_u = nullptr, *final_div = nullptr, *braw = nullptr, *bh = nullptr;
+  double *bvx = nullptr, *bvy = nullptr;
+  double *cg_r[2] = {nullptr, nullptr}, *cg_pa[2] = {nullptr, nullptr}, *cg_pb[2] = {nullptr, nullptr},
+         *cg_q[2] = {nullptr, nullptr};
+  double *part_a = nullptr, *part_b = nullptr, *part_c = nullptr, *part_d = nullptr;
+  double* scal = nullptr;
+  int* ctl = nullptr;
+  int* h_ctl = nullptr;  // pinned
+  double* redbuf = nullptr;  // small buffers for all-reduced scalars (64 x 8)
+  double* vals = nullptr;    // per-step diagnostic slots (16)
+  double* scalar = nullptr;  // heat u / poisson f
+  double* litw[10] = {};     // BiCGStab workspace
+  double* bicg_sc = nullptr;
+  double* h_pinned = nullptr;
+
+  // ---- full-mesh replica (SL, tracers)
+  double *mx = nullptr, *my = nullptr;
+  int32_t* mtri = nullptr;
+  GridDev cgrid{}, tgrid{};
+  bool has_cgrid = false, has_tgrid = false;
+  double *c_full = nullptr, *c_new = nullptr, *ufx = nullptr, *ufy = nullptr;
+  int32_t* dnotfound = nullptr;
+  int32_t ntr = 0;
+  double *trx = nullptr, *try_ = nullptr, *trs = nullptr, *d_eaten = nullptr;
+  int last_it[3] = {0, 0, 0};
+
+  ~Ctx() {
+    if (!host_only) {
+      if (st) (void)hipStreamSynchronize(st);
+      for (void* a : allocs) (void)hipFree(a);
+      if (h_ctl) (void)hipHostFree(h_ctl);
+      if (h_pinned) (void)hipHostFree(h_pinned);
+      if (comm) (void)ncclCommDestroy(comm);
+      if (st) (void)hipStreamDestroy(st);
+    }
+  }
+
+  template <class T>
+  T* dalloc(i64 n) {
+    if (n <= 0) n = 1;
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, sizeof(T) * (size_t)n));
+    HIPCHK(hipMemsetAsync(p, 0, sizeof(T) * (size_t)n, st));
+    allocs.push_back(p);
+    return (T*)p;
+  }
+  template <class T>
+  T* upload(const std::vector<T>& v) {
+    T* p = dalloc<T>((i64)v.size());
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
+    return p;
+  }
+  void need_dev() const {
+    if (host_only) throw Error(PUCFEM_ENODEV, "compute call on a host-only context");
+  }
+  void need_built() const {
+    if (!built) throw Error(PUCFEM_ESTATE, "pucfem_build_operators has not been called");
+  }
+
+  static int nb_for(i64 nslices) { return (int)std::max<i64>(1, std::min<i64>(MAXB, (nslices + 3) / 4)); }
+  int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
+  static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
+
+  // ------------------------------------------------------------------ timing helpers
+  void tstart(hipEvent_t& a) {
+    if (timer.on) {
+      a = timer.get();
+      HIPCHK(hipEventRecord(a, st));
+    }
+  }
+  void tstop(int cls, hipEvent_t a, double bytes) {
+    if (timer.on) {
+      hipEvent_t b = timer.get();
+      HIPCHK(hipEventRecord(b, st));
+      timer.pend.push_back({cls, a, b, bytes});
+    }
+  }
+
+  // ------------------------------------------------------------------ communication
+  Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
+    if (world == 1) return Red{part, nb, MAXB};
+    double* buf = redbuf + 8 * slot;
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
+    KCHK();
+    NCCLCHK(ncclAllReduce(buf, buf, nv, ncclDouble, is_max ? ncclMax : ncclSum, comm, st));
+    return Red{buf, 1, 1};
+  }
+  // reduce partials into vals[slot..slot+nv) (+ all-reduce)
+  void reduce_into(double* part, int nb, int nv, bool is_max, int slot) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, vals + slot);
+    KCHK();
+    if (world > 1)
+      NCCLCHK(ncclAllReduce(vals + slot, vals + slot, nv, ncclDouble, is_max ? ncclMax : ncclSum, comm, st));
+  }
+  // refresh the ghost entries of up to two local vectors
+  void halo(double* a, double* b = nullptr) {
+    if (world == 1 || (lp.send_peer.empty() && lp.recv_peer.empty())) return;
+    const int nv = b ? 2 : 1;
+    if (nsend > 0) {
+      hipLaunchKernelGGL(k_pack, dim3(grid_ew(nsend)), dim3(BS), 0, st, nsend, dsend, a, b, dsendbuf);
+      KCHK();
+    }
+    NCCLCHK(ncclGroupStart());
+    for (size_t k = 0; k < lp.send_peer.size(); ++k) {
+      NCCLCHK(ncclSend(dsendbuf + lp.send_off[k], lp.send_cnt[k], ncclDouble, lp.send_peer[k], comm, st));
+      if (b) NCCLCHK(ncclSend(dsendbuf + nsend + lp.send_off[k], lp.send_cnt[k], ncclDouble, lp.send_peer[k], comm, st));
+    }
+    for (size_t k = 0; k < lp.recv_peer.size(); ++k) {
+      NCCLCHK(ncclRecv(a + lp.n_own + lp.recv_off[k], lp.recv_cnt[k], ncclDouble, lp.recv_peer[k], comm, st));
+      if (b) NCCLCHK(ncclRecv(b + lp.n_own + lp.recv_off[k], lp.recv_cnt[k], ncclDouble, lp.recv_peer[k], comm, st));
+    }
+    NCCLCHK(ncclGroupEnd());
+    (void)nv;
+  }
+  // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
+  void allgather_full(double* full) {
+    if (world == 1) return;
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < world; ++r) {
+      const i64 o = row_start[r], n = row_start[r + 1] - row_start[r];
+      NCCLCHK(ncclBroadcast(full + o, full + o, n, ncclDouble, r, comm, st));
+    }
+    NCCLCHK(ncclGroupEnd());
+  }
+
+  // ------------------------------------------------------------------ CG
+  template <int NR>
+  int cg(const DevSell& A, const double* val, double* const y[NR], const double* const b[NR], double tol,
+         int maxit, int which) {
+    const int nb = nb_for(A.nslices);
+    CgVecs<NR> v;
+    for (int c = 0; c < NR; ++c) {
+      v.y[c] = y[c];
+      v.b[c] = b[c];
+      v.r[c] = cg_r[c];
+      v.po[c] = cg_pa[c];
+      v.pn[c] = cg_pb[c];
+      v.q[c] = cg_q[c];
+    }
+    if (NR == 2) halo(y[0], y[1]);
+    else halo(y[0]);
+    hipLaunchKernelGGL((k_cg_init<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, part_a, part_b);
+    KCHK();
+    Red rr = reduce_global(part_a, nb, NR, false, 0);
+    Red bb = reduce_global(part_b, nb, NR, false, 1);
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    if (NR == 2) halo(cg_r[0], cg_r[1]);
+    else halo(cg_r[0]);
+    const double tol2 = tol * tol;
+    const double bytes_dir = 12.0 * (double)A.nnz + 32.0 * NR * (double)A.nrows;
+    const double bytes_upd = 48.0 * NR * (double)A.nrows;
+    int it = 0;
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
+    for (;;) {
+      for (int k = 0; k < chunk; ++k, ++it) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        tstart(e0);
+        hipLaunchKernelGGL((k_cg_dir<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, rr.p, rr.nb,
+                           rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c);
+        KCHK();
+        tstop(0, e0, bytes_dir);
+        Red pq = reduce_global(part_c, nb, NR, false, 2);
+        tstart(e1);
+        hipLaunchKernelGGL((k_cg_upd<NR>), dim3(nb), dim3(BS), 0, st, v, A.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
+                           part_a);
+        KCHK();
+        tstop(1, e1, bytes_upd);
+        rr = reduce_global(part_a, nb, NR, false, 0);
+        if (NR == 2) halo(cg_r[0], cg_r[1]);
+        else halo(cg_r[0]);
+        for (int c = 0; c < NR; ++c) std::swap(v.po[c], v.pn[c]);
+      }
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (timer.on) timer.flush();
+      if (h_ctl[0]) break;
+      chunk = std::max(4, std::min(64, it / 8));
+    }
+    last_it[which] = h_ctl[1];
+    if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "CG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");
+    if (h_ctl[0] != 1)
+      throw Error(PUCFEM_ENOCONV, "CG did not converge within maxit=" + std::to_string(maxit));
+    return h_ctl[1];
+  }
+
+  // ------------------------------------------------------------------ building blocks of the step
+  void bc(double* a, double* b) {  // makePerBCU + makeDirBCU on owned rows
+    if (ncopy == 0 && ndir == 0) return;
+    hipLaunchKernelGGL(k_bc, dim3(1), dim3(1024), 0, st, ncopy, dcdst, dcsrc, dbctmp, ndir, ddnode, ddval,
+                       dir_ncomp, a, b);
+    KCHK();
+  }
+  int viscous(int& iters) {  // StokesColor.py:540-547
+    const i64 n = lp.n_own;
+    hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy);
+    KCHK();
+    double* y[2] = {yvx, yvy};
+    const double* b[2] = {bvx, bvy};
+    iters = cg<2>(dP, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
+                       (const int32_t*)nullptr);
+    KCHK();
+    bc(usx, usy);
+    halo(usx, usy);
+    return 0;
+  }
+  void div(const double* ax, const double* ay, double* out, bool rhs) {
+    const int nb = nb_for(dP.nslices);
+    hipEvent_t e = nullptr;
+    tstart(e);
+    hipLaunchKernelGGL(k_div, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, ax, ay, das1, out, dmp,
+                       -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
+    KCHK();
+    tstop(2, e, 20.0 * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
+  }
+  int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
+    const int nb = nb_for(dP.nslices);
+    Red sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
+    const i64 n = lp.n_own;
+    hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, dsp,
+                       sb.p, sb.nb, 1.0 / (double)n_free, bh);
+    KCHK();
+    if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
+    double* y[1] = {yst};
+    const double* b[1] = {bh};
+    int it = cg<1>(dPp, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
+    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, dsp, yst, (const double*)nullptr, pout,
+                       (double*)nullptr, dmaster_of);
+    KCHK();
+    halo(pout);
+    return it;
+  }
+  void grad_proj(const double* pp, int mode) {
+    const int nb = nb_for(dP.nslices);
+    hipEvent_t e = nullptr;
+    tstart(e);
+    hipLaunchKernelGGL(k_grad_proj, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, pp, das1, prm.dt, mode, ddir,
+                       usx, usy, ux, uy);
+    KCHK();
+    tstop(2, e, 20.0 * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
+  }
+
+  // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
+  void stokes_step(double* rec, int32_t* its) {
+    int itv = 0;
+    viscous(itv);
+    div(usx, usy, div_star, true);
+    reduce_into(part_d, nb_for(dP.nslices), 1, true, 0);  // max |div u*|
+    const int itp = pressure(yp, p, 1);
+    grad_proj(p, 0);
+    bc(ux, uy);
+    halo(ux, uy);
+    div(ux, uy, div_u, true);
+    const int itp2 = pressure(yp2, p2, 2);
+    grad_proj(p2, 1);
+    halo(ux, uy);
+    div(ux, uy, final_div, false);
+    reduce_into(part_d, nb_for(dP.nslices), 1, true, 1);  // max |final div|
+    if (scheme == PUCFEM_STOKES_COLOR) {
+      const int nb = nb_rows(lp.n_own);
+      hipEvent_t e = nullptr;
+      tstart(e);
+      hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, cgrid, lp.r0, lp.n_own, ux,
+                         uy, prm.dt, c_full, c_new, dwmix, (int32_t*)nullptr, part_a);
+      KCHK();
+      tstop(3, e, 8.0 * 6 * (double)lp.n_own);
+      std::swap(c_full, c_new);
+      allgather_full(c_full);
+      reduce_into(part_a, nb, 3, false, 2);  // sum wc, sum w, not-found
+      hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
+      KCHK();
+      reduce_into(part_b, nb, 1, false, 5);
+    } else {
+      tracer_advance(prm.dt);
+    }
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec);
+    KCHK();
+    its[0] = itv;
+    its[1] = itp;
+    its[2] = itp2;
+  }
+
+  void tracer_advance(double dt) {
+    if (ntr == 0) {
+      HIPCHK(hipMemsetAsync(vals + 6, 0, sizeof(double), st));
+      return;
+    }
+    if (!has_tgrid) throw Error(PUCFEM_ESTATE, "tracer grid not built (scheme is not STOKES_FOOD)");
+    double *fx = ux, *fy = uy;
+    if (world > 1) {  // full replica of u (internal numbering is rank-contiguous)
+      HIPCHK(hipMemcpyAsync(ufx + lp.r0, ux, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(ufy + lp.r0, uy, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+      allgather_full(ufx);
+      allgather_full(ufy);
+      fx = ufx;
+      fy = ufy;
+    }
+    hipLaunchKernelGGL(k_tracer, dim3(1), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, tgrid, fx, fy, ntr, trx,
+                       try_, trs, dt, prm.center_x, prm.center_y, prm.capture_radius, vals + 6);
+    KCHK();
+  }
+
+  // ------------------------------------------------------------------ literal operators (heat / Poisson)
+  int bicgstab(double* x, const double* b, double tol, int maxit) {
+    const i64 n = lp.n_own;
+    const int nb = nb_rows(n), ge = grid_ew(n);
+    double *r = litw[0], *rh = litw[1], *pp = litw[2], *v = litw[3], *s = litw[4], *t = litw[5], *ph = litw[6],
+           *sh = litw[7];
+    auto spmv = [&](const double* in, double* out) {
+      hipLaunchKernelGGL(k_spmv, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), dLitv, in, out);
+      KCHK();
+    };
+    spmv(x, t);
+    hipLaunchKernelGGL(k_axpbypcz, dim3(ge), dim3(BS), 0, st, n, (const double*)nullptr, b, (const double*)nullptr,
+                       (const double*)t, (const double*)nullptr, (const double*)nullptr, 1.0, -1.0, 0.0, r);
+    KCHK();
+    HIPCHK(hipMemcpyAsync(rh, r, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemsetAsync(pp, 0, sizeof(double) * n, st));
+    HIPCHK(hipMemsetAsync(v, 0, sizeof(double) * n, st));
+    const double init[8] = {1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    HIPCHK(hipMemcpyAsync(bicg_sc, init, sizeof(init), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, b, b, (const double*)r, (const double*)r, part_a);
+    KCHK();
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part_a, nb, MAXB, 2, 0, bicg_sc + 8);
+    KCHK();
+    HIPCHK(hipMemcpyAsync(h_pinned, bicg_sc + 8, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const double bb = h_pinned[0];
+    double rr = h_pinned[1];
+    const double tol2 = tol * tol * bb;
+    int it = 0;
+    while (!(rr <= tol2)) {
+      if (it >= maxit || !std::isfinite(rr)) throw Error(PUCFEM_ENOCONV, "BiCGStab did not converge");
+      hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, rh, r, (const double*)nullptr, (const double*)nullptr, part_a);
+      hipLaunchKernelGGL(k_bicg_scalar, dim3(1), dim3(BS), 0, st, 0, part_a, nb, bicg_sc);
+      hipLaunchKernelGGL(k_bicg_p, dim3(ge), dim3(BS), 0, st, n, r, pp, v, dlit_dinv, ph, bicg_sc);
+      spmv(ph, v);
+      hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, rh, v, (const double*)nullptr, (const double*)nullptr, part_a);
+      hipLaunchKernelGGL(k_bicg_scalar, dim3(1), dim3(BS), 0, st, 1, part_a, nb, bicg_sc);
+      hipLaunchKernelGGL(k_bicg_s, dim3(ge), dim3(BS), 0, st, n, r, v, dlit_dinv, s, sh, bicg_sc);
+      spmv(sh, t);
+      hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, t, s, (const double*)t, (const double*)t, part_a);
+      hipLaunchKernelGGL(k_bicg_scalar, dim3(1), dim3(BS), 0, st, 2, part_a, nb, bicg_sc);
+      hipLaunchKernelGGL(k_bicg_x, dim3(ge), dim3(BS), 0, st, n, x, ph, sh, s, t, r, bicg_sc);
+      hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, r, r, (const double*)nullptr, (const double*)nullptr, part_a);
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part_a, nb, MAXB, 1, 0, bicg_sc + 5);
+      KCHK();
+      HIPCHK(hipMemcpyAsync(h_pinned, bicg_sc + 5, sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      rr = h_pinned[0];
+      ++it;
+    }
+    return it;
+  }
+};
+
+Ctx* C(void* p) { return static_cast<Ctx*>(p); }
+
+template <class F>
+int guard(void* ctx, F&& f) {
+  try {
+    f();
+    return PUCFEM_OK;
+  } catch (const Error& e) {
+    (ctx ? C(ctx)->err : g_err) = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    (ctx ? C(ctx)->err : g_err) = "out of host memory";
+    return PUCFEM_ENOMEM;
+  } catch (const std::exception& e) {
+    (ctx ? C(ctx)->err : g_err) = e.what();
+    return PUCFEM_EINVAL;
+  }
+}
+
+void require(bool ok, const std::string& msg) {
+  if (!ok) throw Error(PUCFEM_EINVAL, msg);
+}
+
+// ------------------------------------------------------------------ operator build
+void build(Ctx& c) {
+  require(c.has_mesh, "mesh not uploaded");
+  const pucfem_params& prm = c.prm;
+  c.scheme = prm.scheme;
+  require(prm.scheme >= 0 && prm.scheme <= 3, "bad scheme");
+  const bool stokes = prm.scheme == PUCFEM_STOKES_COLOR || prm.scheme == PUCFEM_STOKES_FOOD;
+  const bool literal = !stokes;
+  require(!(literal && c.world > 1), "heat / Poisson literal operators run on one rank");
+  require(!stokes || prm.sl_k == KNN, "sl_k must be 10 (PointLocator.find default)");
+  HostMesh& m = c.mesh;
+  make_ordering(m, prm.nstrips, c.ord);
+  build_pattern(m, c.ord, c.P);
+  assemble_stokes(m, c.ord, c.P, c.as);
+  const i64 N = m.N;
+
+  // periodic pressure merge maps (internal numbering)
+  c.dof.resize(N);
+  for (i64 i = 0; i < N; ++i) c.dof[i] = (i32)i;
+  c.slave_of.assign(N, -1);
+  c.master_of.assign(N, -1);
+  if (stokes) {
+    for (auto& pr : c.op_pairs) {
+      const i32 mi = c.ord.old2new[pr.first], si = c.ord.old2new[pr.second];
+      require(c.master_of[si] < 0, "duplicate periodic slave: the pressure restatement needs unique slaves");
+      require(c.dof[mi] == mi && c.slave_of[si] < 0, "chained periodic pairs are not supported for Stokes");
+      c.dof[si] = mi;
+      c.master_of[si] = mi;
+      c.slave_of[mi] = si;
+    }
+    c.n_free = N - (i64)c.op_pairs.size();
+    build_pressure(c.P, c.as.K, c.dof, c.slave_of, c.Pp);
+  }
+  if (literal) {
+    assemble_literal(m, c.ord, c.g_tri, c.op_pairs, c.dir_nodes, c.dir_vals,
+                     prm.scheme == PUCFEM_HEAT ? prm.dt : -1.0, c.Lit, c.litb);
+  }
+  // A_visc on P (StokesColor.py:471-475)
+  std::vector<uint8_t> isdir(N, 0);
+  for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
+  const double dtnu = prm.dt * prm.nu;
+  c.Kv.assign(c.P.nnz(), 0.0);
+  for (i64 r = 0; r < N; ++r)
+    for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) {
+      const i32 j = c.P.col[k];
+      if (isdir[r]) c.Kv[k] = (j == r) ? 1.0 : 0.0;
+      else if (isdir[j]) c.Kv[k] = 0.0;
+      else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
+    }
+  // partition + local plan
+  if (stokes) partition_rows(c.P, c.ord, c.world, c.row_start);
+  else c.row_start = {0, N};
+  std::vector<const Csr*> pats;
+  if (stokes) pats = {&c.P, &c.Pp};
+  else pats = {&c.P, &c.Lit};
+  make_local_plan(pats, c.row_start, c.rank, c.lp);
+  build_sell(c.P, c.lp, c.sP);
+  if (stokes) build_sell(c.Pp, c.lp, c.sPp);
+  if (literal) build_sell(c.Lit, c.lp, c.sLit);
+  c.built = true;
+  if (c.host_only) return;
+
+  // ---------------------------------------------------------------- device upload
+  LocalPlan& lp = c.lp;
+  const i64 no = lp.n_own;
+  c.nloc = no + lp.n_ghost;
+  auto dsell = [&](const Sell& S, const Csr& A, DevSell& D) {
+    D.off = c.upload(S.slice_off);
+    D.w = c.upload(S.slice_w);
+    D.col = c.upload(S.col);
+    D.nslices = S.nslices;
+    D.nrows = S.nrows;
+    D.padded = S.padded;
+    D.nnz = A.rowptr[lp.r1] - A.rowptr[lp.r0];
+  };
+  std::vector<double> tmp;
+  dsell(c.sP, c.P, c.dP);
+  sell_values(c.P, lp, c.sP, c.as.K, tmp);
+  c.dK = c.upload(tmp);
+  sell_values(c.P, lp, c.sP, c.as.Gx, tmp);
+  c.dGx = c.upload(tmp);
+  sell_values(c.P, lp, c.sP, c.as.Gy, tmp);
+  c.dGy = c.upload(tmp);
+  // Jacobi symmetric scaling S A S of A_visc
+  auto diag_of = [&](const Csr& A, const std::vector<double>& val, i64 g) {
+    for (i64 k = A.rowptr[g]; k < A.rowptr[g + 1]; ++k)
+      if (A.col[k] == g) return val[k];
+    return 1.0;
+  };
+  auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
+    sg.resize(N);
+    for (i64 g = 0; g < N; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
+    std::vector<double> out(val.size());
+    for (i64 r = 0; r < N; ++r)
+      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) out[k] = sg[r] * val[k] * sg[A.col[k]];
+    return out;
+  };
+  auto local_vec = [&](const std::vector<double>& g) {  // owned + ghost entries of a global vector
+    std::vector<double> v(c.nloc);
+    for (i64 i = 0; i < no; ++i) v[i] = g[lp.r0 + i];
+    for (i64 k = 0; k < lp.n_ghost; ++k) v[no + k] = g[lp.ghost_global[k]];
+    return v;
+  };
+  {
+    std::vector<double> sg;
+    auto kvh = scaled(c.P, c.Kv, sg);
+    sell_values(c.P, lp, c.sP, kvh, tmp);
+    c.dKv = c.upload(tmp);
+    c.dsv = c.upload(local_vec(sg));
+    std::vector<double> sq(N);
+    for (i64 g = 0; g < N; ++g) sq[g] = 1.0 / sg[g];
+    c.dsqv = c.upload(local_vec(sq));
+  }
+  if (stokes) {
+    dsell(c.sPp, c.Pp, c.dPp);
+    std::vector<double> sg;
+    auto kph = scaled(c.Pp, c.Pp.val, sg);
+    sell_values(c.Pp, lp, c.sPp, kph, tmp);
+    c.dKp = c.upload(tmp);
+    c.dsp = c.upload(local_vec(sg));
+  }
+  if (literal) {
+    dsell(c.sLit, c.Lit, c.dLit);
+    sell_values(c.Lit, lp, c.sLit, c.Lit.val, tmp);
+    c.dLitv = c.upload(tmp);
+    std::vector<double> dinv(N);
+    for (i64 g = 0; g < N; ++g) dinv[g] = 1.0 / diag_of(c.Lit, c.Lit.val, g);
+    c.dlit_dinv = c.upload(dinv);
+  }
+  // per-row data
+  {
+    std::vector<double> as1(no), mp(no), wm(no);
+    std::vector<uint8_t> df(no);
+    std::vector<i32> so(no, -1), mo(no, -1);
+    for (i64 i = 0; i < no; ++i) {
+      const i64 g = lp.r0 + i;
+      as1[i] = c.as.asum[g] + 1e-12;
+      mp[i] = c.as.M[g] + 1e-12;
+      wm[i] = m.mk[c.ord.new2old[g]] == 0 ? c.as.M[g] : 0.0;
+      df[i] = isdir[g];
+      if (c.slave_of[g] >= 0) so[i] = to_local(lp, c.slave_of[g]);
+      if (c.master_of[g] >= 0) mo[i] = to_local(lp, c.master_of[g]);
+      require(so[i] < (i32)no && mo[i] < (i32)no, "periodic partner on another rank");
+    }
+    c.das1 = c.upload(as1);
+    c.dmp = c.upload(mp);
+    c.dwmix = c.upload(wm);
+    c.ddir = c.upload(df);
+    c.dslave_of = c.upload(so);
+    c.dmaster_of = c.upload(mo);
+  }
+  // BC lists: sequential copy semantics resolved symbolically (caller numbering), then local
+  {
+    std::vector<i64> src(N);
+    for (i64 i = 0; i < N; ++i) src[i] = i;
+    for (auto& pr : c.bc_pairs) src[pr.second] = src[pr.first];
+    std::vector<i32> cd, cs;
+    for (i64 o = 0; o < N; ++o)
+      if (src[o] != o) {
+        const i64 g = c.ord.old2new[o];
+        if (g < lp.r0 || g >= lp.r1) continue;
+        const i64 gs = c.ord.old2new[src[o]];
+        require(gs >= lp.r0 && gs < lp.r1, "periodic BC source on another rank");
+        cd.push_back((i32)(g - lp.r0));
+        cs.push_back((i32)(gs - lp.r0));
+      }
+    // Dirichlet: last occurrence wins (sequential semantics), owned nodes only
+    std::vector<i64> last(N, -1);
+    for (size_t k = 0; k < c.dir_nodes.size(); ++k) last[c.dir_nodes[k]] = (i64)k;
+    std::vector<i32> dn;
+    std::vector<double> dv;
+    for (size_t k = 0; k < c.dir_nodes.size(); ++k) {
+      if (last[c.dir_nodes[k]] != (i64)k) continue;
+      const i64 g = c.ord.old2new[c.dir_nodes[k]];
+      if (g < lp.r0 || g >= lp.r1) continue;
+      dn.push_back((i32)(g - lp.r0));
+      for (int q = 0; q < c.dir_ncomp; ++q) dv.push_back(c.dir_vals[c.dir_ncomp * k + q]);
+    }
+    c.ncopy = (int)cd.size();
+    c.ndir = (int)dn.size();
+    c.dcdst = c.upload(cd);
+    c.dcsrc = c.upload(cs);
+    c.ddnode = c.upload(dn);
+    c.ddval = c.upload(dv);
+    c.dbctmp = c.dalloc<double>(2 * std::max(1, c.ncopy));
+  }
+  // halo plan
+  c.nsend = (i64)lp.send_local.size();
+  c.dsend = c.upload(lp.send_local);
+  c.dsendbuf = c.dalloc<double>(2 * std::max<i64>(1, c.nsend));
+  // fields + workspace
+  for (double** f : {&c.ux, &c.uy, &c.usx, &c.usy, &c.p, &c.p2, &c.yp, &c.yp2, &c.yvx, &c.yvy, &c.div_star,
+                     &c.div_u, &c.final_div, &c.braw, &c.bh, &c.bvx, &c.bvy, &c.scalar})
+    *f = c.dalloc<double>(c.nloc);
+  for (int q = 0; q < 2; ++q) {
+    c.cg_r[q] = c.dalloc<double>(c.nloc);
+    c.cg_pa[q] = c.dalloc<double>(c.nloc);
+    c.cg_pb[q] = c.dalloc<double>(c.nloc);
+    c.cg_q[q] = c.dalloc<double>(c.nloc);
+  }
+  for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
+  c.scal = c.dalloc<double>(32);
+  c.ctl = c.dalloc<int>(4);
+  c.redbuf = c.dalloc<double>(8 * 64);
+  c.vals = c.dalloc<double>(16);
+  c.bicg_sc = c.dalloc<double>(16);
+  if (literal) {
+    for (int q = 0; q < 9; ++q) c.litw[q] = c.dalloc<double>(c.nloc);
+  }
+  // full-mesh replica in internal numbering
+  {
+    std::vector<double> X(N), Y(N);
+    for (i64 g = 0; g < N; ++g) {
+      X[g] = m.x[c.ord.new2old[g]];
+      Y[g] = m.y[c.ord.new2old[g]];
+    }
+    std::vector<i32> tri(3 * m.T);
+    for (i64 k = 0; k < 3 * m.T; ++k) tri[k] = c.ord.old2new[m.tri[k]];
+    c.mx = c.upload(X);
+    c.my = c.upload(Y);
+    c.mtri = c.upload(tri);
+    auto dgrid = [&](const Grid& G, GridDev& D, bool pts) {
+      D.nx = G.nx;
+      D.ny = G.ny;
+      D.x0 = G.x0;
+      D.y0 = G.y0;
+      D.hx = G.hx;
+      D.hy = G.hy;
+      D.start = c.upload(G.cell_start);
+      D.item = c.upload(G.item);
+      D.px = pts ? c.upload(G.px) : nullptr;
+      D.py = pts ? c.upload(G.py) : nullptr;
+    };
+    if (stokes) {  // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
+      std::vector<double> cx(m.T), cy(m.T);
+      for (i64 t = 0; t < m.T; ++t) {
+        const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
+        cx[t] = (m.x[a] + m.x[b] + m.x[d]) / 3;
+        cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
+      }
+      Grid G;
+      build_centroid_grid(cx, cy, 2.0, G);
+      dgrid(G, c.cgrid, true);
+      c.has_cgrid = true;
+      Grid TG;
+      build_tri_grid(X, Y, tri, 4.0, TG);
+      dgrid(TG, c.tgrid, false);
+      c.has_tgrid = true;
+    }
+    c.c_full = c.dalloc<double>(N);
+    c.c_new = c.dalloc<double>(N);
+    c.dnotfound = c.dalloc<int32_t>(no);
+    if (c.world > 1) {
+      c.ufx = c.dalloc<double>(N);
+      c.ufy = c.dalloc<double>(N);
+    }
+  }
+  // initial state: u = 0 then makeDirBCU (StokesColor.py:482-483); c = 1[x < 0.5] (:493-495)
+  if (stokes) {
+    c.bc(c.ux, c.uy);
+    c.halo(c.ux, c.uy);
+    std::vector<double> c0(N);
+    for (i64 g = 0; g < N; ++g) c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
+    HIPCHK(hipMemcpyAsync(c.c_full, c0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+  }
+  HIPCHK(hipStreamSynchronize(c.st));
+}
+
+}  // namespace
+
+// =====================================================================================================
+extern "C" {
+
+int pucfem_abi_version(void) { return PUCFEM_ABI_VERSION; }
+
+const char* pucfem_last_error(const void* ctx) {
+  return ctx ? static_cast<const Ctx*>(ctx)->err.c_str() : g_err.c_str();
+}
+
+int pucfem_device_count(int32_t* n) {
+  return guard(nullptr, [&] {
+    int k = 0;
+    HIPCHK(hipGetDeviceCount(&k));
+    *n = k;
+  });
+}
+
+int pucfem_ctx_create(int32_t device, void** out) {
+  return guard(nullptr, [&] {
+    auto c = std::make_unique<Ctx>();
+    c->device = device;
+    c->host_only = device < 0;
+    if (!c->host_only) {
+      HIPCHK(hipSetDevice(device));
+      HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      HIPCHK(hipHostMalloc((void**)&c->h_ctl, 4 * sizeof(int), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64 * sizeof(double), hipHostMallocDefault));
+    }
+    *out = c.release();
+  });
+}
+
+int pucfem_rccl_unique_id(uint8_t* out) {
+  return guard(nullptr, [&] {
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == PUCFEM_UNIQUE_ID_BYTES, "unique id size");
+    std::memcpy(out, &id, sizeof(id));
+  });
+}
+
+int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const uint8_t* uid, void** out) {
+  void* p = nullptr;
+  int rc = pucfem_ctx_create(device, &p);
+  if (rc) return rc;
+  rc = guard(p, [&] {
+    Ctx& c = *C(p);
+    require(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
+    c.rank = rank;
+    c.world = world;
+    if (world > 1 && !c.host_only) {
+      ncclUniqueId id;
+      std::memcpy(&id, uid, sizeof(id));
+      NCCLCHK(ncclCommInitRank(&c.comm, world, id, rank));
+    }
+  });
+  if (rc) {
+    g_err = C(p)->err;
+    delete C(p);
+    return rc;
+  }
+  *out = p;
+  return 0;
+}
+
+int pucfem_ctx_destroy(void* ctx) {
+  return guard(nullptr, [&] { delete C(ctx); });
+}
+
+int pucfem_mesh_upload(void* ctx, int64_t N, const double* xy, const int32_t* mk, int64_t T, const int32_t* tris,
+                       int32_t coord_fp32) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(N > 0 && T > 0 && xy && mk && tris, "empty mesh");
+    HostMesh& m = c.mesh;
+    m.N = N;
+    m.T = T;
+    m.x.resize(N);
+    m.y.resize(N);
+    for (i64 i = 0; i < N; ++i) {
+      m.x[i] = xy[2 * i];
+      m.y[i] = xy[2 * i + 1];
+    }
+    m.mk.assign(mk, mk + N);
+    m.tri.assign(tris, tris + 3 * T);
+    for (i64 k = 0; k < 3 * T; ++k) require(m.tri[k] >= 0 && m.tri[k] < N, "triangle index out of range");
+    m.fp32 = coord_fp32 != 0;
+    c.has_mesh = true;
+    c.built = false;
+  });
+}
+
+int pucfem_set_pairs(void* ctx, int32_t kind, int64_t n, const int64_t* pairs) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(c.has_mesh, "mesh first");
+    auto& v = kind == 0 ? c.op_pairs : c.bc_pairs;
+    v.clear();
+    for (i64 k = 0; k < n; ++k) {
+      require(pairs[2 * k] >= 0 && pairs[2 * k] < c.mesh.N && pairs[2 * k + 1] >= 0 && pairs[2 * k + 1] < c.mesh.N,
+              "pair index out of range");
+      v.push_back({pairs[2 * k], pairs[2 * k + 1]});
+    }
+    c.built = false;
+  });
+}
+
+int pucfem_set_dirichlet(void* ctx, int64_t n, const int32_t* nodes, const double* values, int32_t ncomp) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(c.has_mesh, "mesh first");
+    require(ncomp == 1 || ncomp == 2, "ncomp must be 1 or 2");
+    c.dir_nodes.assign(nodes, nodes + n);
+    for (i32 d : c.dir_nodes) require(d >= 0 && d < c.mesh.N, "Dirichlet node out of range");
+    c.dir_vals.assign(values, values + ncomp * n);
+    c.dir_ncomp = ncomp;
+    c.built = false;
+  });
+}
+
+int pucfem_set_source(void* ctx, int64_t T, const float* g) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(c.has_mesh && T == c.mesh.T, "source must have one value per triangle");
+    c.g_tri.assign(g, g + T);
+    c.built = false;
+  });
+}
+
+int pucfem_build_operators(void* ctx, const pucfem_params* prm) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.prm = *prm;
+    c.built = false;
+    build(c);
+  });
+}
+
+// ---- fields
+int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    const i64 N = c.mesh.N, no = c.lp.n_own;
+    auto own2 = [&](double* a, double* b) {
+      require(count == 2 * N, "field must be (N, 2)");
+      std::vector<double> x(no), y(no);
+      for (i64 i = 0; i < no; ++i) {
+        const i64 o = c.ord.new2old[c.lp.r0 + i];
+        x[i] = buf[2 * o];
+        y[i] = buf[2 * o + 1];
+      }
+      HIPCHK(hipMemcpyAsync(a, x.data(), sizeof(double) * no, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipMemcpyAsync(b, y.data(), sizeof(double) * no, hipMemcpyHostToDevice, c.st));
+      c.halo(a, b);
+    };
+    auto own1 = [&](double* a) {
+      require(count == N, "field must be (N,)");
+      std::vector<double> x(no);
+      for (i64 i = 0; i < no; ++i) x[i] = buf[c.ord.new2old[c.lp.r0 + i]];
+      HIPCHK(hipMemcpyAsync(a, x.data(), sizeof(double) * no, hipMemcpyHostToDevice, c.st));
+      c.halo(a);
+    };
+    switch (field) {
+      case PUCFEM_F_U: own2(c.ux, c.uy); break;
+      case PUCFEM_F_USTAR: own2(c.usx, c.usy); break;
+      case PUCFEM_F_SCALAR: own1(c.scalar); break;
+      case PUCFEM_F_C: {
+        require(count == N, "c must be (N,)");
+        std::vector<double> x(N);
+        for (i64 g = 0; g < N; ++g) x[g] = buf[c.ord.new2old[g]];
+        HIPCHK(hipMemcpyAsync(c.c_full, x.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+        break;
+      }
+      case PUCFEM_F_TRACERS: {
+        require(count % 2 == 0, "tracers must be (n, 2)");
+        const i64 n = count / 2;
+        if (n != c.ntr) {
+          c.ntr = (int32_t)n;
+          c.trx = c.dalloc<double>(n);
+          c.try_ = c.dalloc<double>(n);
+          c.trs = c.dalloc<double>(n);
+        }
+        std::vector<double> x(n), y(n);
+        for (i64 k = 0; k < n; ++k) {
+          x[k] = buf[2 * k];
+          y[k] = buf[2 * k + 1];
+        }
+        HIPCHK(hipMemcpyAsync(c.trx, x.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemcpyAsync(c.try_, y.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemsetAsync(c.trs, 0, sizeof(double) * n, c.st));
+        break;
+      }
+      case PUCFEM_F_STATUS:
+        require(count == c.ntr, "status must match the tracer count");
+        HIPCHK(hipMemcpyAsync(c.trs, buf, sizeof(double) * count, hipMemcpyHostToDevice, c.st));
+        break;
+      default: throw Error(PUCFEM_EINVAL, "field cannot be set");
+    }
+    HIPCHK(hipStreamSynchronize(c.st));
+  });
+}
+
+int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    const i64 N = c.mesh.N, no = c.lp.n_own;
+    auto get2 = [&](const double* a, const double* b) {
+      require(count == 2 * N, "field is (N, 2)");
+      std::vector<double> x(no), y(no);
+      HIPCHK(hipMemcpyAsync(x.data(), a, sizeof(double) * no, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(y.data(), b, sizeof(double) * no, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 i = 0; i < no; ++i) {
+        const i64 o = c.ord.new2old[c.lp.r0 + i];
+        buf[2 * o] = x[i];
+        buf[2 * o + 1] = y[i];
+      }
+    };
+    auto get1 = [&](const double* a) {
+      require(count == N, "field is (N,)");
+      std::vector<double> x(no);
+      HIPCHK(hipMemcpyAsync(x.data(), a, sizeof(double) * no, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 i = 0; i < no; ++i) buf[c.ord.new2old[c.lp.r0 + i]] = x[i];
+    };
+    switch (field) {
+      case PUCFEM_F_U: get2(c.ux, c.uy); break;
+      case PUCFEM_F_USTAR: get2(c.usx, c.usy); break;
+      case PUCFEM_F_P: get1(c.p); break;
+      case PUCFEM_F_P2: get1(c.p2); break;
+      case PUCFEM_F_DIV_STAR: get1(c.div_star); break;
+      case PUCFEM_F_DIV_U: get1(c.div_u); break;
+      case PUCFEM_F_FINAL_DIV: get1(c.final_div); break;
+      case PUCFEM_F_SCALAR: get1(c.scalar); break;
+      case PUCFEM_F_C: {
+        require(count == N, "c is (N,)");
+        std::vector<double> x(N);
+        HIPCHK(hipMemcpyAsync(x.data(), c.c_full, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        for (i64 g = 0; g < N; ++g) buf[c.ord.new2old[g]] = x[g];
+        break;
+      }
+      case PUCFEM_F_TRACERS: {
+        require(count == 2 * (i64)c.ntr, "tracers are (n, 2)");
+        std::vector<double> x(c.ntr), y(c.ntr);
+        HIPCHK(hipMemcpyAsync(x.data(), c.trx, sizeof(double) * c.ntr, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipMemcpyAsync(y.data(), c.try_, sizeof(double) * c.ntr, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        for (i64 k = 0; k < c.ntr; ++k) {
+          buf[2 * k] = x[k];
+          buf[2 * k + 1] = y[k];
+        }
+        break;
+      }
+      case PUCFEM_F_STATUS:
+        require(count == c.ntr, "status is (n,)");
+        HIPCHK(hipMemcpyAsync(buf, c.trs, sizeof(double) * count, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        break;
+      default: throw Error(PUCFEM_EINVAL, "unknown field");
+    }
+  });
+}
+
+// ---- stepping
+int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(nsteps >= 0, "nsteps < 0");
+    if (nsteps == 0) return;
+    if (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD) {
+      double* rec = c.dalloc<double>(8 * (i64)nsteps);
+      std::vector<int32_t> its(3 * (size_t)nsteps);
+      for (int s = 0; s < nsteps; ++s) c.stokes_step(rec + 8 * s, its.data() + 3 * s);
+      std::vector<double> h(8 * (size_t)nsteps);
+      HIPCHK(hipMemcpyAsync(h.data(), rec, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      if (c.timer.on) c.timer.flush();
+      HIPCHK(hipFree(rec));
+      c.allocs.erase(std::find(c.allocs.begin(), c.allocs.end(), (void*)rec));
+      if (stats)
+        for (int s = 0; s < nsteps; ++s) {
+          pucfem_step_stats& o = stats[s];
+          const double* r = h.data() + 8 * s;
+          o.max_div_star = r[0];
+          o.max_final_div = r[1];
+          o.mix_I = r[2];
+          o.mix_mu = r[3];
+          o.mix_var = r[4];
+          o.eaten = (int64_t)std::llround(r[5]);
+          o.sl_notfound = (int32_t)std::llround(r[6]);
+          o.it_visc = its[3 * s];
+          o.it_p = its[3 * s + 1];
+          o.it_p2 = its[3 * s + 2];
+        }
+    } else if (c.scheme == PUCFEM_HEAT) {
+      // heatEq.py:321-325: u = solve(A, u + DT*b*0); reapply_periodic_u; reapply_dirchlect_u
+      for (int s = 0; s < nsteps; ++s) {
+        HIPCHK(hipMemcpyAsync(c.litw[8], c.scalar, sizeof(double) * c.lp.n_own, hipMemcpyDeviceToDevice, c.st));
+        const int it = c.bicgstab(c.scalar, c.litw[8], c.prm.rtol_lin, c.prm.maxit_lin);
+        c.bc(c.scalar, nullptr);
+        if (stats) {
+          std::memset(&stats[s], 0, sizeof(pucfem_step_stats));
+          stats[s].it_visc = it;
+        }
+      }
+      HIPCHK(hipStreamSynchronize(c.st));
+    } else {
+      // poisson.py:283-285: f = solve(A, b)
+      HIPCHK(hipMemcpyAsync(c.bh, c.litb.data(), sizeof(double) * c.lp.n_own, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipMemsetAsync(c.scalar, 0, sizeof(double) * c.lp.n_own, c.st));
+      const int it = c.bicgstab(c.scalar, c.bh, c.prm.rtol_lin, c.prm.maxit_lin);
+      HIPCHK(hipStreamSynchronize(c.st));
+      if (stats) {
+        std::memset(&stats[0], 0, sizeof(pucfem_step_stats));
+        stats[0].it_visc = it;
+      }
+    }
+  });
+}
+
+// ---- unit operations (single rank)
+int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1, "pucfem_apply is single-rank");
+    const i64 N = c.mesh.N;
+    auto perm_in = [&](const double* src, int ncomp, double* d0, double* d1) {
+      std::vector<double> a(N), b(N);
+      for (i64 g = 0; g < N; ++g) {
+        const i64 o = c.ord.new2old[g];
+        a[g] = src[ncomp * o];
+        if (ncomp > 1) b[g] = src[ncomp * o + 1];
+      }
+      HIPCHK(hipMemcpyAsync(d0, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      if (ncomp > 1) HIPCHK(hipMemcpyAsync(d1, b.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    };
+    auto perm_out = [&](double* dst, int ncomp, const double* d0, const double* d1) {
+      std::vector<double> a(N), b(N);
+      HIPCHK(hipMemcpyAsync(a.data(), d0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      if (ncomp > 1) HIPCHK(hipMemcpyAsync(b.data(), d1, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 g = 0; g < N; ++g) {
+        const i64 o = c.ord.new2old[g];
+        dst[ncomp * o] = a[g];
+        if (ncomp > 1) dst[ncomp * o + 1] = b[g];
+      }
+    };
+    double *t0 = c.cg_pa[0], *t1 = c.cg_pa[1], *o0 = c.cg_q[0], *o1 = c.cg_q[1];
+    switch (op) {
+      case PUCFEM_OP_K:
+      case PUCFEM_OP_GX:
+      case PUCFEM_OP_GY: {
+        perm_in(x, 1, t0, nullptr);
+        const double* v = op == PUCFEM_OP_K ? c.dK : op == PUCFEM_OP_GX ? c.dGx : c.dGy;
+        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), v, t0, o0);
+        KCHK();
+        perm_out(y, 1, o0, nullptr);
+        break;
+      }
+      case PUCFEM_OP_PRES: {
+        require(c.dKp, "no pressure operator (scheme is not Stokes)");
+        perm_in(x, 1, t0, nullptr);
+        // unscaled action: S^-1 A^ S^-1 x
+        std::vector<double> s(N);
+        HIPCHK(hipMemcpyAsync(s.data(), c.dsp, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        std::vector<double> a(N), xs(N);
+        for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
+        HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dPp.nslices)), dim3(BS), 0, c.st, c.dPp.view(), c.dKp, t0, o0);
+        KCHK();
+        HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        for (i64 g = 0; g < N; ++g) y[c.ord.new2old[g]] = a[g] / s[g];
+        break;
+      }
+      case PUCFEM_OP_LIT: {
+        require(c.dLitv, "no literal operator (scheme is Stokes)");
+        perm_in(x, 1, t0, nullptr);
+        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dLit.nslices)), dim3(BS), 0, c.st, c.dLit.view(), c.dLitv, t0, o0);
+        KCHK();
+        perm_out(y, 1, o0, nullptr);
+        break;
+      }
+      case PUCFEM_OP_DIV: {
+        perm_in(x, 2, t0, t1);
+        hipLaunchKernelGGL(k_div, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dGx, c.dGy, t0, t1,
+                           c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
+        KCHK();
+        perm_out(y, 1, o0, nullptr);
+        break;
+      }
+      case PUCFEM_OP_GRAD: {
+        perm_in(x, 1, t0, nullptr);
+        hipLaunchKernelGGL(k_grad, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dGx, c.dGy, t0,
+                           c.das1, o0, o1);
+        KCHK();
+        perm_out(y, 2, o0, o1);
+        break;
+      }
+      case PUCFEM_OP_VISC: {
+        // unscaled A_visc x = S^-1 A^ S^-1 x
+        std::vector<double> s(N), xs(N), a(N);
+        HIPCHK(hipMemcpyAsync(s.data(), c.dsv, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
+        HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dKv, t0, o0);
+        KCHK();
+        HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipStreamSynchronize(c.st));
+        for (i64 g = 0; g < N; ++g) y[c.ord.new2old[g]] = a[g] / s[g];
+        break;
+      }
+      default: throw Error(PUCFEM_EINVAL, "unknown op");
+    }
+  });
+}
+
+int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol, int32_t maxit, int32_t* iters) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1, "pucfem_solve is single-rank");
+    const i64 N = c.mesh.N;
+    int it = 0;
+    if (op == PUCFEM_OP_VISC) {
+      // rhs = b (as u^n, initial guess b): the viscous CG without BCs
+      std::vector<double> bx(N), by(N);
+      for (i64 g = 0; g < N; ++g) {
+        bx[g] = b[2 * c.ord.new2old[g]];
+        by[g] = b[2 * c.ord.new2old[g] + 1];
+      }
+      HIPCHK(hipMemcpyAsync(c.ux, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipMemcpyAsync(c.uy, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      hipLaunchKernelGGL(k_visc_prep, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, c.ux, c.uy, c.bvx,
+                         c.bvy, c.yvx, c.yvy);
+      KCHK();
+      double* y[2] = {c.yvx, c.yvy};
+      const double* bb[2] = {c.bvx, c.bvy};
+      it = c.cg<2>(c.dP, c.dKv, y, bb, rtol, maxit, 0);
+      hipLaunchKernelGGL(k_cg_fin, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, 2, c.dsv, c.yvx, c.yvy, c.usx, c.usy,
+                         (const int32_t*)nullptr);
+      KCHK();
+      std::vector<double> ox(N), oy(N);
+      HIPCHK(hipMemcpyAsync(ox.data(), c.usx, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(oy.data(), c.usy, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 g = 0; g < N; ++g) {
+        x[2 * c.ord.new2old[g]] = ox[g];
+        x[2 * c.ord.new2old[g] + 1] = oy[g];
+      }
+    } else if (op == PUCFEM_OP_PRES) {
+      require(c.dKp, "no pressure operator");
+      // b = b_p: braw = (M + 1e-12) * b_p, then the same path as the step
+      std::vector<double> mp(N), bp(N), br(N);
+      HIPCHK(hipMemcpyAsync(mp.data(), c.dmp, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      double sum = 0.0;
+      for (i64 g = 0; g < N; ++g) {
+        br[g] = mp[g] * b[c.ord.new2old[g]];
+        sum += br[g];
+      }
+      HIPCHK(hipMemcpyAsync(c.braw, br.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      std::vector<double> part(4 * MAXB, 0.0);
+      part[MAXB] = sum;
+      HIPCHK(hipMemcpyAsync(c.part_d, part.data(), sizeof(double) * part.size(), hipMemcpyHostToDevice, c.st));
+      // pressure() reduces part_d + MAXB over nb_for(dP) blocks: only entry 0 is non-zero
+      HIPCHK(hipMemsetAsync(c.yp, 0, sizeof(double) * c.nloc, c.st));
+      pucfem_params save = c.prm;
+      c.prm.rtol_pres = rtol;
+      c.prm.maxit_pres = maxit;
+      try {
+        it = c.pressure(c.yp, c.p, 1);
+      } catch (...) {
+        c.prm = save;
+        throw;
+      }
+      c.prm = save;
+      std::vector<double> o(N);
+      HIPCHK(hipMemcpyAsync(o.data(), c.p, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 g = 0; g < N; ++g) x[c.ord.new2old[g]] = o[g];
+    } else if (op == PUCFEM_OP_LIT) {
+      require(c.dLitv, "no literal operator");
+      std::vector<double> bb(N), x0(N);
+      for (i64 g = 0; g < N; ++g) {
+        bb[g] = b[c.ord.new2old[g]];
+        x0[g] = x[c.ord.new2old[g]];
+      }
+      HIPCHK(hipMemcpyAsync(c.bh, bb.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipMemcpyAsync(c.scalar, x0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      it = c.bicgstab(c.scalar, c.bh, rtol, maxit);
+      std::vector<double> o(N);
+      HIPCHK(hipMemcpyAsync(o.data(), c.scalar, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      for (i64 g = 0; g < N; ++g) x[c.ord.new2old[g]] = o[g];
+    } else {
+      throw Error(PUCFEM_EINVAL, "op cannot be solved");
+    }
+    if (iters) *iters = it;
+  });
+}
+
+int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, double* cout, int32_t* notfound) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1 && c.has_cgrid, "sl_advect needs a single-rank Stokes context");
+    const i64 N = c.mesh.N;
+    std::vector<double> a(N), bx(N), by(N);
+    for (i64 g = 0; g < N; ++g) {
+      const i64 o = c.ord.new2old[g];
+      a[g] = cin[o];
+      bx[g] = u[2 * o];
+      by[g] = u[2 * o + 1];
+    }
+    double *cf = c.litw[0] ? c.litw[0] : c.cg_pa[0], *cn = c.cg_pb[0], *tx = c.cg_q[0], *ty = c.cg_q[1];
+    HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    const int nb = c.nb_rows(N);
+    hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, c.mesh.T}, c.cgrid, (int64_t)0, N,
+                       tx, ty, dt, cf, cn, c.dwmix, c.dnotfound, c.part_a);
+    KCHK();
+    std::vector<double> o(N);
+    std::vector<int32_t> nf(N);
+    HIPCHK(hipMemcpyAsync(o.data(), cn, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(nf.data(), c.dnotfound, sizeof(int32_t) * N, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipStreamSynchronize(c.st));
+    for (i64 g = 0; g < N; ++g) {
+      cout[c.ord.new2old[g]] = o[g];
+      if (notfound) notfound[c.ord.new2old[g]] = nf[g];
+    }
+  });
+}
+
+int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1, "tracer_step unit op is single-rank");
+    const i64 N = c.mesh.N;
+    std::vector<double> bx(N), by(N);
+    for (i64 g = 0; g < N; ++g) {
+      bx[g] = u[2 * c.ord.new2old[g]];
+      by[g] = u[2 * c.ord.new2old[g] + 1];
+    }
+    HIPCHK(hipMemcpyAsync(c.ux, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(c.uy, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    for (int s = 0; s < nsteps; ++s) c.tracer_advance(dt);
+    HIPCHK(hipStreamSynchronize(c.st));
+  });
+}
+
+int pucfem_mixing_index(void* ctx, const double* cin, double* out3) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1, "mixing_index unit op is single-rank");
+    const i64 N = c.mesh.N;
+    std::vector<double> a(N);
+    for (i64 g = 0; g < N; ++g) a[g] = cin[c.ord.new2old[g]];
+    double* cf = c.cg_pa[0];
+    HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    // pass 1 (sum w c, sum w) reusing the SL partial layout
+    const int nb = c.nb_rows(N);
+    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, (const double*)c.dwmix, (const double*)cf,
+                       (const double*)c.dwmix, (const double*)c.dwmix, c.part_a);
+    KCHK();
+    // part_a[0] = sum w c, part_a[MAXB] = sum w^2 -> recompute sum w separately
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_a, nb, MAXB, 1, 0, c.vals + 2);
+    std::vector<double> ones(N, 1.0);
+    double* on = c.cg_pb[0];
+    HIPCHK(hipMemcpyAsync(on, ones.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, (const double*)c.dwmix, (const double*)on,
+                       (const double*)nullptr, (const double*)nullptr, c.part_b);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
+    hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, c.dwmix, c.vals + 2, 1, 1, c.part_c);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
+    HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
+    double* rec = c.vals + 8;
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec);
+    KCHK();
+    double h[8];
+    HIPCHK(hipMemcpyAsync(h, rec, sizeof(double) * 7, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipStreamSynchronize(c.st));
+    out3[0] = h[2];
+    out3[1] = h[3];
+    out3[2] = h[4];
+  });
+}
+
+// ---- measurement
+int pucfem_timing_enable(void* ctx, int32_t on) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    HIPCHK(hipStreamSynchronize(c.st));
+    c.timer.flush();
+    c.timer.on = on != 0;
+    for (int k = 0; k < 5; ++k) {
+      c.timer.ms[k] = 0;
+      c.timer.bytes[k] = 0;
+      c.timer.n[k] = 0;
+    }
+  });
+}
+
+int pucfem_timing_get(void* ctx, int32_t k, double* ms, int64_t* n, double* bytes) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(k >= 0 && k < 5, "kernel class");
+    if (!c.host_only) {
+      HIPCHK(hipStreamSynchronize(c.st));
+      c.timer.flush();
+    }
+    *ms = c.timer.ms[k];
+    *n = c.timer.n[k];
+    *bytes = c.timer.n[k] ? c.timer.bytes[k] / (double)c.timer.n[k] : 0.0;
+  });
+}
+
+int pucfem_sync(void* ctx) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    if (!c.host_only) HIPCHK(hipStreamSynchronize(c.st));
+  });
+}
+
+int pucfem_info(void* ctx, int64_t* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    o[0] = c.mesh.N;
+    o[1] = c.mesh.T;
+    o[2] = c.P.nnz();
+    o[3] = c.Pp.nnz();
+    o[4] = c.lp.n_own;
+    o[5] = c.lp.n_ghost;
+    o[6] = c.sP.padded;
+    o[7] = c.sPp.padded;
+    o[8] = (int64_t)c.op_pairs.size();
+    o[9] = (int64_t)c.dir_nodes.size();
+  });
+}
+
+// ---- host-only
+int pucfem_refine(int64_t N, const double* xy, const int32_t* mk, int64_t T, const int32_t* tris, int32_t levels,
+                  int64_t* N_out, int64_t* T_out, double* xy_out, int32_t* mk_out, int32_t* tris_out) {
+  return guard(nullptr, [&] {
+    require(levels >= 0 && levels <= 12, "levels in [0, 12]");
+    // sizes: N' = N + E, T' = 4T per level (E from Euler: E = (3T + Eb)/2), computed exactly by refining
+    HostMesh a;
+    a.N = N;
+    a.T = T;
+    a.x.resize(N);
+    a.y.resize(N);
+    for (i64 i = 0; i < N; ++i) {
+      a.x[i] = xy[2 * i];
+      a.y[i] = xy[2 * i + 1];
+    }
+    a.mk.assign(mk, mk + N);
+    a.tri.assign(tris, tris + 3 * T);
+    for (int l = 0; l < levels; ++l) {
+      HostMesh b;
+      red_refine(a, b);
+      a = std::move(b);
+    }
+    *N_out = a.N;
+    *T_out = a.T;
+    if (xy_out) {
+      for (i64 i = 0; i < a.N; ++i) {
+        xy_out[2 * i] = a.x[i];
+        xy_out[2 * i + 1] = a.y[i];
+      }
+      std::copy(a.mk.begin(), a.mk.end(), mk_out);
+      std::copy(a.tri.begin(), a.tri.end(), tris_out);
+    }
+  });
+}
+
+int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, int64_t* rowptr, int64_t* col,
+                        double* val) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    const Csr* A = nullptr;
+    const std::vector<double>* v = nullptr;
+    switch (op) {
+      case PUCFEM_OP_K: A = &c.P; v = &c.as.K; break;
+      case PUCFEM_OP_GX: A = &c.P; v = &c.as.Gx; break;
+      case PUCFEM_OP_GY: A = &c.P; v = &c.as.Gy; break;
+      case PUCFEM_OP_VISC: A = &c.P; v = &c.Kv; break;
+      case PUCFEM_OP_PRES: A = &c.Pp; v = &c.Pp.val; break;
+      case PUCFEM_OP_LIT: A = &c.Lit; v = &c.Lit.val; break;
+      default: throw Error(PUCFEM_EINVAL, "op has no CSR");
+    }
+    require(A->nrows > 0, "operator not built for this scheme");
+    const LocalPlan& lp = c.lp;
+    // owned rows in caller numbering, ascending
+    std::vector<i64> rows;
+    for (i64 g = lp.r0; g < lp.r1; ++g) rows.push_back(c.ord.new2old[g]);
+    std::sort(rows.begin(), rows.end());
+    i64 total = 0;
+    for (i64 o : rows) {
+      const i64 g = c.ord.old2new[o];
+      total += A->rowptr[g + 1] - A->rowptr[g];
+    }
+    *n_rows = (i64)rows.size();
+    *nnz = total;
+    if (!col) return;
+    i64 k = 0;
+    rowptr[0] = 0;
+    std::vector<std::pair<i64, double>> tmp;
+    for (size_t r = 0; r < rows.size(); ++r) {
+      const i64 g = c.ord.old2new[rows[r]];
+      tmp.clear();
+      for (i64 e = A->rowptr[g]; e < A->rowptr[g + 1]; ++e) tmp.push_back({c.ord.new2old[A->col[e]], (*v)[e]});
+      std::sort(tmp.begin(), tmp.end());
+      for (auto& t : tmp) {
+        col[k] = t.first;
+        val[k] = t.second;
+        ++k;
+      }
+      rowptr[r + 1] = k;
+    }
+  });
+}
+
+int pucfem_host_partition(void* ctx, int32_t rank, int32_t world, int64_t* n_own, int64_t* n_ghost, int64_t* owned,
+                          int64_t* ghosts, int32_t* ghost_owner, int64_t* n_send, int64_t* send_ids,
+                          int32_t* send_peer) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    require(rank >= 0 && rank < world, "bad rank");
+    std::vector<i64> rs;
+    partition_rows(c.P, c.ord, world, rs);
+    LocalPlan lp;
+    std::vector<const Csr*> pats = {&c.P};
+    if (c.Pp.nrows) pats.push_back(&c.Pp);
+    make_local_plan(pats, rs, rank, lp);
+    *n_own = lp.n_own;
+    *n_ghost = lp.n_ghost;
+    *n_send = (i64)lp.send_local.size();
+    if (!owned) return;
+    for (i64 i = 0; i < lp.n_own; ++i) owned[i] = c.ord.new2old[lp.r0 + i];
+    for (i64 k = 0; k < lp.n_ghost; ++k) {
+      ghosts[k] = c.ord.new2old[lp.ghost_global[k]];
+      ghost_owner[k] = lp.ghost_owner[k];
+    }
+    for (size_t q = 0; q < lp.send_peer.size(); ++q)
+      for (i64 k = 0; k < lp.send_cnt[q]; ++k) {
+        const i64 idx = lp.send_off[q] + k;
+        send_ids[idx] = c.ord.new2old[lp.r0 + lp.send_local[idx]];
+        send_peer[idx] = lp.send_peer[q];
+      }
+  });
+}
+
+}  // extern "C"

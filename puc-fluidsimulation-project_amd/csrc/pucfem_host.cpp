@@ -1,0 +1,511 @@
+// Host-side runtime of libpucfem (see pucfem_host.hpp).  Built with -ffp-contract=off so the
+// assembly arithmetic is the reference's, operation for operation.
+#include "pucfem_host.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <numeric>
+#include <stdexcept>
+
+namespace pucfem {
+
+// ----------------------------------------------------------------------------- refinement
+void red_refine(const HostMesh& in, HostMesh& out) {
+  const i64 N = in.N, T = in.T;
+  // bucket every edge (a<b) under a, with multiplicity
+  std::vector<i64> bptr(N + 1, 0);
+  for (i64 t = 0; t < T; ++t)
+    for (int e = 0; e < 3; ++e) {
+      i32 a = in.tri[3 * t + e], b = in.tri[3 * t + (e + 1) % 3];
+      bptr[std::min(a, b) + 1]++;
+    }
+  for (i64 i = 0; i < N; ++i) bptr[i + 1] += bptr[i];
+  std::vector<i32> bval(bptr[N]);
+  {
+    std::vector<i64> fill(bptr.begin(), bptr.end() - 1);
+    for (i64 t = 0; t < T; ++t)
+      for (int e = 0; e < 3; ++e) {
+        i32 a = in.tri[3 * t + e], b = in.tri[3 * t + (e + 1) % 3];
+        bval[fill[std::min(a, b)]++] = std::max(a, b);
+      }
+  }
+  // unique edges per bucket, with their multiplicity
+  std::vector<i64> eptr(N + 1, 0);
+  std::vector<i32> eb;
+  std::vector<uint8_t> emult;
+  eb.reserve(bval.size() / 2 + N);
+  for (i64 a = 0; a < N; ++a) {
+    auto s = bval.begin() + bptr[a], e = bval.begin() + bptr[a + 1];
+    std::sort(s, e);
+    for (auto it = s; it != e;) {
+      auto j = it;
+      while (j != e && *j == *it) ++j;
+      eb.push_back(*it);
+      emult.push_back((uint8_t)std::min<i64>(255, j - it));
+      it = j;
+    }
+    eptr[a + 1] = (i64)eb.size();
+  }
+  const i64 E = (i64)eb.size();
+  auto edge_id = [&](i32 a, i32 b) -> i64 {
+    if (a > b) std::swap(a, b);
+    auto s = eb.begin() + eptr[a], e = eb.begin() + eptr[a + 1];
+    auto it = std::lower_bound(s, e, b);
+    return it - eb.begin();
+  };
+  out.N = N + E;
+  out.T = 4 * T;
+  out.fp32 = in.fp32;
+  out.x.resize(out.N);
+  out.y.resize(out.N);
+  out.mk.resize(out.N);
+  std::copy(in.x.begin(), in.x.end(), out.x.begin());
+  std::copy(in.y.begin(), in.y.end(), out.y.begin());
+  std::copy(in.mk.begin(), in.mk.end(), out.mk.begin());
+  for (i64 a = 0; a < N; ++a)
+    for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
+      i32 b = eb[k];
+      i64 n = N + k;
+      out.x[n] = (in.x[a] + in.x[b]) * 0.5;
+      out.y[n] = (in.y[a] + in.y[b]) * 0.5;
+      if (emult[k] == 1)  // boundary edge: midpoint stays on the boundary segment
+        out.mk[n] = (in.mk[a] == 2 && in.mk[b] == 2) ? 2 : 1;
+      else
+        out.mk[n] = 0;
+    }
+  out.tri.resize(3 * out.T);
+  for (i64 t = 0; t < T; ++t) {
+    i32 a = in.tri[3 * t], b = in.tri[3 * t + 1], c = in.tri[3 * t + 2];
+    i32 ab = (i32)(N + edge_id(a, b)), bc = (i32)(N + edge_id(b, c)), ca = (i32)(N + edge_id(c, a));
+    const i32 ch[12] = {a, ab, ca, ab, b, bc, ca, bc, c, ab, bc, ca};
+    std::copy(ch, ch + 12, out.tri.begin() + 12 * t);
+  }
+}
+
+// ----------------------------------------------------------------------------- ordering
+void make_ordering(const HostMesh& m, int nstrips, Ordering& ord) {
+  const i64 N = m.N;
+  int S = nstrips > 0 ? nstrips : (int)std::max<i64>(1, std::llround(std::sqrt((double)N) / 4.0));
+  double ymin = *std::min_element(m.y.begin(), m.y.end());
+  double ymax = *std::max_element(m.y.begin(), m.y.end());
+  double span = ymax > ymin ? ymax - ymin : 1.0;
+  std::vector<i32> strip(N);
+  for (i64 i = 0; i < N; ++i) {
+    i64 s = (i64)std::floor((m.y[i] - ymin) / span * S);
+    strip[i] = (i32)std::min<i64>(S - 1, std::max<i64>(0, s));
+  }
+  ord.new2old.resize(N);
+  std::iota(ord.new2old.begin(), ord.new2old.end(), 0);
+  std::sort(ord.new2old.begin(), ord.new2old.end(), [&](i32 a, i32 b) {
+    if (strip[a] != strip[b]) return strip[a] < strip[b];
+    if (m.x[a] != m.x[b]) return m.x[a] < m.x[b];
+    if (m.y[a] != m.y[b]) return m.y[a] < m.y[b];
+    return a < b;
+  });
+  ord.old2new.assign(N, 0);
+  for (i64 i = 0; i < N; ++i) ord.old2new[ord.new2old[i]] = (i32)i;
+  ord.strip_ptr.assign(S + 1, 0);
+  for (i64 i = 0; i < N; ++i) ord.strip_ptr[strip[i] + 1]++;
+  for (int s = 0; s < S; ++s) ord.strip_ptr[s + 1] += ord.strip_ptr[s];
+}
+
+// ----------------------------------------------------------------------------- pattern
+void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P) {
+  const i64 N = m.N, T = m.T;
+  std::vector<i64> cnt(N + 1, 0);
+  for (i64 t = 0; t < T; ++t)
+    for (int i = 0; i < 3; ++i) cnt[ord.old2new[m.tri[3 * t + i]] + 1] += 3;
+  for (i64 i = 0; i < N; ++i) cnt[i + 1] += cnt[i];
+  std::vector<i32> tmp(cnt[N]);
+  std::vector<i64> fill(cnt.begin(), cnt.end() - 1);
+  for (i64 t = 0; t < T; ++t)
+    for (int i = 0; i < 3; ++i) {
+      i32 r = ord.old2new[m.tri[3 * t + i]];
+      for (int j = 0; j < 3; ++j) tmp[fill[r]++] = ord.old2new[m.tri[3 * t + j]];
+    }
+  P.nrows = N;
+  P.rowptr.assign(N + 1, 0);
+  P.col.clear();
+  P.col.reserve(cnt[N] / 2 + N);
+  for (i64 r = 0; r < N; ++r) {
+    auto s = tmp.begin() + cnt[r], e = tmp.begin() + cnt[r + 1];
+    std::sort(s, e);
+    e = std::unique(s, e);
+    if (s == e) P.col.push_back((i32)r);  // isolated node: keep a diagonal entry
+    P.col.insert(P.col.end(), s, e);
+    P.rowptr[r + 1] = (i64)P.col.size();
+  }
+}
+
+// ----------------------------------------------------------------------------- assembly
+void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A) {
+  const i64 N = m.N, T = m.T, nnz = P.nnz();
+  A.K.assign(nnz, 0.0);
+  A.Gx.assign(nnz, 0.0);
+  A.Gy.assign(nnz, 0.0);
+  A.M.assign(N, 0.0);
+  A.asum.assign(N, 0.0);
+  for (i64 t = 0; t < T; ++t) {
+    const i32 o[3] = {m.tri[3 * t], m.tri[3 * t + 1], m.tri[3 * t + 2]};
+    const i32 n[3] = {ord.old2new[o[0]], ord.old2new[o[1]], ord.old2new[o[2]]};
+    const double x1 = m.x[o[0]], y1 = m.y[o[0]], x2 = m.x[o[1]], y2 = m.y[o[1]], x3 = m.x[o[2]],
+                 y3 = m.y[o[2]];
+    // StokesColor.py:277-283 (buildLumpedMassMatrix): no degenerate skip
+    const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
+    const double area = 0.5 * std::fabs(det);
+    for (int i = 0; i < 3; ++i) A.M[n[i]] += area / 3.0;
+    if (std::fabs(det) < 1e-14) continue;  // StokesColor.py:113, :146, :239
+    const double yd[3] = {y2 - y3, y3 - y1, y1 - y2};
+    const double xd[3] = {x3 - x2, x1 - x3, x2 - x1};
+    const double den = 2 * std::fabs(det);
+    i64 pos[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) pos[i][j] = P.find(n[i], n[j]);
+    for (int i = 0; i < 3; ++i)  // StokesColor.py:120-126
+      for (int j = 0; j < 3; ++j) A.K[pos[i][j]] += (yd[i] * yd[j] + xd[i] * xd[j]) / den;
+    const double inv2A = 1.0 / det;  // StokesColor.py:149 / :241
+    const double a3 = area / 3.0;
+    for (int i = 0; i < 3; ++i) {
+      A.asum[n[i]] += a3;
+      for (int k = 0; k < 3; ++k) {
+        A.Gx[pos[i][k]] += (yd[k] * inv2A) * a3;
+        A.Gy[pos[i][k]] += (xd[k] * inv2A) * a3;
+      }
+    }
+  }
+}
+
+namespace {
+using Row = std::vector<std::pair<i32, double>>;
+void row_add(Row& dst, const Row& src) {  // dst[c] = dst[c] + src[c] (poisson.py:204)
+  Row out;
+  out.reserve(dst.size() + src.size());
+  size_t i = 0, j = 0;
+  while (i < dst.size() || j < src.size()) {
+    if (j == src.size() || (i < dst.size() && dst[i].first < src[j].first)) out.push_back(dst[i++]);
+    else if (i == dst.size() || src[j].first < dst[i].first) out.push_back(src[j++]);
+    else {
+      out.push_back({dst[i].first, dst[i].second + src[j].second});
+      ++i, ++j;
+    }
+  }
+  dst.swap(out);
+}
+}  // namespace
+
+void assemble_literal(const HostMesh& m, const Ordering& ord, const std::vector<float>& g_tri,
+                      const std::vector<std::pair<i64, i64>>& op_pairs_old,
+                      const std::vector<i32>& dir_nodes_old, const std::vector<double>& dir_vals,
+                      double heat_dt, Csr& out, std::vector<double>& b) {
+  const i64 N = m.N, T = m.T;
+  std::vector<Row> rows(N);
+  b.assign(N, 0.0);
+  std::vector<std::map<i32, double>> acc(N);
+  // poisson.py:105-144 -- fp32 element arithmetic, fp64 accumulation in triangle order
+  for (i64 t = 0; t < T; ++t) {
+    const i32 o[3] = {m.tri[3 * t], m.tri[3 * t + 1], m.tri[3 * t + 2]};
+    const float x1 = (float)m.x[o[0]], y1 = (float)m.y[o[0]], x2 = (float)m.x[o[1]],
+                y2 = (float)m.y[o[1]], x3 = (float)m.x[o[2]], y3 = (float)m.y[o[2]];
+    const float ADet = x1 * y2 - x1 * y3 - x2 * y1 + x2 * y3 + x3 * y1 - x3 * y2;
+    if (ADet == 0.0f) continue;
+    const float yd[3] = {y2 - y3, y3 - y1, y1 - y2};
+    const float xd[3] = {x3 - x2, x1 - x3, x2 - x1};
+    const float den = 2.0f * ADet;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const float v = (yd[i] * yd[j] + xd[i] * xd[j]) / den;
+        acc[ord.old2new[o[i]]][ord.old2new[o[j]]] += (double)v;
+      }
+    const float area = 0.5f * ADet;
+    const float s = (g_tri.empty() ? 0.0f : g_tri[t]) * (area / 3.0f);
+    for (int i = 0; i < 3; ++i) b[ord.old2new[o[i]]] += (double)s;
+  }
+  for (i64 r = 0; r < N; ++r) {
+    rows[r].assign(acc[r].begin(), acc[r].end());
+    b[r] = -b[r];  // poisson.py:146 returns -BVector
+  }
+  acc.clear();
+  // poisson.py:202-213 periodic row merge, sequential
+  for (auto& pr : op_pairs_old) {
+    const i32 mi = ord.old2new[pr.first], si = ord.old2new[pr.second];
+    row_add(rows[mi], rows[si]);
+    b[mi] += b[si];
+    rows[si].clear();
+    if (si < mi) rows[si] = {{si, 1.0}, {mi, -1.0}};
+    else rows[si] = {{mi, -1.0}, {si, 1.0}};
+    b[si] = 0.0;
+  }
+  // poisson.py:258-278 Dirichlet rows (columns kept)
+  for (size_t k = 0; k < dir_nodes_old.size(); ++k) {
+    const i32 i = ord.old2new[dir_nodes_old[k]];
+    rows[i] = {{i, 1.0}};
+    b[i] = dir_vals[k];
+  }
+  if (heat_dt > 0) {  // heatEq.py:305  A <- I + DT*A
+    for (i64 r = 0; r < N; ++r) {
+      bool diag = false;
+      for (auto& e : rows[r]) {
+        e.second = heat_dt * e.second;
+        if (e.first == r) {
+          e.second = 1.0 + e.second;
+          diag = true;
+        }
+      }
+      if (!diag) {
+        rows[r].push_back({(i32)r, 1.0});
+        std::sort(rows[r].begin(), rows[r].end());
+      }
+    }
+  }
+  out.nrows = N;
+  out.rowptr.assign(N + 1, 0);
+  out.col.clear();
+  out.val.clear();
+  for (i64 r = 0; r < N; ++r) {
+    for (auto& e : rows[r]) {
+      out.col.push_back(e.first);
+      out.val.push_back(e.second);
+    }
+    out.rowptr[r + 1] = (i64)out.col.size();
+  }
+}
+
+void build_pressure(const Csr& P, const std::vector<double>& K, const std::vector<i32>& dof,
+                    const std::vector<i32>& slave_of, Csr& Pp) {
+  const i64 N = P.nrows;
+  Pp.nrows = N;
+  Pp.rowptr.assign(N + 1, 0);
+  Pp.col.clear();
+  Pp.val.clear();
+  std::vector<std::pair<i32, double>> tmp;
+  for (i64 r = 0; r < N; ++r) {
+    tmp.clear();
+    if (dof[r] != r) {  // slave: identity row, decoupled
+      tmp.push_back({(i32)r, 1.0});
+    } else {
+      auto add_row = [&](i64 src) {
+        for (i64 k = P.rowptr[src]; k < P.rowptr[src + 1]; ++k) tmp.push_back({dof[P.col[k]], K[k]});
+      };
+      add_row(r);
+      if (slave_of[r] >= 0) add_row(slave_of[r]);
+      // combine duplicates in insertion order (stable by column)
+      std::stable_sort(tmp.begin(), tmp.end(),
+                       [](const std::pair<i32, double>& a, const std::pair<i32, double>& b) { return a.first < b.first; });
+      size_t w = 0;
+      for (size_t k = 0; k < tmp.size(); ++k) {
+        if (w > 0 && tmp[w - 1].first == tmp[k].first) tmp[w - 1].second += tmp[k].second;
+        else tmp[w++] = tmp[k];
+      }
+      tmp.resize(w);
+    }
+    for (auto& e : tmp) {
+      Pp.col.push_back(e.first);
+      Pp.val.push_back(e.second);
+    }
+    Pp.rowptr[r + 1] = (i64)Pp.col.size();
+  }
+}
+
+// ----------------------------------------------------------------------------- partition
+void partition_rows(const Csr& P, const Ordering& ord, int world, std::vector<i64>& row_start) {
+  const i64 S = (i64)ord.strip_ptr.size() - 1;
+  if (world < 1 || world > S) throw std::runtime_error("world size exceeds the number of y-strips");
+  row_start.assign(world + 1, 0);
+  row_start[world] = P.nrows;
+  const double total = (double)P.nnz();
+  i64 prev = 0;  // previous cut, as a strip index
+  for (int r = 1; r < world; ++r) {
+    const double target = total * r / world;
+    // first strip boundary past `prev` whose prefix nnz reaches the target, leaving at
+    // least one strip for every remaining rank
+    i64 c = prev + 1;
+    while (c < S - (world - r) && (double)P.rowptr[ord.strip_ptr[c]] < target) ++c;
+    if (c > prev + 1 && (double)P.rowptr[ord.strip_ptr[c]] - target >
+                            target - (double)P.rowptr[ord.strip_ptr[c - 1]])
+      --c;  // the boundary just before is closer to the target
+    row_start[r] = ord.strip_ptr[c];
+    prev = c;
+  }
+}
+
+i32 to_local(const LocalPlan& lp, i32 g) {
+  if (g >= lp.r0 && g < lp.r1) return (i32)(g - lp.r0);
+  auto it = std::lower_bound(lp.ghost_global.begin(), lp.ghost_global.end(), g);
+  if (it == lp.ghost_global.end() || *it != g) throw std::runtime_error("column not in ghost set");
+  return (i32)(lp.n_own + (it - lp.ghost_global.begin()));
+}
+
+void make_local_plan(const std::vector<const Csr*>& pats, const std::vector<i64>& row_start, int rank,
+                     LocalPlan& lp) {
+  const int world = (int)row_start.size() - 1;
+  lp.r0 = row_start[rank];
+  lp.r1 = row_start[rank + 1];
+  lp.n_own = lp.r1 - lp.r0;
+  auto owner = [&](i64 g) {
+    return (i32)(std::upper_bound(row_start.begin(), row_start.end(), g) - row_start.begin() - 1);
+  };
+  std::vector<i32> gh;
+  for (auto* P : pats)
+    for (i64 r = lp.r0; r < lp.r1; ++r)
+      for (i64 k = P->rowptr[r]; k < P->rowptr[r + 1]; ++k)
+        if (P->col[k] < lp.r0 || P->col[k] >= lp.r1) gh.push_back(P->col[k]);
+  std::sort(gh.begin(), gh.end());
+  gh.erase(std::unique(gh.begin(), gh.end()), gh.end());
+  lp.ghost_global = gh;
+  lp.n_ghost = (i64)gh.size();
+  lp.ghost_owner.resize(gh.size());
+  for (size_t k = 0; k < gh.size(); ++k) lp.ghost_owner[k] = owner(gh[k]);
+  lp.recv_peer.clear();
+  lp.recv_off.clear();
+  lp.recv_cnt.clear();
+  for (size_t k = 0; k < gh.size(); ++k) {
+    if (lp.recv_peer.empty() || lp.recv_peer.back() != lp.ghost_owner[k]) {
+      lp.recv_peer.push_back(lp.ghost_owner[k]);
+      lp.recv_off.push_back((i64)k);
+      lp.recv_cnt.push_back(0);
+    }
+    lp.recv_cnt.back()++;
+  }
+  // send lists: what every other rank q needs from my rows (its ghosts inside [r0, r1))
+  lp.send_peer.clear();
+  lp.send_off.clear();
+  lp.send_cnt.clear();
+  lp.send_local.clear();
+  for (int q = 0; q < world; ++q) {
+    if (q == rank) continue;
+    std::vector<i32> need;
+    for (auto* P : pats)
+      for (i64 r = row_start[q]; r < row_start[q + 1]; ++r)
+        for (i64 k = P->rowptr[r]; k < P->rowptr[r + 1]; ++k)
+          if (P->col[k] >= lp.r0 && P->col[k] < lp.r1) need.push_back(P->col[k]);
+    if (need.empty()) continue;
+    std::sort(need.begin(), need.end());
+    need.erase(std::unique(need.begin(), need.end()), need.end());
+    lp.send_peer.push_back(q);
+    lp.send_off.push_back((i64)lp.send_local.size());
+    lp.send_cnt.push_back((i64)need.size());
+    for (i32 g : need) lp.send_local.push_back((i32)(g - lp.r0));
+  }
+}
+
+// ----------------------------------------------------------------------------- SELL-64
+void build_sell(const Csr& A, const LocalPlan& lp, Sell& S) {
+  const i64 n = lp.n_own;
+  S.nrows = n;
+  S.nslices = (n + 63) / 64;
+  S.slice_off.assign(S.nslices + 1, 0);
+  S.slice_w.assign(S.nslices, 0);
+  for (i64 s = 0; s < S.nslices; ++s) {
+    i64 w = 0;
+    for (i64 l = 0; l < 64; ++l) {
+      i64 r = s * 64 + l;
+      if (r < n) w = std::max(w, A.rowptr[lp.r0 + r + 1] - A.rowptr[lp.r0 + r]);
+    }
+    S.slice_w[s] = (i32)w;
+    S.slice_off[s + 1] = S.slice_off[s] + w * 64;
+  }
+  S.padded = S.slice_off[S.nslices];
+  S.col.assign(S.padded, 0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      i64 r = s * 64 + l;
+      i64 len = r < n ? A.rowptr[lp.r0 + r + 1] - A.rowptr[lp.r0 + r] : 0;
+      for (i64 k = 0; k < S.slice_w[s]; ++k) {
+        i32 c = r < n ? (k < len ? to_local(lp, A.col[A.rowptr[lp.r0 + r] + k]) : (i32)r) : 0;
+        S.col[S.slice_off[s] + k * 64 + l] = c;
+      }
+    }
+}
+
+void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
+                 std::vector<double>& out) {
+  out.assign(S.padded, 0.0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      i64 r = s * 64 + l;
+      if (r >= S.nrows) continue;
+      i64 b = A.rowptr[lp.r0 + r], len = A.rowptr[lp.r0 + r + 1] - b;
+      for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
+    }
+}
+
+// ----------------------------------------------------------------------------- grids
+static void grid_dims(double xmin, double xmax, double ymin, double ymax, i64 nitems, double per_cell, Grid& G) {
+  double w = std::max(xmax - xmin, 1e-300), h = std::max(ymax - ymin, 1e-300);
+  double ncell = std::max(1.0, (double)nitems / per_cell);
+  double cs = std::sqrt(w * h / ncell);
+  G.nx = (i32)std::max(1.0, std::min(32768.0, std::ceil(w / cs)));
+  G.ny = (i32)std::max(1.0, std::min(32768.0, std::ceil(h / cs)));
+  G.x0 = xmin;
+  G.y0 = ymin;
+  G.hx = w / G.nx;
+  G.hy = h / G.ny;
+}
+
+static inline i32 cell_of(double v, double v0, double hv, i32 n) {
+  double f = std::floor((v - v0) / hv);
+  if (!(f >= 0)) return 0;
+  if (f >= n) return n - 1;
+  return (i32)f;
+}
+
+void build_centroid_grid(const std::vector<double>& cx, const std::vector<double>& cy, double per_cell, Grid& G) {
+  const i64 T = (i64)cx.size();
+  grid_dims(*std::min_element(cx.begin(), cx.end()), *std::max_element(cx.begin(), cx.end()),
+            *std::min_element(cy.begin(), cy.end()), *std::max_element(cy.begin(), cy.end()), T, per_cell, G);
+  const i64 nc = (i64)G.nx * G.ny;
+  std::vector<i32> cell(T);
+  G.cell_start.assign(nc + 1, 0);
+  for (i64 t = 0; t < T; ++t) {
+    cell[t] = cell_of(cy[t], G.y0, G.hy, G.ny) * G.nx + cell_of(cx[t], G.x0, G.hx, G.nx);
+    G.cell_start[cell[t] + 1]++;
+  }
+  for (i64 c = 0; c < nc; ++c) G.cell_start[c + 1] += G.cell_start[c];
+  G.item.assign(T, 0);
+  G.px.assign(T, 0);
+  G.py.assign(T, 0);
+  std::vector<i32> fill(G.cell_start.begin(), G.cell_start.end() - 1);
+  for (i64 t = 0; t < T; ++t) {  // ascending triangle id inside each cell
+    i32 k = fill[cell[t]]++;
+    G.item[k] = (i32)t;
+    G.px[k] = cx[t];
+    G.py[k] = cy[t];
+  }
+}
+
+void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,
+                    double per_cell, Grid& G) {
+  const i64 T = (i64)tri.size() / 3;
+  grid_dims(*std::min_element(x.begin(), x.end()), *std::max_element(x.begin(), x.end()),
+            *std::min_element(y.begin(), y.end()), *std::max_element(y.begin(), y.end()), T, per_cell, G);
+  const i64 nc = (i64)G.nx * G.ny;
+  G.cell_start.assign(nc + 1, 0);
+  auto bbox = [&](i64 t, i32& cx0, i32& cx1, i32& cy0, i32& cy1) {
+    double xa = std::min({x[tri[3 * t]], x[tri[3 * t + 1]], x[tri[3 * t + 2]]});
+    double xb = std::max({x[tri[3 * t]], x[tri[3 * t + 1]], x[tri[3 * t + 2]]});
+    double ya = std::min({y[tri[3 * t]], y[tri[3 * t + 1]], y[tri[3 * t + 2]]});
+    double yb = std::max({y[tri[3 * t]], y[tri[3 * t + 1]], y[tri[3 * t + 2]]});
+    cx0 = cell_of(xa, G.x0, G.hx, G.nx);
+    cx1 = cell_of(xb, G.x0, G.hx, G.nx);
+    cy0 = cell_of(ya, G.y0, G.hy, G.ny);
+    cy1 = cell_of(yb, G.y0, G.hy, G.ny);
+  };
+  for (i64 t = 0; t < T; ++t) {
+    i32 a, b, c, d;
+    bbox(t, a, b, c, d);
+    for (i32 j = c; j <= d; ++j)
+      for (i32 i = a; i <= b; ++i) G.cell_start[(i64)j * G.nx + i + 1]++;
+  }
+  for (i64 c = 0; c < nc; ++c) G.cell_start[c + 1] += G.cell_start[c];
+  G.item.assign(G.cell_start[nc], 0);
+  std::vector<i32> fill(G.cell_start.begin(), G.cell_start.end() - 1);
+  for (i64 t = 0; t < T; ++t) {
+    i32 a, b, c, d;
+    bbox(t, a, b, c, d);
+    for (i32 j = c; j <= d; ++j)
+      for (i32 i = a; i <= b; ++i) G.item[fill[(i64)j * G.nx + i]++] = (i32)t;
+  }
+}
+
+}  // namespace pucfem

@@ -1,0 +1,116 @@
+// Host-side runtime of libpucfem: mesh refinement, node ordering, operator assembly,
+// partition / halo plan and the SELL-64 device layout.  Pure C++ (no HIP), so it is
+// exercised by the CPU test-suite through a host-only context.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pucfem {
+
+using i32 = int32_t;
+using i64 = int64_t;
+
+struct HostMesh {
+  i64 N = 0, T = 0;
+  std::vector<double> x, y;  // caller numbering
+  std::vector<i32> mk;       // Triangle boundary markers (0 interior, 1 outer, 2 inner body)
+  std::vector<i32> tri;      // T*3, caller numbering, CCW
+  bool fp32 = false;         // coordinates are the fp32 values of poisson.py:40
+};
+
+// Red refinement: every triangle -> 4, edge midpoints appended after the old nodes in
+// (min, max) edge order; boundary-edge midpoints inherit the boundary marker.
+void red_refine(const HostMesh& in, HostMesh& out);
+
+// CSR pattern / matrix with column ids in the INTERNAL (new) numbering.
+struct Csr {
+  i64 nrows = 0;
+  std::vector<i64> rowptr;
+  std::vector<i32> col;
+  std::vector<double> val;
+  i64 nnz() const { return nrows ? rowptr[nrows] : 0; }
+  i64 find(i64 r, i32 c) const {
+    for (i64 k = rowptr[r]; k < rowptr[r + 1]; ++k)
+      if (col[k] == c) return k;
+    return -1;
+  }
+};
+
+// Internal node order: y-strips (so periodic partners x=0 <-> x=1 share a strip and a rank),
+// x-sorted inside a strip.  Ranks own contiguous strip ranges.
+struct Ordering {
+  std::vector<i32> new2old, old2new;
+  std::vector<i64> strip_ptr;  // size S+1, internal-index start of each strip
+};
+void make_ordering(const HostMesh& m, int nstrips, Ordering& ord);
+
+// Node-adjacency pattern (incl. diagonal) in internal numbering, sorted columns.
+void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P);
+
+struct Assembly {
+  std::vector<double> K;     // on P (StokesColor.py:98-128), reference triangle order
+  std::vector<double> Gx, Gy;// on P: lumped gradient/divergence coefficients (StokesColor.py:130-263)
+  std::vector<double> M;     // lumped mass (StokesColor.py:266-284), internal numbering
+  std::vector<double> asum;  // area_sum of calculate_divergence (|det| >= 1e-14 only)
+};
+void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A);
+
+// poisson.py:100-146 in fp32 arithmetic (bit-exact), fp64 accumulation, then the literal
+// periodic row-merge (poisson.py:187-213) and Dirichlet rows (poisson.py:258-278).
+// Returns a CSR in internal numbering with its own pattern, plus the RHS.
+void assemble_literal(const HostMesh& m, const Ordering& ord, const std::vector<float>& g_tri,
+                      const std::vector<std::pair<i64, i64>>& op_pairs_old,
+                      const std::vector<i32>& dir_nodes_old, const std::vector<double>& dir_vals,
+                      double heat_dt /* <= 0: Poisson A; > 0: I + dt*A */, Csr& A,
+                      std::vector<double>& b);
+
+// P^T K P with identity slave rows (the well-posed pressure operator).
+void build_pressure(const Csr& P, const std::vector<double>& K, const std::vector<i32>& dof,
+                    const std::vector<i32>& slave_of, Csr& Pp);
+
+// Partition of the internal index range into `world` contiguous strip ranges, balanced by nnz.
+void partition_rows(const Csr& P, const Ordering& ord, int world, std::vector<i64>& row_start);
+
+// Local view of one rank: owned rows [r0, r1) + sorted ghost list, local column ids.
+struct LocalPlan {
+  i64 r0 = 0, r1 = 0, n_own = 0, n_ghost = 0;
+  std::vector<i32> ghost_global;        // internal ids, sorted
+  std::vector<i32> ghost_owner;
+  std::vector<i32> recv_peer;           // peers we receive from, ascending
+  std::vector<i64> recv_off, recv_cnt;  // into the ghost region
+  std::vector<i32> send_peer;
+  std::vector<i64> send_off, send_cnt;
+  std::vector<i32> send_local;          // owned local ids to pack, per peer contiguous
+};
+// patterns: every pattern whose columns must be resolved (P, Pp, ...)
+void make_local_plan(const std::vector<const Csr*>& pats, const std::vector<i64>& row_start, int rank,
+                     LocalPlan& lp);
+
+// SELL-64: slices of 64 rows, per-slice width = max row length, entries column-major
+// inside a slice (lane = row) so a wave's loads are contiguous.
+struct Sell {
+  i64 nrows = 0, nslices = 0, padded = 0;
+  std::vector<i64> slice_off;  // nslices+1, entry offsets
+  std::vector<i32> slice_w;
+  std::vector<i32> col;        // local column ids
+};
+// rows [r0, r1) of `A` (global internal ids) -> local SELL; values extracted with sell_values().
+void build_sell(const Csr& A, const LocalPlan& lp, Sell& S);
+void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
+                 std::vector<double>& out);
+i32 to_local(const LocalPlan& lp, i32 g);
+
+// Uniform grid of items (centroids / triangle bboxes) for the device point searches.
+struct Grid {
+  i32 nx = 1, ny = 1;
+  double x0 = 0, y0 = 0, hx = 1, hy = 1;
+  std::vector<i32> cell_start;  // nx*ny+1
+  std::vector<i32> item;        // triangle ids
+  std::vector<double> px, py;   // centroid coordinates per entry (centroid grid only)
+};
+void build_centroid_grid(const std::vector<double>& cx, const std::vector<double>& cy, double per_cell, Grid& G);
+void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,
+                    double per_cell, Grid& G);
+
+}  // namespace pucfem

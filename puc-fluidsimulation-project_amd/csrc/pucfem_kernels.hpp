@@ -1,0 +1,94 @@
+// Device kernels of libpucfem (gfx950 / CDNA4, wave64).
+//
+// Layout: every operator is SELL-64 -- one 64-row slice per wavefront, lane = row, entries
+// column-major inside the slice so each `col`/`val` load of a wave is one contiguous 256 / 512 B
+// segment.  A block (256 threads = 4 waves) owns a CONTIGUOUS range of slices (good L2 reuse of
+// the gathered vector on the block's XCD).  Reductions are deterministic: each block writes one
+// partial per value; the consumer kernel re-reduces the partial array in a fixed order in every
+// block (no atomics, identical scalars in all blocks, bit-reproducible run to run).
+//
+// Compiled with -ffp-contract=off: the semi-Lagrangian / tracer / divergence formulas are the
+// reference's, operation for operation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pucfem {
+namespace dev {
+
+constexpr int BS = 256;     // threads per block
+constexpr int MAXB = 1024;  // max blocks of a partial-producing launch (= partial stride)
+constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
+
+struct SellDev {
+  const int64_t* off;  // nslices+1
+  const int32_t* w;    // nslices
+  const int32_t* col;  // padded entries
+  int64_t nslices, nrows;
+};
+
+// ----------------------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// result valid in every thread; `sh` must hold >= 4 doubles
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return ((sh[0] + sh[1]) + (sh[2] + sh[3]));
+}
+__device__ __forceinline__ double block_max(double v, double* sh) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+}
+// Sum of `nb` partials at stride 1 starting at p (fixed order -> identical in every block).
+__device__ __forceinline__ double reduce_partials(const double* p, int nb, double* sh) {
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nb; i += BS) a += p[i];
+  return block_sum(a, sh);
+}
+__device__ __forceinline__ double reduce_partials_max(const double* p, int nb, double* sh) {
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nb; i += BS) a = fmax(a, p[i]);
+  return block_max(a, sh);
+}
+
+// slice range of this block
+__device__ __forceinline__ void block_slices(int64_t nslices, int64_t& s0, int64_t& s1) {
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  s0 = (nslices * b) / nb;
+  s1 = (nslices * (b + 1)) / nb;
+}
+// row range of this block for row-wise (non-SpMV) kernels, aligned to the same slices
+__device__ __forceinline__ void block_rows(int64_t nrows, int64_t& r0, int64_t& r1) {
+  int64_t s0, s1;
+  block_slices((nrows + 63) / 64, s0, s1);
+  r0 = s0 * 64;
+  r1 = s1 * 64 < nrows ? s1 * 64 : nrows;
+}
+
+// Python / numpy float modulo (npy_divmod): result has the sign of the divisor.
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+}  // namespace dev
+}  // namespace pucfem

@@ -1,0 +1,724 @@
+// Device kernels of libpucfem -- see pucfem_kernels.hpp for the layout / reduction conventions.
+// Included by pucfem_api.hip (single translation unit for the device code).
+#pragma once
+#include "pucfem_kernels.hpp"
+
+namespace pucfem {
+namespace dev {
+
+// ----------------------------------------------------------------------------- SpMV
+// y = A x over owned rows (generic; unit `pucfem_apply`, residuals).
+__global__ __launch_bounds__(BS) void k_spmv(SellDev A, const double* __restrict__ val,
+                                             const double* __restrict__ x, double* __restrict__ y) {
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double acc = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      acc += val[e] * x[A.col[e]];
+    }
+    if (row < A.nrows) y[row] = acc;
+  }
+}
+
+// ----------------------------------------------------------------------------- CG (Jacobi-scaled)
+// The solver works on A^ = S A S (S = diag(1/sqrt(a_ii))), so Jacobi-PCG is plain CG on A^.
+// Per iteration two kernels:
+//   dir: beta = rr/rr_prev; p_new = r + beta p_old (recomputed at the gathered columns, so no
+//        separate direction pass); q = A^ p_new; partial <p_new, q>
+//   upd: alpha = rr/<p,q>; y += alpha p; r -= alpha q; partial <r, r>
+// scal layout (doubles): [0..NR) rr_prev slot 0, [4..4+NR) rr_prev slot 1, [8..8+NR) bb, [12..12+NR) rr_cur
+// ctl layout (ints):    [0] 0 running / 1 converged / 2 maxit, [1] iterations
+template <int NR>
+struct CgVecs {
+  double* y[NR];
+  double* r[NR];
+  double* po[NR];
+  double* pn[NR];
+  double* q[NR];
+  const double* b[NR];
+};
+
+template <int NR>
+__global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
+                                                int64_t n_ghost, double* part_rr, double* part_bb) {
+  __shared__ double sh[4];
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double rr[NR], bb[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double acc[NR];
+#pragma unroll
+    for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double a = val[e];
+      const int32_t j = A.col[e];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
+    }
+    if (row < A.nrows) {
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        const double b = v.b[c][row];
+        const double r = b - acc[c];
+        v.r[c][row] = r;
+        v.po[c][row] = 0.0;
+        rr[c] += r * r;
+        bb[c] += b * b;
+      }
+    }
+  }
+  // zero the ghost part of p_old (ghost r arrives by halo exchange)
+  for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
+       g += (int64_t)gridDim.x * BS) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) v.po[c][g] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t = block_sum(rr[c], sh);
+    const double u = block_sum(bb[c], sh);
+    if (threadIdx.x == 0) {
+      part_rr[c * MAXB + blockIdx.x] = t;
+      part_bb[c * MAXB + blockIdx.x] = u;
+    }
+  }
+}
+
+template <int NR>
+__global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
+                                               int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
+                                               const double* part_bb, int nb_bb, int stride_bb, double* scal,
+                                               int* ctl, int it, int maxit, double tol2, double* part_pq) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  double rr[NR], bb[NR], beta[NR];
+  bool conv = true, bad = false;
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    rr[c] = reduce_partials(part_rr + c * stride_rr, nb_rr, sh);
+    bb[c] = it == 0 ? reduce_partials(part_bb + c * stride_bb, nb_bb, sh) : scal[8 + c];
+    conv = conv && (rr[c] <= tol2 * bb[c]);
+    bad = bad || !isfinite(rr[c]);
+  }
+  if (conv || bad || it >= maxit) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      ctl[0] = conv ? 1 : (bad ? 3 : 2);
+      ctl[1] = it;
+    }
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) beta[c] = it == 0 ? 0.0 : rr[c] / scal[(it & 1) * 4 + c];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      scal[((it + 1) & 1) * 4 + c] = rr[c];
+      scal[12 + c] = rr[c];
+      if (it == 0) scal[8 + c] = bb[c];
+    }
+  }
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double pq[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) pq[c] = 0.0;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double acc[NR];
+#pragma unroll
+    for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double a = val[e];
+      const int32_t j = A.col[e];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * v.po[c][j]);
+    }
+    if (row < A.nrows) {
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        const double p = v.r[c][row] + beta[c] * v.po[c][row];
+        v.pn[c][row] = p;
+        v.q[c][row] = acc[c];
+        pq[c] += p * acc[c];
+      }
+    }
+  }
+  for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
+       g += (int64_t)gridDim.x * BS) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) v.pn[c][g] = v.r[c][g] + beta[c] * v.po[c][g];
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t = block_sum(pq[c], sh);
+    if (threadIdx.x == 0) part_pq[c * MAXB + blockIdx.x] = t;
+  }
+}
+
+template <int NR>
+__global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, const double* part_pq, int nb_pq,
+                                               int stride_pq, const double* scal, const int* ctl, double* part_rr) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  double alpha[NR], rr[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double pq = reduce_partials(part_pq + c * stride_pq, nb_pq, sh);
+    alpha[c] = scal[12 + c] / pq;
+    rr[c] = 0.0;
+  }
+  int64_t r0, r1;
+  block_rows(nrows, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      v.y[c][i] += alpha[c] * v.pn[c][i];
+      const double r = v.r[c][i] - alpha[c] * v.q[c][i];
+      v.r[c][i] = r;
+      rr[c] += r * r;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t = block_sum(rr[c], sh);
+    if (threadIdx.x == 0) part_rr[c * MAXB + blockIdx.x] = t;
+  }
+}
+
+// x = S y; slaves (master_of >= 0) take their master's value (p_s = p_m).
+__global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const double* y0, const double* y1,
+                         double* x0, double* x1, const int32_t* __restrict__ master_of) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    int64_t j = i;
+    if (master_of && master_of[i] >= 0) j = master_of[i];
+    x0[i] = s[j] * y0[j];
+    if (nr > 1) x1[i] = s[j] * y1[j];
+  }
+}
+
+// viscous preparation: b^ = S u (rhs), y0 = S^-1 u (warm start x0 = u^n), StokesColor.py:540-545
+__global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
+                            const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
+    bx[i] = s[i] * a;
+    by[i] = s[i] * b;
+    yx[i] = sq[i] * a;
+    yy[i] = sq[i] * b;
+  }
+}
+
+// ----------------------------------------------------------------------------- div / grad
+// calculate_divergence (StokesColor.py:130-165) in operator form: div = (Gx ux + Gy uy) / (area_sum + 1e-12).
+// Optionally the pressure RHS of the row-scaled system: braw = (M + 1e-12) * (-(1/DT) * div)
+// (StokesColor.py:554 with A_pressure = K / (M + 1e-12)).  Partials: [0] max|div|, [1] sum(braw).
+__global__ __launch_bounds__(BS) void k_div(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
+                                            const double* __restrict__ ux, const double* __restrict__ uy,
+                                            const double* __restrict__ as1, double* __restrict__ div,
+                                            const double* __restrict__ mp, double negidt, double* __restrict__ braw,
+                                            double* part) {
+  __shared__ double sh[4];
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double mx = 0.0, sb = 0.0;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double acc = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const int32_t j = A.col[e];
+      acc += gx[e] * ux[j] + gy[e] * uy[j];
+    }
+    if (row < A.nrows) {
+      const double d = acc / as1[row];
+      div[row] = d;
+      mx = fmax(mx, fabs(d));
+      if (braw) {
+        const double b = mp[row] * (negidt * d);
+        braw[row] = b;
+        sb += b;
+      }
+    }
+  }
+  const double t = block_max(mx, sh);
+  const double u = block_sum(sb, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = t;
+    part[MAXB + blockIdx.x] = u;
+  }
+}
+
+// pressure RHS of the merged, range-projected, scaled system (oracle PressureSolver.rhs):
+// b^_i = s_i * (b~_i - mean), b~_m = braw_m + braw_s, b~_s = 0.
+__global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int32_t* __restrict__ slave_of,
+                           const int32_t* __restrict__ master_of, const double* __restrict__ s,
+                           const double* part_sum, int nb, double inv_nfree, double* __restrict__ bh) {
+  __shared__ double sh[4];
+  const double mean = reduce_partials(part_sum, nb, sh) * inv_nfree;
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    double b;
+    if (master_of[i] >= 0) {
+      b = 0.0;
+    } else {
+      b = braw[i];
+      if (slave_of[i] >= 0) b += braw[slave_of[i]];
+      b = s[i] * (b - mean);
+    }
+    bh[i] = b;
+  }
+}
+
+// projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
+// projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
+__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __restrict__ gx,
+                                                  const double* __restrict__ gy, const double* __restrict__ p,
+                                                  const double* __restrict__ as1, double dt, int mode,
+                                                  const uint8_t* __restrict__ dirflag, const double* usx,
+                                                  const double* usy, double* ux, double* uy) {
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double ax = 0.0, ay = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double pj = p[A.col[e]];
+      ax += gx[e] * pj;
+      ay += gy[e] * pj;
+    }
+    if (row < A.nrows) {
+      const double d = as1[row];
+      const double gpx = ax / d, gpy = ay / d;
+      if (mode == 0) {
+        ux[row] = usx[row] - dt * gpx;
+        uy[row] = usy[row] - dt * gpy;
+      } else if (!dirflag[row]) {
+        ux[row] = ux[row] - dt * gpx;
+        uy[row] = uy[row] - dt * gpy;
+      }
+    }
+  }
+}
+
+// gradient only (calculate_gradiant, StokesColor.py:224-263) for the unit op
+__global__ __launch_bounds__(BS) void k_grad(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
+                                             const double* __restrict__ p, const double* __restrict__ as1,
+                                             double* outx, double* outy) {
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double ax = 0.0, ay = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double pj = p[A.col[e]];
+      ax += gx[e] * pj;
+      ay += gy[e] * pj;
+    }
+    if (row < A.nrows) {
+      outx[row] = ax / as1[row];
+      outy[row] = ay / as1[row];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- boundary conditions
+// makePerBCU then makeDirBCU (StokesColor.py:405-431) / reapply_periodic_u + reapply_dirchlect_u
+// (heatEq.py:282-301).  One block: copies are two-phase (gather all sources, then write), which
+// realises the host-resolved sequential semantics; Dirichlet values are written after.
+__global__ __launch_bounds__(1024) void k_bc(int ncopy, const int32_t* __restrict__ cdst, const int32_t* __restrict__ csrc,
+                                             double* tmp, int ndir, const int32_t* __restrict__ dnode,
+                                             const double* __restrict__ dval, int ncomp, double* u0, double* u1) {
+  for (int k = threadIdx.x; k < ncopy; k += blockDim.x) {
+    tmp[2 * k] = u0[csrc[k]];
+    if (ncomp > 1) tmp[2 * k + 1] = u1[csrc[k]];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ncopy; k += blockDim.x) {
+    u0[cdst[k]] = tmp[2 * k];
+    if (ncomp > 1) u1[cdst[k]] = tmp[2 * k + 1];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ndir; k += blockDim.x) {
+    u0[dnode[k]] = dval[ncomp * k];
+    if (ncomp > 1) u1[dnode[k]] = dval[ncomp * k + 1];
+  }
+}
+
+// ----------------------------------------------------------------------------- semi-Lagrangian
+struct MeshDev {
+  const double* x;      // full mesh, internal numbering
+  const double* y;
+  const int32_t* tri;   // T*3 internal node ids, reference triangle order
+  int64_t T;
+};
+struct GridDev {
+  int32_t nx, ny;
+  double x0, y0, hx, hy;
+  const int32_t* start;
+  const int32_t* item;
+  const double* px;
+  const double* py;
+};
+
+__device__ __forceinline__ int32_t gcell(double v, double v0, double hv, int32_t n) {
+  const double f = floor((v - v0) / hv);
+  if (!(f >= 0.0)) return 0;
+  if (f >= (double)n) return n - 1;
+  return (int32_t)f;
+}
+__device__ __forceinline__ bool knn_less(double d, int32_t i, double bd, int32_t bi) {
+  return d < bd || (d == bd && i < bi);
+}
+
+// k nearest centroids of (qx, qy), sorted by (squared distance, triangle id)
+__device__ __forceinline__ void knn10(const GridDev& G, double qx, double qy, double (&bd)[KNN], int32_t (&bi)[KNN]) {
+#pragma unroll
+  for (int p = 0; p < KNN; ++p) {
+    bd[p] = INFINITY;
+    bi[p] = 0x7fffffff;
+  }
+  const int32_t cx = gcell(qx, G.x0, G.hx, G.nx), cy = gcell(qy, G.y0, G.hy, G.ny);
+  const int32_t rmax = max(max(cx, G.nx - 1 - cx), max(cy, G.ny - 1 - cy));
+  for (int32_t r = 0; r <= rmax; ++r) {
+    const int32_t jlo = max(cy - r, 0), jhi = min(cy + r, G.ny - 1);
+    for (int32_t j = jlo; j <= jhi; ++j) {
+      const bool edge_row = (j == cy - r) || (j == cy + r);
+      const int32_t step = edge_row ? 1 : 2 * r;
+      for (int32_t i = cx - r; i <= cx + r; i += (step > 0 ? step : 1)) {
+        if (i < 0 || i >= G.nx) continue;
+        const int64_t c = (int64_t)j * G.nx + i;
+        for (int32_t e = G.start[c]; e < G.start[c + 1]; ++e) {
+          const double dx = G.px[e] - qx, dy = G.py[e] - qy;
+          const double d = dx * dx + dy * dy;
+          const int32_t id = G.item[e];
+          if (!knn_less(d, id, bd[KNN - 1], bi[KNN - 1])) continue;
+          bool placed = false;
+#pragma unroll
+          for (int p = KNN - 1; p > 0; --p) {
+            if (!placed) {
+              if (knn_less(d, id, bd[p - 1], bi[p - 1])) {
+                bd[p] = bd[p - 1];
+                bi[p] = bi[p - 1];
+              } else {
+                bd[p] = d;
+                bi[p] = id;
+                placed = true;
+              }
+            }
+          }
+          if (!placed) {
+            bd[0] = d;
+            bi[0] = id;
+          }
+        }
+        if (step == 0) break;
+      }
+    }
+    // distance from the query to the nearest cell NOT yet visited
+    double dmin = INFINITY;
+    if (cx - r > 0) dmin = fmin(dmin, qx - (G.x0 + (double)(cx - r) * G.hx));
+    if (cx + r < G.nx - 1) dmin = fmin(dmin, (G.x0 + (double)(cx + r + 1) * G.hx) - qx);
+    if (cy - r > 0) dmin = fmin(dmin, qy - (G.y0 + (double)(cy - r) * G.hy));
+    if (cy + r < G.ny - 1) dmin = fmin(dmin, (G.y0 + (double)(cy + r + 1) * G.hy) - qy);
+    if (dmin == INFINITY) break;
+    if (dmin > 0.0 && bd[KNN - 1] < dmin * dmin * (1.0 - 1e-9)) break;
+  }
+}
+
+__device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:353-357
+  double d = a - b;
+  if (d > 0.5) d -= 1.0;
+  if (d < -0.5) d += 1.0;
+  return d;
+}
+
+// advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
+// nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
+// Partials: [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
+__global__ __launch_bounds__(BS) void k_sl(MeshDev M, GridDev G, int64_t row0, int64_t n, const double* __restrict__ ux,
+                                           const double* __restrict__ uy, double dt, const double* __restrict__ c,
+                                           double* __restrict__ cout, const double* __restrict__ wmix,
+                                           int32_t* notfound, double* part) {
+  __shared__ double sh[4];
+  double swc = 0.0, sw = 0.0, nnf = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    const int64_t g = row0 + i;
+    const double xg = M.x[g], yg = M.y[g];
+    double xb = py_mod(xg - dt * ux[i] * 1.0, 1.0);
+    double yb = yg - dt * uy[i] * 1.0;
+    if (yb < 0.0) yb = 1e-12;
+    if (yb > 1.0) yb = 1.0 - 1e-12;
+    double bd[KNN];
+    int32_t bi[KNN];
+    knn10(G, xb, yb, bd, bi);
+    int32_t found = -1;
+#pragma unroll
+    for (int p = 0; p < KNN; ++p) {
+      if (found < 0 && bi[p] != 0x7fffffff) {
+        const int32_t t = bi[p];
+        const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], k = M.tri[3 * t + 2];
+        const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[k], y3 = M.y[k];
+        const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
+        if (fabs(det) >= 1e-14) {
+          const double w1 = ((x2 - xb) * (y3 - yb) - (x3 - xb) * (y2 - yb)) / det;
+          const double w2 = ((x3 - xb) * (y1 - yb) - (x1 - xb) * (y3 - yb)) / det;
+          const double w3 = 1.0 - w1 - w2;
+          if (w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0) found = t;
+        }
+      }
+    }
+    double cn;
+    if (found < 0) {
+      cn = c[g];
+      nnf += 1.0;
+    } else {
+      const int32_t a = M.tri[3 * found], b = M.tri[3 * found + 1], k = M.tri[3 * found + 2];
+      const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[k], y3 = M.y[k];
+      const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
+      const double w1 = (pdx(x2, xb) * (y3 - yb) - pdx(x3, xb) * (y2 - yb)) / det;
+      const double w2 = (pdx(x3, xb) * (y1 - yb) - pdx(x1, xb) * (y3 - yb)) / det;
+      const double w3 = 1.0 - w1 - w2;
+      cn = w1 * c[a] + w2 * c[b] + w3 * c[k];
+    }
+    cout[g] = cn;
+    if (notfound) notfound[i] = found < 0 ? 1 : 0;
+    const double w = wmix ? wmix[i] : 0.0;
+    swc += w * cn;
+    sw += w;
+  }
+  const double a = block_sum(swc, sh), b = block_sum(sw, sh), d = block_sum(nnf, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = a;
+    part[MAXB + blockIdx.x] = b;
+    part[2 * MAXB + blockIdx.x] = d;
+  }
+}
+
+// mixing_index second pass (StokesColor.py:399-401): partial sum w (c - mu)^2, mu from pass 1.
+__global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const double* __restrict__ c,
+                                             const double* __restrict__ wmix, const double* part1, int nb1,
+                                             int stride1, double* part) {
+  __shared__ double sh[4];
+  const double swc = reduce_partials(part1, nb1, sh);
+  const double sw = reduce_partials(part1 + stride1, nb1, sh);
+  const double mu = swc / sw;
+  double acc = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    const double d = c[row0 + i] - mu;
+    acc += wmix[i] * (d * d);
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+// ----------------------------------------------------------------------------- tracers
+// StokesFood.py:482-499: LinearTriInterpolator (matplotlib plane coefficients, NaN outside the
+// mesh), forward Euler, x mod 1, sticky capture.  One thread per tracer; full-mesh u replica.
+__global__ void k_tracer(MeshDev M, GridDev G, const double* __restrict__ ux, const double* __restrict__ uy,
+                         int32_t ntr, double* tx, double* ty, double* status, double dt, double cx, double cy,
+                         double capture, double* eaten_out) {
+  __shared__ double sh[4];
+  double eaten = 0.0;
+  for (int32_t k = threadIdx.x; k < ntr; k += blockDim.x) {
+    const double px = tx[k], py = ty[k];
+    double vx = NAN, vy = NAN;
+    if (isfinite(px) && isfinite(py)) {
+      const int32_t ci = gcell(px, G.x0, G.hx, G.nx), cj = gcell(py, G.y0, G.hy, G.ny);
+      const bool inside = px >= G.x0 && px <= G.x0 + G.nx * G.hx && py >= G.y0 && py <= G.y0 + G.ny * G.hy;
+      const int64_t c = (int64_t)cj * G.nx + ci;
+      int32_t found = -1;
+      if (inside) {
+        for (int32_t e = G.start[c]; e < G.start[c + 1] && found < 0; ++e) {
+          const int32_t t = G.item[e];
+          const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
+          const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[d], y3 = M.y[d];
+          const double o1 = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
+          const double o2 = (x3 - x2) * (py - y2) - (y3 - y2) * (px - x2);
+          const double o3 = (x1 - x3) * (py - y3) - (y1 - y3) * (px - x3);
+          if (o1 >= 0.0 && o2 >= 0.0 && o3 >= 0.0) found = t;
+        }
+      }
+      if (found >= 0) {
+        const int32_t a = M.tri[3 * found], b = M.tri[3 * found + 1], d = M.tri[3 * found + 2];
+        const double x0 = M.x[a], y0 = M.y[a];
+        const double s1x = M.x[b] - x0, s1y = M.y[b] - y0, s2x = M.x[d] - x0, s2y = M.y[d] - y0;
+        const double nz = s1x * s2y - s1y * s2x;
+        double zv[2];
+        const double* uu[2] = {ux, uy};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // Triangulation::calculate_plane_coefficients
+          const double z0 = uu[q][a];
+          const double s1z = uu[q][b] - z0, s2z = uu[q][d] - z0;
+          const double nx = s1y * s2z - s1z * s2y;
+          const double ny = s1z * s2x - s1x * s2z;
+          const double pa = -nx / nz, pb = -ny / nz;
+          const double pc = (nx * x0 + ny * y0 + nz * z0) / nz;
+          zv[q] = pa * px + pb * py + pc;
+        }
+        vx = zv[0];
+        vy = zv[1];
+      }
+    }
+    double nx_ = px + vx * dt, ny_ = py + vy * dt;
+    nx_ = py_mod(nx_, 1.0);
+    tx[k] = nx_;
+    ty[k] = ny_;
+    const double ddx = nx_ - cx, ddy = ny_ - cy;
+    const double dist = sqrt(ddx * ddx + ddy * ddy);
+    if (dist <= capture) status[k] = 1.0;
+    eaten += status[k];
+  }
+  const double t = block_sum(eaten, sh);
+  if (threadIdx.x == 0) *eaten_out = t;
+}
+
+// ----------------------------------------------------------------------------- misc
+// 1-block reduction of nv partial arrays (sum or max) into out[0..nv) (multi-GPU pre-allreduce, stats)
+__global__ __launch_bounds__(BS) void k_reduce(const double* part, int nb, int stride, int nv, int is_max, double* out) {
+  __shared__ double sh[4];
+  for (int v = 0; v < nv; ++v) {
+    const double t = is_max ? reduce_partials_max(part + v * stride, nb, sh) : reduce_partials(part + v * stride, nb, sh);
+    if (threadIdx.x == 0) out[v] = t;
+  }
+}
+
+__global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ a,
+                       const double* __restrict__ b, double* __restrict__ out) {
+  for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < n; k += (int64_t)gridDim.x * BS) {
+    out[k] = a[idx[k]];
+    if (b) out[n + k] = b[idx[k]];
+  }
+}
+
+// per-step diagnostics -> stats record.
+// vals: [0] max|div*| [1] max|final div| [2] sum w c [3] sum w [4] not-found [5] sum w (c-mu)^2 [6] eaten
+// out : [0] max|div*| [1] max|final div| [2] I [3] mu [4] var [5] eaten [6] not-found
+__global__ void k_stats(const double* vals, double* out) {
+  if (threadIdx.x == 0) {
+    const double W = vals[3];
+    const double mu = vals[2] / W, var = vals[5] / W;
+    out[0] = vals[0];
+    out[1] = vals[1];
+    out[2] = var / (mu * (1 - mu) + 1e-16);  // StokesColor.py:402
+    out[3] = mu;
+    out[4] = var;
+    out[5] = vals[6];
+    out[6] = vals[4];
+  }
+}
+
+// ----------------------------------------------------------------------------- BiCGStab pieces (literal operators)
+__global__ __launch_bounds__(BS) void k_dot2(int64_t n, const double* a, const double* b, const double* c,
+                                             const double* d, double* part) {
+  __shared__ double sh[4];
+  double s1 = 0.0, s2 = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    s1 += a[i] * b[i];
+    if (c) s2 += c[i] * d[i];
+  }
+  const double t1 = block_sum(s1, sh), t2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = t1;
+    part[MAXB + blockIdx.x] = t2;
+  }
+}
+// generic: z = a*x + b*y + c*w with coefficients read from device scalars (sign flags on the host)
+__global__ void k_axpbypcz(int64_t n, const double* ca, const double* x, const double* cb, const double* y,
+                           const double* cc, const double* w, double sa, double sb, double sc, double* z) {
+  const double a = sa * (ca ? *ca : 1.0), b = sb * (cb ? *cb : 1.0), c = sc * (cc ? *cc : 1.0);
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    double v = a * x[i];
+    if (y) v += b * y[i];
+    if (w) v += c * w[i];
+    z[i] = v;
+  }
+}
+__global__ void k_mul(int64_t n, const double* a, const double* b, double* z) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) z[i] = a[i] * b[i];
+}
+// scalar bookkeeping of BiCGStab; sc layout: [0] rho_old [1] alpha [2] omega [3] beta [4] rho [5] rr [6] tmp
+__global__ __launch_bounds__(BS) void k_bicg_scalar(int stage, const double* part, int nb, double* sc) {
+  __shared__ double sh[4];
+  const double d1 = reduce_partials(part, nb, sh);
+  const double d2 = reduce_partials(part + MAXB, nb, sh);
+  if (threadIdx.x != 0) return;
+  if (stage == 0) {  // d1 = <r^, r>, d2 = <r, r>
+    sc[3] = (d1 / sc[0]) * (sc[1] / sc[2]);
+    sc[4] = d1;
+    sc[5] = d2;
+  } else if (stage == 1) {  // d1 = <r^, v>
+    sc[1] = sc[4] / d1;
+  } else if (stage == 2) {  // d1 = <t, s>, d2 = <t, t>
+    sc[2] = d1 / d2;
+    sc[0] = sc[4];
+  } else if (stage == 3) {  // d2 = <r, r>
+    sc[5] = d2;
+  }
+}
+
+
+// p = r + beta (p - omega v); ph = Dinv p
+__global__ void k_bicg_p(int64_t n, const double* r, double* p, const double* v, const double* dinv, double* ph,
+                         const double* sc) {
+  const double beta = sc[3], omega = sc[2];
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    const double pv = r[i] + beta * (p[i] - omega * v[i]);
+    p[i] = pv;
+    ph[i] = dinv[i] * pv;
+  }
+}
+// s = r - alpha v; sh = Dinv s
+__global__ void k_bicg_s(int64_t n, const double* r, const double* v, const double* dinv, double* s, double* sh,
+                         const double* sc) {
+  const double alpha = sc[1];
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    const double sv = r[i] - alpha * v[i];
+    s[i] = sv;
+    sh[i] = dinv[i] * sv;
+  }
+}
+// x += alpha ph + omega sh; r = s - omega t
+__global__ void k_bicg_x(int64_t n, double* x, const double* ph, const double* sh, const double* s,
+                         const double* t, double* r, const double* sc) {
+  const double alpha = sc[1], omega = sc[2];
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    x[i] = x[i] + alpha * ph[i] + omega * sh[i];
+    r[i] = s[i] - omega * t[i];
+  }
+}
+
+}  // namespace dev
+}  // namespace pucfem

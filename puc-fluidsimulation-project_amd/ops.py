@@ -1,0 +1,132 @@
+"""Reference-named entry points (StokesColor.py / poisson.py function names and signatures).
+
+The hot-path functions (calculate_divergence, calculate_gradiant, advect_semilagrange, the two
+np.linalg.solve call sites) run on the GPU through a context cached per mesh.  The assembly
+functions return the C++ host-assembled operator (dense for small meshes, as the reference's
+np.zeros((N, N)) matrices; scipy CSR above DENSE_MAX nodes).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .mesh import Mesh, boundary_sets
+from .solver import Context, SquirmerBC, Tolerances, stokes_setup
+
+DENSE_MAX = 8192
+_cache: dict = {}
+
+
+def _key(nodes, triangles):
+    n = np.ascontiguousarray(nodes, dtype=np.float64)
+    t = np.ascontiguousarray(triangles, dtype=np.int32)
+    return (n.shape, t.shape, hash(n.tobytes()), hash(t.tobytes())), n, t
+
+
+def context_for(nodes, triangles, dt=0.05, nu=0.1, bc: SquirmerBC | None = None, device=0):
+    """A single-GPU Stokes context for this mesh (cached by content)."""
+    (k, n, t) = _key(nodes, triangles)
+    k = k + (dt, nu, None if bc is None else (bc.B1, bc.B2))
+    ctx = _cache.get(k)
+    if ctx is None:
+        mesh = Mesh(n, np.zeros(len(n), dtype=np.int32), t)
+        ctx = Context(device)
+        ctx.upload(mesh)
+        ctx.build("color", dt, nu, Tolerances())
+        _cache[k] = ctx
+    return ctx
+
+
+def _stokes_context(mesh: Mesh, dt, nu, bc: SquirmerBC, device=0):
+    k = ("stokes", mesh.N, mesh.T, hash(mesh.coords.tobytes()), hash(mesh.triangles.tobytes()), dt, nu, bc.B1, bc.B2)
+    ctx = _cache.get(k)
+    if ctx is None:
+        ctx = Context(device)
+        ctx.upload(mesh)
+        pairs, nodes, vals = stokes_setup(mesh, bc)
+        ctx.set_pairs(0, pairs)
+        ctx.set_pairs(1, pairs)
+        ctx.set_dirichlet(nodes, vals)
+        ctx.build("color", dt, nu, Tolerances())
+        _cache[k] = ctx
+    return ctx
+
+
+def calculate_divergence(nodes, triangles, u_star):
+    """StokesColor.py:130-165 on the GPU: (N,) lumped nodal divergence."""
+    ctx = context_for(nodes, triangles)
+    return ctx.apply(_lib.OP_DIV, np.asarray(u_star, dtype=np.float64).reshape(-1, 2), (len(nodes),))
+
+
+def calculate_gradiant(nodes, triangles, p_scalar):
+    """StokesColor.py:224-263 on the GPU: (grad_px, grad_py)."""
+    ctx = context_for(nodes, triangles)
+    g = ctx.apply(_lib.OP_GRAD, np.asarray(p_scalar, dtype=np.float64), (len(nodes), 2))
+    return g[:, 0].copy(), g[:, 1].copy()
+
+
+def advect_semilagrange(c, u, DT, nodes, triangles):
+    """StokesColor.py:347-389 on the GPU, in place on c like the reference (c[:] = c_new).
+    Returns the not-found mask (nodes that kept c[n])."""
+    import ctypes as ct
+
+    ctx = context_for(nodes, triangles)
+    cin = np.ascontiguousarray(c, dtype=np.float64)
+    uu = np.ascontiguousarray(u, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros_like(cin)
+    nf = np.zeros(len(cin), dtype=np.int32)
+    _lib.check(ctx.L.pucfem_sl_advect(ctx.h, _lib.dptr(cin), _lib.dptr(uu), float(DT), _lib.dptr(out),
+                                      _lib.iptr(nf)), ctx.h)
+    c[:] = out
+    return nf.astype(bool)
+
+
+def buildStiffnessMatrix(nodes, triangles, g_source=1.0):
+    """StokesColor.py:98-128: (A, -B) with B = 0 (the reference never fills it)."""
+    ctx = context_for(nodes, triangles)
+    A = ctx.host_csr(_lib.OP_K)
+    return (A.toarray() if len(nodes) <= DENSE_MAX else A), np.zeros(len(nodes))
+
+
+def buildLumpedMassMatrix(nodes_coords, triangles):
+    """StokesColor.py:266-284 (host setup): M_i = sum of area/3 over incident triangles."""
+    X = np.asarray(nodes_coords, dtype=np.float64)
+    T = np.asarray(triangles)
+    x1, y1, x2, y2, x3, y3 = X[T[:, 0], 0], X[T[:, 0], 1], X[T[:, 1], 0], X[T[:, 1], 1], X[T[:, 2], 0], X[T[:, 2], 1]
+    det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2)
+    M = np.zeros(len(X))
+    np.add.at(M, T.ravel(), np.repeat(0.5 * np.abs(det) / 3.0, 3))
+    return M
+
+
+def mixing_index_host(mesh: Mesh, c):
+    """mixing_index (StokesColor.py:391-403) of a host field over marker==0 nodes: used once for
+    the initial (I0, mu0, var0) normaliser of the printed progress (StokesColor.py:497)."""
+    M = buildLumpedMassMatrix(mesh.coords, mesh.triangles)
+    mask = np.where(mesh.markers == 0)[0]
+    cc, mm = c[mask], M[mask]
+    W = mm.sum()
+    mu = (mm @ cc) / W
+    var = (mm @ (cc - mu) ** 2) / W
+    return var / (mu * (1 - mu) + 1e-16), mu, var
+
+
+def solve_viscous(mesh: Mesh, rhs, dt=0.05, nu=0.1, bc: SquirmerBC | None = None, rtol=1e-13):
+    """The np.linalg.solve(A_visc, rhs) call sites (StokesColor.py:544-545) for both components."""
+    ctx = _stokes_context(mesh, dt, nu, bc or SquirmerBC(nu=nu))
+    x, it = ctx.solve(_lib.OP_VISC, np.asarray(rhs, dtype=np.float64).reshape(-1, 2), rtol=rtol)
+    return x
+
+
+def solve_pressure(mesh: Mesh, b_p, dt=0.05, nu=0.1, bc: SquirmerBC | None = None, rtol=1e-12):
+    """The np.linalg.solve(A_pressure, b_p) call sites (StokesColor.py:555, :569), restated as the
+    well-posed periodic-merged system; returns the zero-mean pressure."""
+    ctx = _stokes_context(mesh, dt, nu, bc or SquirmerBC(nu=nu))
+    x, it = ctx.solve(_lib.OP_PRES, np.asarray(b_p, dtype=np.float64), rtol=rtol)
+    return x
+
+
+def clear_cache():
+    for c in _cache.values():
+        c.close()
+    _cache.clear()

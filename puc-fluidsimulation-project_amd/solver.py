@@ -1,0 +1,408 @@
+"""Python host over the libpucfem C ABI: contexts, the reference's step loops, solve().
+
+The reference scripts are module-level programs (StokesColor.py:436-602, StokesFood.py:356-541,
+heatEq.py:218-335, poisson.py:218-296).  This module performs the same setup (pairs, Dirichlet
+sets, squirmer boundary values, Poisson load) on the host with the reference's numpy semantics and
+hands the hot path -- assembly, every solve, div/grad, BCs, advection, tracers -- to the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .mesh import Mesh, boundary_sets, filter_wall_pairs, find_boundary_pairs, INNER_BOUNDARY_MARKER
+
+SCHEMES = {"color": _lib.STOKES_COLOR, "food": _lib.STOKES_FOOD, "heat": _lib.HEAT, "poisson": _lib.POISSON}
+
+
+@dataclass
+class SquirmerBC:
+    """Squirmer boundary condition and physics of the Stokes scripts.
+
+    Defaults are StokesColor.py:28-44 (B1=-2, B2=0, v=0.1); StokesFood.py uses v=1.0, DT=0.01
+    and B2 in {0, -5, +5} (neutral / pusher / puller, README.md:43-45)."""
+
+    B1: float = -2.0
+    B2: float = 0.0
+    nu: float = 0.1
+    center: tuple = (0.5, 0.5)
+    outer_value: tuple = (0.0, 0.0)
+    capture_radius: float = 0.28  # SQUIRMER_RADIUS + 0.03 (StokesFood.py:50-51)
+    squirmer_radius: float = 0.25
+
+
+def squirmer_values(coords, inner, B1, B2, center=(0.5, 0.5)):
+    """makeDirBCU inner-body values (StokesColor.py:410-427), evaluated with numpy as the
+    reference does (np.arctan2 / np.sin / np.cos, float64)."""
+    X = np.asarray(coords, dtype=np.float64)
+    rx = X[inner, 0] - center[0]
+    ry = X[inner, 1] - center[1]
+    th = np.arctan2(ry, rx)
+    vt = B1 * np.sin(th) + B2 * np.sin(2 * th)
+    return np.stack([vt * -np.sin(th), vt * np.cos(th)], 1)
+
+
+@dataclass
+class Tolerances:
+    rtol_visc: float = 1e-13
+    rtol_pres: float = 1e-12
+    rtol_lin: float = 1e-14
+    maxit_visc: int = 500
+    maxit_pres: int = 200000
+    maxit_lin: int = 20000
+    warm_start: bool = True
+
+
+class Context:
+    """One libpucfem context (one GPU, or host-only with device=-1)."""
+
+    def __init__(self, device=0, dist=None):
+        L = _lib.lib()
+        p = ct.c_void_p()
+        if dist is None:
+            _lib.check(L.pucfem_ctx_create(int(device), ct.byref(p)))
+        else:
+            rank, world, uid = dist
+            buf = (ct.c_uint8 * 128).from_buffer_copy(bytes(uid))
+            _lib.check(L.pucfem_ctx_create_dist(int(device), int(rank), int(world), buf, ct.byref(p)))
+        self.h = p
+        self.L = L
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.L.pucfem_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _c(self, rc):
+        _lib.check(rc, self.h)
+
+    # ---------------------------------------------------------------- setup
+    def upload(self, mesh: Mesh, coord_fp32=False):
+        X = np.ascontiguousarray(mesh.coords, dtype=np.float64)
+        mk = np.ascontiguousarray(mesh.markers, dtype=np.int32)
+        T = np.ascontiguousarray(mesh.triangles, dtype=np.int32)
+        self._c(self.L.pucfem_mesh_upload(self.h, X.shape[0], _lib.dptr(X), _lib.iptr(mk), T.shape[0],
+                                          _lib.iptr(T), int(coord_fp32)))
+        self.N = X.shape[0]
+        self.T = T.shape[0]
+
+    def set_pairs(self, kind, pairs):
+        P = np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 2))
+        self._c(self.L.pucfem_set_pairs(self.h, kind, P.shape[0], _lib.lptr(P)))
+
+    def set_dirichlet(self, nodes, values):
+        n = np.ascontiguousarray(nodes, dtype=np.int32)
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        ncomp = 1 if v.ndim == 1 else v.shape[1]
+        self._c(self.L.pucfem_set_dirichlet(self.h, len(n), _lib.iptr(n), _lib.dptr(v), ncomp))
+
+    def set_source(self, g_tri):
+        g = np.ascontiguousarray(g_tri, dtype=np.float32)
+        self._c(self.L.pucfem_set_source(self.h, len(g), _lib.fptr(g)))
+
+    def build(self, scheme, dt, nu=0.0, tol: Tolerances | None = None, capture=0.28, center=(0.5, 0.5), nstrips=0):
+        tol = tol or Tolerances()
+        p = _lib.Params(scheme=SCHEMES.get(scheme, scheme), nstrips=nstrips, dt=dt, nu=nu, rtol_visc=tol.rtol_visc,
+                        rtol_pres=tol.rtol_pres, rtol_lin=tol.rtol_lin, maxit_visc=tol.maxit_visc,
+                        maxit_pres=tol.maxit_pres, maxit_lin=tol.maxit_lin, warm_start=int(tol.warm_start),
+                        sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1])
+        self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
+
+    # ---------------------------------------------------------------- fields / steps
+    def set_field(self, f, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        self._c(self.L.pucfem_set_field(self.h, f, _lib.dptr(a), a.size))
+
+    def get_field(self, f, shape):
+        out = np.zeros(shape)
+        self._c(self.L.pucfem_get_field(self.h, f, _lib.dptr(out), out.size))
+        return out
+
+    def step(self, n=1):
+        st = (_lib.StepStats * max(n, 1))()
+        self._c(self.L.pucfem_step(self.h, n, st))
+        return [st[i] for i in range(n)]
+
+    def apply(self, op, x, out_shape):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros(out_shape)
+        self._c(self.L.pucfem_apply(self.h, op, _lib.dptr(x), _lib.dptr(y)))
+        return y
+
+    def solve(self, op, b, x0=None, rtol=1e-13, maxit=100000):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.zeros_like(b) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).copy()
+        it = ct.c_int32()
+        self._c(self.L.pucfem_solve(self.h, op, _lib.dptr(b), _lib.dptr(x), rtol, maxit, ct.byref(it)))
+        return x, it.value
+
+    def info(self):
+        o = (ct.c_int64 * 10)()
+        self._c(self.L.pucfem_info(self.h, o))
+        keys = ["N", "T", "nnz_P", "nnz_Pp", "n_own", "n_ghost", "sell_P", "sell_Pp", "n_pairs", "n_dirichlet"]
+        return dict(zip(keys, list(o)))
+
+    def timing(self, on):
+        self._c(self.L.pucfem_timing_enable(self.h, int(on)))
+
+    def timing_get(self, kclass):
+        ms, n, b = ct.c_double(), ct.c_int64(), ct.c_double()
+        self._c(self.L.pucfem_timing_get(self.h, kclass, ct.byref(ms), ct.byref(n), ct.byref(b)))
+        return ms.value, n.value, b.value
+
+    def sync(self):
+        self._c(self.L.pucfem_sync(self.h))
+
+    def host_csr(self, op):
+        """Host-assembled operator (this rank's rows, caller numbering) as scipy CSR (rows, N)."""
+        import scipy.sparse as sp
+
+        nr, nnz = ct.c_int64(), ct.c_int64()
+        self._c(self.L.pucfem_host_get_csr(self.h, op, ct.byref(nr), ct.byref(nnz), None, None, None))
+        rp = np.zeros(nr.value + 1, dtype=np.int64)
+        col = np.zeros(nnz.value, dtype=np.int64)
+        val = np.zeros(nnz.value)
+        self._c(self.L.pucfem_host_get_csr(self.h, op, ct.byref(nr), ct.byref(nnz), _lib.lptr(rp), _lib.lptr(col),
+                                           _lib.dptr(val)))
+        return sp.csr_matrix((val, col, rp), shape=(nr.value, self.N))
+
+    def host_partition(self, rank, world):
+        no, ng, ns = ct.c_int64(), ct.c_int64(), ct.c_int64()
+        self._c(self.L.pucfem_host_partition(self.h, rank, world, ct.byref(no), ct.byref(ng), None, None, None,
+                                             ct.byref(ns), None, None))
+        owned = np.zeros(no.value, dtype=np.int64)
+        ghosts = np.zeros(ng.value, dtype=np.int64)
+        gown = np.zeros(ng.value, dtype=np.int32)
+        sid = np.zeros(ns.value, dtype=np.int64)
+        speer = np.zeros(ns.value, dtype=np.int32)
+        self._c(self.L.pucfem_host_partition(self.h, rank, world, ct.byref(no), ct.byref(ng), _lib.lptr(owned),
+                                             _lib.lptr(ghosts), _lib.iptr(gown), ct.byref(ns), _lib.lptr(sid),
+                                             _lib.iptr(speer)))
+        return dict(owned=owned, ghosts=ghosts, ghost_owner=gown, send_ids=sid, send_peer=speer)
+
+
+# ------------------------------------------------------------------------------------------------
+def stokes_setup(mesh: Mesh, bc: SquirmerBC):
+    """Host-side setup of StokesColor.py:441-464: filtered periodic pairs, Dirichlet list and values."""
+    X = mesh.coords
+    pairs = filter_wall_pairs(X, find_boundary_pairs(X, L=1.0))
+    wall, inner, dirichlet, interior = boundary_sets(X, mesh.markers)
+    vals_inner = squirmer_values(X, inner, bc.B1, bc.B2, bc.center)
+    nodes = np.concatenate([wall, inner]).astype(np.int32)
+    vals = np.concatenate([np.tile(np.asarray(bc.outer_value, dtype=np.float64), (len(wall), 1)), vals_inner])
+    return pairs, nodes, vals
+
+
+class StokesSimulation:
+    """The StokesColor.py (scheme='color') / StokesFood.py (scheme='food') time loop on one GPU,
+    or on one rank of a torch.distributed job (dist=(rank, world, unique_id))."""
+
+    def __init__(self, mesh: Mesh, bc: SquirmerBC | None = None, dt=0.05, scheme="color", device=0,
+                 tol: Tolerances | None = None, dist=None, tracers=None, nstrips=0):
+        self.mesh = mesh
+        self.bc = bc or SquirmerBC()
+        self.dt = dt
+        self.scheme = scheme
+        self.ctx = Context(device, dist)
+        self.ctx.upload(mesh)
+        pairs, nodes, vals = stokes_setup(mesh, self.bc)
+        self.pairs = pairs
+        self.ctx.set_pairs(0, pairs)
+        self.ctx.set_pairs(1, pairs)
+        self.ctx.set_dirichlet(nodes, vals)
+        self.ctx.build(scheme, dt, self.bc.nu, tol, self.bc.capture_radius, self.bc.center, nstrips)
+        self.step_count = 0
+        self.history = []
+        if scheme == "food":
+            from .tracers import tracer_init
+
+            pts = tracer_init(self.bc.squirmer_radius, self.bc.center) if tracers is None else tracers
+            self.ctx.set_field(_lib.F_TRACERS, pts)
+
+    def step(self, n=1):
+        st = self.ctx.step(n)
+        self.step_count += n
+        self.history.extend(st)
+        return st
+
+    @property
+    def u(self):
+        return self.ctx.get_field(_lib.F_U, (self.mesh.N, 2))
+
+    @u.setter
+    def u(self, v):
+        self.ctx.set_field(_lib.F_U, v)
+
+    @property
+    def c(self):
+        return self.ctx.get_field(_lib.F_C, (self.mesh.N,))
+
+    @c.setter
+    def c(self, v):
+        self.ctx.set_field(_lib.F_C, v)
+
+    def field(self, f, ncomp=1):
+        return self.ctx.get_field(f, (self.mesh.N, ncomp) if ncomp > 1 else (self.mesh.N,))
+
+    @property
+    def tracers(self):
+        n = self._ntr()
+        return self.ctx.get_field(_lib.F_TRACERS, (n, 2))
+
+    @property
+    def tracer_status(self):
+        return self.ctx.get_field(_lib.F_STATUS, (self._ntr(),)).astype(np.int64)
+
+    def _ntr(self):
+        from .tracers import tracer_init
+
+        return len(tracer_init(self.bc.squirmer_radius, self.bc.center))
+
+    def close(self):
+        self.ctx.close()
+
+
+def _literal_setup(mesh32: Mesh):
+    """poisson.py:221-278 / heatEq.py:222-301 host setup on fp32 coordinates."""
+    X = mesh32.coords
+    assert X.dtype == np.float32, "poisson / heat read float32 coordinates (poisson.py:40)"
+    pairs_all = find_boundary_pairs(X, L=1.0)
+    op_pairs = filter_wall_pairs(X, pairs_all)
+    y = X[:, 1]
+    wall = (np.abs(y - np.float32(0.0)) < 1e-6) | (np.abs(y - np.float32(1.0)) < 1e-6)
+    inner = mesh32.markers == INNER_BOUNDARY_MARKER
+    nodes = np.where(wall | inner)[0].astype(np.int32)
+    vals = np.where(inner[nodes], 0.0, 1.0)  # INNER_BOUNDARY_VALUE 0.0, OUTER (wall) 1.0
+    return pairs_all, op_pairs, nodes, vals
+
+
+def g_source_default(x, y):
+    """poisson.py:235-236"""
+    return 50 * np.sin(3 * y)
+
+
+def poisson_load(mesh32: Mesh, g_source=g_source_default):
+    """g(centroid) per triangle in the coordinates' dtype (poisson.py:135-139)."""
+    X, T = mesh32.coords, mesh32.triangles
+    x = X[T, 0]
+    y = X[T, 1]
+    three = X.dtype.type(3)
+    return g_source((x[:, 0] + x[:, 1] + x[:, 2]) / three, (y[:, 0] + y[:, 1] + y[:, 2]) / three)
+
+
+def poisson_solve(mesh: Mesh, g_source=g_source_default, device=0, tol: Tolerances | None = None):
+    """poisson.py end to end on the GPU: fp32 assembly, literal periodic row merge and Dirichlet
+    rows, BiCGStab on the literal operator.  Returns f (N,)."""
+    m32 = mesh if mesh.coords.dtype == np.float32 else mesh.as_fp32()
+    pairs_all, op_pairs, nodes, vals = _literal_setup(m32)
+    ctx = Context(device)
+    ctx.upload(Mesh(m32.coords.astype(np.float64), m32.markers, m32.triangles), coord_fp32=True)
+    ctx.set_pairs(0, op_pairs)
+    ctx.set_pairs(1, pairs_all)
+    ctx.set_dirichlet(nodes, vals)
+    ctx.set_source(poisson_load(m32, g_source))
+    ctx.build("poisson", dt=0.0, tol=tol)
+    ctx.step(1)
+    f = ctx.get_field(_lib.F_SCALAR, (m32.N,))
+    ctx.close()
+    return f
+
+
+class HeatSimulation:
+    """heatEq.py: backward Euler (I + DT*A) u^{n+1} = u^n on the Poisson operator incl. BC rows,
+    then reapply_periodic_u (unfiltered pairs) and reapply_dirchlect_u."""
+
+    def __init__(self, mesh: Mesh, dt=0.02, device=0, tol: Tolerances | None = None):
+        m32 = mesh if mesh.coords.dtype == np.float32 else mesh.as_fp32()
+        self.mesh = m32
+        pairs_all, op_pairs, nodes, vals = _literal_setup(m32)
+        self.ctx = Context(device)
+        self.ctx.upload(Mesh(m32.coords.astype(np.float64), m32.markers, m32.triangles), coord_fp32=True)
+        self.ctx.set_pairs(0, op_pairs)
+        self.ctx.set_pairs(1, pairs_all)
+        self.ctx.set_dirichlet(nodes, vals)
+        self.ctx.set_source(poisson_load(m32))
+        self.ctx.build("heat", dt=dt, tol=tol)
+        # heatEq.py:308-310: u = 0; reapply periodic; reapply Dirichlet
+        u0 = np.zeros(m32.N)
+        for m, s in pairs_all:
+            u0[s] = u0[m]
+        u0[nodes] = vals
+        self.ctx.set_field(_lib.F_SCALAR, u0)
+
+    def step(self, n=1):
+        return self.ctx.step(n)
+
+    @property
+    def u(self):
+        return self.ctx.get_field(_lib.F_SCALAR, (self.mesh.N,))
+
+    def close(self):
+        self.ctx.close()
+
+
+@dataclass
+class Result:
+    scheme: str
+    steps: int
+    u: np.ndarray | None = None
+    c: np.ndarray | None = None
+    p: np.ndarray | None = None
+    tracers: np.ndarray | None = None
+    tracer_status: np.ndarray | None = None
+    scalar: np.ndarray | None = None
+    stats: list = field(default_factory=list)
+
+
+def solve(mesh: Mesh, bc: SquirmerBC | None = None, dt=None, steps=1, scheme="color", device=0,
+          tol: Tolerances | None = None, log=None):
+    """The north-star call surface: run `steps` steps of a reference script's loop on the GPU.
+
+    scheme 'color' = StokesColor.py, 'food' = StokesFood.py, 'heat' = heatEq.py (steps of
+    backward Euler), 'poisson' = poisson.py (one steady solve).  `log`, if given, receives the
+    reference's per-step print line (StokesColor.py:586 / StokesFood.py:505)."""
+    if scheme in ("color", "food"):
+        bc = bc or (SquirmerBC() if scheme == "color" else SquirmerBC(nu=1.0))
+        dt = dt if dt is not None else (0.05 if scheme == "color" else 0.01)
+        sim = StokesSimulation(mesh, bc, dt, scheme, device, tol)
+        st = sim.step(steps) if steps else []
+        res = Result(scheme, steps, u=sim.u, p=sim.field(_lib.F_P), stats=st)
+        if scheme == "color":
+            res.c = sim.c
+            if log:
+                _, _, var0 = _mixing0(mesh, sim)
+                for k, s in enumerate(st):
+                    log(f"Step: {k}, Div(u*): {s.max_div_star:.2e}, Final Div(u): {s.max_final_div:.2e}, "
+                        f"Color mixing progress={1.0 - s.mix_var / (var0 + 1e-16):.3f}")
+        else:
+            res.tracers, res.tracer_status = sim.tracers, sim.tracer_status
+            if log:
+                for k, s in enumerate(st):
+                    log(f"Step: {k}, Div(u*): {s.max_div_star:.2e}, Final Div(u): {s.max_final_div:.2e}, "
+                        f"Eaten (Red): {s.eaten}, Uneaten (Blue): {len(res.tracer_status) - s.eaten}")
+        sim.close()
+        return res
+    if scheme == "heat":
+        h = HeatSimulation(mesh, dt if dt is not None else 0.02, device, tol)
+        st = h.step(steps)
+        res = Result(scheme, steps, scalar=h.u, stats=st)
+        h.close()
+        return res
+    if scheme == "poisson":
+        return Result(scheme, 1, scalar=poisson_solve(mesh, device=device, tol=tol))
+    raise ValueError(f"unknown scheme {scheme!r}")
+
+
+def _mixing0(mesh, sim):
+    """I0, mu0, var0 of the initial dye field c = 1[x < 0.5] (StokesColor.py:493-497)."""
+    c0 = np.zeros(mesh.N)
+    c0[mesh.coords[:, 0] < 0.5] = 1.0
+    from .ops import mixing_index_host
+
+    return mixing_index_host(mesh, c0)

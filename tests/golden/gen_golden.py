@@ -315,12 +315,28 @@ def gen_long():
     return out
 
 
+def export_meshes():
+    """Package data: the reference's Triangle meshes as .npz (parsed with the reference's own
+    readNode/readEle, so the fp64 coordinates are the exact decimal-to-double values)."""
+    C = _extract("code/StokesColor.py")
+    P = _extract("code/poisson.py")
+    dst = os.path.join(os.path.dirname(os.path.dirname(OUT)), "puc-fluidsimulation-project_amd", "data")
+    os.makedirs(dst, exist_ok=True)
+    for name, (node, ele, poly) in MESHES.items():
+        X, mk = C["readNode"](os.path.join(REF, node))
+        T = C["readEle"](os.path.join(REF, ele))
+        seg, segm = P["readPoly"](os.path.join(REF, poly))
+        np.savez_compressed(os.path.join(dst, f"{name}.npz"), coords=X, markers=mk, triangles=T,
+                            segments=seg, segment_markers=segm)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--long", action="store_true")
     ap.add_argument("--only", default=None)
     a = ap.parse_args()
     _install_stubs()
+    export_meshes()
     if a.long:
         np.savez_compressed(os.path.join(OUT, "long_mesh1.npz"), **gen_long())
         return
