@@ -87,8 +87,11 @@ def main():
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup
-    if a.warmup:
-        sim.step(a.warmup)
+    log = (lambda *m: print(*m, file=sys.stderr, flush=True)) if rank == 0 else (lambda *m: None)
+    log(f"[bench] setup {t_setup:.1f}s: {info}")
+    for k in range(a.warmup):
+        st = sim.step(1)[0]
+        log(f"[bench] warmup step {k}: CG visc/p/p2 = {st.it_visc}/{st.it_p}/{st.it_p2}")
     sim.ctx.timing(True)
     barrier()
     sim.ctx.sync()
@@ -98,6 +101,7 @@ def main():
     barrier()
     dt_local = time.perf_counter() - t0
     elapsed = allmax(dt_local)
+    log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
     ms_dir, n_dir, bytes_dir = sim.ctx.timing_get(0)
     ms_upd, n_upd, bytes_upd = sim.ctx.timing_get(1)
     sim.ctx.timing(False)
