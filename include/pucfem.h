@@ -164,6 +164,9 @@ int pucfem_timing_enable(void* ctx, int32_t on);
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);
+/* micro-benchmark of the dominant kernel (k_cg_dir) variants on the pressure operator:
+   variant 0 plain loop, 1 unrolled, 2 non-temporal, 3 unrolled + non-temporal; average ms/launch */
+int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters, double* ms_out);
 /* sizes of the internal operators: out[0]=N, [1]=T, [2]=nnz(P), [3]=nnz(Pp), [4]=n_own,
    [5]=n_ghost, [6]=padded SELL entries (P), [7]=padded SELL entries (Pp), [8]=n_pairs, [9]=n_dirichlet */
 int pucfem_info(void* ctx, int64_t* out10);

@@ -224,6 +224,7 @@ struct Ctx {
       hipEvent_t b = timer.get();
       HIPCHK(hipEventRecord(b, st));
       timer.pend.push_back({cls, a, b, bytes});
+      if (timer.pend.size() > 4096) timer.flush();  // bounded number of live events
     }
   }
 
@@ -305,17 +306,19 @@ struct Ctx {
     for (;;) {
       for (int k = 0; k < chunk; ++k, ++it) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        tstart(e0);
+        // HIP-event timing samples every 8th iteration (bounded event count for long solves)
+        const bool samp = (it & 7) == 0;
+        if (samp) tstart(e0);
         hipLaunchKernelGGL((k_cg_dir<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, rr.p, rr.nb,
                            rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c);
         KCHK();
-        tstop(0, e0, bytes_dir);
+        if (samp) tstop(0, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, NR, false, 2);
-        tstart(e1);
+        if (samp) tstart(e1);
         hipLaunchKernelGGL((k_cg_upd<NR>), dim3(nb), dim3(BS), 0, st, v, A.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
                            part_a);
         KCHK();
-        tstop(1, e1, bytes_upd);
+        if (samp) tstop(1, e1, bytes_upd);
         rr = reduce_global(part_a, nb, NR, false, 0);
         if (NR == 2) halo(cg_r[0], cg_r[1]);
         else halo(cg_r[0]);
@@ -1569,6 +1572,55 @@ int pucfem_host_partition(void* ctx, int32_t rank, int32_t world, int64_t* n_own
         send_ids[idx] = c.ord.new2old[lp.r0 + lp.send_local[idx]];
         send_peer[idx] = lp.send_peer[q];
       }
+  });
+}
+
+
+// ---- kernel micro-benchmark (tools/spmv_variants.py): k_cg_dir variants on the pressure operator
+int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters, double* ms_out) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.dKp, "needs a Stokes context");
+    const DevSell& A = c.dPp;
+    const int nb = nblocks > 0 ? std::min(nblocks, MAXB) : Ctx::nb_for(A.nslices);
+    CgVecs<1> v;
+    v.y[0] = c.yp;
+    v.b[0] = c.bh;
+    v.r[0] = c.cg_r[0];
+    v.po[0] = c.cg_pa[0];
+    v.pn[0] = c.cg_pb[0];
+    v.q[0] = c.cg_q[0];
+    std::vector<double> ones(c.nloc, 1.0);
+    HIPCHK(hipMemcpyAsync(c.cg_r[0], ones.data(), sizeof(double) * c.nloc, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(c.cg_pa[0], ones.data(), sizeof(double) * c.nloc, hipMemcpyHostToDevice, c.st));
+    const double sc[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+    HIPCHK(hipMemcpyAsync(c.scal, sc, sizeof(sc), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(c.part_a, sc, sizeof(double), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemsetAsync(c.ctl, 0, 2 * sizeof(int), c.st));
+    auto launch = [&]() {
+      switch (variant) {
+        case 0: hipLaunchKernelGGL((k_cg_dir<1, 0, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 1: hipLaunchKernelGGL((k_cg_dir<1, 8, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 2: hipLaunchKernelGGL((k_cg_dir<1, 0, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        default: hipLaunchKernelGGL((k_cg_dir<1, 8, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+      }
+      KCHK();
+    };
+    launch();
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, c.st));
+    for (int k = 0; k < iters; ++k) launch();
+    HIPCHK(hipEventRecord(b, c.st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_out = ms / iters;
   });
 }
 

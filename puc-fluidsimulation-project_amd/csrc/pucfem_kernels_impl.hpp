@@ -97,7 +97,65 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restr
   }
 }
 
-template <int NR>
+template <class T>
+__device__ __forceinline__ T ldnt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+// One SELL slice of q = A^ (r + beta p_old): WMAX > 0 unrolls the entry loop (all index/value
+// loads issued before the dependent gathers); NT streams the matrix with non-temporal loads so it
+// does not evict the gathered vectors from L2 / MALL.
+template <int NR, int WMAX, bool NT>
+__device__ __forceinline__ void dir_slice(const SellDev& A, const double* __restrict__ val, const CgVecs<NR>& v,
+                                          const double (&beta)[NR], int64_t s, int lane, double (&pq)[NR]) {
+  const int64_t off = A.off[s];
+  const int w = A.w[s];
+  const int64_t row = s * 64 + lane;
+  double acc[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+  if (WMAX > 0 && w <= WMAX) {
+    int32_t cj[WMAX > 0 ? WMAX : 1];
+    double a[WMAX > 0 ? WMAX : 1];
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k) {
+      if (k < w) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        cj[k] = NT ? ldnt(A.col + e) : A.col[e];
+        a[k] = NT ? ldnt(val + e) : val[e];
+      } else {
+        cj[k] = 0;
+        a[k] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k) {
+      if (k < w) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * v.po[c][cj[k]]);
+      }
+    }
+  } else {
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double a = NT ? ldnt(val + e) : val[e];
+      const int32_t j = NT ? ldnt(A.col + e) : A.col[e];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * v.po[c][j]);
+    }
+  }
+  if (row < A.nrows) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      const double p = v.r[c][row] + beta[c] * v.po[c][row];
+      v.pn[c][row] = p;
+      v.q[c][row] = acc[c];
+      pq[c] += p * acc[c];
+    }
+  }
+}
+
+template <int NR, int WMAX = 8, bool NT = true>
 __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
@@ -136,30 +194,7 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restri
   double pq[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t off = A.off[s];
-    const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
-    double acc[NR];
-#pragma unroll
-    for (int c = 0; c < NR; ++c) acc[c] = 0.0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      const double a = val[e];
-      const int32_t j = A.col[e];
-#pragma unroll
-      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * v.po[c][j]);
-    }
-    if (row < A.nrows) {
-#pragma unroll
-      for (int c = 0; c < NR; ++c) {
-        const double p = v.r[c][row] + beta[c] * v.po[c][row];
-        v.pn[c][row] = p;
-        v.q[c][row] = acc[c];
-        pq[c] += p * acc[c];
-      }
-    }
-  }
+  for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT>(A, val, v, beta, s, lane, pq);
   for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
