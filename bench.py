@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
     ap.add_argument("--rtol-pres", type=float, default=1e-8)
+    ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
+                    help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--fine-steps", type=int, default=200)
@@ -83,7 +85,7 @@ def main():
 
     t_setup = time.time()
     mesh = pf.load_mesh("fine", refine=a.level)
-    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres)
+    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond)
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup
@@ -125,7 +127,8 @@ def main():
             "workload": f"StokesColor neutral squirmer step, mesh_fine refined x{a.level}",
             "nodes": info["N"] if world == 1 else mesh.N, "triangles": mesh.T,
             "dt": 0.05, "nu": 0.1, "B1": -2.0, "B2": 0.0,
-            "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
+            "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "pressure_precond": sim.ctx.precond,
+            "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
         },
         "cg_iters_per_s": cg_iters / elapsed,
         "cg_iters_per_step": {"visc_2rhs": [s.it_visc for s in stats], "p": [s.it_p for s in stats],

@@ -67,6 +67,10 @@ typedef struct pucfem_params {
   int32_t sl_k;        /* PointLocator k (StokesColor.py:324), 10 */
   double capture_radius; /* StokesFood.py:50-51, 0.28 */
   double center_x, center_y; /* squirmer centre (0.5, 0.5) */
+  int32_t precond;     /* pressure solve: 0 = Jacobi-CG, 1 = geometric-multigrid-preconditioned CG
+                          (needs pucfem_set_hierarchy) */
+  int32_t mg_degree;   /* Chebyshev smoothing steps per level, pre and post (2) */
+  double mg_ratio;     /* Chebyshev interval [lmax / mg_ratio, lmax] (10) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -133,6 +137,10 @@ int pucfem_set_dirichlet(void* ctx, int64_t n, const int32_t* nodes, const doubl
 /* Poisson load g(centroid) per triangle, evaluated by the host in the reference's dtype
    (poisson.py:135-144, g = 50 sin(3y) in fp32). */
 int pucfem_set_source(void* ctx, int64_t n_tris, const float* g_tri);
+/* Multigrid hierarchy: the uploaded mesh must be `levels` red refinements (pucfem_refine) of this
+   coarse mesh; the library rebuilds the intermediate levels and checks the result bit for bit. */
+int pucfem_set_hierarchy(void* ctx, int64_t n_nodes0, const double* xy0, const int32_t* markers0,
+                         int64_t n_tris0, const int32_t* tris0, int32_t levels);
 int pucfem_build_operators(void* ctx, const pucfem_params* params);
 
 /* ---- fields ---------------------------------------------------------------------- */

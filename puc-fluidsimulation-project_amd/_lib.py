@@ -34,7 +34,8 @@ class Params(ct.Structure):
         ("rtol_visc", ct.c_double), ("rtol_pres", ct.c_double), ("rtol_lin", ct.c_double),
         ("maxit_visc", ct.c_int32), ("maxit_pres", ct.c_int32), ("maxit_lin", ct.c_int32),
         ("warm_start", ct.c_int32), ("sl_k", ct.c_int32), ("capture_radius", ct.c_double),
-        ("center_x", ct.c_double), ("center_y", ct.c_double),
+        ("center_x", ct.c_double), ("center_y", ct.c_double), ("precond", ct.c_int32),
+        ("mg_degree", ct.c_int32), ("mg_ratio", ct.c_double),
     ]
 
 
@@ -65,6 +66,7 @@ SIGNATURES = {
     "pucfem_set_pairs": ([_P, ct.c_int32, ct.c_int64, _I64], ct.c_int),
     "pucfem_set_dirichlet": ([_P, ct.c_int64, _I32, _D, ct.c_int32], ct.c_int),
     "pucfem_set_source": ([_P, ct.c_int64, _F], ct.c_int),
+    "pucfem_set_hierarchy": ([_P, ct.c_int64, _D, _I32, ct.c_int64, _I32, ct.c_int32], ct.c_int),
     "pucfem_build_operators": ([_P, ct.POINTER(Params)], ct.c_int),
     "pucfem_set_field": ([_P, ct.c_int32, _D, ct.c_int64], ct.c_int),
     "pucfem_get_field": ([_P, ct.c_int32, _D, ct.c_int64], ct.c_int),

@@ -98,6 +98,28 @@ struct Timer {
   }
 };
 
+// One level of the geometric multigrid hierarchy (pressure preconditioner).  Level 0 is the
+// coarsest (the caller's base mesh, solved densely), the last level is the simulation mesh.
+struct MgLevel {
+  HostMesh mesh;            // coarse levels only (the finest is Ctx::mesh)
+  std::vector<i32> ea, eb;  // edge endpoints of the level below (midpoint parents), caller numbering
+  Ordering ord;
+  Csr P, Pp, Pr, R;         // pattern, merged pressure operator, prolongation from l-1, restriction to l-1
+  std::vector<i32> dof, master_of, slave_of;
+  std::vector<std::pair<i64, i64>> pairs;
+  std::vector<i64> rs;      // partition of this level's internal ids
+  LocalPlan lp;
+  double lmax = 2.0;
+  // device
+  Sell sA, sPr, sR;         // host SELL images (built with the plans, also on host-only contexts)
+  DevSell dA, dPr, dR;
+  double *Aval = nullptr, *Prval = nullptr, *Rval = nullptr, *dinv = nullptr;
+  double *x = nullptr, *x2 = nullptr, *b = nullptr, *d = nullptr, *res = nullptr;
+  int32_t* dsend = nullptr;
+  double* dsendbuf = nullptr;
+  i64 nsend = 0, nloc = 0;
+};
+
 struct Ctx {
   std::string err;
   int device = -1;
@@ -175,6 +197,17 @@ struct Ctx {
   double *trx = nullptr, *try_ = nullptr, *trs = nullptr, *d_eaten = nullptr;
   int last_it[3] = {0, 0, 0};
 
+  // ---- multigrid
+  HostMesh coarse;
+  int mg_levels = 0;  // refinements from `coarse` to `mesh` (0: no hierarchy given)
+  bool use_mg = false;
+  std::vector<MgLevel> mg;
+  double* dKp_raw = nullptr;        // unscaled finest pressure operator on sPp
+  double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
+  double *cfull_b = nullptr, *cfull_x = nullptr;
+  int32_t* cgather = nullptr;       // coarsest local (owned + ghost) -> coarsest internal id
+  double* z = nullptr;              // preconditioned residual (finest)
+
   ~Ctx() {
     if (!host_only) {
       if (st) (void)hipStreamSynchronize(st);
@@ -245,24 +278,27 @@ struct Ctx {
       NCCLCHK(ncclAllReduce(vals + slot, vals + slot, nv, ncclDouble, is_max ? ncclMax : ncclSum, comm, st));
   }
   // refresh the ghost entries of up to two local vectors
-  void halo(double* a, double* b = nullptr) {
-    if (world == 1 || (lp.send_peer.empty() && lp.recv_peer.empty())) return;
-    const int nv = b ? 2 : 1;
-    if (nsend > 0) {
-      hipLaunchKernelGGL(k_pack, dim3(grid_ew(nsend)), dim3(BS), 0, st, nsend, dsend, a, b, dsendbuf);
+  void halo(double* a, double* b = nullptr) { halo_lp(lp, dsend, dsendbuf, nsend, a, b); }
+  void halo_lp(const LocalPlan& P, const int32_t* sidx, double* sbuf, i64 ns, double* a, double* b = nullptr) {
+    if (world == 1 || (P.send_peer.empty() && P.recv_peer.empty())) return;
+    if (ns > 0) {
+      hipLaunchKernelGGL(k_pack, dim3(grid_ew(ns)), dim3(BS), 0, st, ns, sidx, a, b, sbuf);
       KCHK();
     }
     NCCLCHK(ncclGroupStart());
-    for (size_t k = 0; k < lp.send_peer.size(); ++k) {
-      NCCLCHK(ncclSend(dsendbuf + lp.send_off[k], lp.send_cnt[k], ncclDouble, lp.send_peer[k], comm, st));
-      if (b) NCCLCHK(ncclSend(dsendbuf + nsend + lp.send_off[k], lp.send_cnt[k], ncclDouble, lp.send_peer[k], comm, st));
+    for (size_t k = 0; k < P.send_peer.size(); ++k) {
+      NCCLCHK(ncclSend(sbuf + P.send_off[k], P.send_cnt[k], ncclDouble, P.send_peer[k], comm, st));
+      if (b) NCCLCHK(ncclSend(sbuf + ns + P.send_off[k], P.send_cnt[k], ncclDouble, P.send_peer[k], comm, st));
     }
-    for (size_t k = 0; k < lp.recv_peer.size(); ++k) {
-      NCCLCHK(ncclRecv(a + lp.n_own + lp.recv_off[k], lp.recv_cnt[k], ncclDouble, lp.recv_peer[k], comm, st));
-      if (b) NCCLCHK(ncclRecv(b + lp.n_own + lp.recv_off[k], lp.recv_cnt[k], ncclDouble, lp.recv_peer[k], comm, st));
+    for (size_t k = 0; k < P.recv_peer.size(); ++k) {
+      NCCLCHK(ncclRecv(a + P.n_own + P.recv_off[k], P.recv_cnt[k], ncclDouble, P.recv_peer[k], comm, st));
+      if (b) NCCLCHK(ncclRecv(b + P.n_own + P.recv_off[k], P.recv_cnt[k], ncclDouble, P.recv_peer[k], comm, st));
     }
     NCCLCHK(ncclGroupEnd());
-    (void)nv;
+  }
+  void mg_halo(MgLevel& L, double* a) {
+    if (&L == &mg.back()) halo(a);
+    else halo_lp(L.lp, L.dsend, L.dsendbuf, L.nsend, a);
   }
   // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
   void allgather_full(double* full) {
@@ -337,6 +373,146 @@ struct Ctx {
     return h_ctl[1];
   }
 
+  // ------------------------------------------------------------------ multigrid V-cycle / PCG
+  // Chebyshev smoothing of degree prm.mg_degree on [lmax / mg_ratio, lmax] for D^-1 A.
+  // x_in (nullable: zero initial guess) -> returns the buffer holding the result.
+  double* mg_smooth(MgLevel& L, const DevSell& A, const double* val, const double* b, double* xin, double* xa,
+                    double* xb, const double* rdot, double* part) {
+    const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
+    const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
+    double rho_old = 1.0 / sigma;
+    const int nb = nb_for(A.nslices);
+    double* cur = xin;
+    const int deg = std::max(1, prm.mg_degree);
+    for (int k = 0; k < deg; ++k) {
+      double c1 = 0.0, c2 = 1.0 / theta;
+      if (k > 0) {
+        const double rho = 1.0 / (2.0 * sigma - rho_old);
+        c1 = rho * rho_old;
+        c2 = 2.0 * rho / delta;
+        rho_old = rho;
+      }
+      double* out = (cur == xa) ? xb : xa;
+      const bool first = cur == nullptr;
+      if (!first) mg_halo(L, cur);
+      const bool last = k == deg - 1;
+      hipLaunchKernelGGL(k_cheb, dim3(nb), dim3(BS), 0, st, A.view(), val, L.dinv, b, first ? out : cur, out, L.d, c1,
+                         c2, first ? 1 : 0, ctl, last ? rdot : (const double*)nullptr, part);
+      KCHK();
+      cur = out;
+    }
+    return cur;
+  }
+  // z = M^-1 r on level l (b = r_l); the finest level passes rdot = r for the <r, z> partials
+  double* vcycle(int l, const double* b, const double* rdot, double* part) {
+    MgLevel& L = mg[l];
+    const bool finest = l == (int)mg.size() - 1;
+    const DevSell& A = finest ? dPp : L.dA;
+    const double* Av = finest ? dKp_raw : L.Aval;
+    double* xa = finest ? z : L.x;
+    double* xb = L.x2;
+    if (l == 0) {
+      // coarsest: dense pseudo-inverse, replicated on every rank
+      const i64 N0 = (i64)L.ord.new2old.size();
+      if (world == 1) {
+        hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0, dAinv, b,
+                           xa, ctl);
+        KCHK();
+      } else {
+        HIPCHK(hipMemcpyAsync(cfull_b + L.lp.r0, b, sizeof(double) * L.lp.n_own, hipMemcpyDeviceToDevice, st));
+        NCCLCHK(ncclGroupStart());
+        for (int r = 0; r < world; ++r)
+          NCCLCHK(ncclBroadcast(cfull_b + L.rs[r], cfull_b + L.rs[r], L.rs[r + 1] - L.rs[r], ncclDouble, r, comm, st));
+        NCCLCHK(ncclGroupEnd());
+        hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0, dAinv,
+                           cfull_b, cfull_x, ctl);
+        hipLaunchKernelGGL(k_gather, dim3(grid_ew(L.nloc)), dim3(BS), 0, st, L.nloc, cgather, cfull_x, xa, ctl);
+        KCHK();
+      }
+      return xa;
+    }
+    double* x = mg_smooth(L, A, Av, b, nullptr, xa, xb, nullptr, nullptr);
+    mg_halo(L, x);
+    hipLaunchKernelGGL(k_resid, dim3(nb_for(A.nslices)), dim3(BS), 0, st, A.view(), Av, b, x, L.res, ctl);
+    KCHK();
+    mg_halo(L, L.res);
+    MgLevel& C = mg[l - 1];
+    hipLaunchKernelGGL(k_transfer, dim3(nb_for(L.dR.nslices)), dim3(BS), 0, st, L.dR.view(), L.Rval, L.res, C.b, 0,
+                       ctl);
+    KCHK();
+    double* xc = vcycle(l - 1, C.b, nullptr, nullptr);
+    mg_halo(C, xc);
+    hipLaunchKernelGGL(k_transfer, dim3(nb_for(L.dPr.nslices)), dim3(BS), 0, st, L.dPr.view(), L.Prval, xc, x, 1,
+                       ctl);
+    KCHK();
+    double* other = (x == xa) ? xb : xa;
+    double* out = mg_smooth(L, A, Av, b, x, x, other, rdot, part);
+    if (finest && out != z) HIPCHK(hipMemcpyAsync(z, out, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+    return out;
+  }
+  // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
+  int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
+    const int nb = nb_for(dPp.nslices);
+    CgVecs<1> v;
+    v.y[0] = y;
+    v.b[0] = b;
+    v.r[0] = z;  // the gathered "r" of k_cg_dir is the preconditioned residual
+    v.po[0] = cg_pa[0];
+    v.pn[0] = cg_pb[0];
+    v.q[0] = cg_q[0];
+    CgVecs<1> vi = v;
+    vi.r[0] = cg_r[0];
+    halo(y);
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    hipLaunchKernelGGL((k_cg_init<1>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, vi, lp.n_ghost, part_a, part_b);
+    KCHK();
+    Red rr = reduce_global(part_a, nb, 1, false, 0);
+    Red bb = reduce_global(part_b, nb, 1, false, 1);
+    halo(cg_r[0]);
+    vcycle((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+    Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
+    halo(z);
+    const double tol2 = tol * tol;
+    const double bytes_dir = 12.0 * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
+    const double bytes_upd = 48.0 * (double)dPp.nrows;
+    int it = 0;
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
+    for (;;) {
+      for (int k = 0; k < chunk; ++k, ++it) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        tstart(e0);
+        hipLaunchKernelGGL((k_cg_dir<1>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, v, lp.n_ghost, rz.p, rz.nb,
+                           rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c, rr.p, rr.nb,
+                           rr.stride);
+        KCHK();
+        tstop(0, e0, bytes_dir);
+        Red pq = reduce_global(part_c, nb, 1, false, 2);
+        tstart(e1);
+        CgVecs<1> vu = v;
+        vu.r[0] = cg_r[0];
+        hipLaunchKernelGGL((k_cg_upd<1>), dim3(nb), dim3(BS), 0, st, vu, dPp.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
+                           part_a);
+        KCHK();
+        tstop(1, e1, bytes_upd);
+        rr = reduce_global(part_a, nb, 1, false, 0);
+        halo(cg_r[0]);
+        vcycle((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+        rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
+        halo(z);
+        std::swap(v.po[0], v.pn[0]);
+      }
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (timer.on) timer.flush();
+      if (h_ctl[0]) break;
+      chunk = std::max(2, std::min(16, it / 4));
+    }
+    last_it[which] = h_ctl[1];
+    if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "MG-PCG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");
+    if (h_ctl[0] != 1) throw Error(PUCFEM_ENOCONV, "MG-PCG did not converge within maxit=" + std::to_string(maxit));
+    return h_ctl[1];
+  }
+
   // ------------------------------------------------------------------ building blocks of the step
   void bc(double* a, double* b) {  // makePerBCU + makeDirBCU on owned rows
     if (ncopy == 0 && ndir == 0) return;
@@ -371,14 +547,20 @@ struct Ctx {
     const int nb = nb_for(dP.nslices);
     Red sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
     const i64 n = lp.n_own;
-    hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, dsp,
+    const double* sc = use_mg ? nullptr : dsp;  // the MG path solves the unscaled system
+    hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
                        sb.p, sb.nb, 1.0 / (double)n_free, bh);
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
-    double* y[1] = {yst};
-    const double* b[1] = {bh};
-    int it = cg<1>(dPp, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
-    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, dsp, yst, (const double*)nullptr, pout,
+    int it;
+    if (use_mg) {
+      it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
+    } else {
+      double* y[1] = {yst};
+      const double* b[1] = {bh};
+      it = cg<1>(dPp, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
+    }
+    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
                        (double*)nullptr, dmaster_of);
     KCHK();
     halo(pout);
@@ -531,6 +713,94 @@ void require(bool ok, const std::string& msg) {
   if (!ok) throw Error(PUCFEM_EINVAL, msg);
 }
 
+// ------------------------------------------------------------------ multigrid hierarchy (host)
+double lmax_estimate(const Csr& A) {
+  // min(Gershgorin bound, 1.1 x 30-step power iteration) of D^-1 A
+  const i64 n = A.nrows;
+  std::vector<double> dinv(n), x(n), y(n);
+  double gersh = 0.0;
+  for (i64 r = 0; r < n; ++r) {
+    double d = 1.0, s = 0.0;
+    for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+      if (A.col[k] == r) d = A.val[k];
+      s += std::fabs(A.val[k]);
+    }
+    dinv[r] = 1.0 / d;
+    gersh = std::max(gersh, s / d);
+  }
+  for (i64 i = 0; i < n; ++i) x[i] = 1.0 + 0.5 * std::sin((double)i);
+  double lam = 0.0;
+  for (int it = 0; it < 30; ++it) {
+    double nx = 0.0, ny = 0.0;
+    for (i64 r = 0; r < n; ++r) {
+      double a = 0.0;
+      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) a += A.val[k] * x[A.col[k]];
+      y[r] = dinv[r] * a;
+      nx += x[r] * x[r];
+      ny += y[r] * y[r];
+    }
+    lam = std::sqrt(ny / nx);
+    const double inv = 1.0 / std::sqrt(ny);
+    for (i64 r = 0; r < n; ++r) x[r] = y[r] * inv;
+  }
+  return std::min(gersh, 1.1 * lam);
+}
+
+void build_mg_host(Ctx& c) {
+  const int Lv = c.mg_levels;
+  c.mg.clear();
+  c.mg.resize(Lv + 1);
+  c.mg[0].mesh = c.coarse;
+  for (int l = 1; l <= Lv; ++l) {
+    HostMesh tmp;
+    red_refine(c.mg[l - 1].mesh, tmp, &c.mg[l].ea, &c.mg[l].eb);
+    if (l < Lv) {
+      c.mg[l].mesh = std::move(tmp);
+    } else {
+      require(tmp.N == c.mesh.N && tmp.T == c.mesh.T && tmp.x == c.mesh.x && tmp.y == c.mesh.y &&
+                  tmp.tri == c.mesh.tri,
+              "the uploaded mesh is not the red refinement of the hierarchy's coarse mesh");
+    }
+  }
+  const i64 N = c.mesh.N;
+  const int S = c.prm.nstrips > 0 ? c.prm.nstrips : auto_strips(N);
+  const double ymin = *std::min_element(c.mesh.y.begin(), c.mesh.y.end());
+  const double ymax = *std::max_element(c.mesh.y.begin(), c.mesh.y.end());
+  for (int l = 0; l < Lv; ++l) {
+    MgLevel& L = c.mg[l];
+    make_ordering_fixed(L.mesh, S, ymin, ymax, L.ord);
+    build_pattern(L.mesh, L.ord, L.P);
+    Assembly A;
+    assemble_stokes(L.mesh, L.ord, L.P, A);
+    L.pairs = level_pairs(L.mesh, 1.0, 1e-6, 1.0);
+    const i64 n = L.mesh.N;
+    L.dof.resize(n);
+    for (i64 i = 0; i < n; ++i) L.dof[i] = (i32)i;
+    L.master_of.assign(n, -1);
+    L.slave_of.assign(n, -1);
+    for (auto& pr : L.pairs) {
+      const i32 mi = L.ord.old2new[pr.first], si = L.ord.old2new[pr.second];
+      require(L.master_of[si] < 0 && L.dof[mi] == mi && L.slave_of[si] < 0, "multigrid level has chained pairs");
+      L.dof[si] = mi;
+      L.master_of[si] = mi;
+      L.slave_of[mi] = si;
+    }
+    build_pressure(L.P, A.K, L.dof, L.slave_of, L.Pp);
+    L.P = Csr();  // only the merged operator is needed on coarse levels
+  }
+  MgLevel& F = c.mg[Lv];
+  F.ord = c.ord;
+  F.dof = c.dof;
+  F.master_of = c.master_of;
+  for (int l = 1; l <= Lv; ++l) {
+    MgLevel& L = c.mg[l];
+    const MgLevel& C = c.mg[l - 1];
+    build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
+    transpose(L.Pr, C.mesh.N, L.R);
+  }
+  for (int l = 0; l <= Lv; ++l) c.mg[l].lmax = lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
+}
+
 // ------------------------------------------------------------------ operator build
 void build(Ctx& c) {
   require(c.has_mesh, "mesh not uploaded");
@@ -564,6 +834,8 @@ void build(Ctx& c) {
     c.n_free = N - (i64)c.op_pairs.size();
     build_pressure(c.P, c.as.K, c.dof, c.slave_of, c.Pp);
   }
+  c.use_mg = stokes && prm.precond == 1 && c.mg_levels > 0;
+  if (c.use_mg) build_mg_host(c);
   if (literal) {
     assemble_literal(m, c.ord, c.g_tri, c.op_pairs, c.dir_nodes, c.dir_vals,
                      prm.scheme == PUCFEM_HEAT ? prm.dt : -1.0, c.Lit, c.litb);
@@ -586,7 +858,38 @@ void build(Ctx& c) {
   std::vector<const Csr*> pats;
   if (stokes) pats = {&c.P, &c.Pp};
   else pats = {&c.P, &c.Lit};
-  make_local_plan(pats, c.row_start, c.rank, c.lp);
+  if (!c.use_mg) {
+    make_local_plan(pats, c.row_start, c.rank, c.lp);
+  } else {
+    // every level cut at the same strips (y-cuts) as the finest partition
+    const int Lv = c.mg_levels;
+    std::vector<i64> cut(c.world + 1);
+    for (int r = 0; r <= c.world; ++r)
+      cut[r] = std::lower_bound(c.ord.strip_ptr.begin(), c.ord.strip_ptr.end(), c.row_start[r]) - c.ord.strip_ptr.begin();
+    for (int l = 0; l <= Lv; ++l) {
+      MgLevel& L = c.mg[l];
+      L.rs.resize(c.world + 1);
+      for (int r = 0; r <= c.world; ++r) L.rs[r] = L.ord.strip_ptr[cut[r]];
+    }
+    for (int l = 0; l <= Lv; ++l) {
+      MgLevel& L = c.mg[l];
+      std::vector<PatRows> pr;
+      pr.push_back({l == Lv ? &c.Pp : &L.Pp, &L.rs});
+      if (l >= 1) pr.push_back({&L.R, &c.mg[l - 1].rs});
+      if (l < Lv) pr.push_back({&c.mg[l + 1].Pr, &c.mg[l + 1].rs});
+      if (l == Lv) pr.push_back({&c.P, &L.rs});
+      make_local_plan2(pr, L.rs, c.rank, L.lp);
+    }
+    c.lp = c.mg[Lv].lp;
+    for (int l = 0; l <= Lv; ++l) {  // host SELL images; resolving every column validates the plans
+      MgLevel& L = c.mg[l];
+      if (l < Lv) build_sell_x(L.Pp, L.rs[c.rank], L.lp.n_own, L.lp, L.sA);
+      if (l >= 1) {
+        build_sell_x(L.Pr, L.rs[c.rank], L.lp.n_own, c.mg[l - 1].lp, L.sPr);
+        build_sell_x(L.R, c.mg[l - 1].rs[c.rank], c.mg[l - 1].lp.n_own, L.lp, L.sR);
+      }
+    }
+  }
   build_sell(c.P, c.lp, c.sP);
   if (stokes) build_sell(c.Pp, c.lp, c.sPp);
   if (literal) build_sell(c.Lit, c.lp, c.sLit);
@@ -651,6 +954,75 @@ void build(Ctx& c) {
     sell_values(c.Pp, lp, c.sPp, kph, tmp);
     c.dKp = c.upload(tmp);
     c.dsp = c.upload(local_vec(sg));
+  }
+  if (c.use_mg) {
+    const int Lv = c.mg_levels;
+    sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
+    c.dKp_raw = c.upload(tmp);
+    c.z = c.dalloc<double>(c.nloc);
+    for (int l = 0; l <= Lv; ++l) {
+      MgLevel& L = c.mg[l];
+      const Csr& A = l == Lv ? c.Pp : L.Pp;
+      const i64 n = L.lp.n_own;
+      L.nloc = n + L.lp.n_ghost;
+      std::vector<double> dv(n);
+      for (i64 i = 0; i < n; ++i) dv[i] = 1.0 / diag_of(A, A.val, L.rs[c.rank] + i);
+      L.dinv = c.upload(dv);
+      if (l < Lv) {
+        const Sell& S = L.sA;
+        sell_values_x(A, L.rs[c.rank], S, A.val, tmp);
+        L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
+                       A.rowptr[L.rs[c.rank] + n] - A.rowptr[L.rs[c.rank]], S.padded};
+        L.Aval = c.upload(tmp);
+        L.nsend = (i64)L.lp.send_local.size();
+        L.dsend = c.upload(L.lp.send_local);
+        L.dsendbuf = c.dalloc<double>(2 * std::max<i64>(1, L.nsend));
+      }
+      if (l >= 1) {
+        const MgLevel& C = c.mg[l - 1];
+        const Sell& S = L.sPr;
+        sell_values_x(L.Pr, L.rs[c.rank], S, L.Pr.val, tmp);
+        L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows, 0, S.padded};
+        L.Prval = c.upload(tmp);
+        const Sell& R = L.sR;
+        sell_values_x(L.R, C.rs[c.rank], R, L.R.val, tmp);
+        L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), R.nslices, R.nrows, 0, R.padded};
+        L.Rval = c.upload(tmp);
+      }
+      for (double** f : {&L.x, &L.x2, &L.b, &L.d, &L.res}) *f = c.dalloc<double>(L.nloc);
+    }
+    // coarsest: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
+    {
+      MgLevel& L0 = c.mg[0];
+      const i64 n0 = L0.mesh.N;
+      require(n0 <= 8192, "multigrid coarse level too large for the dense coarse solve (<= 8192 nodes)");
+      std::vector<double> D(n0 * n0, 0.0);
+      const Csr& A = L0.Pp;
+      double dsum = 0.0;
+      i64 nf = 0;
+      for (i64 r = 0; r < n0; ++r) {
+        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) D[r * n0 + A.col[k]] += A.val[k];
+        if (L0.master_of[r] < 0) {
+          dsum += diag_of(A, A.val, r);
+          ++nf;
+        }
+      }
+      const double cc = dsum / (double)nf / (double)nf;
+      for (i64 i = 0; i < n0; ++i)
+        if (L0.master_of[i] < 0)
+          for (i64 j = 0; j < n0; ++j)
+            if (L0.master_of[j] < 0) D[i * n0 + j] += cc;
+      require(spd_inverse(D, n0), "coarse operator is not SPD after regularisation");
+      c.dAinv = c.upload(D);
+      if (c.world > 1) {
+        c.cfull_b = c.dalloc<double>(n0);
+        c.cfull_x = c.dalloc<double>(n0);
+        std::vector<i32> gi(L0.nloc);
+        for (i64 i = 0; i < L0.lp.n_own; ++i) gi[i] = (i32)(L0.lp.r0 + i);
+        for (i64 k = 0; k < L0.lp.n_ghost; ++k) gi[L0.lp.n_own + k] = L0.lp.ghost_global[k];
+        c.cgather = c.upload(gi);
+      }
+    }
   }
   if (literal) {
     dsell(c.sLit, c.Lit, c.dLit);
@@ -917,6 +1289,29 @@ int pucfem_set_dirichlet(void* ctx, int64_t n, const int32_t* nodes, const doubl
     for (i32 d : c.dir_nodes) require(d >= 0 && d < c.mesh.N, "Dirichlet node out of range");
     c.dir_vals.assign(values, values + ncomp * n);
     c.dir_ncomp = ncomp;
+    c.built = false;
+  });
+}
+
+int pucfem_set_hierarchy(void* ctx, int64_t N0, const double* xy0, const int32_t* mk0, int64_t T0,
+                         const int32_t* tris0, int32_t levels) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(levels >= 0 && levels <= 12, "levels in [0, 12]");
+    require(N0 > 0 && T0 > 0, "empty coarse mesh");
+    HostMesh& m = c.coarse;
+    m.N = N0;
+    m.T = T0;
+    m.x.resize(N0);
+    m.y.resize(N0);
+    for (i64 i = 0; i < N0; ++i) {
+      m.x[i] = xy0[2 * i];
+      m.y[i] = xy0[2 * i + 1];
+    }
+    m.mk.assign(mk0, mk0 + N0);
+    m.tri.assign(tris0, tris0 + 3 * T0);
+    for (i64 k = 0; k < 3 * T0; ++k) require(m.tri[k] >= 0 && m.tri[k] < N0, "coarse triangle index out of range");
+    c.mg_levels = levels;
     c.built = false;
   });
 }
@@ -1503,6 +1898,35 @@ int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, in
     c.need_built();
     const Csr* A = nullptr;
     const std::vector<double>* v = nullptr;
+    if (op >= 100) {  // multigrid level matrices (CPU tests): 100 + 3 l + {0: Pp_l, 1: Pr_l, 2: R_l}
+      const int l = (op - 100) / 3, kind = (op - 100) % 3;
+      require(c.use_mg && l >= 0 && l <= c.mg_levels, "no such multigrid level");
+      const int Lv = c.mg_levels;
+      const MgLevel& L = c.mg[l];
+      require(kind == 0 || l >= 1, "level 0 has no transfer operators");
+      const Csr& M = kind == 0 ? (l == Lv ? c.Pp : L.Pp) : kind == 1 ? L.Pr : L.R;
+      const Ordering& ro = kind == 2 ? c.mg[l - 1].ord : L.ord;
+      const Ordering& co = kind == 1 ? c.mg[l - 1].ord : L.ord;
+      *n_rows = M.nrows;
+      *nnz = M.nnz();
+      if (!col) return;
+      i64 k = 0;
+      rowptr[0] = 0;
+      std::vector<std::pair<i64, double>> tmp;
+      for (i64 o = 0; o < M.nrows; ++o) {
+        const i64 g = ro.old2new[o];
+        tmp.clear();
+        for (i64 e = M.rowptr[g]; e < M.rowptr[g + 1]; ++e) tmp.push_back({co.new2old[M.col[e]], M.val[e]});
+        std::sort(tmp.begin(), tmp.end());
+        for (auto& t : tmp) {
+          col[k] = t.first;
+          val[k] = t.second;
+          ++k;
+        }
+        rowptr[o + 1] = k;
+      }
+      return;
+    }
     switch (op) {
       case PUCFEM_OP_K: A = &c.P; v = &c.as.K; break;
       case PUCFEM_OP_GX: A = &c.P; v = &c.as.Gx; break;

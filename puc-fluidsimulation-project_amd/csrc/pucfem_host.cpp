@@ -11,7 +11,7 @@
 namespace pucfem {
 
 // ----------------------------------------------------------------------------- refinement
-void red_refine(const HostMesh& in, HostMesh& out) {
+void red_refine(const HostMesh& in, HostMesh& out, std::vector<i32>* edge_a, std::vector<i32>* edge_b) {
   const i64 N = in.N, T = in.T;
   // bucket every edge (a<b) under a, with multiplicity
   std::vector<i64> bptr(N + 1, 0);
@@ -74,6 +74,15 @@ void red_refine(const HostMesh& in, HostMesh& out) {
       else
         out.mk[n] = 0;
     }
+  if (edge_a && edge_b) {
+    edge_a->resize(E);
+    edge_b->resize(E);
+    for (i64 a = 0; a < N; ++a)
+      for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
+        (*edge_a)[k] = (i32)a;
+        (*edge_b)[k] = eb[k];
+      }
+  }
   out.tri.resize(3 * out.T);
   for (i64 t = 0; t < T; ++t) {
     i32 a = in.tri[3 * t], b = in.tri[3 * t + 1], c = in.tri[3 * t + 2];
@@ -84,11 +93,15 @@ void red_refine(const HostMesh& in, HostMesh& out) {
 }
 
 // ----------------------------------------------------------------------------- ordering
+int auto_strips(i64 N) { return (int)std::max<i64>(1, std::llround(std::sqrt((double)N) / 4.0)); }
+
 void make_ordering(const HostMesh& m, int nstrips, Ordering& ord) {
+  make_ordering_fixed(m, nstrips > 0 ? nstrips : auto_strips(m.N), *std::min_element(m.y.begin(), m.y.end()),
+                      *std::max_element(m.y.begin(), m.y.end()), ord);
+}
+
+void make_ordering_fixed(const HostMesh& m, int S, double ymin, double ymax, Ordering& ord) {
   const i64 N = m.N;
-  int S = nstrips > 0 ? nstrips : (int)std::max<i64>(1, std::llround(std::sqrt((double)N) / 4.0));
-  double ymin = *std::min_element(m.y.begin(), m.y.end());
-  double ymax = *std::max_element(m.y.begin(), m.y.end());
   double span = ymax > ymin ? ymax - ymin : 1.0;
   std::vector<i32> strip(N);
   for (i64 i = 0; i < N; ++i) {
@@ -506,6 +519,211 @@ void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, 
     for (i32 j = c; j <= d; ++j)
       for (i32 i = a; i <= b; ++i) G.item[fill[(i64)j * G.nx + i]++] = (i32)t;
   }
+}
+
+// ----------------------------------------------------------------------------- multigrid helpers
+std::vector<std::pair<i64, i64>> level_pairs(const HostMesh& m, double L, double tol, double H) {
+  std::vector<i64> left, right;
+  for (i64 i = 0; i < m.N; ++i) {
+    if (std::fabs(m.x[i]) < tol) left.push_back(i);
+    if (std::fabs(m.x[i] - L) < tol) right.push_back(i);
+  }
+  std::vector<std::pair<i64, i64>> out;
+  if (left.empty() || right.empty()) return out;
+  std::vector<i64> rs = right;
+  std::sort(rs.begin(), rs.end(), [&](i64 a, i64 b) { return m.y[a] != m.y[b] ? m.y[a] < m.y[b] : a < b; });
+  for (i64 l : left) {
+    const double y = m.y[l];
+    if (std::fabs(y - 0.0) < tol || std::fabs(y - H) < tol) continue;
+    auto it = std::lower_bound(rs.begin(), rs.end(), y, [&](i64 a, double v) { return m.y[a] < v; });
+    i64 best = -1;
+    double bd = INFINITY;
+    for (auto jt : {it - 1, it}) {
+      if (jt < rs.begin() || jt >= rs.end()) continue;
+      const double d = std::fabs(m.y[*jt] - y);
+      if (d < bd || (d == bd && *jt < best)) {
+        bd = d;
+        best = *jt;
+      }
+    }
+    out.push_back({l, best});
+  }
+  return out;
+}
+
+void build_prolongation(i64 Nc, const std::vector<i32>& ea, const std::vector<i32>& eb, const Ordering& of,
+                        const Ordering& oc, const std::vector<i32>& dof_c, const std::vector<i32>& master_of_f,
+                        Csr& P) {
+  const i64 Nf = (i64)of.new2old.size();
+  P.nrows = Nf;
+  P.rowptr.assign(Nf + 1, 0);
+  P.col.clear();
+  P.val.clear();
+  for (i64 g = 0; g < Nf; ++g) {
+    if (master_of_f[g] < 0) {
+      const i64 o = of.new2old[g];
+      if (o < Nc) {
+        P.col.push_back(dof_c[oc.old2new[o]]);
+        P.val.push_back(1.0);
+      } else {
+        i32 a = dof_c[oc.old2new[ea[o - Nc]]], b = dof_c[oc.old2new[eb[o - Nc]]];
+        if (a == b) {
+          P.col.push_back(a);
+          P.val.push_back(1.0);
+        } else {
+          if (b < a) std::swap(a, b);
+          P.col.push_back(a);
+          P.val.push_back(0.5);
+          P.col.push_back(b);
+          P.val.push_back(0.5);
+        }
+      }
+    }
+    P.rowptr[g + 1] = (i64)P.col.size();
+  }
+}
+
+void transpose(const Csr& A, i64 ncols, Csr& At) {
+  At.nrows = ncols;
+  At.rowptr.assign(ncols + 1, 0);
+  for (i64 k = 0; k < A.nnz(); ++k) At.rowptr[A.col[k] + 1]++;
+  for (i64 c = 0; c < ncols; ++c) At.rowptr[c + 1] += At.rowptr[c];
+  At.col.assign(A.nnz(), 0);
+  At.val.assign(A.nnz(), 0.0);
+  std::vector<i64> fill(At.rowptr.begin(), At.rowptr.end() - 1);
+  for (i64 r = 0; r < A.nrows; ++r)
+    for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+      const i64 d = fill[A.col[k]]++;
+      At.col[d] = (i32)r;
+      At.val[d] = A.val[k];
+    }
+}
+
+bool spd_inverse(std::vector<double>& A, i64 n) {
+  // Cholesky A = L L^T (lower, in place), then inv = L^-T L^-1
+  for (i64 j = 0; j < n; ++j) {
+    double d = A[j * n + j];
+    for (i64 k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+    if (!(d > 0)) return false;
+    d = std::sqrt(d);
+    A[j * n + j] = d;
+    for (i64 i = j + 1; i < n; ++i) {
+      double s = A[i * n + j];
+      for (i64 k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = s / d;
+    }
+  }
+  // Linv (lower) into W
+  std::vector<double> W(n * n, 0.0);
+  for (i64 j = 0; j < n; ++j) {
+    W[j * n + j] = 1.0 / A[j * n + j];
+    for (i64 i = j + 1; i < n; ++i) {
+      double s = 0.0;
+      for (i64 k = j; k < i; ++k) s -= A[i * n + k] * W[k * n + j];
+      W[i * n + j] = s / A[i * n + i];
+    }
+  }
+  // inv = W^T W
+  for (i64 i = 0; i < n; ++i)
+    for (i64 j = 0; j <= i; ++j) {
+      double s = 0.0;
+      for (i64 k = i; k < n; ++k) s += W[k * n + i] * W[k * n + j];
+      A[i * n + j] = s;
+      A[j * n + i] = s;
+    }
+  return true;
+}
+
+void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& row_start, int rank, LocalPlan& lp) {
+  const int world = (int)row_start.size() - 1;
+  lp.r0 = row_start[rank];
+  lp.r1 = row_start[rank + 1];
+  lp.n_own = lp.r1 - lp.r0;
+  auto owner = [&](i64 g) {
+    return (i32)(std::upper_bound(row_start.begin(), row_start.end(), g) - row_start.begin() - 1);
+  };
+  auto cols_of = [&](int q, std::vector<i32>& out, i64 lo, i64 hi, bool inside) {
+    for (auto& pr : pats) {
+      const Csr& A = *pr.A;
+      const std::vector<i64>& rs = *pr.rows;
+      for (i64 r = rs[q]; r < rs[q + 1]; ++r)
+        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+          const i32 c = A.col[k];
+          const bool in = c >= lo && c < hi;
+          if (in == inside) out.push_back(c);
+        }
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+  };
+  std::vector<i32> gh;
+  cols_of(rank, gh, lp.r0, lp.r1, false);
+  lp.ghost_global = gh;
+  lp.n_ghost = (i64)gh.size();
+  lp.ghost_owner.resize(gh.size());
+  for (size_t k = 0; k < gh.size(); ++k) lp.ghost_owner[k] = owner(gh[k]);
+  lp.recv_peer.clear();
+  lp.recv_off.clear();
+  lp.recv_cnt.clear();
+  for (size_t k = 0; k < gh.size(); ++k) {
+    if (lp.recv_peer.empty() || lp.recv_peer.back() != lp.ghost_owner[k]) {
+      lp.recv_peer.push_back(lp.ghost_owner[k]);
+      lp.recv_off.push_back((i64)k);
+      lp.recv_cnt.push_back(0);
+    }
+    lp.recv_cnt.back()++;
+  }
+  lp.send_peer.clear();
+  lp.send_off.clear();
+  lp.send_cnt.clear();
+  lp.send_local.clear();
+  for (int q = 0; q < world; ++q) {
+    if (q == rank) continue;
+    std::vector<i32> need;
+    cols_of(q, need, lp.r0, lp.r1, true);
+    // q only needs those of my rows that are not its own (q's rows are outside my range anyway)
+    if (need.empty()) continue;
+    lp.send_peer.push_back(q);
+    lp.send_off.push_back((i64)lp.send_local.size());
+    lp.send_cnt.push_back((i64)need.size());
+    for (i32 g : need) lp.send_local.push_back((i32)(g - lp.r0));
+  }
+}
+
+void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S) {
+  S.nrows = n;
+  S.nslices = (n + 63) / 64;
+  S.slice_off.assign(S.nslices + 1, 0);
+  S.slice_w.assign(S.nslices, 0);
+  for (i64 s = 0; s < S.nslices; ++s) {
+    i64 w = 0;
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 r = s * 64 + l;
+      if (r < n) w = std::max(w, A.rowptr[r0 + r + 1] - A.rowptr[r0 + r]);
+    }
+    S.slice_w[s] = (i32)w;
+    S.slice_off[s + 1] = S.slice_off[s] + w * 64;
+  }
+  S.padded = S.slice_off[S.nslices];
+  S.col.assign(S.padded, 0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 r = s * 64 + l;
+      const i64 len = r < n ? A.rowptr[r0 + r + 1] - A.rowptr[r0 + r] : 0;
+      for (i64 k = 0; k < S.slice_w[s]; ++k)
+        S.col[S.slice_off[s] + k * 64 + l] = k < len ? to_local(cols, A.col[A.rowptr[r0 + r] + k]) : 0;
+    }
+}
+
+void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out) {
+  out.assign(S.padded, 0.0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 r = s * 64 + l;
+      if (r >= S.nrows) continue;
+      const i64 b = A.rowptr[r0 + r], len = A.rowptr[r0 + r + 1] - b;
+      for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
+    }
 }
 
 }  // namespace pucfem

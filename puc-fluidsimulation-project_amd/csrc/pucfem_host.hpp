@@ -21,7 +21,8 @@ struct HostMesh {
 
 // Red refinement: every triangle -> 4, edge midpoints appended after the old nodes in
 // (min, max) edge order; boundary-edge midpoints inherit the boundary marker.
-void red_refine(const HostMesh& in, HostMesh& out);
+void red_refine(const HostMesh& in, HostMesh& out, std::vector<i32>* edge_a = nullptr,
+                std::vector<i32>* edge_b = nullptr);
 
 // CSR pattern / matrix with column ids in the INTERNAL (new) numbering.
 struct Csr {
@@ -44,6 +45,10 @@ struct Ordering {
   std::vector<i64> strip_ptr;  // size S+1, internal-index start of each strip
 };
 void make_ordering(const HostMesh& m, int nstrips, Ordering& ord);
+// same strips (count and y-bounds) for every level of a hierarchy, so a node keeps its strip --
+// and its rank -- on every level it appears on
+void make_ordering_fixed(const HostMesh& m, int nstrips, double ymin, double ymax, Ordering& ord);
+int auto_strips(i64 N);
 
 // Node-adjacency pattern (incl. diagonal) in internal numbering, sorted columns.
 void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P);
@@ -72,6 +77,20 @@ void build_pressure(const Csr& P, const std::vector<double>& K, const std::vecto
 // Partition of the internal index range into `world` contiguous strip ranges, balanced by nnz.
 void partition_rows(const Csr& P, const Ordering& ord, int world, std::vector<i64>& row_start);
 
+// Periodic (master, slave) pairs of a multigrid level (caller numbering): left x~0 node with the
+// right x~L node of nearest y (ties: lowest index), masters on y=0|H dropped (StokesColor.py:449-457).
+std::vector<std::pair<i64, i64>> level_pairs(const HostMesh& m, double L, double tol, double H);
+
+// Prolongation level c -> level f (f = red refinement of c): rows = fine internal ids, cols = coarse
+// internal ids mapped through the coarse periodic dof map; copies weight 1, edge midpoints 1/2+1/2;
+// fine periodic slaves get empty rows (their merged value lives on the master).
+void build_prolongation(i64 Nc, const std::vector<i32>& edge_a, const std::vector<i32>& edge_b,
+                        const Ordering& of, const Ordering& oc, const std::vector<i32>& dof_c,
+                        const std::vector<i32>& master_of_f, Csr& P);
+void transpose(const Csr& A, i64 ncols, Csr& At);
+// Dense inverse of a (regularised) SPD matrix, row-major n x n, by Cholesky.  Returns false if not SPD.
+bool spd_inverse(std::vector<double>& A, i64 n);
+
 // Local view of one rank: owned rows [r0, r1) + sorted ghost list, local column ids.
 struct LocalPlan {
   i64 r0 = 0, r1 = 0, n_own = 0, n_ghost = 0;
@@ -86,6 +105,14 @@ struct LocalPlan {
 // patterns: every pattern whose columns must be resolved (P, Pp, ...)
 void make_local_plan(const std::vector<const Csr*>& pats, const std::vector<i64>& row_start, int rank,
                      LocalPlan& lp);
+// general form: each pattern reads THIS level's vectors through its columns, but its rows may be
+// partitioned by another level's ranges (restriction rows live on the coarse level, ...)
+struct PatRows {
+  const Csr* A;
+  const std::vector<i64>* rows;  // owner ranges of A's rows
+};
+void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& row_start, int rank,
+                      LocalPlan& lp);
 
 // SELL-64: slices of 64 rows, per-slice width = max row length, entries column-major
 // inside a slice (lane = row) so a wave's loads are contiguous.
@@ -99,6 +126,9 @@ struct Sell {
 void build_sell(const Csr& A, const LocalPlan& lp, Sell& S);
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
                  std::vector<double>& out);
+// rows [r0, r0 + n) of A, columns resolved in `cols` (another level's plan)
+void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S);
+void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
 i32 to_local(const LocalPlan& lp, i32 g);
 
 // Uniform grid of items (centroids / triangle bboxes) for the device point searches.

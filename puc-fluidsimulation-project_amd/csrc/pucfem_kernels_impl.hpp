@@ -159,7 +159,10 @@ template <int NR, int WMAX = 8, bool NT = true>
 __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
-                                               int* ctl, int it, int maxit, double tol2, double* part_pq) {
+                                               int* ctl, int it, int maxit, double tol2, double* part_pq,
+                                               const double* part_cv = nullptr, int nb_cv = 0, int stride_cv = 0) {
+  // part_rr: numerator of beta (<r,r> for CG, <r,z> for preconditioned CG); part_cv (if given):
+  // <r,r> for the convergence test; part_bb: <b,b>.
   __shared__ double sh[4];
   if (ctl[0]) return;
   double rr[NR], bb[NR], beta[NR];
@@ -168,8 +171,9 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restri
   for (int c = 0; c < NR; ++c) {
     rr[c] = reduce_partials(part_rr + c * stride_rr, nb_rr, sh);
     bb[c] = it == 0 ? reduce_partials(part_bb + c * stride_bb, nb_bb, sh) : scal[8 + c];
-    conv = conv && (rr[c] <= tol2 * bb[c]);
-    bad = bad || !isfinite(rr[c]);
+    const double cv = part_cv ? reduce_partials(part_cv + c * stride_cv, nb_cv, sh) : rr[c];
+    conv = conv && (cv <= tol2 * bb[c]);
+    bad = bad || !isfinite(rr[c]) || !isfinite(cv);
   }
   if (conv || bad || it >= maxit) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -243,8 +247,9 @@ __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const 
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     int64_t j = i;
     if (master_of && master_of[i] >= 0) j = master_of[i];
-    x0[i] = s[j] * y0[j];
-    if (nr > 1) x1[i] = s[j] * y1[j];
+    const double sj = s ? s[j] : 1.0;
+    x0[i] = sj * y0[j];
+    if (nr > 1) x1[i] = sj * y1[j];
   }
 }
 
@@ -317,7 +322,7 @@ __global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int
     } else {
       b = braw[i];
       if (slave_of[i] >= 0) b += braw[slave_of[i]];
-      b = s[i] * (b - mean);
+      b = s ? s[i] * (b - mean) : (b - mean);
     }
     bh[i] = b;
   }
@@ -753,6 +758,114 @@ __global__ void k_bicg_x(int64_t n, double* x, const double* ph, const double* s
     x[i] = x[i] + alpha * ph[i] + omega * sh[i];
     r[i] = s[i] - omega * t[i];
   }
+}
+
+
+// ----------------------------------------------------------------------------- multigrid (pressure)
+// One Chebyshev step of the Jacobi-preconditioned smoother on A x = b (see pucfem_api.hip mg_smooth):
+//   first: d = c2 Dinv b (x_in = 0), x_out = d
+//   else : d = c1 d + c2 Dinv (b - A x_in), x_out = x_in + d
+// rdot != null: partial <rdot, x_out> (the <r, z> of the preconditioned CG).
+__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const double* __restrict__ val, const double* __restrict__ dinv,
+                                             const double* __restrict__ b, const double* __restrict__ xin,
+                                             double* __restrict__ xout, double* __restrict__ d, double c1, double c2,
+                                             int first, const int* ctl, const double* __restrict__ rdot, double* part) {
+  __shared__ double sh[4];
+  if (ctl && ctl[0]) return;
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double acc_rz = 0.0;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t row = s * 64 + lane;
+    double ax = 0.0;
+    if (!first) {
+      const int64_t off = A.off[s];
+      const int w = A.w[s];
+      for (int k = 0; k < w; ++k) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        ax += ldnt(val + e) * xin[ldnt(A.col + e)];
+      }
+    }
+    if (row < A.nrows) {
+      double dn, xo;
+      if (first) {
+        dn = c2 * dinv[row] * b[row];
+        xo = dn;
+      } else {
+        dn = c1 * d[row] + c2 * dinv[row] * (b[row] - ax);
+        xo = xin[row] + dn;
+      }
+      d[row] = dn;
+      xout[row] = xo;
+      if (rdot) acc_rz += rdot[row] * xo;
+    }
+  }
+  if (rdot) {
+    const double t = block_sum(acc_rz, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+  }
+}
+
+// res = b - A x
+__global__ __launch_bounds__(BS) void k_resid(SellDev A, const double* __restrict__ val, const double* __restrict__ b,
+                                              const double* __restrict__ x, double* __restrict__ res, const int* ctl) {
+  if (ctl && ctl[0]) return;
+  int64_t s0, s1;
+  block_slices(A.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = A.off[s];
+    const int w = A.w[s];
+    const int64_t row = s * 64 + lane;
+    double ax = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      ax += ldnt(val + e) * x[ldnt(A.col + e)];
+    }
+    if (row < A.nrows) res[row] = b[row] - ax;
+  }
+}
+
+// y = T x (restriction) or y += T x (prolongation, add = 1)
+__global__ __launch_bounds__(BS) void k_transfer(SellDev T, const double* __restrict__ val, const double* __restrict__ x,
+                                                 double* __restrict__ y, int add, const int* ctl) {
+  if (ctl && ctl[0]) return;
+  int64_t s0, s1;
+  block_slices(T.nslices, s0, s1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t s = s0 + wv; s < s1; s += 4) {
+    const int64_t off = T.off[s];
+    const int w = T.w[s];
+    const int64_t row = s * 64 + lane;
+    double acc = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      acc += val[e] * x[T.col[e]];
+    }
+    if (row < T.nrows) y[row] = add ? y[row] + acc : acc;
+  }
+}
+
+// coarse solve: y = Ainv x (dense, n x n row-major, replicated); one wave per row
+__global__ __launch_bounds__(BS) void k_dense_mv(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x,
+                                                 double* __restrict__ y, const int* ctl) {
+  if (ctl && ctl[0]) return;
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    const double* a = Ainv + row * n;
+    double acc = 0.0;
+    for (int64_t j = lane; j < n; j += 64) acc += a[j] * x[j];
+    acc = wave_sum(acc);
+    if (lane == 0) y[row] = acc;
+  }
+}
+
+// out[i] = full[idx[i]] (local owned + ghost entries from a replicated vector)
+__global__ void k_gather(int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ full,
+                         double* __restrict__ out, const int* ctl) {
+  if (ctl && ctl[0]) return;
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = full[idx[i]];
 }
 
 }  // namespace dev

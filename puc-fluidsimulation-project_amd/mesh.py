@@ -144,6 +144,8 @@ class Mesh:
     name: str = ""
     segments: np.ndarray | None = field(default=None, repr=False)
     segment_markers: np.ndarray | None = field(default=None, repr=False)
+    base: "Mesh | None" = field(default=None, repr=False)  # coarse mesh this one was red-refined from
+    levels: int = 0                                         # number of red refinements from `base`
 
     @property
     def N(self):
@@ -177,7 +179,8 @@ class Mesh:
         mko = np.empty(n2.value, dtype=np.int32)
         To = np.empty((t2.value, 3), dtype=np.int32)
         _lib.check(L.pucfem_refine(*args, ct.byref(n2), ct.byref(t2), _lib.dptr(Xo), _lib.iptr(mko), _lib.iptr(To)))
-        return Mesh(Xo, mko, To, name=f"{self.name}+L{levels}")
+        root = self.base if self.base is not None else self
+        return Mesh(Xo, mko, To, name=f"{self.name}+L{levels}", base=root, levels=self.levels + levels)
 
 
 def load_mesh(name="fine", refine=0):

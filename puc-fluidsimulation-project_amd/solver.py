@@ -54,6 +54,9 @@ class Tolerances:
     maxit_pres: int = 200000
     maxit_lin: int = 20000
     warm_start: bool = True
+    precond: str = "auto"  # pressure: "jacobi", "mg" (geometric multigrid, needs a refined mesh) or "auto"
+    mg_degree: int = 2
+    mg_ratio: float = 10.0
 
 
 class Context:
@@ -106,12 +109,23 @@ class Context:
         g = np.ascontiguousarray(g_tri, dtype=np.float32)
         self._c(self.L.pucfem_set_source(self.h, len(g), _lib.fptr(g)))
 
+    def set_hierarchy(self, base: Mesh, levels: int):
+        X = np.ascontiguousarray(base.coords, dtype=np.float64)
+        mk = np.ascontiguousarray(base.markers, dtype=np.int32)
+        T = np.ascontiguousarray(base.triangles, dtype=np.int32)
+        self._c(self.L.pucfem_set_hierarchy(self.h, X.shape[0], _lib.dptr(X), _lib.iptr(mk), T.shape[0],
+                                            _lib.iptr(T), int(levels)))
+        self.has_hierarchy = levels > 0
+
     def build(self, scheme, dt, nu=0.0, tol: Tolerances | None = None, capture=0.28, center=(0.5, 0.5), nstrips=0):
         tol = tol or Tolerances()
+        mg = tol.precond == "mg" or (tol.precond == "auto" and getattr(self, "has_hierarchy", False))
         p = _lib.Params(scheme=SCHEMES.get(scheme, scheme), nstrips=nstrips, dt=dt, nu=nu, rtol_visc=tol.rtol_visc,
                         rtol_pres=tol.rtol_pres, rtol_lin=tol.rtol_lin, maxit_visc=tol.maxit_visc,
                         maxit_pres=tol.maxit_pres, maxit_lin=tol.maxit_lin, warm_start=int(tol.warm_start),
-                        sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1])
+                        sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1],
+                        precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio)
+        self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
     # ---------------------------------------------------------------- fields / steps
@@ -216,6 +230,9 @@ class StokesSimulation:
         self.ctx.set_pairs(0, pairs)
         self.ctx.set_pairs(1, pairs)
         self.ctx.set_dirichlet(nodes, vals)
+        tol = tol or Tolerances()
+        if mesh.base is not None and mesh.levels > 0 and tol.precond in ("mg", "auto"):
+            self.ctx.set_hierarchy(mesh.base, mesh.levels)
         self.ctx.build(scheme, dt, self.bc.nu, tol, self.bc.capture_radius, self.bc.center, nstrips)
         self.step_count = 0
         self.history = []

@@ -209,3 +209,32 @@ def test_refined_mesh_step_properties():
     assert st[0].it_visc == 0 and st[1].it_visc > 0
     assert all(s.it_p > 0 and s.it_p2 > 0 for s in st)
     sim.close()
+
+
+def test_mg_pressure_solve_matches_oracle(golden):
+    """Geometric-multigrid-preconditioned CG (pressure) on mesh_fine refined twice vs the oracle."""
+    mesh = pf.load_mesh("fine", refine=2)
+    sim = stokes(mesh, tol=S.Tolerances(precond="mg"))
+    assert sim.ctx.precond == "mg"
+    X, T = mesh.coords, mesh.triangles
+    ps = O.PressureSolver(O.stiffness(X, T), O.lumped_mass(X, T), sim.pairs)
+    b = -20.0 * O.divergence(X, T, np.random.default_rng(3).standard_normal((mesh.N, 2)))
+    p_ref = ps.solve(b)
+    p, it = sim.ctx.solve(L.OP_PRES, b, rtol=1e-12)
+    p = p - p[ps.free].mean()
+    assert rel(p, p_ref) < 1e-8
+    assert it < 40, it
+    sim.close()
+
+
+def test_mg_and_jacobi_steps_agree():
+    """The two pressure preconditioners give the same Stokes steps (tolerance-limited)."""
+    mesh = pf.load_mesh("fine", refine=2)
+    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg"))
+    b = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="jacobi"))
+    sa, sb = a.step(3), b.step(3)
+    assert np.abs(a.u - b.u).max() < 1e-7
+    assert np.abs(a.c - b.c).max() < 1e-7
+    assert all(x.it_p < 40 for x in sa) and all(x.it_p > 200 for x in sb)
+    a.close()
+    b.close()
