@@ -196,6 +196,9 @@ struct Ctx {
   int32_t ntr = 0;
   double *trx = nullptr, *try_ = nullptr, *trs = nullptr, *d_eaten = nullptr;
   int last_it[3] = {0, 0, 0};
+  int* dits = nullptr;  // per-step iteration counts written by single-workgroup solves (no host sync)
+  int cur_step = 0;
+  bool block_cg = true;  // small operators: whole CG in one workgroup
 
   // ---- multigrid
   HostMesh coarse;
@@ -315,6 +318,29 @@ struct Ctx {
   template <int NR>
   int cg(const DevSell& A, const double* val, double* const y[NR], const double* const b[NR], double tol,
          int maxit, int which) {
+    if (world == 1 && block_cg && A.nrows <= (int64_t)CGB_THREADS * CGB_MAXR) {
+      const size_t vec = (size_t)NR * A.nrows * sizeof(double);
+      const size_t mat = (size_t)A.padded * (sizeof(double) + sizeof(int32_t));
+      const bool mat_lds = vec + mat <= (size_t)150 * 1024;
+      const size_t lds = vec + (mat_lds ? mat : 0);
+      static bool attr[3] = {false, false, false};
+      if (!attr[NR]) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_cg_block<NR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   150 * 1024));
+        attr[NR] = true;
+      }
+      int* slot = dits ? dits + 3 * cur_step + which : nullptr;
+      hipLaunchKernelGGL((k_cg_block<NR>), dim3(1), dim3(CGB_THREADS), lds, st, A.view(), val, y[0],
+                         NR > 1 ? y[1] : (double*)nullptr, b[0], NR > 1 ? b[1] : (const double*)nullptr, tol * tol,
+                         maxit, mat_lds ? 1 : 0, ctl, slot);
+      KCHK();
+      if (dits) return -1;  // collected after the step loop
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "CG residual is not finite");
+      if (h_ctl[0] != 1) throw Error(PUCFEM_ENOCONV, "CG did not converge within maxit=" + std::to_string(maxit));
+      return h_ctl[1];
+    }
     const int nb = nb_for(A.nslices);
     CgVecs<NR> v;
     for (int c = 0; c < NR; ++c) {
@@ -1474,14 +1500,35 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
     if (nsteps == 0) return;
     if (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD) {
       double* rec = c.dalloc<double>(8 * (i64)nsteps);
+      int* dits = c.dalloc<int>(3 * (i64)nsteps);
       std::vector<int32_t> its(3 * (size_t)nsteps);
-      for (int s = 0; s < nsteps; ++s) c.stokes_step(rec + 8 * s, its.data() + 3 * s);
+      c.dits = dits;
+      try {
+        for (int s = 0; s < nsteps; ++s) {
+          c.cur_step = s;
+          c.stokes_step(rec + 8 * s, its.data() + 3 * s);
+        }
+      } catch (...) {
+        c.dits = nullptr;
+        throw;
+      }
+      c.dits = nullptr;
       std::vector<double> h(8 * (size_t)nsteps);
+      std::vector<int> hd(3 * (size_t)nsteps);
       HIPCHK(hipMemcpyAsync(h.data(), rec, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(hd.data(), dits, sizeof(int) * hd.size(), hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
       if (c.timer.on) c.timer.flush();
-      HIPCHK(hipFree(rec));
-      c.allocs.erase(std::find(c.allocs.begin(), c.allocs.end(), (void*)rec));
+      for (void* q : {(void*)rec, (void*)dits}) {
+        HIPCHK(hipFree(q));
+        c.allocs.erase(std::find(c.allocs.begin(), c.allocs.end(), q));
+      }
+      for (size_t k = 0; k < its.size(); ++k)
+        if (its[k] < 0) {
+          if (hd[k] < 0) throw Error(PUCFEM_ENOCONV, "single-workgroup CG did not converge (step " +
+                                                         std::to_string(k / 3) + ")");
+          its[k] = hd[k];
+        }
       if (stats)
         for (int s = 0; s < nsteps; ++s) {
           pucfem_step_stats& o = stats[s];

@@ -868,5 +868,180 @@ __global__ void k_gather(int64_t n, const int32_t* __restrict__ idx, const doubl
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = full[idx[i]];
 }
 
+
+// ----------------------------------------------------------------------------- small-mesh CG
+// The whole CG solve in ONE workgroup of 1024 threads (16 waves) for operators of <= 4096 rows
+// (mesh_fine: 1,067): the search direction lives in LDS, y / r / q of a thread's rows in
+// registers, and -- when it fits -- the SELL matrix is staged into LDS once, so an iteration is
+// an LDS-resident SpMV plus two block reductions (no kernel boundaries, no host round trips).
+constexpr int CGB_THREADS = 1024;
+constexpr int CGB_MAXR = 4;  // rows per thread -> n <= 4096
+
+__device__ __forceinline__ double bsum1024(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w];
+  return t;
+}
+
+template <int NR>
+__global__ __launch_bounds__(CGB_THREADS) void k_cg_block(SellDev A, const double* __restrict__ val, double* y0,
+                                                          double* y1, const double* b0, const double* b1,
+                                                          double tol2, int maxit, int mat_lds, int* ctl,
+                                                          int* it_out) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ double red[16];
+  const int n = (int)A.nrows;
+  const int tid = threadIdx.x;
+  double* p = lds;                                     // NR * n
+  const int64_t pad = A.off[A.nslices];
+  double* mval = lds + NR * n;                         // pad (if mat_lds)
+  int32_t* mcol = reinterpret_cast<int32_t*>(mval + (mat_lds ? pad : 0));
+  if (mat_lds) {
+    for (int64_t e = tid; e < pad; e += CGB_THREADS) {
+      mval[e] = val[e];
+      mcol[e] = A.col[e];
+    }
+  }
+  double* yv[2] = {y0, y1};
+  const double* bv[2] = {b0, b1};
+  double y[NR][CGB_MAXR], r[NR][CGB_MAXR], q[NR][CGB_MAXR];
+  __syncthreads();
+  // r = b - A y ; p = r
+  double rr[NR], bb[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    rr[c] = 0.0;
+    bb[c] = 0.0;
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+      y[c][k] = i < n ? yv[c][i] : 0.0;
+    }
+  }
+  // stage y in p (the SpMV gathers from LDS)
+#pragma unroll
+  for (int c = 0; c < NR; ++c)
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+      if (i < n) p[c * n + i] = y[c][k];
+    }
+  __syncthreads();
+  auto spmv = [&](double (&out)[NR][CGB_MAXR]) {
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) out[c][k] = 0.0;
+      if (i < n) {
+        const int64_t s = i >> 6;
+        const int lane = i & 63;
+        const int64_t off = A.off[s];
+        const int w = A.w[s];
+        for (int kk = 0; kk < w; ++kk) {
+          const int64_t e = off + (int64_t)kk * 64 + lane;
+          const double a = mat_lds ? mval[e] : val[e];
+          const int32_t j = mat_lds ? mcol[e] : A.col[e];
+#pragma unroll
+          for (int c = 0; c < NR; ++c) out[c][k] += a * p[c * n + j];
+        }
+      }
+    }
+  };
+  spmv(q);
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    double a = 0.0, bsq = 0.0;
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+      const double bi = i < n ? bv[c][i] : 0.0;
+      r[c][k] = i < n ? bi - q[c][k] : 0.0;
+      a += r[c][k] * r[c][k];
+      bsq += bi * bi;
+    }
+    rr[c] = bsum1024(a, red);
+    bb[c] = bsum1024(bsq, red);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NR; ++c)
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+      if (i < n) p[c * n + i] = r[c][k];
+    }
+  __syncthreads();
+  int it = 0;
+  int status = 0;
+  for (;;) {
+    bool conv = true, bad = false;
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      conv = conv && (rr[c] <= tol2 * bb[c]);
+      bad = bad || !isfinite(rr[c]);
+    }
+    if (conv || bad || it >= maxit) {
+      status = conv ? 1 : (bad ? 3 : 2);
+      break;
+    }
+    spmv(q);
+    double alpha[NR], beta[NR];
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < CGB_MAXR; ++k) {
+        const int i = tid + k * CGB_THREADS;
+        if (i < n) a += p[c * n + i] * q[c][k];
+      }
+      alpha[c] = rr[c] / bsum1024(a, red);
+    }
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < CGB_MAXR; ++k) {
+        const int i = tid + k * CGB_THREADS;
+        if (i < n) {
+          y[c][k] += alpha[c] * p[c * n + i];
+          r[c][k] -= alpha[c] * q[c][k];
+          a += r[c][k] * r[c][k];
+        }
+      }
+      const double rn = bsum1024(a, red);
+      beta[c] = rn / rr[c];
+      rr[c] = rn;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NR; ++c)
+#pragma unroll
+      for (int k = 0; k < CGB_MAXR; ++k) {
+        const int i = tid + k * CGB_THREADS;
+        if (i < n) p[c * n + i] = r[c][k] + beta[c] * p[c * n + i];
+      }
+    __syncthreads();
+    ++it;
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c)
+#pragma unroll
+    for (int k = 0; k < CGB_MAXR; ++k) {
+      const int i = tid + k * CGB_THREADS;
+      if (i < n) yv[c][i] = y[c][k];
+    }
+  if (tid == 0) {
+    ctl[0] = status;
+    ctl[1] = it;
+    if (it_out) *it_out = status == 1 ? it : -it - 1;
+  }
+}
+
 }  // namespace dev
 }  // namespace pucfem
