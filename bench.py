@@ -104,8 +104,13 @@ def main():
     dt_local = time.perf_counter() - t0
     elapsed = allmax(dt_local)
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
-    ms_dir, n_dir, bytes_dir = sim.ctx.timing_get(0)
-    ms_upd, n_upd, bytes_upd = sim.ctx.timing_get(1)
+    names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl"]
+    ktab = {}
+    for k, nm in enumerate(names):
+        ms, n, b = sim.ctx.timing_get(k)
+        if n:
+            ktab[nm] = {"launches_timed": n, "avg_launch_ms": ms / n, "bytes_per_launch": b,
+                        "achieved_GBps": b / (ms / n * 1e-3) / 1e9}
     sim.ctx.timing(False)
     cg_iters = sum(2 * s.it_visc + s.it_p + s.it_p2 for s in stats)  # viscous CG is 2-RHS
     cg_iter_launches = sum(s.it_visc + s.it_p + s.it_p2 for s in stats)
@@ -137,25 +142,25 @@ def main():
                         "mix_var": stats[-1].mix_var},
         "setup_s": t_setup,
     }
-    # roofline of the dominant kernel: k_cg_dir (SpMV + direction update of the Jacobi-CG),
-    # algorithmic bytes 12*nnz + 32*NRHS*n per launch, timed with HIP events on the library stream
-    if n_dir:
-        avg_ms = ms_dir / n_dir
-        ach = bytes_dir / (avg_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel: the finest-level Chebyshev smoother step (k_cheb) when the
+    # pressure is multigrid-preconditioned, else the CG SpMV+direction kernel (k_cg_dir).  Algorithmic
+    # bytes per launch = 12*nnz (fp64 value + int32 column) + 48*N (x gather, b, d, 1/diag; x, d
+    # writes) for k_cheb; 12*nnz + 32*NRHS*N for k_cg_dir.  Timed with HIP events on the library stream.
+    dom = names[0] if names[0] in ktab else names[1]
+    if dom in ktab:
+        kd = ktab[dom]
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                d = json.load(open(pmc))
-                key = f"L{a.level}_n{world}"
-                traffic = d.get(key, {}).get("k_cg_dir_hbm_bytes_per_launch")
+                traffic = json.load(open(pmc)).get(f"L{a.level}_n{world}", {}).get(dom.split()[0])
             except Exception:
                 traffic = None
-        rec["roofline"] = {"bound": "hbm", "kernel": "k_cg_dir", "achieved": ach, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                           "bytes_per_launch": bytes_dir, "avg_launch_ms": avg_ms, "launches": n_dir,
-                           "k_cg_upd": {"avg_launch_ms": ms_upd / max(n_upd, 1),
-                                        "achieved": bytes_upd / max(ms_upd / max(n_upd, 1), 1e-9) / 1e6}}
+        rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "achieved": kd["achieved_GBps"],
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kd["achieved_GBps"] / HBM_PEAK_GBS,
+                           "traffic": traffic, "bytes_per_launch": kd["bytes_per_launch"],
+                           "avg_launch_ms": kd["avg_launch_ms"], "launches_timed": kd["launches_timed"]}
+    rec["kernels"] = ktab
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats)
     if rank == 0 and world == 1 and not a.no_secondary:
@@ -168,55 +173,40 @@ def main():
 
 
 def cpu_baseline(pf, level, stats):
-    """The oracle (numpy/scipy restatement, oracle/) timed on a bounded sample on this host.
-
-    Sample: mesh_fine refined min(level, 5) times (L5 = 894,208 nodes).  Timed pieces: Jacobi-PCG
-    iterations on the merged pressure operator and on A_visc (the HIP solver's algorithm),
-    divergence + gradient (reference-order element loops), one semi-Lagrangian step (KDTree k=10).
-    CPU seconds per step = (measured pieces) x (nnz ratio to the benchmarked level) with the GPU
-    run's own CG iteration counts."""
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    """The oracle (oracle/fem_ref.py StokesRef: the reference's step with scipy sparse direct solves
+    in place of dense LU) timed on this host for a bounded sample: 3 full StokesColor steps on mesh_fine
+    refined min(level, 4) times (225,152 nodes at x4).  steps/s is scaled to the benchmarked mesh
+    linearly in the node count -- a LOWER bound on the CPU cost (the sparse LU solves grow faster than
+    linearly), so the reported CPU rate is optimistic for the CPU."""
     import numpy as np
 
     import oracle as O
 
-    lv = min(level, 5)
+    lv = min(level, 4)
     m = pf.load_mesh("fine", refine=lv)
-    X, mk, T = m.coords, m.markers, m.triangles
-    pairs = O.filter_wall_pairs(X, O.find_boundary_pairs(X))
-    wall, inner, dirichlet, interior = O.boundary_sets(X, mk)
-    K = O.stiffness(X, T)
-    Ap = O.pressure_operator(K, pairs)
-    Av = O.visc_matrix(K, 0.05, 0.1, dirichlet)
-    rng = np.random.default_rng(0)
-    b = rng.standard_normal(m.N)
-    b -= b.mean()
-    it_s = 20
     t = time.perf_counter()
-    O.jacobi_pcg(Ap, b, np.zeros(m.N), it_s)
-    t_pcg = (time.perf_counter() - t) / it_s
+    ref = O.StokesRef(m.coords, m.markers, m.triangles, 0.05, 0.1, -2.0, 0.0, "color")
+    t_setup = time.perf_counter() - t
+    u, c = ref.initial()
+    out = ref.step(u, c)  # first step outside the timing (warm caches)
+    u, c = out["u"], out["c"]
+    n = 3
     t = time.perf_counter()
-    O.jacobi_pcg(Av, b, np.zeros(m.N), it_s)
-    t_vcg = (time.perf_counter() - t) / it_s
-    u = rng.standard_normal((m.N, 2))
-    t = time.perf_counter()
-    O.divergence(X, T, u)
-    O.gradient(X, T, u[:, 0])
-    t_dg = (time.perf_counter() - t) / 2
-    c0 = (X[:, 0] < 0.5).astype(float)
-    t = time.perf_counter()
-    O.sl_advect(c0, 0.02 * u, 0.05, X, T)
-    t_sl = time.perf_counter() - t
-    scale = 4.0 ** (level - lv)  # nnz / nodes / triangles all grow 4x per red refinement
-    it_p = np.mean([s.it_p + s.it_p2 for s in stats])
-    it_v = np.mean([s.it_visc for s in stats])
-    sec_step = scale * (it_p * t_pcg + 2 * it_v * t_vcg + 5 * t_dg + t_sl)
-    return {"value": 1.0 / sec_step, "unit": "timesteps/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle (numpy/scipy, 1 thread) on mesh_fine x{lv} ({m.N} nodes): "
-                       f"{it_s} Jacobi-PCG iters each of the pressure and viscous operators, div+grad, one SL "
-                       f"step; scaled x{scale:g} to x{level} with the GPU run's CG iterations/step "
-                       f"(p+p2 {it_p:.0f}, visc {it_v:.0f})"),
-            "sample_seconds": {"pcg_iter": t_pcg, "visc_iter": t_vcg, "div_or_grad": t_dg, "sl": t_sl}}
+    for _ in range(n):
+        out = ref.step(u, c)
+        u, c = out["u"], out["c"]
+    sps = n / (time.perf_counter() - t)
+    n_full = stats_nodes(pf, level)
+    scale = m.N / n_full
+    return {"value": sps * scale, "unit": "timesteps/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle StokesRef (scipy splu solves, numpy element loops, KDTree SL; 1 thread) on "
+                       f"mesh_fine x{lv} ({m.N} nodes): {n} steps at {sps:.4f} steps/s, factorisation setup "
+                       f"{t_setup:.1f}s excluded; scaled x{scale:.5f} (node ratio) to x{level}")}
+
+
+def stats_nodes(pf, level):
+    n = {0: 1067, 5: 894208, 7: 14230528}.get(level)
+    return n if n is not None else pf.load_mesh("fine", refine=level).N
 
 
 def secondary_fine(pf, steps):

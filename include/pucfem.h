@@ -168,7 +168,8 @@ int pucfem_mixing_index(void* ctx, const double* c, double* out3);
 /* ---- measurement ------------------------------------------------------------------ */
 /* HIP-event timing of each kernel class on the context's stream (bench.py roofline). */
 int pucfem_timing_enable(void* ctx, int32_t on);
-/* kernel classes: 0 = CG SpMV+direction (dominant), 1 = CG update, 2 = div/grad, 3 = SL, 4 = other */
+/* kernel classes: 0 = multigrid Chebyshev smoother on the finest level (k_cheb), 1 = CG SpMV+direction
+   (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl) */
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);

@@ -24,6 +24,8 @@ using namespace pucfem::dev;
 
 namespace {
 
+constexpr int64_t DENSE_MAX = 1500;  // small-mesh direct-solve threshold (mesh_fine: 1,067 nodes)
+
 struct Error : std::runtime_error {
   int code;
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
@@ -199,6 +201,15 @@ struct Ctx {
   int* dits = nullptr;  // per-step iteration counts written by single-workgroup solves (no host sync)
   int cur_step = 0;
   bool block_cg = true;  // small operators: whole CG in one workgroup
+  // small meshes (N <= DENSE_MAX, one rank): both linear solves are dense direct solves with
+  // precomputed inverses -- the reference's np.linalg.solve, factorised once instead of per call
+  bool dense = false;
+  double *dVinv = nullptr, *dPinv = nullptr;
+  // small meshes: one StokesColor/StokesFood step captured once into a hipGraph and replayed
+  bool graph_mode = false;
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  double* gstats = nullptr;
 
   // ---- multigrid
   HostMesh coarse;
@@ -214,6 +225,8 @@ struct Ctx {
   ~Ctx() {
     if (!host_only) {
       if (st) (void)hipStreamSynchronize(st);
+      if (gexec) (void)hipGraphExecDestroy(gexec);
+      if (graph) (void)hipGraphDestroy(graph);
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_pinned) (void)hipHostFree(h_pinned);
@@ -374,13 +387,13 @@ struct Ctx {
         hipLaunchKernelGGL((k_cg_dir<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, rr.p, rr.nb,
                            rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c);
         KCHK();
-        if (samp) tstop(0, e0, bytes_dir);
+        if (samp) tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, NR, false, 2);
         if (samp) tstart(e1);
         hipLaunchKernelGGL((k_cg_upd<NR>), dim3(nb), dim3(BS), 0, st, v, A.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
                            part_a);
         KCHK();
-        if (samp) tstop(1, e1, bytes_upd);
+        if (samp) tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, NR, false, 0);
         if (NR == 2) halo(cg_r[0], cg_r[1]);
         else halo(cg_r[0]);
@@ -422,9 +435,14 @@ struct Ctx {
       const bool first = cur == nullptr;
       if (!first) mg_halo(L, cur);
       const bool last = k == deg - 1;
+      const bool timed = &L == &mg.back() && !first;
+      hipEvent_t e0 = nullptr;
+      if (timed) tstart(e0);
       hipLaunchKernelGGL(k_cheb, dim3(nb), dim3(BS), 0, st, A.view(), val, L.dinv, b, first ? out : cur, out, L.d, c1,
                          c2, first ? 1 : 0, ctl, last ? rdot : (const double*)nullptr, part);
       KCHK();
+      // algorithmic bytes: matrix 12 nnz + x gather, b, d, dinv reads + x, d writes (8 B each per row)
+      if (timed) tstop(0, e0, 12.0 * (double)A.nnz + 48.0 * (double)A.nrows);
       cur = out;
     }
     return cur;
@@ -511,7 +529,7 @@ struct Ctx {
                            rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c, rr.p, rr.nb,
                            rr.stride);
         KCHK();
-        tstop(0, e0, bytes_dir);
+        tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, 1, false, 2);
         tstart(e1);
         CgVecs<1> vu = v;
@@ -519,7 +537,7 @@ struct Ctx {
         hipLaunchKernelGGL((k_cg_upd<1>), dim3(nb), dim3(BS), 0, st, vu, dPp.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
                            part_a);
         KCHK();
-        tstop(1, e1, bytes_upd);
+        tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, 1, false, 0);
         halo(cg_r[0]);
         vcycle((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
@@ -548,6 +566,14 @@ struct Ctx {
   }
   int viscous(int& iters) {  // StokesColor.py:540-547
     const i64 n = lp.n_own;
+    if (dense) {  // u* = A_visc^-1 (u + DT * 0)
+      hipLaunchKernelGGL(k_dense_mv2, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dVinv, ux, uy,
+                         usx, usy);
+      KCHK();
+      iters = 0;
+      bc(usx, usy);
+      return 0;
+    }
     hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy);
     KCHK();
     double* y[2] = {yvx, yvy};
@@ -567,19 +593,24 @@ struct Ctx {
     hipLaunchKernelGGL(k_div, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, ax, ay, das1, out, dmp,
                        -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
     KCHK();
-    tstop(2, e, 20.0 * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
+    tstop(3, e, 20.0 * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
   }
   int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
     const int nb = nb_for(dP.nslices);
     Red sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
     const i64 n = lp.n_own;
-    const double* sc = use_mg ? nullptr : dsp;  // the MG path solves the unscaled system
+    const double* sc = (use_mg || dense) ? nullptr : dsp;  // MG and dense paths solve the unscaled system
     hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
                        sb.p, sb.nb, 1.0 / (double)n_free, bh);
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     int it;
-    if (use_mg) {
+    if (dense) {
+      hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
+                         (const int*)nullptr);
+      KCHK();
+      it = 0;
+    } else if (use_mg) {
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
     } else {
       double* y[1] = {yst};
@@ -599,7 +630,7 @@ struct Ctx {
     hipLaunchKernelGGL(k_grad_proj, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, pp, das1, prm.dt, mode, ddir,
                        usx, usy, ux, uy);
     KCHK();
-    tstop(2, e, 20.0 * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
+    tstop(3, e, 20.0 * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
   }
 
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
@@ -625,8 +656,12 @@ struct Ctx {
       hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, cgrid, lp.r0, lp.n_own, ux,
                          uy, prm.dt, c_full, c_new, dwmix, (int32_t*)nullptr, part_a);
       KCHK();
-      tstop(3, e, 8.0 * 6 * (double)lp.n_own);
-      std::swap(c_full, c_new);
+      tstop(4, e, 8.0 * 6 * (double)lp.n_own);
+      if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
+        HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+      } else {
+        std::swap(c_full, c_new);
+      }
       allgather_full(c_full);
       reduce_into(part_a, nb, 3, false, 2);  // sum wc, sum w, not-found
       hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
@@ -1050,6 +1085,28 @@ void build(Ctx& c) {
       }
     }
   }
+  c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1;
+  if (c.dense) {
+    // A_visc^-1 and the pseudo-inverse of the merged pressure operator (constants on the free dofs
+    // regularised, as for the multigrid coarse level)
+    std::vector<double> Dv(N * N, 0.0), Dp(N * N, 0.0);
+    for (i64 r = 0; r < N; ++r) {
+      for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) Dv[r * N + c.P.col[k]] = c.Kv[k];
+      for (i64 k = c.Pp.rowptr[r]; k < c.Pp.rowptr[r + 1]; ++k) Dp[r * N + c.Pp.col[k]] += c.Pp.val[k];
+    }
+    double dsum = 0.0;
+    for (i64 r = 0; r < N; ++r)
+      if (c.master_of[r] < 0) dsum += Dp[r * N + r];
+    const double cc = dsum / (double)c.n_free / (double)c.n_free;
+    for (i64 i = 0; i < N; ++i)
+      if (c.master_of[i] < 0)
+        for (i64 j = 0; j < N; ++j)
+          if (c.master_of[j] < 0) Dp[i * N + j] += cc;
+    require(spd_inverse(Dv, N), "A_visc is not SPD");
+    require(spd_inverse(Dp, N), "regularised pressure operator is not SPD");
+    c.dVinv = c.upload(Dv);
+    c.dPinv = c.upload(Dp);
+  }
   if (literal) {
     dsell(c.sLit, c.Lit, c.dLit);
     sell_values(c.Lit, lp, c.sLit, c.Lit.val, tmp);
@@ -1356,6 +1413,13 @@ int pucfem_build_operators(void* ctx, const pucfem_params* prm) {
     Ctx& c = *C(ctx);
     c.prm = *prm;
     c.built = false;
+    if (c.gexec) {
+      (void)hipGraphExecDestroy(c.gexec);
+      (void)hipGraphDestroy(c.graph);
+      c.gexec = nullptr;
+      c.graph = nullptr;
+      c.graph_mode = false;
+    }
     build(c);
   });
 }
@@ -1502,17 +1566,44 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       double* rec = c.dalloc<double>(8 * (i64)nsteps);
       int* dits = c.dalloc<int>(3 * (i64)nsteps);
       std::vector<int32_t> its(3 * (size_t)nsteps);
-      c.dits = dits;
-      try {
-        for (int s = 0; s < nsteps; ++s) {
-          c.cur_step = s;
-          c.stokes_step(rec + 8 * s, its.data() + 3 * s);
+      if (c.dense && !c.timer.on) {
+        // direct-solve small-mesh path: every step is the same sequence of ~25 launches with no
+        // host synchronisation -> capture it once, replay it per step
+        if (!c.gexec) {
+          c.gstats = c.dalloc<double>(8);
+          HIPCHK(hipStreamSynchronize(c.st));
+          c.graph_mode = true;
+          int32_t tmp[3];
+          HIPCHK(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
+          try {
+            c.stokes_step(c.gstats, tmp);
+          } catch (...) {
+            hipGraph_t g;
+            (void)hipStreamEndCapture(c.st, &g);
+            c.graph_mode = false;
+            throw;
+          }
+          HIPCHK(hipStreamEndCapture(c.st, &c.graph));
+          HIPCHK(hipGraphInstantiate(&c.gexec, c.graph, nullptr, nullptr, 0));
         }
-      } catch (...) {
+        for (int s = 0; s < nsteps; ++s) {
+          HIPCHK(hipGraphLaunch(c.gexec, c.st));
+          HIPCHK(hipMemcpyAsync(rec + 8 * s, c.gstats, 8 * sizeof(double), hipMemcpyDeviceToDevice, c.st));
+        }
+      } else {
+        c.graph_mode = c.gexec != nullptr;  // once captured, keep c in its fixed buffer
+        c.dits = dits;
+        try {
+          for (int s = 0; s < nsteps; ++s) {
+            c.cur_step = s;
+            c.stokes_step(rec + 8 * s, its.data() + 3 * s);
+          }
+        } catch (...) {
+          c.dits = nullptr;
+          throw;
+        }
         c.dits = nullptr;
-        throw;
       }
-      c.dits = nullptr;
       std::vector<double> h(8 * (size_t)nsteps);
       std::vector<int> hd(3 * (size_t)nsteps);
       HIPCHK(hipMemcpyAsync(h.data(), rec, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c.st));

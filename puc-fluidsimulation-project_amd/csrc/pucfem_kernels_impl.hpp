@@ -762,6 +762,40 @@ __global__ void k_bicg_x(int64_t n, double* x, const double* ph, const double* s
 
 
 // ----------------------------------------------------------------------------- multigrid (pressure)
+// sum_k A[row, k] x[col_k] for one SELL slice lane: entry loop unrolled to WMAX (index / value loads
+// issued before the dependent gathers), matrix streamed with non-temporal loads.
+template <int WMAX>
+__device__ __forceinline__ double sell_row_dot(const SellDev& A, const double* __restrict__ val,
+                                               const double* __restrict__ x, int64_t s, int lane) {
+  const int64_t off = A.off[s];
+  const int w = A.w[s];
+  double acc = 0.0;
+  if (w <= WMAX) {
+    int32_t cj[WMAX];
+    double a[WMAX];
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k) {
+      if (k < w) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        cj[k] = ldnt(A.col + e);
+        a[k] = ldnt(val + e);
+      } else {
+        cj[k] = 0;
+        a[k] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k)
+      if (k < w) acc += a[k] * x[cj[k]];
+  } else {
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      acc += ldnt(val + e) * x[ldnt(A.col + e)];
+    }
+  }
+  return acc;
+}
+
 // One Chebyshev step of the Jacobi-preconditioned smoother on A x = b (see pucfem_api.hip mg_smooth):
 //   first: d = c2 Dinv b (x_in = 0), x_out = d
 //   else : d = c1 d + c2 Dinv (b - A x_in), x_out = x_in + d
@@ -778,15 +812,7 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const double* __restrict
   double acc_rz = 0.0;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = s * 64 + lane;
-    double ax = 0.0;
-    if (!first) {
-      const int64_t off = A.off[s];
-      const int w = A.w[s];
-      for (int k = 0; k < w; ++k) {
-        const int64_t e = off + (int64_t)k * 64 + lane;
-        ax += ldnt(val + e) * xin[ldnt(A.col + e)];
-      }
-    }
+    const double ax = first ? 0.0 : sell_row_dot<8>(A, val, xin, s, lane);
     if (row < A.nrows) {
       double dn, xo;
       if (first) {
@@ -815,14 +841,8 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, const double* __restric
   block_slices(A.nslices, s0, s1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t off = A.off[s];
-    const int w = A.w[s];
     const int64_t row = s * 64 + lane;
-    double ax = 0.0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      ax += ldnt(val + e) * x[ldnt(A.col + e)];
-    }
+    const double ax = sell_row_dot<8>(A, val, x, s, lane);
     if (row < A.nrows) res[row] = b[row] - ax;
   }
 }
@@ -1040,6 +1060,29 @@ __global__ __launch_bounds__(CGB_THREADS) void k_cg_block(SellDev A, const doubl
     ctl[0] = status;
     ctl[1] = it;
     if (it_out) *it_out = status == 1 ? it : -it - 1;
+  }
+}
+
+
+// dense 2-RHS matvec (small-mesh direct viscous solve): y0 = A x0, y1 = A x1; one wave per row
+__global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x0,
+                                                  const double* __restrict__ x1, double* __restrict__ y0,
+                                                  double* __restrict__ y1) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    const double* a = Ainv + row * n;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t j = lane; j < n; j += 64) {
+      const double v = a[j];
+      s0 += v * x0[j];
+      s1 += v * x1[j];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+      y0[row] = s0;
+      y1[row] = s1;
+    }
   }
 }
 
