@@ -120,6 +120,9 @@ int pucfem_ctx_create(int32_t device, void** out_ctx);
 int pucfem_rccl_unique_id(uint8_t* out_id /* PUCFEM_UNIQUE_ID_BYTES */);
 int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const uint8_t* unique_id,
                            void** out_ctx);
+/* A unique id that starts with the 16 bytes "PUCFEM-LOCALCOMM" selects the in-process test backend:
+   `world` contexts created from host threads of ONE process exchange data with device-to-device
+   copies instead of RCCL (multi-rank validation on a one-GPU machine). */
 int pucfem_ctx_destroy(void* ctx);
 
 /* ---- mesh + boundary conditions (replaces readNode/readEle globals, StokesColor.py:437-464) */

@@ -15,12 +15,22 @@
 #include <vector>
 
 #include "pucfem.h"
+#include "pucfem_comm.hpp"
 #include "pucfem_host.hpp"
 #include "pucfem_kernels.hpp"
 #include "pucfem_kernels_impl.hpp"
 
 using namespace pucfem;
 using namespace pucfem::dev;
+
+// LocalComm reduction (fixed rank order -> identical result on every rank)
+__global__ void pucfem::k_comm_reduce(int world, int is_max, size_t n, const double* const* bufs, double* out) {
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) {
+    double a = bufs[0][i];
+    for (int r = 1; r < world; ++r) a = is_max ? fmax(a, bufs[r][i]) : a + bufs[r][i];
+    out[i] = a;
+  }
+}
 
 namespace {
 
@@ -127,7 +137,7 @@ struct Ctx {
   int device = -1;
   bool host_only = true;
   int rank = 0, world = 1;
-  ncclComm_t comm = nullptr;
+  std::unique_ptr<Comm> comm;
   hipStream_t st = nullptr;
   std::vector<void*> allocs;
   Timer timer;
@@ -230,7 +240,7 @@ struct Ctx {
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_pinned) (void)hipHostFree(h_pinned);
-      if (comm) (void)ncclCommDestroy(comm);
+      comm.reset();
       if (st) (void)hipStreamDestroy(st);
     }
   }
@@ -283,7 +293,7 @@ struct Ctx {
     double* buf = redbuf + 8 * slot;
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
     KCHK();
-    NCCLCHK(ncclAllReduce(buf, buf, nv, ncclDouble, is_max ? ncclMax : ncclSum, comm, st));
+    comm->allreduce(buf, nv, is_max, st);
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
@@ -291,7 +301,7 @@ struct Ctx {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, vals + slot);
     KCHK();
     if (world > 1)
-      NCCLCHK(ncclAllReduce(vals + slot, vals + slot, nv, ncclDouble, is_max ? ncclMax : ncclSum, comm, st));
+      comm->allreduce(vals + slot, nv, is_max, st);
   }
   // refresh the ghost entries of up to two local vectors
   void halo(double* a, double* b = nullptr) { halo_lp(lp, dsend, dsendbuf, nsend, a, b); }
@@ -301,16 +311,16 @@ struct Ctx {
       hipLaunchKernelGGL(k_pack, dim3(grid_ew(ns)), dim3(BS), 0, st, ns, sidx, a, b, sbuf);
       KCHK();
     }
-    NCCLCHK(ncclGroupStart());
+    comm->group_start();
     for (size_t k = 0; k < P.send_peer.size(); ++k) {
-      NCCLCHK(ncclSend(sbuf + P.send_off[k], P.send_cnt[k], ncclDouble, P.send_peer[k], comm, st));
-      if (b) NCCLCHK(ncclSend(sbuf + ns + P.send_off[k], P.send_cnt[k], ncclDouble, P.send_peer[k], comm, st));
+      comm->send(sbuf + P.send_off[k], P.send_cnt[k], P.send_peer[k], st);
+      if (b) comm->send(sbuf + ns + P.send_off[k], P.send_cnt[k], P.send_peer[k], st);
     }
     for (size_t k = 0; k < P.recv_peer.size(); ++k) {
-      NCCLCHK(ncclRecv(a + P.n_own + P.recv_off[k], P.recv_cnt[k], ncclDouble, P.recv_peer[k], comm, st));
-      if (b) NCCLCHK(ncclRecv(b + P.n_own + P.recv_off[k], P.recv_cnt[k], ncclDouble, P.recv_peer[k], comm, st));
+      comm->recv(a + P.n_own + P.recv_off[k], P.recv_cnt[k], P.recv_peer[k], st);
+      if (b) comm->recv(b + P.n_own + P.recv_off[k], P.recv_cnt[k], P.recv_peer[k], st);
     }
-    NCCLCHK(ncclGroupEnd());
+    comm->group_end(st);
   }
   void mg_halo(MgLevel& L, double* a) {
     if (&L == &mg.back()) halo(a);
@@ -319,12 +329,12 @@ struct Ctx {
   // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
   void allgather_full(double* full) {
     if (world == 1) return;
-    NCCLCHK(ncclGroupStart());
+    comm->group_start();
     for (int r = 0; r < world; ++r) {
       const i64 o = row_start[r], n = row_start[r + 1] - row_start[r];
-      NCCLCHK(ncclBroadcast(full + o, full + o, n, ncclDouble, r, comm, st));
+      comm->bcast(full + o, n, r, st);
     }
-    NCCLCHK(ncclGroupEnd());
+    comm->group_end(st);
   }
 
   // ------------------------------------------------------------------ CG
@@ -464,10 +474,9 @@ struct Ctx {
         KCHK();
       } else {
         HIPCHK(hipMemcpyAsync(cfull_b + L.lp.r0, b, sizeof(double) * L.lp.n_own, hipMemcpyDeviceToDevice, st));
-        NCCLCHK(ncclGroupStart());
-        for (int r = 0; r < world; ++r)
-          NCCLCHK(ncclBroadcast(cfull_b + L.rs[r], cfull_b + L.rs[r], L.rs[r + 1] - L.rs[r], ncclDouble, r, comm, st));
-        NCCLCHK(ncclGroupEnd());
+        comm->group_start();
+        for (int r = 0; r < world; ++r) comm->bcast(cfull_b + L.rs[r], L.rs[r + 1] - L.rs[r], r, st);
+        comm->group_end(st);
         hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0, dAinv,
                            cfull_b, cfull_x, ctl);
         hipLaunchKernelGGL(k_gather, dim3(grid_ew(L.nloc)), dim3(BS), 0, st, L.nloc, cgather, cfull_x, xa, ctl);
@@ -1307,9 +1316,19 @@ int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const ui
     c.rank = rank;
     c.world = world;
     if (world > 1 && !c.host_only) {
-      ncclUniqueId id;
-      std::memcpy(&id, uid, sizeof(id));
-      NCCLCHK(ncclCommInitRank(&c.comm, world, id, rank));
+      static const char kLocal[] = "PUCFEM-LOCALCOMM";
+      if (std::memcmp(uid, kLocal, sizeof(kLocal) - 1) == 0) {
+        // test backend: W ranks as W contexts (host threads) of one process
+        c.comm = std::make_unique<LocalComm>(std::string((const char*)uid, PUCFEM_UNIQUE_ID_BYTES), world, rank);
+      } else {
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof(id));
+        try {
+          c.comm = std::make_unique<NcclComm>(world, id, rank);
+        } catch (const std::exception& e) {
+          throw Error(PUCFEM_ENCCL, e.what());
+        }
+      }
     }
   });
   if (rc) {

@@ -1,0 +1,87 @@
+"""Multi-rank path on ONE GPU: W contexts in W host threads exchange halos / reductions /
+broadcasts through the LocalComm backend (same call sequence as RCCL, device-to-device copies).
+The partitioned run must reproduce the single-rank run (CG reductions are summed in a different
+order across ranks, hence the 1e-9 tolerance instead of bit equality)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import has_gpu, load_pkg
+
+pytestmark = pytest.mark.gpu
+pf = load_pkg()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not has_gpu():
+        pytest.fail("no HIP device visible")
+
+
+def run_ranks(mesh, world, scheme, tol, steps, bc, dt):
+    uid = b"PUCFEM-LOCALCOMM" + os.urandom(112)
+    out = [None] * world
+    errs = []
+
+    def worker(r):
+        try:
+            sim = pf.StokesSimulation(mesh, bc, dt, scheme, device=0, tol=tol, dist=(r, world, uid))
+            st = sim.step(steps)
+            res = {"u": sim.u, "info": sim.ctx.info(), "stats": st}
+            if scheme == "color":
+                res["c"] = sim.c
+            else:
+                res["tracers"] = sim.tracers
+                res["status"] = sim.tracer_status
+            out[r] = res
+            sim.close()
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    assert not errs, errs
+    assert all(o is not None for o in out)
+    return out
+
+
+@pytest.mark.parametrize("world,precond", [(2, "mg"), (3, "mg"), (2, "jacobi")])
+def test_color_partitioned_matches_single_rank(world, precond):
+    mesh = pf.load_mesh("fine", refine=3)
+    tol = pf.Tolerances(rtol_pres=1e-12, rtol_visc=1e-13, precond=precond)
+    bc = pf.SquirmerBC()
+    out = run_ranks(mesh, world, "color", tol, 3, bc, 0.05)
+    assert sum(o["info"]["n_own"] for o in out) == mesh.N
+    assert all(o["info"]["n_ghost"] > 0 for o in out)
+    u = sum(o["u"] for o in out)  # every rank fills its owned rows
+    ref = pf.StokesSimulation(mesh, bc, 0.05, "color", tol=tol)
+    st = ref.step(3)
+    assert np.abs(u - ref.u).max() < 1e-9
+    for o in out:
+        assert np.abs(o["c"] - ref.c).max() < 1e-9  # replicated dye field
+        for a, b in zip(o["stats"], st):
+            assert abs(a.max_div_star - b.max_div_star) < 1e-9 * b.max_div_star
+            assert abs(a.mix_var - b.mix_var) < 1e-12
+    ref.close()
+
+
+def test_food_partitioned_matches_single_rank():
+    mesh = pf.load_mesh("fine", refine=2)
+    tol = pf.Tolerances(rtol_pres=1e-12, rtol_visc=1e-13)
+    bc = pf.SquirmerBC(B2=-5.0, nu=1.0)
+    out = run_ranks(mesh, 2, "food", tol, 3, bc, 0.01)
+    ref = pf.StokesSimulation(mesh, bc, 0.01, "food", tol=tol)
+    st = ref.step(3)
+    tr = ref.tracers
+    for o in out:
+        assert np.array_equal(np.isnan(o["tracers"]), np.isnan(tr))
+        ok = ~np.isnan(tr)
+        assert np.abs(o["tracers"][ok] - tr[ok]).max() < 1e-9
+        assert np.array_equal(o["status"], ref.tracer_status)
+        assert o["stats"][-1].eaten == st[-1].eaten
+    ref.close()
