@@ -71,6 +71,7 @@ typedef struct pucfem_params {
                           (needs pucfem_set_hierarchy) */
   int32_t mg_degree;   /* Chebyshev smoothing steps per level, pre and post (2) */
   double mg_ratio;     /* Chebyshev interval [lmax / mg_ratio, lmax] (10) */
+  int32_t mg_post;     /* post-smoothing steps (0: same as mg_degree) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */

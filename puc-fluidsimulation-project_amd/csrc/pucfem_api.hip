@@ -426,13 +426,13 @@ struct Ctx {
   // Chebyshev smoothing of degree prm.mg_degree on [lmax / mg_ratio, lmax] for D^-1 A.
   // x_in (nullable: zero initial guess) -> returns the buffer holding the result.
   double* mg_smooth(MgLevel& L, const DevSell& A, const double* val, const double* b, double* xin, double* xa,
-                    double* xb, const double* rdot, double* part) {
+                    double* xb, const double* rdot, double* part, int deg_req = 0) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
     const int nb = nb_for(A.nslices);
     double* cur = xin;
-    const int deg = std::max(1, prm.mg_degree);
+    const int deg = std::max(1, deg_req > 0 ? deg_req : prm.mg_degree);
     for (int k = 0; k < deg; ++k) {
       double c1 = 0.0, c2 = 1.0 / theta;
       if (k > 0) {
@@ -499,7 +499,7 @@ struct Ctx {
                        ctl);
     KCHK();
     double* other = (x == xa) ? xb : xa;
-    double* out = mg_smooth(L, A, Av, b, x, x, other, rdot, part);
+    double* out = mg_smooth(L, A, Av, b, x, x, other, rdot, part, prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
     if (finest && out != z) HIPCHK(hipMemcpyAsync(z, out, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
     return out;
   }

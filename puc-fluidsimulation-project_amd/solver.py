@@ -57,6 +57,7 @@ class Tolerances:
     precond: str = "auto"  # pressure: "jacobi", "mg" (geometric multigrid, needs a refined mesh) or "auto"
     mg_degree: int = 2
     mg_ratio: float = 10.0
+    mg_post: int = 0
 
 
 class Context:
@@ -124,7 +125,7 @@ class Context:
                         rtol_pres=tol.rtol_pres, rtol_lin=tol.rtol_lin, maxit_visc=tol.maxit_visc,
                         maxit_pres=tol.maxit_pres, maxit_lin=tol.maxit_lin, warm_start=int(tol.warm_start),
                         sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1],
-                        precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio)
+                        precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio, mg_post=tol.mg_post)
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
