@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
     ap.add_argument("--rtol-pres", type=float, default=1e-8)
+    ap.add_argument("--mg-double", action="store_true", help="fp64 V-cycle instead of the fp32 one")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -85,7 +86,7 @@ def main():
 
     t_setup = time.time()
     mesh = pf.load_mesh("fine", refine=a.level)
-    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond)
+    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond, mg_single=not a.mg_double)
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup
@@ -104,7 +105,9 @@ def main():
     dt_local = time.perf_counter() - t0
     elapsed = allmax(dt_local)
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
-    names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl"]
+    names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl",
+             "k_resid (MG residual, finest level)", "k_transfer (restriction from finest)",
+             "k_transfer (prolongation to finest)"]
     ktab = {}
     for k, nm in enumerate(names):
         ms, n, b = sim.ctx.timing_get(k)
@@ -127,6 +130,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
+        "precond_dtype": "f64" if a.mg_double or a.precond != "mg" else "f32",
         "data": "synthetic (deterministic red-refined mesh_fine, reference initial state)",
         "config": {
             "workload": f"StokesColor neutral squirmer step, mesh_fine refined x{a.level}",
@@ -144,8 +148,10 @@ def main():
     }
     # roofline of the dominant kernel: the finest-level Chebyshev smoother step (k_cheb) when the
     # pressure is multigrid-preconditioned, else the CG SpMV+direction kernel (k_cg_dir).  Algorithmic
-    # bytes per launch = 12*nnz (fp64 value + int32 column) + 48*N (x gather, b, d, 1/diag; x, d
-    # writes) for k_cheb; 12*nnz + 32*NRHS*N for k_cg_dir.  Timed with HIP events on the library stream.
+    # bytes per launch for k_cheb in the fp32 cycle = 8*nnz (fp32 value + int32 column) + per row 4 B
+    # each for x (gathered once), dinv, d read, d write, x write + 8 B fp64 rhs (the CG residual), plus
+    # 8 B r for <r, z> and fp64 z on the last post-smoothing step (12*nnz + 48*N in the fp64 cycle);
+    # 12*nnz + 32*NRHS*N for k_cg_dir.  Timed with HIP events on the library stream.
     dom = names[0] if names[0] in ktab else names[1]
     if dom in ktab:
         kd = ktab[dom]

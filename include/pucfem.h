@@ -72,6 +72,8 @@ typedef struct pucfem_params {
   int32_t mg_degree;   /* Chebyshev smoothing steps per level, pre and post (2) */
   double mg_ratio;     /* Chebyshev interval [lmax / mg_ratio, lmax] (10) */
   int32_t mg_post;     /* post-smoothing steps (0: same as mg_degree) */
+  int32_t mg_single;   /* 1: fp32 V-cycle (values, vectors, halos) inside the fp64 CG */
+  int64_t mg_rep_nodes; /* multi-rank: coarse levels up to this many nodes are replicated (0: 300000) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -173,7 +175,9 @@ int pucfem_mixing_index(void* ctx, const double* c, double* out3);
 /* HIP-event timing of each kernel class on the context's stream (bench.py roofline). */
 int pucfem_timing_enable(void* ctx, int32_t on);
 /* kernel classes: 0 = multigrid Chebyshev smoother on the finest level (k_cheb), 1 = CG SpMV+direction
-   (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl) */
+   (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl),
+   5 = multigrid residual on the finest level (k_resid), 6 = restriction from the finest level,
+   7 = prolongation to the finest level (k_transfer) */
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);

@@ -75,9 +75,10 @@ struct Timer {
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
-  double ms[5] = {0, 0, 0, 0, 0};
-  double bytes[5] = {0, 0, 0, 0, 0};
-  int64_t n[5] = {0, 0, 0, 0, 0};
+  static constexpr int NCLS = 8;
+  double ms[NCLS] = {};
+  double bytes[NCLS] = {};
+  int64_t n[NCLS] = {};
   hipEvent_t get() {
     if (pool.empty()) {
       hipEvent_t e;
@@ -110,6 +111,12 @@ struct Timer {
   }
 };
 
+template <typename T>
+struct MgBufs {
+  T *Aval = nullptr, *Prval = nullptr, *Rval = nullptr, *dinv = nullptr;
+  T *x = nullptr, *x2 = nullptr, *b = nullptr, *d = nullptr, *res = nullptr, *sendbuf = nullptr;
+};
+
 // One level of the geometric multigrid hierarchy (pressure preconditioner).  Level 0 is the
 // coarsest (the caller's base mesh, solved densely), the last level is the simulation mesh.
 struct MgLevel {
@@ -125,12 +132,20 @@ struct MgLevel {
   // device
   Sell sA, sPr, sR;         // host SELL images (built with the plans, also on host-only contexts)
   DevSell dA, dPr, dR;
-  double *Aval = nullptr, *Prval = nullptr, *Rval = nullptr, *dinv = nullptr;
-  double *x = nullptr, *x2 = nullptr, *b = nullptr, *d = nullptr, *res = nullptr;
+  MgBufs<double> f64;       // the V-cycle's values and vectors: one of the two sets is allocated
+  MgBufs<float> f32;        // (fp32 = the mixed-precision cycle, prm.mg_single)
   int32_t* dsend = nullptr;
-  double* dsendbuf = nullptr;
   i64 nsend = 0, nloc = 0;
+  // multi-rank runs: coarse levels of <= mg_rep_nodes nodes are REPLICATED (every rank holds and
+  // smooths the whole level, no halos); the restriction into the finest replicated level computes
+  // the rows of the strip partition (rs) and an all-gather (broadcast group) completes the vector
+  bool rep = false;
+  i64 r_r0 = 0;  // first row of this level's restriction operator (rows live on level l-1)
+  i64 own0(int rank) const { return rep ? 0 : rs[rank]; }
 };
+template <typename T> MgBufs<T>& bufs(MgLevel& L);
+template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
+template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
 struct Ctx {
   std::string err;
@@ -228,8 +243,7 @@ struct Ctx {
   std::vector<MgLevel> mg;
   double* dKp_raw = nullptr;        // unscaled finest pressure operator on sPp
   double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
-  double *cfull_b = nullptr, *cfull_x = nullptr;
-  int32_t* cgather = nullptr;       // coarsest local (owned + ghost) -> coarsest internal id
+  bool mg_single = false;                        // fp32 V-cycle
   double* z = nullptr;              // preconditioned residual (finest)
 
   ~Ctx() {
@@ -268,6 +282,9 @@ struct Ctx {
   }
 
   static int nb_for(i64 nslices) { return (int)std::max<i64>(1, std::min<i64>(MAXB, (nslices + 3) / 4)); }
+  // grid of the V-cycle kernels that produce no partials (more waves in flight than MAXB blocks)
+  int mg_nb_max = 4096;
+  int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
@@ -305,10 +322,11 @@ struct Ctx {
   }
   // refresh the ghost entries of up to two local vectors
   void halo(double* a, double* b = nullptr) { halo_lp(lp, dsend, dsendbuf, nsend, a, b); }
-  void halo_lp(const LocalPlan& P, const int32_t* sidx, double* sbuf, i64 ns, double* a, double* b = nullptr) {
+  template <typename T>
+  void halo_lp(const LocalPlan& P, const int32_t* sidx, T* sbuf, i64 ns, T* a, T* b = nullptr) {
     if (world == 1 || (P.send_peer.empty() && P.recv_peer.empty())) return;
     if (ns > 0) {
-      hipLaunchKernelGGL(k_pack, dim3(grid_ew(ns)), dim3(BS), 0, st, ns, sidx, a, b, sbuf);
+      hipLaunchKernelGGL(k_pack<T>, dim3(grid_ew(ns)), dim3(BS), 0, st, ns, sidx, a, b, sbuf);
       KCHK();
     }
     comm->group_start();
@@ -322,9 +340,10 @@ struct Ctx {
     }
     comm->group_end(st);
   }
-  void mg_halo(MgLevel& L, double* a) {
-    if (&L == &mg.back()) halo(a);
-    else halo_lp(L.lp, L.dsend, L.dsendbuf, L.nsend, a);
+  template <typename T>
+  void mg_halo(MgLevel& L, T* a) {
+    if (&L == &mg.back()) halo_lp(lp, dsend, bufs<T>(L).sendbuf, nsend, a);
+    else halo_lp(L.lp, L.dsend, bufs<T>(L).sendbuf, L.nsend, a);
   }
   // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
   void allgather_full(double* full) {
@@ -423,16 +442,19 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ multigrid V-cycle / PCG
-  // Chebyshev smoothing of degree prm.mg_degree on [lmax / mg_ratio, lmax] for D^-1 A.
-  // x_in (nullable: zero initial guess) -> returns the buffer holding the result.
-  double* mg_smooth(MgLevel& L, const DevSell& A, const double* val, const double* b, double* xin, double* xa,
-                    double* xb, const double* rdot, double* part, int deg_req = 0) {
+  // Chebyshev smoothing (deg steps) on [lmax / mg_ratio, lmax] for D^-1 A.
+  // x_in (nullable: zero initial guess) -> returns the buffer holding the result; with zout the
+  // last step writes its result (in fp64) to zout instead and nullptr is returned.
+  template <typename T, typename TB>
+  T* mg_smooth(MgLevel& L, const DevSell& A, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb, double* zout,
+               const double* rdot, double* part, int deg) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
-    const int nb = nb_for(A.nslices);
-    double* cur = xin;
-    const int deg = std::max(1, deg_req > 0 ? deg_req : prm.mg_degree);
+    T* cur = xin;
+    deg = std::max(1, deg);
+    const bool finest = &L == &mg.back();
+    double c20 = 0.0;
     for (int k = 0; k < deg; ++k) {
       double c1 = 0.0, c2 = 1.0 / theta;
       if (k > 0) {
@@ -441,67 +463,107 @@ struct Ctx {
         c2 = 2.0 * rho / delta;
         rho_old = rho;
       }
-      double* out = (cur == xa) ? xb : xa;
-      const bool first = cur == nullptr;
-      if (!first) mg_halo(L, cur);
+      // zero initial guess and >= 2 steps: step 0 is folded into step 1 (mode 2; b's ghosts are
+      // current, see vcycle)
+      const bool fuse = cur == nullptr && k == 0 && deg >= 2;
+      if (fuse) {
+        c20 = c2;
+        continue;
+      }
+      const int mode = (cur == nullptr && k == 0) ? 0 : (cur == nullptr ? 2 : 1);
+      T* out = (cur == xa) ? xb : xa;
+      if (mode == 1) mg_halo(L, cur);
       const bool last = k == deg - 1;
-      const bool timed = &L == &mg.back() && !first;
+      const bool timed = finest && mode != 0;
       hipEvent_t e0 = nullptr;
       if (timed) tstart(e0);
-      hipLaunchKernelGGL(k_cheb, dim3(nb), dim3(BS), 0, st, A.view(), val, L.dinv, b, first ? out : cur, out, L.d, c1,
-                         c2, first ? 1 : 0, ctl, last ? rdot : (const double*)nullptr, part);
+      const double* rd = last ? rdot : nullptr;
+      const bool toz = last && zout;
+      const int nb = rd ? nb_for(A.nslices) : nb_mg(A.nslices);
+      const T* xi = mode == 1 ? cur : nullptr;
+      if (toz)
+        hipLaunchKernelGGL((k_cheb<T, TB, double>), dim3(nb), dim3(BS), 0, st, A.view(), B.Aval, B.dinv, b, xi, zout,
+                           B.d, c1, c2, c20, mode, ctl, rd, part);
+      else
+        hipLaunchKernelGGL((k_cheb<T, TB, T>), dim3(nb), dim3(BS), 0, st, A.view(), B.Aval, B.dinv, b, xi, out, B.d,
+                           c1, c2, c20, mode, ctl, rd, part);
       KCHK();
-      // algorithmic bytes: matrix 12 nnz + x gather, b, d, dinv reads + x, d writes (8 B each per row)
-      if (timed) tstop(0, e0, 12.0 * (double)A.nnz + 48.0 * (double)A.nrows);
-      cur = out;
+      // algorithmic bytes: matrix (value + int32 column) per entry; per row x_in (mode 1) or b and
+      // dinv (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r
+      if (timed) {
+        const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
+        const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
+        tstop(0, e0, (double)(sizeof(T) + 4) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row));
+      }
+      cur = toz ? nullptr : out;
     }
     return cur;
   }
-  // z = M^-1 r on level l (b = r_l); the finest level passes rdot = r for the <r, z> partials
-  double* vcycle(int l, const double* b, const double* rdot, double* part) {
+  // z = M^-1 r on level l (b = r_l); the finest level passes rdot = r for the <r, z> partials and
+  // writes z (fp64) directly from its last smoothing step
+  template <typename T, typename TB>
+  T* vcycle(int l, const TB* b, const double* rdot, double* part) {
     MgLevel& L = mg[l];
+    MgBufs<T>& B = bufs<T>(L);
     const bool finest = l == (int)mg.size() - 1;
     const DevSell& A = finest ? dPp : L.dA;
-    const double* Av = finest ? dKp_raw : L.Aval;
-    double* xa = finest ? z : L.x;
-    double* xb = L.x2;
+    T* xa = B.x;
+    T* xb = B.x2;
     if (l == 0) {
-      // coarsest: dense pseudo-inverse, replicated on every rank
-      const i64 N0 = (i64)L.ord.new2old.size();
-      if (world == 1) {
-        hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0, dAinv, b,
-                           xa, ctl);
+      if constexpr (std::is_same<T, TB>::value) {
+        // coarsest: dense pseudo-inverse (replicated on every rank of a multi-rank run)
+        const i64 N0 = (i64)L.ord.new2old.size();
+        hipLaunchKernelGGL(k_dense_mv<T>, dim3((unsigned)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0,
+                           dAinv, b, xa, ctl);
         KCHK();
+        return xa;
       } else {
-        HIPCHK(hipMemcpyAsync(cfull_b + L.lp.r0, b, sizeof(double) * L.lp.n_own, hipMemcpyDeviceToDevice, st));
-        comm->group_start();
-        for (int r = 0; r < world; ++r) comm->bcast(cfull_b + L.rs[r], L.rs[r + 1] - L.rs[r], r, st);
-        comm->group_end(st);
-        hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0, dAinv,
-                           cfull_b, cfull_x, ctl);
-        hipLaunchKernelGGL(k_gather, dim3(grid_ew(L.nloc)), dim3(BS), 0, st, L.nloc, cgather, cfull_x, xa, ctl);
-        KCHK();
+        throw Error(PUCFEM_ESTATE, "multigrid hierarchy has a single level");
       }
-      return xa;
     }
-    double* x = mg_smooth(L, A, Av, b, nullptr, xa, xb, nullptr, nullptr);
+    if constexpr (std::is_same<T, TB>::value) {
+      // coarse levels: the fused first smoothing step reads b at ghost columns
+      if (prm.mg_degree >= 2) mg_halo(L, const_cast<T*>(b));
+    }
+    T* x = mg_smooth<T, TB>(L, A, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, prm.mg_degree);
     mg_halo(L, x);
-    hipLaunchKernelGGL(k_resid, dim3(nb_for(A.nslices)), dim3(BS), 0, st, A.view(), Av, b, x, L.res, ctl);
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    if (finest) tstart(e0);
+    hipLaunchKernelGGL((k_resid<T, TB>), dim3(nb_mg(A.nslices)), dim3(BS), 0, st, A.view(), B.Aval, b, x, B.res, ctl);
     KCHK();
-    mg_halo(L, L.res);
+    // matrix entries, x gathered once, b read, res written
+    if (finest) tstop(5, e0, (double)(sizeof(T) + 4) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB)));
+    mg_halo(L, B.res);
     MgLevel& C = mg[l - 1];
-    hipLaunchKernelGGL(k_transfer, dim3(nb_for(L.dR.nslices)), dim3(BS), 0, st, L.dR.view(), L.Rval, L.res, C.b, 0,
+    MgBufs<T>& CB = bufs<T>(C);
+    if (finest) tstart(e1);
+    const bool gather = C.rep && !L.rep && world > 1;  // into the finest replicated level
+    T* cb = gather ? CB.b + L.r_r0 : CB.b;
+    hipLaunchKernelGGL(k_transfer<T>, dim3(nb_mg(L.dR.nslices)), dim3(BS), 0, st, L.dR.view(), B.Rval, B.res, cb, 0,
                        ctl);
     KCHK();
-    double* xc = vcycle(l - 1, C.b, nullptr, nullptr);
+    // restriction: entries (value + column), fine residual read once, coarse rhs written
+    if (finest) tstop(6, e1, (double)(sizeof(T) + 4) * (double)L.dR.nnz + (double)sizeof(T) * (double)(A.nrows + L.dR.nrows));
+    if (gather) {
+      comm->group_start();
+      for (int r = 0; r < world; ++r) comm->bcast(CB.b + C.rs[r], C.rs[r + 1] - C.rs[r], r, st);
+      comm->group_end(st);
+    }
+    T* xc = vcycle<T, T>(l - 1, CB.b, nullptr, nullptr);
     mg_halo(C, xc);
-    hipLaunchKernelGGL(k_transfer, dim3(nb_for(L.dPr.nslices)), dim3(BS), 0, st, L.dPr.view(), L.Prval, xc, x, 1,
+    if (finest) tstart(e2);
+    hipLaunchKernelGGL(k_transfer<T>, dim3(nb_mg(L.dPr.nslices)), dim3(BS), 0, st, L.dPr.view(), B.Prval, xc, x, 1,
                        ctl);
     KCHK();
-    double* other = (x == xa) ? xb : xa;
-    double* out = mg_smooth(L, A, Av, b, x, x, other, rdot, part, prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
-    if (finest && out != z) HIPCHK(hipMemcpyAsync(z, out, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-    return out;
+    // prolongation: entries, coarse x read once, fine x read + written
+    if (finest) tstop(7, e2, (double)(sizeof(T) + 4) * (double)L.dPr.nnz + (double)sizeof(T) * (double)(2 * A.nrows + L.dR.nrows));
+    T* other = (x == xa) ? xb : xa;
+    return mg_smooth<T, TB>(L, A, B, b, x, x, other, finest ? z : nullptr, rdot, part,
+                            prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
+  }
+  void precondition() {  // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB
+    if (mg_single) vcycle<float, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+    else vcycle<double, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
   }
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
@@ -522,7 +584,7 @@ struct Ctx {
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
     halo(cg_r[0]);
-    vcycle((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+    precondition();
     Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
     halo(z);
     const double tol2 = tol * tol;
@@ -549,7 +611,7 @@ struct Ctx {
         tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, 1, false, 0);
         halo(cg_r[0]);
-        vcycle((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+        precondition();
         rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
         halo(z);
         std::swap(v.po[0], v.pn[0]);
@@ -615,7 +677,7 @@ struct Ctx {
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     int it;
     if (dense) {
-      hipLaunchKernelGGL(k_dense_mv, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
+      hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
                          (const int*)nullptr);
       KCHK();
       it = 0;
@@ -872,6 +934,71 @@ void build_mg_host(Ctx& c) {
 }
 
 // ------------------------------------------------------------------ operator build
+double diag_of(const Csr& A, const std::vector<double>& val, i64 g) {
+  for (i64 k = A.rowptr[g]; k < A.rowptr[g + 1]; ++k)
+    if (A.col[k] == g) return val[k];
+  return 1.0;
+}
+
+template <typename T>
+T* upload_as(Ctx& c, const std::vector<double>& v) {
+  if constexpr (std::is_same<T, double>::value) {
+    return c.upload(v);
+  } else {
+    std::vector<T> w(v.begin(), v.end());
+    return c.upload(w);
+  }
+}
+
+// device values and work vectors of every multigrid level in the V-cycle's type T.
+// kp_vals: the finest operator's SELL values (fp64, = dKp_raw), reused for fp64 cycles.
+template <typename T>
+void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
+  const int Lv = c.mg_levels;
+  std::vector<double> tmp;
+  for (int l = 0; l <= Lv; ++l) {
+    MgLevel& L = c.mg[l];
+    MgBufs<T>& B = bufs<T>(L);
+    const Csr& A = l == Lv ? c.Pp : L.Pp;
+    const i64 n = L.lp.n_own;
+    L.nloc = n + L.lp.n_ghost;
+    // 1 / diag on owned AND ghost rows (the fused first smoothing step evaluates x1 = c Dinv b at
+    // gathered columns)
+    std::vector<double> dv(L.nloc);
+    const i64 r0 = L.own0(c.rank);
+    for (i64 i = 0; i < n; ++i) dv[i] = 1.0 / diag_of(A, A.val, r0 + i);
+    for (i64 k = 0; k < L.lp.n_ghost; ++k) dv[n + k] = 1.0 / diag_of(A, A.val, L.lp.ghost_global[k]);
+    B.dinv = upload_as<T>(c, dv);
+    if (l < Lv) {
+      const Sell& S = L.sA;
+      sell_values_x(A, r0, S, A.val, tmp);
+      L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
+                     A.rowptr[r0 + n] - A.rowptr[r0], S.padded};
+      B.Aval = upload_as<T>(c, tmp);
+      L.nsend = (i64)L.lp.send_local.size();
+      L.dsend = c.upload(L.lp.send_local);
+      B.sendbuf = c.dalloc<T>(std::max<i64>(1, L.nsend));
+    } else {
+      if constexpr (std::is_same<T, double>::value) B.Aval = c.dKp_raw;
+      else B.Aval = upload_as<T>(c, kp_vals);
+      B.sendbuf = c.dalloc<T>(std::max<i64>(1, (i64)c.lp.send_local.size()));
+    }
+    if (l >= 1) {
+      const Sell& S = L.sPr;
+      sell_values_x(L.Pr, r0, S, L.Pr.val, tmp);
+      L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
+                      L.Pr.rowptr[r0 + n] - L.Pr.rowptr[r0], S.padded};
+      B.Prval = upload_as<T>(c, tmp);
+      const Sell& R = L.sR;
+      sell_values_x(L.R, L.r_r0, R, L.R.val, tmp);
+      L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), R.nslices, R.nrows,
+                     L.R.rowptr[L.r_r0 + R.nrows] - L.R.rowptr[L.r_r0], R.padded};
+      B.Rval = upload_as<T>(c, tmp);
+    }
+    for (T** f : {&B.x, &B.x2, &B.b, &B.d, &B.res}) *f = c.dalloc<T>(L.nloc);
+  }
+}
+
 void build(Ctx& c) {
   require(c.has_mesh, "mesh not uploaded");
   const pucfem_params& prm = c.prm;
@@ -941,8 +1068,17 @@ void build(Ctx& c) {
       L.rs.resize(c.world + 1);
       for (int r = 0; r <= c.world; ++r) L.rs[r] = L.ord.strip_ptr[cut[r]];
     }
+    // replicated coarse levels (multi-rank): level 0 always, then every level up to mg_rep_nodes
+    const i64 rep_max = prm.mg_rep_nodes > 0 ? prm.mg_rep_nodes : 300000;
+    for (int l = 0; l < Lv; ++l) c.mg[l].rep = c.world > 1 && (l == 0 || c.mg[l].mesh.N <= rep_max);
+    for (int l = 1; l < Lv; ++l) c.mg[l].rep = c.mg[l].rep && c.mg[l - 1].rep;
     for (int l = 0; l <= Lv; ++l) {
       MgLevel& L = c.mg[l];
+      if (L.rep) {  // the whole level on every rank: a single-rank plan (no ghosts)
+        const std::vector<i64> full = {0, (i64)L.mesh.N};
+        make_local_plan2({{&L.Pp, &full}}, full, 0, L.lp);
+        continue;
+      }
       std::vector<PatRows> pr;
       pr.push_back({l == Lv ? &c.Pp : &L.Pp, &L.rs});
       if (l >= 1) pr.push_back({&L.R, &c.mg[l - 1].rs});
@@ -953,10 +1089,16 @@ void build(Ctx& c) {
     c.lp = c.mg[Lv].lp;
     for (int l = 0; l <= Lv; ++l) {  // host SELL images; resolving every column validates the plans
       MgLevel& L = c.mg[l];
-      if (l < Lv) build_sell_x(L.Pp, L.rs[c.rank], L.lp.n_own, L.lp, L.sA);
+      if (l < Lv) build_sell_x(L.Pp, L.own0(c.rank), L.lp.n_own, L.lp, L.sA);
       if (l >= 1) {
-        build_sell_x(L.Pr, L.rs[c.rank], L.lp.n_own, c.mg[l - 1].lp, L.sPr);
-        build_sell_x(L.R, c.mg[l - 1].rs[c.rank], c.mg[l - 1].lp.n_own, L.lp, L.sR);
+        const MgLevel& C = c.mg[l - 1];
+        build_sell_x(L.Pr, L.own0(c.rank), L.lp.n_own, C.lp, L.sPr);
+        // restriction rows: the coarse level's owned rows; into a replicated level from a
+        // distributed one, this rank's strip rows of it (completed by the all-gather)
+        const bool gather = C.rep && !L.rep;
+        L.r_r0 = gather ? C.rs[c.rank] : C.own0(c.rank);
+        const i64 nr = gather ? C.rs[c.rank + 1] - C.rs[c.rank] : C.lp.n_own;
+        build_sell_x(L.R, L.r_r0, nr, L.lp, L.sR);
       }
     }
   }
@@ -988,11 +1130,6 @@ void build(Ctx& c) {
   sell_values(c.P, lp, c.sP, c.as.Gy, tmp);
   c.dGy = c.upload(tmp);
   // Jacobi symmetric scaling S A S of A_visc
-  auto diag_of = [&](const Csr& A, const std::vector<double>& val, i64 g) {
-    for (i64 k = A.rowptr[g]; k < A.rowptr[g + 1]; ++k)
-      if (A.col[k] == g) return val[k];
-    return 1.0;
-  };
   auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
     sg.resize(N);
     for (i64 g = 0; g < N; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
@@ -1026,41 +1163,12 @@ void build(Ctx& c) {
     c.dsp = c.upload(local_vec(sg));
   }
   if (c.use_mg) {
-    const int Lv = c.mg_levels;
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
     c.dKp_raw = c.upload(tmp);
     c.z = c.dalloc<double>(c.nloc);
-    for (int l = 0; l <= Lv; ++l) {
-      MgLevel& L = c.mg[l];
-      const Csr& A = l == Lv ? c.Pp : L.Pp;
-      const i64 n = L.lp.n_own;
-      L.nloc = n + L.lp.n_ghost;
-      std::vector<double> dv(n);
-      for (i64 i = 0; i < n; ++i) dv[i] = 1.0 / diag_of(A, A.val, L.rs[c.rank] + i);
-      L.dinv = c.upload(dv);
-      if (l < Lv) {
-        const Sell& S = L.sA;
-        sell_values_x(A, L.rs[c.rank], S, A.val, tmp);
-        L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
-                       A.rowptr[L.rs[c.rank] + n] - A.rowptr[L.rs[c.rank]], S.padded};
-        L.Aval = c.upload(tmp);
-        L.nsend = (i64)L.lp.send_local.size();
-        L.dsend = c.upload(L.lp.send_local);
-        L.dsendbuf = c.dalloc<double>(2 * std::max<i64>(1, L.nsend));
-      }
-      if (l >= 1) {
-        const MgLevel& C = c.mg[l - 1];
-        const Sell& S = L.sPr;
-        sell_values_x(L.Pr, L.rs[c.rank], S, L.Pr.val, tmp);
-        L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows, 0, S.padded};
-        L.Prval = c.upload(tmp);
-        const Sell& R = L.sR;
-        sell_values_x(L.R, C.rs[c.rank], R, L.R.val, tmp);
-        L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), R.nslices, R.nrows, 0, R.padded};
-        L.Rval = c.upload(tmp);
-      }
-      for (double** f : {&L.x, &L.x2, &L.b, &L.d, &L.res}) *f = c.dalloc<double>(L.nloc);
-    }
+    c.mg_single = c.prm.mg_single != 0;
+    if (c.mg_single) mg_alloc<float>(c, tmp);
+    else mg_alloc<double>(c, tmp);
     // coarsest: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
     {
       MgLevel& L0 = c.mg[0];
@@ -1084,14 +1192,6 @@ void build(Ctx& c) {
             if (L0.master_of[j] < 0) D[i * n0 + j] += cc;
       require(spd_inverse(D, n0), "coarse operator is not SPD after regularisation");
       c.dAinv = c.upload(D);
-      if (c.world > 1) {
-        c.cfull_b = c.dalloc<double>(n0);
-        c.cfull_x = c.dalloc<double>(n0);
-        std::vector<i32> gi(L0.nloc);
-        for (i64 i = 0; i < L0.lp.n_own; ++i) gi[i] = (i32)(L0.lp.r0 + i);
-        for (i64 k = 0; k < L0.lp.n_ghost; ++k) gi[L0.lp.n_own + k] = L0.lp.ghost_global[k];
-        c.cgather = c.upload(gi);
-      }
     }
   }
   c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1;
@@ -1287,6 +1387,7 @@ int pucfem_ctx_create(int32_t device, void** out) {
     auto c = std::make_unique<Ctx>();
     c->device = device;
     c->host_only = device < 0;
+    if (const char* e = std::getenv("PUCFEM_MG_BLOCKS")) c->mg_nb_max = std::max(1, std::atoi(e));  // tuning knob
     if (!c->host_only) {
       HIPCHK(hipSetDevice(device));
       HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
@@ -1967,7 +2068,7 @@ int pucfem_timing_enable(void* ctx, int32_t on) {
     HIPCHK(hipStreamSynchronize(c.st));
     c.timer.flush();
     c.timer.on = on != 0;
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < Timer::NCLS; ++k) {
       c.timer.ms[k] = 0;
       c.timer.bytes[k] = 0;
       c.timer.n[k] = 0;
@@ -1978,7 +2079,7 @@ int pucfem_timing_enable(void* ctx, int32_t on) {
 int pucfem_timing_get(void* ctx, int32_t k, double* ms, int64_t* n, double* bytes) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
-    require(k >= 0 && k < 5, "kernel class");
+    require(k >= 0 && k < Timer::NCLS, "kernel class");
     if (!c.host_only) {
       HIPCHK(hipStreamSynchronize(c.st));
       c.timer.flush();

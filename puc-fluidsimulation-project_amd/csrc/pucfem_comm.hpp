@@ -22,14 +22,24 @@
 
 namespace pucfem {
 
+// element type of a point-to-point / broadcast transfer (the mixed-precision V-cycle moves fp32)
+enum class Dt { F64, F32 };
+inline size_t dt_size(Dt t) { return t == Dt::F64 ? 8 : 4; }
+template <typename T> constexpr Dt dt_of();
+template <> constexpr Dt dt_of<double>() { return Dt::F64; }
+template <> constexpr Dt dt_of<float>() { return Dt::F32; }
+
 struct Comm {
   virtual ~Comm() {}
   virtual void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) = 0;
   virtual void group_start() = 0;
-  virtual void send(const double* p, size_t n, int peer, hipStream_t st) = 0;
-  virtual void recv(double* p, size_t n, int peer, hipStream_t st) = 0;
-  virtual void bcast(double* p, size_t n, int root, hipStream_t st) = 0;  // in place
+  virtual void send(const void* p, size_t n, Dt t, int peer, hipStream_t st) = 0;
+  virtual void recv(void* p, size_t n, Dt t, int peer, hipStream_t st) = 0;
+  virtual void bcast(void* p, size_t n, Dt t, int root, hipStream_t st) = 0;  // in place
   virtual void group_end(hipStream_t st) = 0;
+  template <typename T> void send(const T* p, size_t n, int peer, hipStream_t st) { send(p, n, dt_of<T>(), peer, st); }
+  template <typename T> void recv(T* p, size_t n, int peer, hipStream_t st) { recv(p, n, dt_of<T>(), peer, st); }
+  template <typename T> void bcast(T* p, size_t n, int root, hipStream_t st) { bcast(p, n, dt_of<T>(), root, st); }
 };
 
 inline void nccl_check(ncclResult_t r, const char* what) {
@@ -46,14 +56,15 @@ struct NcclComm : Comm {
     nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, is_max ? ncclMax : ncclSum, c, st), "allreduce");
   }
   void group_start() override { nccl_check(ncclGroupStart(), "group start"); }
-  void send(const double* p, size_t n, int peer, hipStream_t st) override {
-    nccl_check(ncclSend(p, n, ncclDouble, peer, c, st), "send");
+  static ncclDataType_t nt(Dt t) { return t == Dt::F64 ? ncclDouble : ncclFloat; }
+  void send(const void* p, size_t n, Dt t, int peer, hipStream_t st) override {
+    nccl_check(ncclSend(p, n, nt(t), peer, c, st), "send");
   }
-  void recv(double* p, size_t n, int peer, hipStream_t st) override {
-    nccl_check(ncclRecv(p, n, ncclDouble, peer, c, st), "recv");
+  void recv(void* p, size_t n, Dt t, int peer, hipStream_t st) override {
+    nccl_check(ncclRecv(p, n, nt(t), peer, c, st), "recv");
   }
-  void bcast(double* p, size_t n, int root, hipStream_t st) override {
-    nccl_check(ncclBroadcast(p, p, n, ncclDouble, root, c, st), "broadcast");
+  void bcast(void* p, size_t n, Dt t, int root, hipStream_t st) override {
+    nccl_check(ncclBroadcast(p, p, n, nt(t), root, c, st), "broadcast");
   }
   void group_end(hipStream_t) override { nccl_check(ncclGroupEnd(), "group end"); }
 };
@@ -70,8 +81,8 @@ struct LocalShared {
   long gen = 0;
   struct Op {
     int kind;  // 0 send, 1 recv, 2 bcast
-    double* p;
-    size_t n;
+    void* p;
+    size_t n;  // bytes
     int peer;  // send/recv partner, bcast root
   };
   std::vector<std::vector<Op>> ops;
@@ -154,11 +165,15 @@ struct LocalComm : Comm {
     S->barrier();
   }
   void group_start() override { pending.clear(); }
-  void send(const double* p, size_t n, int peer, hipStream_t) override {
-    pending.push_back({0, const_cast<double*>(p), n, peer});
+  void send(const void* p, size_t n, Dt t, int peer, hipStream_t) override {
+    pending.push_back({0, const_cast<void*>(p), n * dt_size(t), peer});
   }
-  void recv(double* p, size_t n, int peer, hipStream_t) override { pending.push_back({1, p, n, peer}); }
-  void bcast(double* p, size_t n, int root, hipStream_t) override { pending.push_back({2, p, n, root}); }
+  void recv(void* p, size_t n, Dt t, int peer, hipStream_t) override {
+    pending.push_back({1, p, n * dt_size(t), peer});
+  }
+  void bcast(void* p, size_t n, Dt t, int root, hipStream_t) override {
+    pending.push_back({2, p, n * dt_size(t), root});
+  }
   void group_end(hipStream_t st) override {
     chk(hipEventRecord(S->ready[rank], st));
     S->ops[rank] = pending;
@@ -178,7 +193,7 @@ struct LocalComm : Comm {
           }
         if (!src || src->n != op.n) throw std::runtime_error("LocalComm: unmatched send/recv");
         chk(hipStreamWaitEvent(st, S->ready[p], 0));
-        chk(hipMemcpyAsync(op.p, src->p, op.n * sizeof(double), hipMemcpyDeviceToDevice, st));
+        chk(hipMemcpyAsync(op.p, src->p, op.n, hipMemcpyDeviceToDevice, st));
       } else if (op.kind == 2) {
         const int q = op.peer;
         int k = nb++, seen = 0;
@@ -191,7 +206,7 @@ struct LocalComm : Comm {
             }
           if (!src || src->n != op.n || src->peer != q) throw std::runtime_error("LocalComm: unmatched broadcast");
           chk(hipStreamWaitEvent(st, S->ready[q], 0));
-          chk(hipMemcpyAsync(op.p, src->p, op.n * sizeof(double), hipMemcpyDeviceToDevice, st));
+          chk(hipMemcpyAsync(op.p, src->p, op.n, hipMemcpyDeviceToDevice, st));
         }
       }
     }

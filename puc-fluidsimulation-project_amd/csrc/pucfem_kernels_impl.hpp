@@ -653,8 +653,9 @@ __global__ __launch_bounds__(BS) void k_reduce(const double* part, int nb, int s
   }
 }
 
-__global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ a,
-                       const double* __restrict__ b, double* __restrict__ out) {
+template <typename T>
+__global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const T* __restrict__ a, const T* __restrict__ b,
+                       T* __restrict__ out) {
   for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < n; k += (int64_t)gridDim.x * BS) {
     out[k] = a[idx[k]];
     if (b) out[n + k] = b[idx[k]];
@@ -764,15 +765,15 @@ __global__ void k_bicg_x(int64_t n, double* x, const double* ph, const double* s
 // ----------------------------------------------------------------------------- multigrid (pressure)
 // sum_k A[row, k] x[col_k] for one SELL slice lane: entry loop unrolled to WMAX (index / value loads
 // issued before the dependent gathers), matrix streamed with non-temporal loads.
-template <int WMAX>
-__device__ __forceinline__ double sell_row_dot(const SellDev& A, const double* __restrict__ val,
-                                               const double* __restrict__ x, int64_t s, int lane) {
+template <int WMAX, typename T, typename G>
+__device__ __forceinline__ T sell_row_dot_g(const SellDev& A, const T* __restrict__ val, const G& gx, int64_t s,
+                                            int lane) {
   const int64_t off = A.off[s];
   const int w = A.w[s];
-  double acc = 0.0;
+  T acc = 0;
   if (w <= WMAX) {
     int32_t cj[WMAX];
-    double a[WMAX];
+    T a[WMAX];
 #pragma unroll
     for (int k = 0; k < WMAX; ++k) {
       if (k < w) {
@@ -781,50 +782,69 @@ __device__ __forceinline__ double sell_row_dot(const SellDev& A, const double* _
         a[k] = ldnt(val + e);
       } else {
         cj[k] = 0;
-        a[k] = 0.0;
+        a[k] = 0;
       }
     }
 #pragma unroll
     for (int k = 0; k < WMAX; ++k)
-      if (k < w) acc += a[k] * x[cj[k]];
+      if (k < w) acc += a[k] * gx(cj[k]);
   } else {
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
-      acc += ldnt(val + e) * x[ldnt(A.col + e)];
+      acc += ldnt(val + e) * gx(ldnt(A.col + e));
     }
   }
   return acc;
 }
+template <int WMAX, typename T>
+__device__ __forceinline__ T sell_row_dot(const SellDev& A, const T* __restrict__ val, const T* __restrict__ x,
+                                          int64_t s, int lane) {
+  return sell_row_dot_g<WMAX>(A, val, [x](int32_t j) { return x[j]; }, s, lane);
+}
 
-// One Chebyshev step of the Jacobi-preconditioned smoother on A x = b (see pucfem_api.hip mg_smooth):
-//   first: d = c2 Dinv b (x_in = 0), x_out = d
-//   else : d = c1 d + c2 Dinv (b - A x_in), x_out = x_in + d
+// Chebyshev smoothing step of the Jacobi-preconditioned smoother on A x = b (pucfem_api.hip
+// mg_smooth), mode
+//   0: first step from x = 0:  d = c2 Dinv b, x_out = d
+//   1: general step:           d = c1 d + c2 Dinv (b - A x_in), x_out = x_in + d
+//   2: steps 1 and 2 fused:    x1 = c20 Dinv b is recomputed at the gathered columns (b and Dinv
+//                              carry ghost entries), then step 2 as mode 1 with d = x1 -- bit-identical
+//                              to modes 0 + 1 and one pass over the level's vectors cheaper
 // rdot != null: partial <rdot, x_out> (the <r, z> of the preconditioned CG).
-__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const double* __restrict__ val, const double* __restrict__ dinv,
-                                             const double* __restrict__ b, const double* __restrict__ xin,
-                                             double* __restrict__ xout, double* __restrict__ d, double c1, double c2,
-                                             int first, const int* ctl, const double* __restrict__ rdot, double* part) {
+// T: the V-cycle's storage/arithmetic type (float in the mixed-precision cycle, double otherwise);
+// TB: the right-hand side (the CG residual, double, on the finest level); TO: the output (double
+// for the final step that writes the preconditioned residual z).
+template <typename T, typename TB, typename TO>
+__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const T* __restrict__ val, const T* __restrict__ dinv,
+                                             const TB* __restrict__ b, const T* __restrict__ xin,
+                                             TO* __restrict__ xout, T* __restrict__ d, double c1, double c2,
+                                             double c20, int mode, const int* ctl, const double* __restrict__ rdot,
+                                             double* part) {
   __shared__ double sh[4];
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
   double acc_rz = 0.0;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = s * 64 + lane;
-    const double ax = first ? 0.0 : sell_row_dot<8>(A, val, xin, s, lane);
+    T ax = 0;
+    if (mode == 1) ax = sell_row_dot<8>(A, val, xin, s, lane);
+    else if (mode == 2) ax = sell_row_dot_g<8>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
     if (row < A.nrows) {
-      double dn, xo;
-      if (first) {
-        dn = c2 * dinv[row] * b[row];
+      T dn, xo;
+      if (mode == 0) {
+        dn = tc2 * dinv[row] * (T)b[row];
         xo = dn;
       } else {
-        dn = c1 * d[row] + c2 * dinv[row] * (b[row] - ax);
-        xo = xin[row] + dn;
+        const T x1 = mode == 2 ? tc20 * dinv[row] * (T)b[row] : xin[row];
+        const T d1 = mode == 2 ? x1 : d[row];
+        dn = tc1 * d1 + tc2 * dinv[row] * ((T)b[row] - ax);
+        xo = x1 + dn;
       }
       d[row] = dn;
-      xout[row] = xo;
-      if (rdot) acc_rz += rdot[row] * xo;
+      xout[row] = (TO)xo;
+      if (rdot) acc_rz += rdot[row] * (double)xo;
     }
   }
   if (rdot) {
@@ -834,56 +854,60 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const double* __restrict
 }
 
 // res = b - A x
-__global__ __launch_bounds__(BS) void k_resid(SellDev A, const double* __restrict__ val, const double* __restrict__ b,
-                                              const double* __restrict__ x, double* __restrict__ res, const int* ctl) {
+template <typename T, typename TB>
+__global__ __launch_bounds__(BS) void k_resid(SellDev A, const T* __restrict__ val, const TB* __restrict__ b,
+                                              const T* __restrict__ x, T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = s * 64 + lane;
-    const double ax = sell_row_dot<8>(A, val, x, s, lane);
-    if (row < A.nrows) res[row] = b[row] - ax;
+    const T ax = sell_row_dot<8>(A, val, x, s, lane);
+    if (row < A.nrows) res[row] = (T)b[row] - ax;
   }
 }
 
 // y = T x (restriction) or y += T x (prolongation, add = 1)
-__global__ __launch_bounds__(BS) void k_transfer(SellDev T, const double* __restrict__ val, const double* __restrict__ x,
-                                                 double* __restrict__ y, int add, const int* ctl) {
+template <typename T>
+__global__ __launch_bounds__(BS) void k_transfer(SellDev M, const T* __restrict__ val, const T* __restrict__ x,
+                                                 T* __restrict__ y, int add, const int* ctl) {
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
-  block_slices(T.nslices, s0, s1);
+  block_slices(M.nslices, s0, s1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t off = T.off[s];
-    const int w = T.w[s];
+    const int64_t off = M.off[s];
+    const int w = M.w[s];
     const int64_t row = s * 64 + lane;
-    double acc = 0.0;
+    T acc = 0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
-      acc += val[e] * x[T.col[e]];
+      acc += val[e] * x[M.col[e]];
     }
-    if (row < T.nrows) y[row] = add ? y[row] + acc : acc;
+    if (row < M.nrows) y[row] = add ? y[row] + acc : acc;
   }
 }
 
-// coarse solve: y = Ainv x (dense, n x n row-major, replicated); one wave per row
-__global__ __launch_bounds__(BS) void k_dense_mv(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x,
-                                                 double* __restrict__ y, const int* ctl) {
+// coarse solve: y = Ainv x (dense, n x n row-major fp64, replicated); one wave per row
+template <typename T>
+__global__ __launch_bounds__(BS) void k_dense_mv(int64_t n, const double* __restrict__ Ainv, const T* __restrict__ x,
+                                                 T* __restrict__ y, const int* ctl) {
   if (ctl && ctl[0]) return;
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
     const double* a = Ainv + row * n;
     double acc = 0.0;
-    for (int64_t j = lane; j < n; j += 64) acc += a[j] * x[j];
+    for (int64_t j = lane; j < n; j += 64) acc += a[j] * (double)x[j];
     acc = wave_sum(acc);
-    if (lane == 0) y[row] = acc;
+    if (lane == 0) y[row] = (T)acc;
   }
 }
 
 // out[i] = full[idx[i]] (local owned + ghost entries from a replicated vector)
-__global__ void k_gather(int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ full,
-                         double* __restrict__ out, const int* ctl) {
+template <typename T>
+__global__ void k_gather(int64_t n, const int32_t* __restrict__ idx, const T* __restrict__ full, T* __restrict__ out,
+                         const int* ctl) {
   if (ctl && ctl[0]) return;
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = full[idx[i]];
 }

@@ -58,6 +58,8 @@ class Tolerances:
     mg_degree: int = 2
     mg_ratio: float = 10.0
     mg_post: int = 0
+    mg_rep_nodes: int = 0  # multi-rank: replicate coarse levels up to this size (0: library default)
+    mg_single: bool = True  # fp32 V-cycle inside the fp64 CG (same iteration counts, ~30% fewer bytes)
 
 
 class Context:
@@ -125,7 +127,8 @@ class Context:
                         rtol_pres=tol.rtol_pres, rtol_lin=tol.rtol_lin, maxit_visc=tol.maxit_visc,
                         maxit_pres=tol.maxit_pres, maxit_lin=tol.maxit_lin, warm_start=int(tol.warm_start),
                         sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1],
-                        precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio, mg_post=tol.mg_post)
+                        precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio, mg_post=tol.mg_post,
+                        mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes)
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 

@@ -50,10 +50,13 @@ def run_ranks(mesh, world, scheme, tol, steps, bc, dt):
     return out
 
 
-@pytest.mark.parametrize("world,precond", [(2, "mg"), (3, "mg"), (2, "jacobi")])
-def test_color_partitioned_matches_single_rank(world, precond):
+# rep: multigrid levels up to this many nodes are replicated on every rank (1: only the coarsest,
+# so every other level is partitioned with halos; 0: library default, here all but the finest)
+@pytest.mark.parametrize("world,precond,single,rep", [(2, "mg", False, 0), (3, "mg", False, 1), (2, "jacobi", False, 0),
+                                                      (3, "mg", True, 1), (2, "mg", True, 5000)])
+def test_color_partitioned_matches_single_rank(world, precond, single, rep):
     mesh = pf.load_mesh("fine", refine=3)
-    tol = pf.Tolerances(rtol_pres=1e-12, rtol_visc=1e-13, precond=precond)
+    tol = pf.Tolerances(rtol_pres=1e-12, rtol_visc=1e-13, precond=precond, mg_single=single, mg_rep_nodes=rep)
     bc = pf.SquirmerBC()
     out = run_ranks(mesh, world, "color", tol, 3, bc, 0.05)
     assert sum(o["info"]["n_own"] for o in out) == mesh.N

@@ -211,10 +211,12 @@ def test_refined_mesh_step_properties():
     sim.close()
 
 
-def test_mg_pressure_solve_matches_oracle(golden):
-    """Geometric-multigrid-preconditioned CG (pressure) on mesh_fine refined twice vs the oracle."""
+@pytest.mark.parametrize("single", [False, True])
+def test_mg_pressure_solve_matches_oracle(golden, single):
+    """Geometric-multigrid-preconditioned CG (pressure) on mesh_fine refined twice vs the oracle;
+    single: the fp32 V-cycle inside the fp64 CG (the attainable accuracy is the CG's)."""
     mesh = pf.load_mesh("fine", refine=2)
-    sim = stokes(mesh, tol=S.Tolerances(precond="mg"))
+    sim = stokes(mesh, tol=S.Tolerances(precond="mg", mg_single=single))
     assert sim.ctx.precond == "mg"
     X, T = mesh.coords, mesh.triangles
     ps = O.PressureSolver(O.stiffness(X, T), O.lumped_mass(X, T), sim.pairs)
@@ -227,10 +229,11 @@ def test_mg_pressure_solve_matches_oracle(golden):
     sim.close()
 
 
-def test_mg_and_jacobi_steps_agree():
+@pytest.mark.parametrize("single", [False, True])
+def test_mg_and_jacobi_steps_agree(single):
     """The two pressure preconditioners give the same Stokes steps (tolerance-limited)."""
     mesh = pf.load_mesh("fine", refine=2)
-    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg"))
+    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", mg_single=single))
     b = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="jacobi"))
     sa, sb = a.step(3), b.step(3)
     assert np.abs(a.u - b.u).max() < 1e-7

@@ -9,16 +9,22 @@ level = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 mesh = pf.load_mesh("fine", refine=level)
 rng = np.random.default_rng(0)
 b = None
-for pre, post, ratio in [(2, 2, 10), (1, 1, 10), (1, 2, 10), (2, 1, 10), (3, 3, 10), (2, 2, 4), (2, 2, 30), (1, 1, 4), (3, 2, 10)]:
-    tol = pf.Tolerances(precond="mg", mg_degree=pre, mg_post=post, mg_ratio=ratio)
+configs = [(2, 2, 10, False), (2, 2, 10, True), (3, 3, 10, True), (1, 1, 10, True), (3, 2, 10, True)]
+if "single" in sys.argv[2:]:
+    configs = [(2, 2, 10, True)]
+for pre, post, ratio, single in configs:
+    tol = pf.Tolerances(precond="mg", mg_degree=pre, mg_post=post, mg_ratio=ratio, mg_single=single)
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", tol=tol)
     if b is None:
         u = rng.standard_normal((mesh.N, 2))
         b = -20.0 * sim.ctx.apply(L.OP_DIV, u, (mesh.N,))
     sim.ctx.solve(L.OP_PRES, b, rtol=1e-8)
     sim.ctx.sync()
-    t = time.perf_counter()
+    sim.ctx.timing(True)
     _, it = sim.ctx.solve(L.OP_PRES, b, rtol=1e-8)
-    dt = time.perf_counter() - t
-    print(json.dumps({"level": level, "pre": pre, "post": post, "ratio": ratio, "iters": it, "ms": 1e3 * dt}), flush=True)
+    _, it12 = sim.ctx.solve(L.OP_PRES, b, rtol=1e-12)
+    tm = {k: sim.ctx.timing_get(k) for k in range(8)}
+    sim.ctx.timing(False)
+    print(json.dumps({"level": level, "pre": pre, "post": post, "ratio": ratio, "single": single, "iters": it,
+                      "iters_1e-12": it12, "timing": tm}), flush=True)
     sim.close()

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE pass, WRITE_SIZE pass).
+
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--level 7 --world 1]
+
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's memory-side request
+counters, FETCH_SIZE under-reports wide streaming reads by exactly 2x on gfx950, and other access
+widths must be calibrated on a known byte count in one's own access pattern.  The calibration
+kernel here is the pressure CG update k_cg_upd<1>: a pure 8-B/lane stream whose algorithmic traffic
+is exactly 32 B/row read (y, p, r, q) and 16 B/row written (y, r), with nrows taken from the bench
+line.  The read and write scale factors it yields are applied to every kernel; the raw counter
+values (rocprofv3 units) are kept next to the corrected bytes.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection csv under {d}")
+    per = defaultdict(list)  # kernel -> values (one per dispatch)
+    for f in files:
+        with open(f, newline="") as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return per
+
+
+def short(name):
+    """k_cheb<float, double, float>(...) -> k_cheb<float,double,float>"""
+    name = re.sub(r"^void\s+", "", name)
+    name = re.sub(r"\(.*$", "", name)
+    name = re.sub(r"pucfem::|\(anonymous namespace\)::", "", name)
+    return name.replace(" ", "")
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    level = 7
+    world = 1
+    if "--level" in sys.argv:
+        level = int(sys.argv[sys.argv.index("--level") + 1])
+    if "--world" in sys.argv:
+        world = int(sys.argv[sys.argv.index("--world") + 1])
+    fetch = load(fdir, "FETCH_SIZE")
+    write = load(wdir, "WRITE_SIZE")
+    kern = sorted(set(fetch) | set(write))
+    # rows of the finest pressure operator: from the bench line of the PMC pass
+    nrows = None
+    for f in glob.glob(os.path.join(os.path.dirname(out), "bench.out")):
+        try:
+            rec = json.loads(open(f).read().strip().splitlines()[-1])
+            nrows = rec["config"]["nodes"]
+        except Exception:
+            pass
+    cal = [k for k in kern if short(k).startswith("k_cg_upd<1>")]
+    res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
+    fr = fw = None
+    if cal and nrows:
+        fv = fetch.get(cal[0], [])
+        wv = write.get(cal[0], [])
+        if fv and wv:
+            f_avg = sum(fv) / len(fv)
+            w_avg = sum(wv) / len(wv)
+            fr = 32.0 * nrows / f_avg if f_avg > 0 else None
+            fw = 16.0 * nrows / w_avg if w_avg > 0 else None
+    res["calibration"] = {"kernel": "k_cg_upd<1>", "nrows": nrows, "read_bytes_per_unit": fr,
+                          "write_bytes_per_unit": fw,
+                          "note": "units -> bytes from a known 8-B/lane stream (32 B/row read, 16 B/row written)"}
+    for k in kern:
+        fv, wv = fetch.get(k, []), write.get(k, [])
+        e = {"dispatches_fetch": len(fv), "dispatches_write": len(wv),
+             "fetch_raw_avg": sum(fv) / len(fv) if fv else None,
+             "write_raw_avg": sum(wv) / len(wv) if wv else None}
+        if fr and fw and fv and wv:
+            e["read_bytes"] = e["fetch_raw_avg"] * fr
+            e["write_bytes"] = e["write_raw_avg"] * fw
+            e["hbm_bytes_per_launch"] = e["read_bytes"] + e["write_bytes"]
+        res["kernels"][short(k)] = e
+    # the bench's roofline kernels: finest-level instances (fp64 right-hand side) of k_cheb, k_cg_dir
+    summary = {}
+    for key, pat in (("k_cheb", r"^k_cheb<\w+,double,"), ("k_cg_dir", r"^k_cg_dir<1,")):
+        ks = [k for k in res["kernels"] if re.match(pat, k) and "hbm_bytes_per_launch" in res["kernels"][k]]
+        if ks:
+            n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
+            summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
+                               for k in ks) / n
+    res[f"L{level}_n{world}"] = summary
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({"calibration": res["calibration"], f"L{level}_n{world}": summary}))
+
+
+if __name__ == "__main__":
+    main()
