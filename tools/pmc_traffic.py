@@ -2,14 +2,16 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE pass, WRITE_SIZE pass).
 
 Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--level 7 --world 1]
+       pmc_traffic.py OLD_OUT.json - OUT_JSON     (re-derive from raw averages kept in an earlier output)
 
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's memory-side request
 counters, FETCH_SIZE under-reports wide streaming reads by exactly 2x on gfx950, and other access
-widths must be calibrated on a known byte count in one's own access pattern.  The calibration
-kernel here is the pressure CG update k_cg_upd<1>: a pure 8-B/lane stream whose algorithmic traffic
-is exactly 32 B/row read (y, p, r, q) and 16 B/row written (y, r), with nrows taken from the bench
-line.  The read and write scale factors it yields are applied to every kernel; the raw counter
-values (rocprofv3 units) are kept next to the corrected bytes.
+widths must be calibrated on a known byte count in one's own access pattern.  The guide's
+corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_visc_prep, a pure 8-B/lane
+elementwise kernel whose algorithmic traffic is exactly 32 B/row each way (nrows from the bench
+line): measured r1f, both equal the algorithmic bytes to 0.01 %.  Raw counter values are kept next
+to the corrected bytes.  Caveat: the L2 is write-back, so up to ~32 MiB of one kernel's dirty lines
+are evicted (and counted) during the next kernel.
 """
 import csv
 import glob
@@ -38,7 +40,7 @@ def short(name):
     """k_cheb<float, double, float>(...) -> k_cheb<float,double,float>"""
     name = re.sub(r"^void\s+", "", name)
     name = re.sub(r"\(.*$", "", name)
-    name = re.sub(r"pucfem::|\(anonymous namespace\)::", "", name)
+    name = re.sub(r"pucfem::|dev::|\(anonymous namespace\)::", "", name)
     return name.replace(" ", "")
 
 
@@ -50,8 +52,13 @@ def main():
         level = int(sys.argv[sys.argv.index("--level") + 1])
     if "--world" in sys.argv:
         world = int(sys.argv[sys.argv.index("--world") + 1])
-    fetch = load(fdir, "FETCH_SIZE")
-    write = load(wdir, "WRITE_SIZE")
+    if fdir.endswith(".json"):  # re-derive from an earlier output's raw per-kernel averages
+        old = json.load(open(fdir))["kernels"]
+        fetch = {k: [v["fetch_raw_avg"]] * v["dispatches_fetch"] for k, v in old.items() if v["fetch_raw_avg"] is not None}
+        write = {k: [v["write_raw_avg"]] * v["dispatches_write"] for k, v in old.items() if v["write_raw_avg"] is not None}
+    else:
+        fetch = load(fdir, "FETCH_SIZE")
+        write = load(wdir, "WRITE_SIZE")
     kern = sorted(set(fetch) | set(write))
     # rows of the finest pressure operator: from the bench line of the PMC pass
     nrows = None
@@ -61,20 +68,22 @@ def main():
             nrows = rec["config"]["nodes"]
         except Exception:
             pass
-    cal = [k for k in kern if short(k).startswith("k_cg_upd<1>")]
+    # gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a
+    # streaming read, WRITE_SIZE counts streaming stores exactly; both in KiB.  Checked on k_visc_prep,
+    # a pure 8-B/lane elementwise kernel with exactly 32 B/row read (ux, uy, s, sq) and 32 B/row
+    # written (bvx, bvy, yvx, yvy): the corrected values must equal the algorithmic bytes.
     res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
-    fr = fw = None
-    if cal and nrows:
-        fv = fetch.get(cal[0], [])
-        wv = write.get(cal[0], [])
-        if fv and wv:
-            f_avg = sum(fv) / len(fv)
-            w_avg = sum(wv) / len(wv)
-            fr = 32.0 * nrows / f_avg if f_avg > 0 else None
-            fw = 16.0 * nrows / w_avg if w_avg > 0 else None
-    res["calibration"] = {"kernel": "k_cg_upd<1>", "nrows": nrows, "read_bytes_per_unit": fr,
-                          "write_bytes_per_unit": fw,
-                          "note": "units -> bytes from a known 8-B/lane stream (32 B/row read, 16 B/row written)"}
+    fr, fw = 2.0 * 1024.0, 1.0 * 1024.0
+    check = None
+    cal = [k for k in kern if short(k).endswith("k_visc_prep")]
+    if cal and nrows and fetch.get(cal[0]) and write.get(cal[0]):
+        f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
+        w_avg = sum(write[cal[0]]) / len(write[cal[0]])
+        check = {"kernel": "k_visc_prep", "nrows": nrows, "algorithmic_read": 32.0 * nrows,
+                 "corrected_read": f_avg * fr, "algorithmic_write": 32.0 * nrows, "corrected_write": w_avg * fw}
+    res["calibration"] = {"read_bytes_per_unit": fr, "write_bytes_per_unit": fw,
+                          "note": "FETCH_SIZE x2 KiB, WRITE_SIZE x1 KiB (guide's gfx950 corrections)",
+                          "check": check}
     for k in kern:
         fv, wv = fetch.get(k, []), write.get(k, [])
         e = {"dispatches_fetch": len(fv), "dispatches_write": len(wv),
