@@ -217,6 +217,8 @@ struct Ctx {
   double *mx = nullptr, *my = nullptr;
   int32_t* mtri = nullptr;
   GridDev cgrid{}, tgrid{};
+  LocDev lgrid{};
+  double* part_sl = nullptr;  // k_sl partials, 3 x SLB
   bool has_cgrid = false, has_tgrid = false;
   double *c_full = nullptr, *c_new = nullptr, *ufx = nullptr, *ufy = nullptr;
   int32_t* dnotfound = nullptr;
@@ -286,6 +288,8 @@ struct Ctx {
   int mg_nb_max = 4096;
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
+  // semi-Lagrangian grid: latency-bound gathers want more waves in flight than MAXB blocks give
+  static int nb_sl(i64 n) { return (int)std::max<i64>(1, std::min<i64>(SLB, (n + 4 * 64 - 1) / (4 * 64))); }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
   // ------------------------------------------------------------------ timing helpers
@@ -314,8 +318,8 @@ struct Ctx {
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
-  void reduce_into(double* part, int nb, int nv, bool is_max, int slot) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, vals + slot);
+  void reduce_into(double* part, int nb, int nv, bool is_max, int slot, int stride = MAXB) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, stride, nv, is_max ? 1 : 0, vals + slot);
     KCHK();
     if (world > 1)
       comm->allreduce(vals + slot, nv, is_max, st);
@@ -721,11 +725,11 @@ struct Ctx {
     div(ux, uy, final_div, false);
     reduce_into(part_d, nb_for(dP.nslices), 1, true, 1);  // max |final div|
     if (scheme == PUCFEM_STOKES_COLOR) {
-      const int nb = nb_rows(lp.n_own);
+      const int nb = nb_sl(lp.n_own);
       hipEvent_t e = nullptr;
       tstart(e);
-      hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, cgrid, lp.r0, lp.n_own, ux,
-                         uy, prm.dt, c_full, c_new, dwmix, (int32_t*)nullptr, part_a);
+      hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, lgrid, cgrid, lp.r0, lp.n_own,
+                         ux, uy, prm.dt, c_full, c_new, dwmix, (int32_t*)nullptr, part_sl);
       KCHK();
       tstop(4, e, 8.0 * 6 * (double)lp.n_own);
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
@@ -734,10 +738,11 @@ struct Ctx {
         std::swap(c_full, c_new);
       }
       allgather_full(c_full);
-      reduce_into(part_a, nb, 3, false, 2);  // sum wc, sum w, not-found
-      hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
+      reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+      const int nbm = nb_rows(lp.n_own);
+      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
       KCHK();
-      reduce_into(part_b, nb, 1, false, 5);
+      reduce_into(part_b, nbm, 1, false, 5);
     } else {
       tracer_advance(prm.dt);
     }
@@ -1296,6 +1301,7 @@ void build(Ctx& c) {
     c.cg_q[q] = c.dalloc<double>(c.nloc);
   }
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
+  c.part_sl = c.dalloc<double>(3 * SLB);
   c.scal = c.dalloc<double>(32);
   c.ctl = c.dalloc<int>(4);
   c.redbuf = c.dalloc<double>(8 * 64);
@@ -1343,6 +1349,21 @@ void build(Ctx& c) {
       build_tri_grid(X, Y, tri, 4.0, TG);
       dgrid(TG, c.tgrid, false);
       c.has_tgrid = true;
+      // semi-Lagrangian point location: inflated-bbox grid (~1 triangle per cell) + packed records
+      Grid LG;
+      build_tri_grid(X, Y, tri, 1.0, LG, 1e-6);
+      GridDev lg{};
+      dgrid(LG, lg, false);
+      std::vector<double> rec(8 * (size_t)m.T);
+      for (i64 t = 0; t < m.T; ++t) {
+        for (int v = 0; v < 3; ++v) {
+          rec[8 * t + 2 * v] = X[tri[3 * t + v]];
+          rec[8 * t + 2 * v + 1] = Y[tri[3 * t + v]];
+        }
+        rec[8 * t + 6] = cx[t];
+        rec[8 * t + 7] = cy[t];
+      }
+      c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item, c.upload(rec)};
     }
     c.c_full = c.dalloc<double>(N);
     c.c_new = c.dalloc<double>(N);
@@ -1986,9 +2007,9 @@ int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, d
     HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
     HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
     HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    const int nb = c.nb_rows(N);
-    hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, c.mesh.T}, c.cgrid, (int64_t)0, N,
-                       tx, ty, dt, cf, cn, c.dwmix, c.dnotfound, c.part_a);
+    const int nb = c.nb_sl(N);
+    hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, c.mesh.T}, c.lgrid, c.cgrid,
+                       (int64_t)0, N, tx, ty, dt, cf, cn, c.dwmix, c.dnotfound, c.part_sl);
     KCHK();
     std::vector<double> o(N);
     std::vector<int32_t> nf(N);

@@ -488,7 +488,7 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
 }
 
 void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,
-                    double per_cell, Grid& G) {
+                    double per_cell, Grid& G, double inflate) {
   const i64 T = (i64)tri.size() / 3;
   grid_dims(*std::min_element(x.begin(), x.end()), *std::max_element(x.begin(), x.end()),
             *std::min_element(y.begin(), y.end()), *std::max_element(y.begin(), y.end()), T, per_cell, G);
@@ -499,6 +499,13 @@ void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, 
     double xb = std::max({x[tri[3 * t]], x[tri[3 * t + 1]], x[tri[3 * t + 2]]});
     double ya = std::min({y[tri[3 * t]], y[tri[3 * t + 1]], y[tri[3 * t + 2]]});
     double yb = std::max({y[tri[3 * t]], y[tri[3 * t + 1]], y[tri[3 * t + 2]]});
+    if (inflate > 0) {  // relative to the triangle's extent, plus an absolute floor
+      const double m = inflate * std::max(xb - xa, yb - ya) + 1e-14;
+      xa -= m;
+      xb += m;
+      ya -= m;
+      yb += m;
+    }
     cx0 = cell_of(xa, G.x0, G.hx, G.nx);
     cx1 = cell_of(xb, G.x0, G.hx, G.nx);
     cy0 = cell_of(ya, G.y0, G.hy, G.ny);

@@ -140,7 +140,9 @@ struct Grid {
   std::vector<double> px, py;   // centroid coordinates per entry (centroid grid only)
 };
 void build_centroid_grid(const std::vector<double>& cx, const std::vector<double>& cy, double per_cell, Grid& G);
+// inflate > 0: each bbox grows by inflate * (its extent) + 1e-14 on every side, so a point that a
+// rounding-sensitive weight test accepts on a triangle's edge is still listed with that triangle
 void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,
-                    double per_cell, Grid& G);
+                    double per_cell, Grid& G, double inflate = 0.0);
 
 }  // namespace pucfem

@@ -437,59 +437,65 @@ __device__ __forceinline__ bool knn_less(double d, int32_t i, double bd, int32_t
   return d < bd || (d == bd && i < bi);
 }
 
-// k nearest centroids of (qx, qy), sorted by (squared distance, triangle id)
-__device__ __forceinline__ void knn10(const GridDev& G, double qx, double qy, double (&bd)[KNN], int32_t (&bi)[KNN]) {
-#pragma unroll
-  for (int p = 0; p < KNN; ++p) {
-    bd[p] = INFINITY;
-    bi[p] = 0x7fffffff;
-  }
-  const int32_t cx = gcell(qx, G.x0, G.hx, G.nx), cy = gcell(qy, G.y0, G.hy, G.ny);
-  const int32_t rmax = max(max(cx, G.nx - 1 - cx), max(cy, G.ny - 1 - cy));
-  for (int32_t r = 0; r <= rmax; ++r) {
-    const int32_t jlo = max(cy - r, 0), jhi = min(cy + r, G.ny - 1);
-    for (int32_t j = jlo; j <= jhi; ++j) {
-      const bool edge_row = (j == cy - r) || (j == cy + r);
-      const int32_t step = edge_row ? 1 : 2 * r;
-      for (int32_t i = cx - r; i <= cx + r; i += (step > 0 ? step : 1)) {
-        if (i < 0 || i >= G.nx) continue;
-        const int64_t c = (int64_t)j * G.nx + i;
-        for (int32_t e = G.start[c]; e < G.start[c + 1]; ++e) {
-          const double dx = G.px[e] - qx, dy = G.py[e] - qy;
-          const double d = dx * dx + dy * dy;
-          const int32_t id = G.item[e];
-          if (!knn_less(d, id, bd[KNN - 1], bi[KNN - 1])) continue;
-          bool placed = false;
-#pragma unroll
-          for (int p = KNN - 1; p > 0; --p) {
-            if (!placed) {
-              if (knn_less(d, id, bd[p - 1], bi[p - 1])) {
-                bd[p] = bd[p - 1];
-                bi[p] = bi[p - 1];
-              } else {
-                bd[p] = d;
-                bi[p] = id;
-                placed = true;
-              }
-            }
-          }
-          if (!placed) {
-            bd[0] = d;
-            bi[0] = id;
-          }
-        }
-        if (step == 0) break;
+// Point location for the semi-Lagrangian step (PointLocator.find, StokesColor.py:314-345).
+// The reference takes the k=10 nearest centroids in (distance, id) order and returns the first
+// whose barycentric weights are all >= 0.  Restated exactly, without sorting 10 candidates:
+//   1. every triangle that passes the weight test for q has q inside it up to rounding, so it is
+//      listed in q's cell of the inflated-bbox grid L; among those that pass, take the one with the
+//      smallest (d^2, id) key T*.  A triangle whose weights are all >= SL_MARGIN contains q with a
+//      margin no other triangle's test can reach, so the scan stops at it;
+//   2. T* is the answer iff fewer than 10 centroids have a key below T*'s (its rank is < 10):
+//      counted over the centroid-grid cells that meet the box [q - R, q + R]^2, R = sqrt(d*^2).
+// Otherwise no triangle among the 10 nearest passes and the reference keeps c[n].
+struct LocDev {
+  int32_t nx, ny;
+  double x0, y0, hx, hy;
+  const int32_t* start;  // nx*ny+1
+  const int32_t* item;   // triangle ids, ascending per cell
+  const double* rec;     // per triangle: x1 y1 x2 y2 x3 y3 cx cy (64 B; cx, cy as the centroid grid's)
+};
+constexpr double SL_MARGIN = 1e-6;
+
+// -> triangle id, or -1 (no triangle among the KNN nearest centroids contains q)
+__device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, double qx, double qy) {
+  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
+  const int64_t cell = (int64_t)cj * L.nx + ci;
+  int32_t best = 0x7fffffff;
+  double bestd = INFINITY;
+  const int32_t e1 = L.start[cell + 1];
+  for (int32_t e = L.start[cell]; e < e1; ++e) {
+    const int32_t t = L.item[e];
+    const double* r = L.rec + 8 * (int64_t)t;
+    const double x1 = r[0], y1 = r[1], x2 = r[2], y2 = r[3], x3 = r[4], y3 = r[5];
+    const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
+    if (!(fabs(det) >= 1e-14)) continue;
+    const double w1 = ((x2 - qx) * (y3 - qy) - (x3 - qx) * (y2 - qy)) / det;
+    const double w2 = ((x3 - qx) * (y1 - qy) - (x1 - qx) * (y3 - qy)) / det;
+    const double w3 = 1.0 - w1 - w2;
+    if (w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0) {
+      const double dx = r[6] - qx, dy = r[7] - qy;
+      const double d = dx * dx + dy * dy;
+      if (knn_less(d, t, bestd, best)) {
+        bestd = d;
+        best = t;
       }
+      if (w1 >= SL_MARGIN && w2 >= SL_MARGIN && w3 >= SL_MARGIN) break;
     }
-    // distance from the query to the nearest cell NOT yet visited
-    double dmin = INFINITY;
-    if (cx - r > 0) dmin = fmin(dmin, qx - (G.x0 + (double)(cx - r) * G.hx));
-    if (cx + r < G.nx - 1) dmin = fmin(dmin, (G.x0 + (double)(cx + r + 1) * G.hx) - qx);
-    if (cy - r > 0) dmin = fmin(dmin, qy - (G.y0 + (double)(cy - r) * G.hy));
-    if (cy + r < G.ny - 1) dmin = fmin(dmin, (G.y0 + (double)(cy + r + 1) * G.hy) - qy);
-    if (dmin == INFINITY) break;
-    if (dmin > 0.0 && bd[KNN - 1] < dmin * dmin * (1.0 - 1e-9)) break;
   }
+  if (best == 0x7fffffff) return -1;
+  const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
+  const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
+  const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
+  int cnt = 0;
+  for (int32_t j = j0; j <= j1; ++j) {
+    const int32_t f0 = G.start[(int64_t)j * G.nx + i0], f1 = G.start[(int64_t)j * G.nx + i1 + 1];
+    for (int32_t e = f0; e < f1; ++e) {  // cells i0..i1 of row j are one contiguous entry range
+      const double dx = G.px[e] - qx, dy = G.py[e] - qy;
+      const double d = dx * dx + dy * dy;
+      if (knn_less(d, G.item[e], bestd, best) && ++cnt >= KNN) return -1;
+    }
+  }
+  return best;
 }
 
 __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:353-357
@@ -502,10 +508,13 @@ __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:3
 // advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
 // nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
 // Partials: [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
-__global__ __launch_bounds__(BS) void k_sl(MeshDev M, GridDev G, int64_t row0, int64_t n, const double* __restrict__ ux,
-                                           const double* __restrict__ uy, double dt, const double* __restrict__ c,
-                                           double* __restrict__ cout, const double* __restrict__ wmix,
-                                           int32_t* notfound, double* part) {
+// advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
+// nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
+// Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
+__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LocDev L, GridDev G, int64_t row0, int64_t n,
+                                           const double* __restrict__ ux, const double* __restrict__ uy, double dt,
+                                           const double* __restrict__ c, double* __restrict__ cout,
+                                           const double* __restrict__ wmix, int32_t* notfound, double* part) {
   __shared__ double sh[4];
   double swc = 0.0, sw = 0.0, nnf = 0.0;
   int64_t r0, r1;
@@ -517,32 +526,15 @@ __global__ __launch_bounds__(BS) void k_sl(MeshDev M, GridDev G, int64_t row0, i
     double yb = yg - dt * uy[i] * 1.0;
     if (yb < 0.0) yb = 1e-12;
     if (yb > 1.0) yb = 1.0 - 1e-12;
-    double bd[KNN];
-    int32_t bi[KNN];
-    knn10(G, xb, yb, bd, bi);
-    int32_t found = -1;
-#pragma unroll
-    for (int p = 0; p < KNN; ++p) {
-      if (found < 0 && bi[p] != 0x7fffffff) {
-        const int32_t t = bi[p];
-        const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], k = M.tri[3 * t + 2];
-        const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[k], y3 = M.y[k];
-        const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
-        if (fabs(det) >= 1e-14) {
-          const double w1 = ((x2 - xb) * (y3 - yb) - (x3 - xb) * (y2 - yb)) / det;
-          const double w2 = ((x3 - xb) * (y1 - yb) - (x1 - xb) * (y3 - yb)) / det;
-          const double w3 = 1.0 - w1 - w2;
-          if (w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0) found = t;
-        }
-      }
-    }
+    const int32_t found = sl_locate(L, G, xb, yb);
     double cn;
     if (found < 0) {
       cn = c[g];
       nnf += 1.0;
     } else {
       const int32_t a = M.tri[3 * found], b = M.tri[3 * found + 1], k = M.tri[3 * found + 2];
-      const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[k], y3 = M.y[k];
+      const double* r = L.rec + 8 * (int64_t)found;
+      const double x1 = r[0], y1 = r[1], x2 = r[2], y2 = r[3], x3 = r[4], y3 = r[5];
       const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
       const double w1 = (pdx(x2, xb) * (y3 - yb) - pdx(x3, xb) * (y2 - yb)) / det;
       const double w2 = (pdx(x3, xb) * (y1 - yb) - pdx(x1, xb) * (y3 - yb)) / det;
@@ -558,8 +550,8 @@ __global__ __launch_bounds__(BS) void k_sl(MeshDev M, GridDev G, int64_t row0, i
   const double a = block_sum(swc, sh), b = block_sum(sw, sh), d = block_sum(nnf, sh);
   if (threadIdx.x == 0) {
     part[blockIdx.x] = a;
-    part[MAXB + blockIdx.x] = b;
-    part[2 * MAXB + blockIdx.x] = d;
+    part[SLB + blockIdx.x] = b;
+    part[2 * SLB + blockIdx.x] = d;
   }
 }
 
