@@ -37,6 +37,13 @@ def parse():
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
     ap.add_argument("--rtol-pres", type=float, default=1e-8)
     ap.add_argument("--mg-double", action="store_true", help="fp64 V-cycle instead of the fp32 one")
+    ap.add_argument("--mg-vals", default="f16", choices=["f16", "f32", "coarse-f16"],
+                    help="fp32 V-cycle operator storage: fp16 on every level, fp32, or fp16 below the finest level")
+    ap.add_argument("--index32", action="store_true", help="int32 SELL columns instead of int16 deltas")
+    ap.add_argument("--mg-pre", type=int, default=2, help="Chebyshev pre-smoothing degree")
+    ap.add_argument("--mg-post", type=int, default=2, help="Chebyshev post-smoothing degree")
+    ap.add_argument("--mg-ratio", type=float, default=10.0, help="Chebyshev interval [lmax / ratio, lmax]")
+    ap.add_argument("--mg-kind", type=int, default=1, choices=[1, 4], help="Chebyshev smoother of the first / fourth kind")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -86,7 +93,10 @@ def main():
 
     t_setup = time.time()
     mesh = pf.load_mesh("fine", refine=a.level)
-    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond, mg_single=not a.mg_double)
+    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond, mg_single=not a.mg_double,
+                        mg_f16_vals={"f16": True, "f32": False, "coarse-f16": "coarse"}[a.mg_vals],
+                        index16=not a.index32, mg_degree=a.mg_pre, mg_post=a.mg_post, mg_ratio=a.mg_ratio,
+                        mg_kind=a.mg_kind)
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup
@@ -130,13 +140,18 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "precond_dtype": "f64" if a.mg_double or a.precond != "mg" else "f32",
+        "precond_dtype": "f64" if a.mg_double or a.precond != "mg" else {
+            "f16": "f32 (fp16-stored operators)", "f32": "f32",
+            "coarse-f16": "f32 (fp16-stored coarse operators)"}[a.mg_vals],
+        "storage": {"index16": [info.get("index16_P"), info.get("index16_Pp")],
+                    "mg_vals": a.mg_vals, "finest_f16": info.get("mg_f16_vals")},
         "data": "synthetic (deterministic red-refined mesh_fine, reference initial state)",
         "config": {
             "workload": f"StokesColor neutral squirmer step, mesh_fine refined x{a.level}",
             "nodes": info["N"] if world == 1 else mesh.N, "triangles": mesh.T,
             "dt": 0.05, "nu": 0.1, "B1": -2.0, "B2": 0.0,
             "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "pressure_precond": sim.ctx.precond,
+            "mg_cheb": {"kind": a.mg_kind, "pre": a.mg_pre, "post": a.mg_post, "ratio": a.mg_ratio},
             "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
         },
         "cg_iters_per_s": cg_iters / elapsed,
@@ -148,10 +163,11 @@ def main():
     }
     # roofline of the dominant kernel: the finest-level Chebyshev smoother step (k_cheb) when the
     # pressure is multigrid-preconditioned, else the CG SpMV+direction kernel (k_cg_dir).  Algorithmic
-    # bytes per launch for k_cheb in the fp32 cycle = 8*nnz (fp32 value + int32 column) + per row 4 B
-    # each for x (gathered once), dinv, d read, d write, x write + 8 B fp64 rhs (the CG residual), plus
-    # 8 B r for <r, z> and fp64 z on the last post-smoothing step (12*nnz + 48*N in the fp64 cycle);
-    # 12*nnz + 32*NRHS*N for k_cg_dir.  Timed with HIP events on the library stream.
+    # bytes per launch for k_cheb in the fp32 cycle = (value + column bytes) * nnz -- 2 + 2 with fp16
+    # values and int16 column deltas, 4 + 4 without -- + per row 4 B each for x (gathered once), dinv,
+    # d read, d write, x write + 8 B fp64 rhs (the CG residual), plus 8 B r for <r, z> and fp64 z on the
+    # last post-smoothing step; (8 + column bytes) * nnz + 32*NRHS*N for k_cg_dir.  The library counts
+    # them per launch (tstop); timed with HIP events on the library stream.
     dom = names[0] if names[0] in ktab else names[1]
     if dom in ktab:
         kd = ktab[dom]

@@ -74,6 +74,12 @@ typedef struct pucfem_params {
   int32_t mg_post;     /* post-smoothing steps (0: same as mg_degree) */
   int32_t mg_single;   /* 1: fp32 V-cycle (values, vectors, halos) inside the fp64 CG */
   int64_t mg_rep_nodes; /* multi-rank: coarse levels up to this many nodes are replicated (0: 300000) */
+  int32_t mg_f32_vals; /* fp32 cycle: 0 = level operators stored in fp16 when every value is representable
+                          (arithmetic stays fp32), 1 = all stored in fp32, 2 = the finest in fp32 and
+                          the coarser levels in fp16 */
+  int32_t idx32;       /* 0 = int16 column deltas for square operators whose band fits, 1 = int32 columns */
+  int32_t mg_kind;     /* smoother polynomial: 0/1 = Chebyshev (first kind) on [lmax / mg_ratio, lmax],
+                          4 = Chebyshev of the fourth kind on [0, lmax] (Lottes 2022; no mg_ratio) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -185,8 +191,10 @@ int pucfem_sync(void* ctx);
    variant 0 plain loop, 1 unrolled, 2 non-temporal, 3 unrolled + non-temporal; average ms/launch */
 int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters, double* ms_out);
 /* sizes of the internal operators: out[0]=N, [1]=T, [2]=nnz(P), [3]=nnz(Pp), [4]=n_own,
-   [5]=n_ghost, [6]=padded SELL entries (P), [7]=padded SELL entries (Pp), [8]=n_pairs, [9]=n_dirichlet */
-int pucfem_info(void* ctx, int64_t* out10);
+   [5]=n_ghost, [6]=padded SELL entries (P), [7]=padded SELL entries (Pp), [8]=n_pairs, [9]=n_dirichlet,
+   [10]=storage flags (bit 0: P has int16 columns, bit 1: Pp has int16 columns, bit 2: the finest
+   V-cycle operator is stored in fp16), [11]=multigrid levels (0: none) */
+int pucfem_info(void* ctx, int64_t* out12);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

@@ -60,9 +60,18 @@ struct DevSell {
   int64_t* off = nullptr;
   int32_t* w = nullptr;
   int32_t* col = nullptr;
+  int16_t* c16 = nullptr;  // int16 column deltas (square operators whose band fits), else null
   int64_t nslices = 0, nrows = 0, nnz = 0, padded = 0;
-  SellDev view() const { return SellDev{off, w, col, nslices, nrows}; }
+  SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16}; }
+  double idx_bytes() const { return c16 ? 2.0 : 4.0; }  // per stored entry
 };
+// f(std::true_type) when A carries int16 columns, f(std::false_type) otherwise: one launch site
+// instantiates both SpMV variants
+template <class F>
+void with_c16(const DevSell& A, F&& f) {
+  if (A.c16) f(std::true_type{});
+  else f(std::false_type{});
+}
 
 struct Red {  // a (possibly globally reduced) partial array
   const double* p;
@@ -115,6 +124,20 @@ template <typename T>
 struct MgBufs {
   T *Aval = nullptr, *Prval = nullptr, *Rval = nullptr, *dinv = nullptr;
   T *x = nullptr, *x2 = nullptr, *b = nullptr, *d = nullptr, *res = nullptr, *sendbuf = nullptr;
+  // fp16 copy of the level operator's values (fp32 cycle, when every value is representable): the
+  // smoother and residual stream 2 B per entry instead of 4, arithmetic stays fp32
+  _Float16* Aval16 = nullptr;
+  template <class F>
+  void with_vals(F&& f) const {
+    if constexpr (std::is_same<T, float>::value) {
+      if (Aval16) {
+        f((const _Float16*)Aval16);
+        return;
+      }
+    }
+    f((const T*)Aval);
+  }
+  double val_bytes() const { return Aval16 ? 2.0 : (double)sizeof(T); }
 };
 
 // One level of the geometric multigrid hierarchy (pressure preconditioner).  Level 0 is the
@@ -247,6 +270,7 @@ struct Ctx {
   double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
   bool mg_single = false;                        // fp32 V-cycle
   double* z = nullptr;              // preconditioned residual (finest)
+  float* r32 = nullptr;             // fp32 copy of the CG residual: the fp32 V-cycle's right-hand side
 
   ~Ctx() {
     if (!host_only) {
@@ -275,6 +299,11 @@ struct Ctx {
     T* p = dalloc<T>((i64)v.size());
     if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
     return p;
+  }
+  // int16 column deltas for a square operator's SELL (prm.idx32 = 0 and the band fits)
+  void attach_c16(const Sell& S, DevSell& D) {
+    std::vector<int16_t> c16;
+    if (!prm.idx32 && sell_col16(S, c16)) D.c16 = upload(c16);
   }
   void need_dev() const {
     if (host_only) throw Error(PUCFEM_ENODEV, "compute call on a host-only context");
@@ -399,7 +428,10 @@ struct Ctx {
     }
     if (NR == 2) halo(y[0], y[1]);
     else halo(y[0]);
-    hipLaunchKernelGGL((k_cg_init<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, part_a, part_b);
+    with_c16(A, [&](auto c16) {
+      hipLaunchKernelGGL((k_cg_init<NR, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost,
+                         part_a, part_b);
+    });
     KCHK();
     Red rr = reduce_global(part_a, nb, NR, false, 0);
     Red bb = reduce_global(part_b, nb, NR, false, 1);
@@ -407,7 +439,7 @@ struct Ctx {
     if (NR == 2) halo(cg_r[0], cg_r[1]);
     else halo(cg_r[0]);
     const double tol2 = tol * tol;
-    const double bytes_dir = 12.0 * (double)A.nnz + 32.0 * NR * (double)A.nrows;
+    const double bytes_dir = (8.0 + A.idx_bytes()) * (double)A.nnz + 32.0 * NR * (double)A.nrows;
     const double bytes_upd = 48.0 * NR * (double)A.nrows;
     int it = 0;
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
@@ -417,8 +449,11 @@ struct Ctx {
         // HIP-event timing samples every 8th iteration (bounded event count for long solves)
         const bool samp = (it & 7) == 0;
         if (samp) tstart(e0);
-        hipLaunchKernelGGL((k_cg_dir<NR>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost, rr.p, rr.nb,
-                           rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c);
+        with_c16(A, [&](auto c16) {
+          hipLaunchKernelGGL((k_cg_dir<NR, 8, true, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), val, v,
+                             lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
+                             part_c);
+        });
         KCHK();
         if (samp) tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, NR, false, 2);
@@ -446,7 +481,10 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ multigrid V-cycle / PCG
-  // Chebyshev smoothing (deg steps) on [lmax / mg_ratio, lmax] for D^-1 A.
+  // Polynomial smoothing (deg steps) for D^-1 A: Chebyshev on [lmax / mg_ratio, lmax] (mg_kind 1), or
+  // the fourth-kind Chebyshev recurrence on [0, lmax] (mg_kind 4, Lottes 2022: d_0 = 4/(3 lmax) D^-1 r,
+  // d_i = (2i-1)/(2i+3) d_(i-1) + (8i+4)/((2i+3) lmax) D^-1 r_i).  Both are d = c1 d + c2 D^-1 (b - A x),
+  // x += d with step-dependent scalars.
   // x_in (nullable: zero initial guess) -> returns the buffer holding the result; with zout the
   // last step writes its result (in fp64) to zout instead and nullptr is returned.
   template <typename T, typename TB>
@@ -461,7 +499,10 @@ struct Ctx {
     double c20 = 0.0;
     for (int k = 0; k < deg; ++k) {
       double c1 = 0.0, c2 = 1.0 / theta;
-      if (k > 0) {
+      if (prm.mg_kind == 4) {
+        c1 = k == 0 ? 0.0 : (2.0 * k - 1.0) / (2.0 * k + 3.0);
+        c2 = k == 0 ? 4.0 / (3.0 * lmax) : (8.0 * k + 4.0) / ((2.0 * k + 3.0) * lmax);
+      } else if (k > 0) {
         const double rho = 1.0 / (2.0 * sigma - rho_old);
         c1 = rho * rho_old;
         c2 = 2.0 * rho / delta;
@@ -485,19 +526,25 @@ struct Ctx {
       const bool toz = last && zout;
       const int nb = rd ? nb_for(A.nslices) : nb_mg(A.nslices);
       const T* xi = mode == 1 ? cur : nullptr;
-      if (toz)
-        hipLaunchKernelGGL((k_cheb<T, TB, double>), dim3(nb), dim3(BS), 0, st, A.view(), B.Aval, B.dinv, b, xi, zout,
-                           B.d, c1, c2, c20, mode, ctl, rd, part);
-      else
-        hipLaunchKernelGGL((k_cheb<T, TB, T>), dim3(nb), dim3(BS), 0, st, A.view(), B.Aval, B.dinv, b, xi, out, B.d,
-                           c1, c2, c20, mode, ctl, rd, part);
+      B.with_vals([&](auto* val) {
+        using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
+        with_c16(A, [&](auto c16) {
+          constexpr bool C = decltype(c16)::value;
+          if (toz)
+            hipLaunchKernelGGL((k_cheb<T, TB, double, VT, C>), dim3(nb), dim3(BS), 0, st, A.view(), val, B.dinv, b, xi,
+                               zout, B.d, c1, c2, c20, mode, ctl, rd, part);
+          else
+            hipLaunchKernelGGL((k_cheb<T, TB, T, VT, C>), dim3(nb), dim3(BS), 0, st, A.view(), val, B.dinv, b, xi, out,
+                               B.d, c1, c2, c20, mode, ctl, rd, part);
+        });
+      });
       KCHK();
       // algorithmic bytes: matrix (value + int32 column) per entry; per row x_in (mode 1) or b and
       // dinv (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r
       if (timed) {
         const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
         const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
-        tstop(0, e0, (double)(sizeof(T) + 4) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row));
+        tstop(0, e0, (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row));
       }
       cur = toz ? nullptr : out;
     }
@@ -533,10 +580,17 @@ struct Ctx {
     mg_halo(L, x);
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (finest) tstart(e0);
-    hipLaunchKernelGGL((k_resid<T, TB>), dim3(nb_mg(A.nslices)), dim3(BS), 0, st, A.view(), B.Aval, b, x, B.res, ctl);
+    B.with_vals([&](auto* val) {
+      using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
+      with_c16(A, [&](auto c16) {
+        hipLaunchKernelGGL((k_resid<T, TB, VT, decltype(c16)::value>), dim3(nb_mg(A.nslices)), dim3(BS), 0, st,
+                           A.view(), val, b, x, B.res, ctl);
+      });
+    });
     KCHK();
     // matrix entries, x gathered once, b read, res written
-    if (finest) tstop(5, e0, (double)(sizeof(T) + 4) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB)));
+    if (finest)
+      tstop(5, e0, (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB)));
     mg_halo(L, B.res);
     MgLevel& C = mg[l - 1];
     MgBufs<T>& CB = bufs<T>(C);
@@ -565,9 +619,15 @@ struct Ctx {
     return mg_smooth<T, TB>(L, A, B, b, x, x, other, finest ? z : nullptr, rdot, part,
                             prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
   }
-  void precondition() {  // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB
-    if (mg_single) vcycle<float, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
-    else vcycle<double, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+  // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
+  // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
+  void precondition() {
+    if (mg_single) {
+      vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], part_d + 2 * MAXB);
+    } else {
+      halo(cg_r[0]);
+      vcycle<double, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+    }
   }
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
@@ -583,26 +643,31 @@ struct Ctx {
     vi.r[0] = cg_r[0];
     halo(y);
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
-    hipLaunchKernelGGL((k_cg_init<1>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, vi, lp.n_ghost, part_a, part_b);
+    float* r32o = mg_single ? r32 : nullptr;
+    with_c16(dPp, [&](auto c16) {
+      hipLaunchKernelGGL((k_cg_init<1, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, vi,
+                         lp.n_ghost, part_a, part_b, r32o);
+    });
     KCHK();
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
-    halo(cg_r[0]);
     precondition();
     Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
     halo(z);
     const double tol2 = tol * tol;
-    const double bytes_dir = 12.0 * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
-    const double bytes_upd = 48.0 * (double)dPp.nrows;
+    const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
+    const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)dPp.nrows;  // + the fp32 r copy
     int it = 0;
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
     for (;;) {
       for (int k = 0; k < chunk; ++k, ++it) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         tstart(e0);
-        hipLaunchKernelGGL((k_cg_dir<1>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, v, lp.n_ghost, rz.p, rz.nb,
-                           rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2, part_c, rr.p, rr.nb,
-                           rr.stride);
+        with_c16(dPp, [&](auto c16) {
+          hipLaunchKernelGGL((k_cg_dir<1, 8, true, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(),
+                             dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it,
+                             maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+        });
         KCHK();
         tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, 1, false, 2);
@@ -610,11 +675,10 @@ struct Ctx {
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
         hipLaunchKernelGGL((k_cg_upd<1>), dim3(nb), dim3(BS), 0, st, vu, dPp.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
-                           part_a);
+                           part_a, r32o);
         KCHK();
         tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, 1, false, 0);
-        halo(cg_r[0]);
         precondition();
         rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
         halo(z);
@@ -665,10 +729,12 @@ struct Ctx {
     const int nb = nb_for(dP.nslices);
     hipEvent_t e = nullptr;
     tstart(e);
-    hipLaunchKernelGGL(k_div, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, ax, ay, das1, out, dmp,
-                       -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
+    with_c16(dP, [&](auto c16) {
+      hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, ax, ay, das1,
+                         out, dmp, -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
+    });
     KCHK();
-    tstop(3, e, 20.0 * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
+    tstop(3, e, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
   }
   int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
     const int nb = nb_for(dP.nslices);
@@ -702,10 +768,12 @@ struct Ctx {
     const int nb = nb_for(dP.nslices);
     hipEvent_t e = nullptr;
     tstart(e);
-    hipLaunchKernelGGL(k_grad_proj, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, pp, das1, prm.dt, mode, ddir,
-                       usx, usy, ux, uy);
+    with_c16(dP, [&](auto c16) {
+      hipLaunchKernelGGL(k_grad_proj<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, pp, das1,
+                         prm.dt, mode, ddir, usx, usy, ux, uy);
+    });
     KCHK();
-    tstop(3, e, 20.0 * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
+    tstop(3, e, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
   }
 
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
@@ -780,7 +848,10 @@ struct Ctx {
     double *r = litw[0], *rh = litw[1], *pp = litw[2], *v = litw[3], *s = litw[4], *t = litw[5], *ph = litw[6],
            *sh = litw[7];
     auto spmv = [&](const double* in, double* out) {
-      hipLaunchKernelGGL(k_spmv, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), dLitv, in, out);
+      with_c16(dLit, [&](auto c16) {
+        hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), dLitv,
+                           in, out);
+      });
       KCHK();
     };
     spmv(x, t);
@@ -828,6 +899,13 @@ struct Ctx {
 };
 
 Ctx* C(void* p) { return static_cast<Ctx*>(p); }
+
+void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y) {
+  with_c16(A, [&](auto c16) {
+    hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(Ctx::nb_for(A.nslices)), dim3(BS), 0, st, A.view(), val, x,
+                       y);
+  });
+}
 
 template <class F>
 int guard(void* ctx, F&& f) {
@@ -899,13 +977,9 @@ void build_mg_host(Ctx& c) {
               "the uploaded mesh is not the red refinement of the hierarchy's coarse mesh");
     }
   }
-  const i64 N = c.mesh.N;
-  const int S = c.prm.nstrips > 0 ? c.prm.nstrips : auto_strips(N);
-  const double ymin = *std::min_element(c.mesh.y.begin(), c.mesh.y.end());
-  const double ymax = *std::max_element(c.mesh.y.begin(), c.mesh.y.end());
   for (int l = 0; l < Lv; ++l) {
     MgLevel& L = c.mg[l];
-    make_ordering_fixed(L.mesh, S, ymin, ymax, L.ord);
+    make_ordering_cuts(L.mesh, c.ord.cuts, L.ord);
     build_pattern(L.mesh, L.ord, L.P);
     Assembly A;
     assemble_stokes(L.mesh, L.ord, L.P, A);
@@ -945,6 +1019,18 @@ double diag_of(const Csr& A, const std::vector<double>& val, i64 g) {
   return 1.0;
 }
 
+// fp16 image of operator values for the fp32 V-cycle: null when disabled (prm.mg_f32_vals 1: every
+// level, 2: the finest level) or when some value is not a finite fp16 (|v| >= 65504)
+_Float16* upload_f16(Ctx& c, const std::vector<double>& v, bool finest) {
+  if (c.prm.mg_f32_vals == 1 || (c.prm.mg_f32_vals == 2 && finest)) return nullptr;
+  std::vector<_Float16> h(v.size());
+  for (size_t k = 0; k < v.size(); ++k) {
+    if (!(std::fabs(v[k]) < 65504.0)) return nullptr;
+    h[k] = (_Float16)v[k];
+  }
+  return c.upload(h);
+}
+
 template <typename T>
 T* upload_as(Ctx& c, const std::vector<double>& v) {
   if constexpr (std::is_same<T, double>::value) {
@@ -977,26 +1063,32 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
     if (l < Lv) {
       const Sell& S = L.sA;
       sell_values_x(A, r0, S, A.val, tmp);
-      L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
+      L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
                      A.rowptr[r0 + n] - A.rowptr[r0], S.padded};
+      c.attach_c16(S, L.dA);
       B.Aval = upload_as<T>(c, tmp);
+      if constexpr (std::is_same<T, float>::value) B.Aval16 = upload_f16(c, tmp, false);
       L.nsend = (i64)L.lp.send_local.size();
       L.dsend = c.upload(L.lp.send_local);
       B.sendbuf = c.dalloc<T>(std::max<i64>(1, L.nsend));
     } else {
-      if constexpr (std::is_same<T, double>::value) B.Aval = c.dKp_raw;
-      else B.Aval = upload_as<T>(c, kp_vals);
+      if constexpr (std::is_same<T, double>::value) {
+        B.Aval = c.dKp_raw;
+      } else {
+        B.Aval = upload_as<T>(c, kp_vals);
+        B.Aval16 = upload_f16(c, kp_vals, true);
+      }
       B.sendbuf = c.dalloc<T>(std::max<i64>(1, (i64)c.lp.send_local.size()));
     }
     if (l >= 1) {
       const Sell& S = L.sPr;
       sell_values_x(L.Pr, r0, S, L.Pr.val, tmp);
-      L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), S.nslices, S.nrows,
+      L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
                       L.Pr.rowptr[r0 + n] - L.Pr.rowptr[r0], S.padded};
       B.Prval = upload_as<T>(c, tmp);
       const Sell& R = L.sR;
       sell_values_x(L.R, L.r_r0, R, L.R.val, tmp);
-      L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), R.nslices, R.nrows,
+      L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), nullptr, R.nslices, R.nrows,
                      L.R.rowptr[L.r_r0 + R.nrows] - L.R.rowptr[L.r_r0], R.padded};
       B.Rval = upload_as<T>(c, tmp);
     }
@@ -1121,6 +1213,7 @@ void build(Ctx& c) {
     D.off = c.upload(S.slice_off);
     D.w = c.upload(S.slice_w);
     D.col = c.upload(S.col);
+    c.attach_c16(S, D);
     D.nslices = S.nslices;
     D.nrows = S.nrows;
     D.padded = S.padded;
@@ -1171,6 +1264,7 @@ void build(Ctx& c) {
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
     c.dKp_raw = c.upload(tmp);
     c.z = c.dalloc<double>(c.nloc);
+    c.r32 = c.dalloc<float>(c.nloc);
     c.mg_single = c.prm.mg_single != 0;
     if (c.mg_single) mg_alloc<float>(c, tmp);
     else mg_alloc<double>(c, tmp);
@@ -1838,7 +1932,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_GY: {
         perm_in(x, 1, t0, nullptr);
         const double* v = op == PUCFEM_OP_K ? c.dK : op == PUCFEM_OP_GX ? c.dGx : c.dGy;
-        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), v, t0, o0);
+        spmv_on(c.st, c.dP, v, t0, o0);
         KCHK();
         perm_out(y, 1, o0, nullptr);
         break;
@@ -1853,7 +1947,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         std::vector<double> a(N), xs(N);
         for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
         HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dPp.nslices)), dim3(BS), 0, c.st, c.dPp.view(), c.dKp, t0, o0);
+        spmv_on(c.st, c.dPp, c.dKp, t0, o0);
         KCHK();
         HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipStreamSynchronize(c.st));
@@ -1863,23 +1957,27 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_LIT: {
         require(c.dLitv, "no literal operator (scheme is Stokes)");
         perm_in(x, 1, t0, nullptr);
-        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dLit.nslices)), dim3(BS), 0, c.st, c.dLit.view(), c.dLitv, t0, o0);
+        spmv_on(c.st, c.dLit, c.dLitv, t0, o0);
         KCHK();
         perm_out(y, 1, o0, nullptr);
         break;
       }
       case PUCFEM_OP_DIV: {
         perm_in(x, 2, t0, t1);
-        hipLaunchKernelGGL(k_div, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dGx, c.dGy, t0, t1,
-                           c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
+        with_c16(c.dP, [&](auto c16) {
+          hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st,
+                             c.dP.view(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
+        });
         KCHK();
         perm_out(y, 1, o0, nullptr);
         break;
       }
       case PUCFEM_OP_GRAD: {
         perm_in(x, 1, t0, nullptr);
-        hipLaunchKernelGGL(k_grad, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dGx, c.dGy, t0,
-                           c.das1, o0, o1);
+        with_c16(c.dP, [&](auto c16) {
+          hipLaunchKernelGGL(k_grad<decltype(c16)::value>, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st,
+                             c.dP.view(), c.dGx, c.dGy, t0, c.das1, o0, o1);
+        });
         KCHK();
         perm_out(y, 2, o0, o1);
         break;
@@ -1891,7 +1989,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         HIPCHK(hipStreamSynchronize(c.st));
         for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
         HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-        hipLaunchKernelGGL(k_spmv, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st, c.dP.view(), c.dKv, t0, o0);
+        spmv_on(c.st, c.dP, c.dKv, t0, o0);
         KCHK();
         HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipStreamSynchronize(c.st));
@@ -2132,6 +2230,8 @@ int pucfem_info(void* ctx, int64_t* o) {
     o[7] = c.sPp.padded;
     o[8] = (int64_t)c.op_pairs.size();
     o[9] = (int64_t)c.dir_nodes.size();
+    o[10] = (c.dP.c16 ? 1 : 0) | (c.dPp.c16 ? 2 : 0) | (!c.mg.empty() && c.mg.back().f32.Aval16 ? 4 : 0);
+    o[11] = (int64_t)c.mg.size();
   });
 }
 
@@ -2304,10 +2404,12 @@ int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters,
     HIPCHK(hipMemsetAsync(c.ctl, 0, 2 * sizeof(int), c.st));
     auto launch = [&]() {
       switch (variant) {
-        case 0: hipLaunchKernelGGL((k_cg_dir<1, 0, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        case 1: hipLaunchKernelGGL((k_cg_dir<1, 8, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        case 2: hipLaunchKernelGGL((k_cg_dir<1, 0, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        default: hipLaunchKernelGGL((k_cg_dir<1, 8, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 0: hipLaunchKernelGGL((k_cg_dir<1, 0, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 1: hipLaunchKernelGGL((k_cg_dir<1, 8, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 2: hipLaunchKernelGGL((k_cg_dir<1, 0, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 3: hipLaunchKernelGGL((k_cg_dir<1, 8, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        default: require(A.c16 != nullptr, "variant 4 needs int16 columns");
+                 hipLaunchKernelGGL((k_cg_dir<1, 8, true, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
       }
       KCHK();
     };

@@ -93,21 +93,35 @@ void red_refine(const HostMesh& in, HostMesh& out, std::vector<i32>* edge_a, std
 }
 
 // ----------------------------------------------------------------------------- ordering
-int auto_strips(i64 N) { return (int)std::max<i64>(1, std::llround(std::sqrt((double)N) / 4.0)); }
+// sqrt(N)/2 strips of equal node count: a strip is ~2 node spacings high and 2 sqrt(N) nodes long,
+// so a stiffness neighbour lies within one strip of its row and a periodic master's columns (its
+// slave's neighbours, at the far end of the same or the next strip) within two -- a band of
+// ~4 sqrt(N) that fits int16 column deltas up to the ~10M-node meshes (L7: ~15k)
+int auto_strips(i64 N) { return (int)std::max<i64>(1, std::llround(std::sqrt((double)N) / 2.0)); }
 
 void make_ordering(const HostMesh& m, int nstrips, Ordering& ord) {
-  make_ordering_fixed(m, nstrips > 0 ? nstrips : auto_strips(m.N), *std::min_element(m.y.begin(), m.y.end()),
-                      *std::max_element(m.y.begin(), m.y.end()), ord);
+  const i64 N = m.N;
+  const int S = nstrips > 0 ? nstrips : auto_strips(N);
+  std::vector<double> ys(m.y.begin(), m.y.end());
+  std::sort(ys.begin(), ys.end());
+  std::vector<double> cuts;
+  for (int s = 1; s < S; ++s) {
+    // first distinct-value boundary at or after the equal-count target
+    i64 k = std::max<i64>(1, (i64)((double)N * s / S));
+    while (k < N && ys[k] == ys[k - 1]) ++k;
+    if (k >= N) break;
+    const double c = 0.5 * (ys[k - 1] + ys[k]);
+    if (cuts.empty() || c > cuts.back()) cuts.push_back(c);
+  }
+  make_ordering_cuts(m, cuts, ord);
 }
 
-void make_ordering_fixed(const HostMesh& m, int S, double ymin, double ymax, Ordering& ord) {
+void make_ordering_cuts(const HostMesh& m, const std::vector<double>& cuts, Ordering& ord) {
   const i64 N = m.N;
-  double span = ymax > ymin ? ymax - ymin : 1.0;
+  const int S = (int)cuts.size() + 1;
+  ord.cuts = cuts;
   std::vector<i32> strip(N);
-  for (i64 i = 0; i < N; ++i) {
-    i64 s = (i64)std::floor((m.y[i] - ymin) / span * S);
-    strip[i] = (i32)std::min<i64>(S - 1, std::max<i64>(0, s));
-  }
+  for (i64 i = 0; i < N; ++i) strip[i] = (i32)(std::upper_bound(cuts.begin(), cuts.end(), m.y[i]) - cuts.begin());
   ord.new2old.resize(N);
   std::iota(ord.new2old.begin(), ord.new2old.end(), 0);
   std::sort(ord.new2old.begin(), ord.new2old.end(), [&](i32 a, i32 b) {
@@ -429,6 +443,21 @@ void build_sell(const Csr& A, const LocalPlan& lp, Sell& S) {
         S.col[S.slice_off[s] + k * 64 + l] = c;
       }
     }
+}
+
+bool sell_col16(const Sell& S, std::vector<int16_t>& out) {
+  std::vector<int16_t> o(S.padded, 0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      if (s * 64 + l >= S.nrows) continue;
+      for (i64 k = 0; k < S.slice_w[s]; ++k) {
+        const i64 e = S.slice_off[s] + k * 64 + l, d = (i64)S.col[e] - s * 64;
+        if (d < INT16_MIN || d > INT16_MAX) return false;
+        o[e] = (int16_t)d;
+      }
+    }
+  out.swap(o);
+  return true;
 }
 
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,

@@ -43,11 +43,14 @@ struct Csr {
 struct Ordering {
   std::vector<i32> new2old, old2new;
   std::vector<i64> strip_ptr;  // size S+1, internal-index start of each strip
+  std::vector<double> cuts;    // S-1 increasing y values separating the strips
 };
+// y-strips holding equal node counts (cuts between distinct y values, so nodes of equal y -- the
+// periodic partners -- share a strip), x-sorted inside a strip
 void make_ordering(const HostMesh& m, int nstrips, Ordering& ord);
-// same strips (count and y-bounds) for every level of a hierarchy, so a node keeps its strip --
-// and its rank -- on every level it appears on
-void make_ordering_fixed(const HostMesh& m, int nstrips, double ymin, double ymax, Ordering& ord);
+// the given strips (cut values) for every level of a hierarchy, so a node keeps its strip -- and its
+// rank -- on every level it appears on
+void make_ordering_cuts(const HostMesh& m, const std::vector<double>& cuts, Ordering& ord);
 int auto_strips(i64 N);
 
 // Node-adjacency pattern (incl. diagonal) in internal numbering, sorted columns.
@@ -126,6 +129,9 @@ struct Sell {
 void build_sell(const Csr& A, const LocalPlan& lp, Sell& S);
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
                  std::vector<double>& out);
+// int16 image of a square operator's SELL columns: col - (first row of the slice); rows past nrows
+// point at the slice's first row.  false (out untouched) when some column is out of int16 range.
+bool sell_col16(const Sell& S, std::vector<int16_t>& out);
 // rows [r0, r0 + n) of A, columns resolved in `cols` (another level's plan)
 void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S);
 void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);

@@ -26,7 +26,21 @@ struct SellDev {
   const int32_t* w;    // nslices
   const int32_t* col;  // padded entries
   int64_t nslices, nrows;
+  const int16_t* c16;  // same entries as int16 deltas from the slice's first row (band fits), or null
 };
+
+template <class T>
+__device__ __forceinline__ T ldnt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+// column of entry e of the slice whose first row is `base`.  C16: the operator's band fits int16, so
+// the index stream is 2 B/entry instead of 4 (strip ordering keeps every neighbour within a few
+// strips of its row); NT: streamed with non-temporal loads (the gathered vector keeps L2 / MALL).
+template <bool C16, bool NT = true>
+__device__ __forceinline__ int32_t sell_col(const SellDev& A, int64_t e, int32_t base) {
+  if constexpr (C16) return base + (int32_t)(NT ? ldnt(A.c16 + e) : A.c16[e]);
+  else return NT ? ldnt(A.col + e) : A.col[e];
+}
 
 // ----------------------------------------------------------------------------- reductions
 __device__ __forceinline__ double wave_sum(double v) {
@@ -64,6 +78,29 @@ __device__ __forceinline__ double reduce_partials_max(const double* p, int nb, d
   double a = 0.0;
   for (int i = threadIdx.x; i < nb; i += BS) a = fmax(a, p[i]);
   return block_max(a, sh);
+}
+
+// wave index inside the block as a wave-uniform (scalar) value: slice indices derived from it stay
+// in SGPRs, so per-slice offsets / widths are scalar loads and width branches are uniform
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+template <int N>
+struct Wn {
+  static constexpr int value = N;
+};
+// f(Wn<w>{}) for the common SELL slice widths -- straight-line code in which every index / value
+// load of the slice issues before the dependent gathers -- and f(Wn<0>{}) (a runtime-width loop)
+// otherwise.  w must be wave-uniform.
+template <class F>
+__device__ __forceinline__ void by_width(int w, F&& f) {
+  switch (w) {
+    case 6: f(Wn<6>{}); break;
+    case 7: f(Wn<7>{}); break;
+    case 8: f(Wn<8>{}); break;
+    case 9: f(Wn<9>{}); break;
+    case 10: f(Wn<10>{}); break;
+    default: f(Wn<0>{}); break;
+  }
 }
 
 // slice range of this block

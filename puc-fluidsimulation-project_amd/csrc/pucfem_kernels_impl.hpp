@@ -8,19 +8,21 @@ namespace dev {
 
 // ----------------------------------------------------------------------------- SpMV
 // y = A x over owned rows (generic; unit `pucfem_apply`, residuals).
+template <bool C16>
 __global__ __launch_bounds__(BS) void k_spmv(SellDev A, const double* __restrict__ val,
                                              const double* __restrict__ x, double* __restrict__ y) {
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
     const int64_t row = s * 64 + lane;
+    const int32_t base = (int32_t)(s * 64);
     double acc = 0.0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
-      acc += val[e] * x[A.col[e]];
+      acc += val[e] * x[sell_col<C16, false>(A, e, base)];
     }
     if (row < A.nrows) y[row] = acc;
   }
@@ -44,13 +46,16 @@ struct CgVecs {
   const double* b[NR];
 };
 
-template <int NR>
+// r32 (optional): fp32 copy of r for the mixed-precision V-cycle, whose right-hand side is only
+// ever used in fp32 (bit-identical to converting inside the cycle, at half the bytes per read)
+template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
-                                                int64_t n_ghost, double* part_rr, double* part_bb) {
+                                                int64_t n_ghost, double* part_rr, double* part_bb,
+                                                float* __restrict__ r32 = nullptr) {
   __shared__ double sh[4];
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   double rr[NR], bb[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
@@ -58,13 +63,14 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restr
     const int64_t off = A.off[s];
     const int w = A.w[s];
     const int64_t row = s * 64 + lane;
+    const int32_t base = (int32_t)(s * 64);
     double acc[NR];
 #pragma unroll
     for (int c = 0; c < NR; ++c) acc[c] = 0.0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
       const double a = val[e];
-      const int32_t j = A.col[e];
+      const int32_t j = sell_col<C16, false>(A, e, base);
 #pragma unroll
       for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
     }
@@ -74,6 +80,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restr
         const double b = v.b[c][row];
         const double r = b - acc[c];
         v.r[c][row] = r;
+        if (r32) r32[row] = (float)r;
         v.po[c][row] = 0.0;
         rr[c] += r * r;
         bb[c] += b * b;
@@ -97,52 +104,51 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restr
   }
 }
 
-template <class T>
-__device__ __forceinline__ T ldnt(const T* p) {
-  return __builtin_nontemporal_load(p);
-}
-
 // One SELL slice of q = A^ (r + beta p_old): WMAX > 0 unrolls the entry loop (all index/value
 // loads issued before the dependent gathers); NT streams the matrix with non-temporal loads so it
 // does not evict the gathered vectors from L2 / MALL.
-template <int NR, int WMAX, bool NT>
+template <int NR, int WMAX, bool NT, bool C16>
 __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __restrict__ val, const CgVecs<NR>& v,
                                           const double (&beta)[NR], int64_t s, int lane, double (&pq)[NR]) {
   const int64_t off = A.off[s];
   const int w = A.w[s];
   const int64_t row = s * 64 + lane;
+  const int32_t base = (int32_t)(s * 64);
   double acc[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) acc[c] = 0.0;
-  if (WMAX > 0 && w <= WMAX) {
-    int32_t cj[WMAX > 0 ? WMAX : 1];
-    double a[WMAX > 0 ? WMAX : 1];
-#pragma unroll
-    for (int k = 0; k < WMAX; ++k) {
-      if (k < w) {
-        const int64_t e = off + (int64_t)k * 64 + lane;
-        cj[k] = NT ? ldnt(A.col + e) : A.col[e];
-        a[k] = NT ? ldnt(val + e) : val[e];
-      } else {
-        cj[k] = 0;
-        a[k] = 0.0;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < WMAX; ++k) {
-      if (k < w) {
-#pragma unroll
-        for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * v.po[c][cj[k]]);
-      }
-    }
-  } else {
+  auto generic = [&]() {
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
       const double a = NT ? ldnt(val + e) : val[e];
-      const int32_t j = NT ? ldnt(A.col + e) : A.col[e];
+      const int32_t j = sell_col<C16, NT>(A, e, base);
 #pragma unroll
       for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * v.po[c][j]);
     }
+  };
+  if constexpr (WMAX > 0) {
+    by_width(w, [&](auto wc) {
+      constexpr int WN = decltype(wc)::value;
+      if constexpr (WN > 0) {
+        int32_t cj[WN];
+        double a[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          cj[k] = sell_col<C16, NT>(A, e, base);
+          a[k] = NT ? ldnt(val + e) : val[e];
+        }
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+#pragma unroll
+          for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * v.po[c][cj[k]]);
+        }
+      } else {
+        generic();
+      }
+    });
+  } else {
+    generic();
   }
   if (row < A.nrows) {
 #pragma unroll
@@ -155,7 +161,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
   }
 }
 
-template <int NR, int WMAX = 8, bool NT = true>
+template <int NR, int WMAX, bool NT, bool C16>
 __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
@@ -194,11 +200,11 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restri
   }
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   double pq[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT>(A, val, v, beta, s, lane, pq);
+  for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, s, lane, pq);
   for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
@@ -213,7 +219,8 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restri
 
 template <int NR>
 __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, const double* part_pq, int nb_pq,
-                                               int stride_pq, const double* scal, const int* ctl, double* part_rr) {
+                                               int stride_pq, const double* scal, const int* ctl, double* part_rr,
+                                               float* __restrict__ r32 = nullptr) {
   __shared__ double sh[4];
   if (ctl[0]) return;
   double alpha[NR], rr[NR];
@@ -231,6 +238,7 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
       v.y[c][i] += alpha[c] * v.pn[c][i];
       const double r = v.r[c][i] - alpha[c] * v.q[c][i];
       v.r[c][i] = r;
+      if (NR == 1 && r32) r32[i] = (float)r;
       rr[c] += r * r;
     }
   }
@@ -269,6 +277,7 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
 // calculate_divergence (StokesColor.py:130-165) in operator form: div = (Gx ux + Gy uy) / (area_sum + 1e-12).
 // Optionally the pressure RHS of the row-scaled system: braw = (M + 1e-12) * (-(1/DT) * div)
 // (StokesColor.py:554 with A_pressure = K / (M + 1e-12)).  Partials: [0] max|div|, [1] sum(braw).
+template <bool C16>
 __global__ __launch_bounds__(BS) void k_div(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
                                             const double* __restrict__ ux, const double* __restrict__ uy,
                                             const double* __restrict__ as1, double* __restrict__ div,
@@ -277,18 +286,36 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, const double* __restrict_
   __shared__ double sh[4];
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   double mx = 0.0, sb = 0.0;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
     const int64_t row = s * 64 + lane;
+    const int32_t base = (int32_t)(s * 64);
     double acc = 0.0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      const int32_t j = A.col[e];
-      acc += gx[e] * ux[j] + gy[e] * uy[j];
-    }
+    by_width(w, [&](auto wc) {
+      constexpr int WN = decltype(wc)::value;
+      if constexpr (WN > 0) {
+        int32_t cj[WN];
+        double ax[WN], ay[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          cj[k] = sell_col<C16>(A, e, base);
+          ax[k] = ldnt(gx + e);
+          ay[k] = ldnt(gy + e);
+        }
+#pragma unroll
+        for (int k = 0; k < WN; ++k) acc += ax[k] * ux[cj[k]] + ay[k] * uy[cj[k]];
+      } else {
+        for (int k = 0; k < w; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          const int32_t j = sell_col<C16>(A, e, base);
+          acc += ldnt(gx + e) * ux[j] + ldnt(gy + e) * uy[j];
+        }
+      }
+    });
     if (row < A.nrows) {
       const double d = acc / as1[row];
       div[row] = d;
@@ -330,6 +357,7 @@ __global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int
 
 // projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
 // projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
+template <bool C16>
 __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __restrict__ gx,
                                                   const double* __restrict__ gy, const double* __restrict__ p,
                                                   const double* __restrict__ as1, double dt, int mode,
@@ -337,18 +365,40 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __res
                                                   const double* usy, double* ux, double* uy) {
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
     const int64_t row = s * 64 + lane;
+    const int32_t base = (int32_t)(s * 64);
     double ax = 0.0, ay = 0.0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      const double pj = p[A.col[e]];
-      ax += gx[e] * pj;
-      ay += gy[e] * pj;
-    }
+    by_width(w, [&](auto wc) {
+      constexpr int WN = decltype(wc)::value;
+      if constexpr (WN > 0) {
+        int32_t cj[WN];
+        double vx[WN], vy[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          cj[k] = sell_col<C16>(A, e, base);
+          vx[k] = ldnt(gx + e);
+          vy[k] = ldnt(gy + e);
+        }
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          const double pj = p[cj[k]];
+          ax += vx[k] * pj;
+          ay += vy[k] * pj;
+        }
+      } else {
+        for (int k = 0; k < w; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          const double pj = p[sell_col<C16>(A, e, base)];
+          ax += ldnt(gx + e) * pj;
+          ay += ldnt(gy + e) * pj;
+        }
+      }
+    });
     if (row < A.nrows) {
       const double d = as1[row];
       const double gpx = ax / d, gpy = ay / d;
@@ -364,20 +414,22 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __res
 }
 
 // gradient only (calculate_gradiant, StokesColor.py:224-263) for the unit op
+template <bool C16>
 __global__ __launch_bounds__(BS) void k_grad(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
                                              const double* __restrict__ p, const double* __restrict__ as1,
                                              double* outx, double* outy) {
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
     const int64_t row = s * 64 + lane;
+    const int32_t base = (int32_t)(s * 64);
     double ax = 0.0, ay = 0.0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
-      const double pj = p[A.col[e]];
+      const double pj = p[sell_col<C16, false>(A, e, base)];
       ax += gx[e] * pj;
       ay += gy[e] * pj;
     }
@@ -757,41 +809,41 @@ __global__ void k_bicg_x(int64_t n, double* x, const double* ph, const double* s
 // ----------------------------------------------------------------------------- multigrid (pressure)
 // sum_k A[row, k] x[col_k] for one SELL slice lane: entry loop unrolled to WMAX (index / value loads
 // issued before the dependent gathers), matrix streamed with non-temporal loads.
-template <int WMAX, typename T, typename G>
-__device__ __forceinline__ T sell_row_dot_g(const SellDev& A, const T* __restrict__ val, const G& gx, int64_t s,
+// VT: the stored value type (fp16 in the mixed-precision V-cycle, widened to T for the arithmetic).
+// s must be wave-uniform (see wave_id); entries are summed in k order for every width.
+template <bool C16, typename T, typename VT, typename G>
+__device__ __forceinline__ T sell_row_dot_g(const SellDev& A, const VT* __restrict__ val, const G& gx, int64_t s,
                                             int lane) {
   const int64_t off = A.off[s];
   const int w = A.w[s];
+  const int32_t base = (int32_t)(s * 64);
   T acc = 0;
-  if (w <= WMAX) {
-    int32_t cj[WMAX];
-    T a[WMAX];
+  by_width(w, [&](auto wc) {
+    constexpr int WN = decltype(wc)::value;
+    if constexpr (WN > 0) {
+      int32_t cj[WN];
+      VT a[WN];
 #pragma unroll
-    for (int k = 0; k < WMAX; ++k) {
-      if (k < w) {
+      for (int k = 0; k < WN; ++k) {
         const int64_t e = off + (int64_t)k * 64 + lane;
-        cj[k] = ldnt(A.col + e);
+        cj[k] = sell_col<C16>(A, e, base);
         a[k] = ldnt(val + e);
-      } else {
-        cj[k] = 0;
-        a[k] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < WN; ++k) acc += (T)a[k] * gx(cj[k]);
+    } else {
+      for (int k = 0; k < w; ++k) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        acc += (T)ldnt(val + e) * gx(sell_col<C16>(A, e, base));
       }
     }
-#pragma unroll
-    for (int k = 0; k < WMAX; ++k)
-      if (k < w) acc += a[k] * gx(cj[k]);
-  } else {
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      acc += ldnt(val + e) * gx(ldnt(A.col + e));
-    }
-  }
+  });
   return acc;
 }
-template <int WMAX, typename T>
-__device__ __forceinline__ T sell_row_dot(const SellDev& A, const T* __restrict__ val, const T* __restrict__ x,
+template <bool C16, typename T, typename VT>
+__device__ __forceinline__ T sell_row_dot(const SellDev& A, const VT* __restrict__ val, const T* __restrict__ x,
                                           int64_t s, int lane) {
-  return sell_row_dot_g<WMAX>(A, val, [x](int32_t j) { return x[j]; }, s, lane);
+  return sell_row_dot_g<C16, T>(A, val, [x](int32_t j) { return x[j]; }, s, lane);
 }
 
 // Chebyshev smoothing step of the Jacobi-preconditioned smoother on A x = b (pucfem_api.hip
@@ -805,8 +857,8 @@ __device__ __forceinline__ T sell_row_dot(const SellDev& A, const T* __restrict_
 // T: the V-cycle's storage/arithmetic type (float in the mixed-precision cycle, double otherwise);
 // TB: the right-hand side (the CG residual, double, on the finest level); TO: the output (double
 // for the final step that writes the preconditioned residual z).
-template <typename T, typename TB, typename TO>
-__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const T* __restrict__ val, const T* __restrict__ dinv,
+template <typename T, typename TB, typename TO, typename VT, bool C16>
+__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const VT* __restrict__ val, const T* __restrict__ dinv,
                                              const TB* __restrict__ b, const T* __restrict__ xin,
                                              TO* __restrict__ xout, T* __restrict__ d, double c1, double c2,
                                              double c20, int mode, const int* ctl, const double* __restrict__ rdot,
@@ -815,14 +867,15 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const T* __restrict__ va
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
   double acc_rz = 0.0;
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = s * 64 + lane;
     T ax = 0;
-    if (mode == 1) ax = sell_row_dot<8>(A, val, xin, s, lane);
-    else if (mode == 2) ax = sell_row_dot_g<8>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
+    if (mode == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
+    else if (mode == 2)
+      ax = sell_row_dot_g<C16, T>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
     if (row < A.nrows) {
       T dn, xo;
       if (mode == 0) {
@@ -846,16 +899,16 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const T* __restrict__ va
 }
 
 // res = b - A x
-template <typename T, typename TB>
-__global__ __launch_bounds__(BS) void k_resid(SellDev A, const T* __restrict__ val, const TB* __restrict__ b,
+template <typename T, typename TB, typename VT, bool C16>
+__global__ __launch_bounds__(BS) void k_resid(SellDev A, const VT* __restrict__ val, const TB* __restrict__ b,
                                               const T* __restrict__ x, T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
   block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = s * 64 + lane;
-    const T ax = sell_row_dot<8>(A, val, x, s, lane);
+    const T ax = sell_row_dot<C16>(A, val, x, s, lane);
     if (row < A.nrows) res[row] = (T)b[row] - ax;
   }
 }
@@ -867,7 +920,7 @@ __global__ __launch_bounds__(BS) void k_transfer(SellDev M, const T* __restrict_
   if (ctl && ctl[0]) return;
   int64_t s0, s1;
   block_slices(M.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = M.off[s];
     const int w = M.w[s];

@@ -60,6 +60,9 @@ class Tolerances:
     mg_post: int = 0
     mg_rep_nodes: int = 0  # multi-rank: replicate coarse levels up to this size (0: library default)
     mg_single: bool = True  # fp32 V-cycle inside the fp64 CG (same iteration counts, ~30% fewer bytes)
+    mg_f16_vals: bool | str = True  # fp32 cycle: level operators stored in fp16 (fp32 arithmetic); "coarse": all but the finest
+    index16: bool = True  # int16 column deltas where the operator band fits
+    mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
 
 
 class Context:
@@ -128,7 +131,9 @@ class Context:
                         maxit_pres=tol.maxit_pres, maxit_lin=tol.maxit_lin, warm_start=int(tol.warm_start),
                         sl_k=10, capture_radius=capture, center_x=center[0], center_y=center[1],
                         precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio, mg_post=tol.mg_post,
-                        mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes)
+                        mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes,
+                        mg_f32_vals=2 if tol.mg_f16_vals == "coarse" else int(not tol.mg_f16_vals),
+                        idx32=int(not tol.index16), mg_kind=tol.mg_kind)
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
@@ -161,10 +166,13 @@ class Context:
         return x, it.value
 
     def info(self):
-        o = (ct.c_int64 * 10)()
+        o = (ct.c_int64 * 12)()
         self._c(self.L.pucfem_info(self.h, o))
         keys = ["N", "T", "nnz_P", "nnz_Pp", "n_own", "n_ghost", "sell_P", "sell_Pp", "n_pairs", "n_dirichlet"]
-        return dict(zip(keys, list(o)))
+        d = dict(zip(keys, list(o)))
+        d["index16_P"], d["index16_Pp"], d["mg_f16_vals"] = bool(o[10] & 1), bool(o[10] & 2), bool(o[10] & 4)
+        d["mg_levels"] = o[11]
+        return d
 
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))

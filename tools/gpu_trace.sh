@@ -1,0 +1,15 @@
+#!/bin/bash
+# Kernel timeline of the bench's timed steps (rocprofv3 --kernel-trace only), summarised by
+# tools/trace_step.py.  Usage: tools/gpu_trace.sh TAG [bench args]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+TAG=${1:-trace}; shift
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+rm -rf /tmp/tr_$TAG
+timeout -k 10 600 rocprofv3 --kernel-trace -d /tmp/tr_$TAG -o run --output-format csv -- \
+  python "$ROOT/bench.py" --no-cpu-baseline --no-secondary "$@" > "$OUT/bench.out" 2> "$OUT/bench.err"
+rc=$?; echo "rocprof rc=$rc" >&2; [ $rc -ne 0 ] && { tail -5 "$OUT/bench.err" >&2; exit $rc; }
+f=$(find /tmp/tr_$TAG -name "*kernel_trace.csv" | head -1)
+python "$ROOT/tools/trace_step.py" "$f" > "$OUT/trace_summary.txt" && cat "$OUT/trace_summary.txt" >&2
