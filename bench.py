@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
     ap.add_argument("--rtol-pres", type=float, default=1e-8)
     ap.add_argument("--mg-double", action="store_true", help="fp64 V-cycle instead of the fp32 one")
-    ap.add_argument("--mg-vals", default="f16", choices=["f16", "f32", "coarse-f16"],
+    ap.add_argument("--mg-vals", default="f32", choices=["f16", "f32", "coarse-f16"],
                     help="fp32 V-cycle operator storage: fp16 on every level, fp32, or fp16 below the finest level")
     ap.add_argument("--index32", action="store_true", help="int32 SELL columns instead of int16 deltas")
     ap.add_argument("--mg-pre", type=int, default=2, help="Chebyshev pre-smoothing degree")

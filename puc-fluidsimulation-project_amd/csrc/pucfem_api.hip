@@ -6,6 +6,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -314,7 +316,7 @@ struct Ctx {
 
   static int nb_for(i64 nslices) { return (int)std::max<i64>(1, std::min<i64>(MAXB, (nslices + 3) / 4)); }
   // grid of the V-cycle kernels that produce no partials (more waves in flight than MAXB blocks)
-  int mg_nb_max = 4096;
+  int mg_nb_max = 16384;
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
   // semi-Lagrangian grid: latency-bound gathers want more waves in flight than MAXB blocks give
@@ -338,12 +340,14 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ communication
+  // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
+  // the all-reduce across ranks): consumers read one scalar instead of re-reducing up to MAXB
+  // partials in each of their blocks
   Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
-    if (world == 1) return Red{part, nb, MAXB};
     double* buf = redbuf + 8 * slot;
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
     KCHK();
-    comm->allreduce(buf, nv, is_max, st);
+    if (world > 1) comm->allreduce(buf, nv, is_max, st);
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
@@ -1019,6 +1023,20 @@ double diag_of(const Csr& A, const std::vector<double>& val, i64 g) {
   return 1.0;
 }
 
+// binary SELL image: int64 nslices, nrows, padded; int64 slice_off[nslices+1]; int32 slice_w[nslices];
+// int32 col[padded]; double val[padded]
+void dump_sell(const char* path, const Sell& S, const std::vector<double>& val) {
+  FILE* f = std::fopen(path, "wb");
+  require(f != nullptr, std::string("cannot write ") + path);
+  const int64_t h[3] = {S.nslices, S.nrows, S.padded};
+  std::fwrite(h, sizeof(h), 1, f);
+  std::fwrite(S.slice_off.data(), sizeof(int64_t), S.slice_off.size(), f);
+  std::fwrite(S.slice_w.data(), sizeof(int32_t), S.slice_w.size(), f);
+  std::fwrite(S.col.data(), sizeof(int32_t), S.col.size(), f);
+  std::fwrite(val.data(), sizeof(double), val.size(), f);
+  std::fclose(f);
+}
+
 // fp16 image of operator values for the fp32 V-cycle: null when disabled (prm.mg_f32_vals 1: every
 // level, 2: the finest level) or when some value is not a finite fp16 (|v| >= 65504)
 _Float16* upload_f16(Ctx& c, const std::vector<double>& v, bool finest) {
@@ -1203,6 +1221,14 @@ void build(Ctx& c) {
   if (stokes) build_sell(c.Pp, c.lp, c.sPp);
   if (literal) build_sell(c.Lit, c.lp, c.sLit);
   c.built = true;
+  // tooling hook (tools/spmv_lab.hip --real): the pressure operator's SELL image
+  if (const char* path = std::getenv("PUCFEM_DUMP_SELL")) {
+    if (stokes) {
+      std::vector<double> v;
+      sell_values(c.Pp, c.lp, c.sPp, c.Pp.val, v);
+      dump_sell(path, c.sPp, v);
+    }
+  }
   if (c.host_only) return;
 
   // ---------------------------------------------------------------- device upload

@@ -17,7 +17,7 @@ namespace pucfem {
 namespace dev {
 
 constexpr int BS = 256;     // threads per block
-constexpr int MAXB = 1024;  // max blocks of a partial-producing launch (= partial stride)
+constexpr int MAXB = 8192;  // max blocks of a partial-producing launch (= partial stride)
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
 constexpr int SLB = 4096;   // max blocks (= partial stride) of the semi-Lagrangian kernel
 

@@ -60,7 +60,9 @@ class Tolerances:
     mg_post: int = 0
     mg_rep_nodes: int = 0  # multi-rank: replicate coarse levels up to this size (0: library default)
     mg_single: bool = True  # fp32 V-cycle inside the fp64 CG (same iteration counts, ~30% fewer bytes)
-    mg_f16_vals: bool | str = True  # fp32 cycle: level operators stored in fp16 (fp32 arithmetic); "coarse": all but the finest
+    # fp32 cycle: level operators stored in fp16 (fp32 arithmetic); "coarse": all but the finest.  Off by
+    # default: at L7 it saves ~10% of the smoother's bytes but costs ~1 extra CG iteration per solve
+    mg_f16_vals: bool | str = False
     index16: bool = True  # int16 column deltas where the operator band fits
     mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
 
