@@ -345,14 +345,14 @@ struct Ctx {
   // partials in each of their blocks
   Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
     double* buf = redbuf + 8 * slot;
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
     KCHK();
     if (world > 1) comm->allreduce(buf, nv, is_max, st);
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
   void reduce_into(double* part, int nb, int nv, bool is_max, int slot, int stride = MAXB) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part, nb, stride, nv, is_max ? 1 : 0, vals + slot);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, vals + slot);
     KCHK();
     if (world > 1)
       comm->allreduce(vals + slot, nv, is_max, st);
@@ -869,7 +869,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(bicg_sc, init, sizeof(init), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, b, b, (const double*)r, (const double*)r, part_a);
     KCHK();
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part_a, nb, MAXB, 2, 0, bicg_sc + 8);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, bicg_sc + 8);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_pinned, bicg_sc + 8, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -891,7 +891,7 @@ struct Ctx {
       hipLaunchKernelGGL(k_bicg_scalar, dim3(1), dim3(BS), 0, st, 2, part_a, nb, bicg_sc);
       hipLaunchKernelGGL(k_bicg_x, dim3(ge), dim3(BS), 0, st, n, x, ph, sh, s, t, r, bicg_sc);
       hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, r, r, (const double*)nullptr, (const double*)nullptr, part_a);
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, st, part_a, nb, MAXB, 1, 0, bicg_sc + 5);
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_a, nb, MAXB, 1, 0, bicg_sc + 5);
       KCHK();
       HIPCHK(hipMemcpyAsync(h_pinned, bicg_sc + 5, sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -1204,7 +1204,7 @@ void build(Ctx& c) {
     c.lp = c.mg[Lv].lp;
     for (int l = 0; l <= Lv; ++l) {  // host SELL images; resolving every column validates the plans
       MgLevel& L = c.mg[l];
-      if (l < Lv) build_sell_x(L.Pp, L.own0(c.rank), L.lp.n_own, L.lp, L.sA);
+      if (l < Lv) build_sell_x(L.Pp, L.own0(c.rank), L.lp.n_own, L.lp, L.sA, true);
       if (l >= 1) {
         const MgLevel& C = c.mg[l - 1];
         build_sell_x(L.Pr, L.own0(c.rank), L.lp.n_own, C.lp, L.sPr);
@@ -2183,15 +2183,15 @@ int pucfem_mixing_index(void* ctx, const double* cin, double* out3) {
                        (const double*)c.dwmix, (const double*)c.dwmix, c.part_a);
     KCHK();
     // part_a[0] = sum w c, part_a[MAXB] = sum w^2 -> recompute sum w separately
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_a, nb, MAXB, 1, 0, c.vals + 2);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_a, nb, MAXB, 1, 0, c.vals + 2);
     std::vector<double> ones(N, 1.0);
     double* on = c.cg_pb[0];
     HIPCHK(hipMemcpyAsync(on, ones.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
     hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, (const double*)c.dwmix, (const double*)on,
                        (const double*)nullptr, (const double*)nullptr, c.part_b);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
     hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, c.dwmix, c.vals + 2, 1, 1, c.part_c);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BS), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
     HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
     double* rec = c.vals + 8;
     hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec);

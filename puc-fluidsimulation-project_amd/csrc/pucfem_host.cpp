@@ -726,7 +726,7 @@ void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& 
   }
 }
 
-void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S) {
+void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S, bool pad_self) {
   S.nrows = n;
   S.nslices = (n + 63) / 64;
   S.slice_off.assign(S.nslices + 1, 0);
@@ -747,7 +747,8 @@ void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S) {
       const i64 r = s * 64 + l;
       const i64 len = r < n ? A.rowptr[r0 + r + 1] - A.rowptr[r0 + r] : 0;
       for (i64 k = 0; k < S.slice_w[s]; ++k)
-        S.col[S.slice_off[s] + k * 64 + l] = k < len ? to_local(cols, A.col[A.rowptr[r0 + r] + k]) : 0;
+        S.col[S.slice_off[s] + k * 64 + l] =
+            k < len ? to_local(cols, A.col[A.rowptr[r0 + r] + k]) : (pad_self && r < n ? (i32)r : 0);
     }
 }
 

@@ -133,7 +133,9 @@ void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::ve
 // point at the slice's first row.  false (out untouched) when some column is out of int16 range.
 bool sell_col16(const Sell& S, std::vector<int16_t>& out);
 // rows [r0, r0 + n) of A, columns resolved in `cols` (another level's plan)
-void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S);
+// pad_self: padding entries point at their own row (square operators: keeps the band, see
+// sell_col16); otherwise at column 0
+void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S, bool pad_self = false);
 void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
 i32 to_local(const LocalPlan& lp, i32 g);
 

@@ -688,12 +688,37 @@ __global__ void k_tracer(MeshDev M, GridDev G, const double* __restrict__ ux, co
 }
 
 // ----------------------------------------------------------------------------- misc
-// 1-block reduction of nv partial arrays (sum or max) into out[0..nv) (multi-GPU pre-allreduce, stats)
-__global__ __launch_bounds__(BS) void k_reduce(const double* part, int nb, int stride, int nv, int is_max, double* out) {
-  __shared__ double sh[4];
+// 1-block reduction of nv partial arrays (sum or max) into out[0..nv): the consumers of a producer
+// kernel's partials read one scalar.  RB threads, each with RU independent loads in flight (the
+// partials are L2 / MALL misses; a dependent load chain per thread would take nb / RB round trips).
+// Fixed combination order: deterministic for a given nb.
+constexpr int RB = 1024, RU = 8;
+__global__ __launch_bounds__(RB) void k_reduce(const double* part, int nb, int stride, int nv, int is_max, double* out) {
+  __shared__ double sh[RB / 64];
   for (int v = 0; v < nv; ++v) {
-    const double t = is_max ? reduce_partials_max(part + v * stride, nb, sh) : reduce_partials(part + v * stride, nb, sh);
-    if (threadIdx.x == 0) out[v] = t;
+    const double* p = part + (int64_t)v * stride;
+    double a[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) a[u] = 0.0;  // partial maxima are of |.|, >= 0
+    for (int b0 = threadIdx.x; b0 < nb; b0 += RB * RU) {
+      double t[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) t[u] = b0 + u * RB < nb ? p[b0 + u * RB] : 0.0;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) a[u] = is_max ? fmax(a[u], t[u]) : a[u] + t[u];
+    }
+    double x = a[0];
+#pragma unroll
+    for (int u = 1; u < RU; ++u) x = is_max ? fmax(x, a[u]) : x + a[u];
+    x = is_max ? wave_max(x) : wave_sum(x);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double y = sh[0];
+      for (int w = 1; w < RB / 64; ++w) y = is_max ? fmax(y, sh[w]) : y + sh[w];
+      out[v] = y;
+    }
   }
 }
 
