@@ -1474,14 +1474,16 @@ void build(Ctx& c) {
       build_tri_grid(X, Y, tri, 1.0, LG, 1e-6);
       GridDev lg{};
       dgrid(LG, lg, false);
-      std::vector<double> rec(8 * (size_t)m.T);
+      const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
+      std::vector<double> rec(8 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
       for (i64 t = 0; t < m.T; ++t) {
         for (int v = 0; v < 3; ++v) {
           rec[8 * t + 2 * v] = X[tri[3 * t + v]];
           rec[8 * t + 2 * v + 1] = Y[tri[3 * t + v]];
         }
-        rec[8 * t + 6] = cx[t];
-        rec[8 * t + 7] = cy[t];
+        int32_t tail[4] = {tri[3 * t], tri[3 * t + 1], tri[3 * t + 2], 0};
+        std::memcpy(&tail[3], &rho2[t], sizeof(float));
+        std::memcpy(&rec[8 * t + 6], tail, sizeof(tail));
       }
       c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item, c.upload(rec)};
     }

@@ -7,6 +7,7 @@
 #include <map>
 #include <numeric>
 #include <stdexcept>
+#include <thread>
 
 namespace pucfem {
 
@@ -514,6 +515,58 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
     G.px[k] = cx[t];
     G.py[k] = cy[t];
   }
+}
+
+std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy,
+                                        int k) {
+  const i64 T = (i64)cx.size();
+  std::vector<float> out(T, INFINITY);
+  if (T <= k) return out;
+  auto work = [&](i64 t0, i64 t1) {
+    std::vector<double> best(k);
+    for (i64 t = t0; t < t1; ++t) {
+      const double qx = cx[t], qy = cy[t];
+      std::fill(best.begin(), best.end(), INFINITY);  // ascending k smallest squared distances
+      const i32 ci = cell_of(qx, G.x0, G.hx, G.nx), cj = cell_of(qy, G.y0, G.hy, G.ny);
+      for (i32 r = 0;; ++r) {
+        const i32 jlo = std::max(cj - r, 0), jhi = std::min(cj + r, G.ny - 1);
+        for (i32 j = jlo; j <= jhi; ++j) {
+          const bool edge = j == cj - r || j == cj + r;
+          for (i32 i = ci - r; i <= ci + r; i += (edge || r == 0) ? 1 : 2 * r) {
+            if (i < 0 || i >= G.nx) continue;
+            const i64 c = (i64)j * G.nx + i;
+            for (i32 e = G.cell_start[c]; e < G.cell_start[c + 1]; ++e) {
+              if (G.item[e] == (i32)t) continue;
+              const double dx = G.px[e] - qx, dy = G.py[e] - qy, d = dx * dx + dy * dy;
+              if (d >= best[k - 1]) continue;
+              int p = k - 1;
+              while (p > 0 && best[p - 1] > d) {
+                best[p] = best[p - 1];
+                --p;
+              }
+              best[p] = d;
+            }
+          }
+        }
+        // every unvisited cell is at least this far from q
+        double dmin = INFINITY;
+        if (ci - r > 0) dmin = std::min(dmin, qx - (G.x0 + (ci - r) * G.hx));
+        if (ci + r < G.nx - 1) dmin = std::min(dmin, G.x0 + (ci + r + 1) * G.hx - qx);
+        if (cj - r > 0) dmin = std::min(dmin, qy - (G.y0 + (cj - r) * G.hy));
+        if (cj + r < G.ny - 1) dmin = std::min(dmin, G.y0 + (cj + r + 1) * G.hy - qy);
+        if (dmin == INFINITY || (dmin > 0 && best[k - 1] < dmin * dmin * (1.0 - 1e-9))) break;
+      }
+      // round down: the device's acceptance test must never see a larger radius than the true one
+      float f = (float)best[k - 1];
+      if ((double)f > best[k - 1]) f = std::nextafter(f, 0.0f);
+      out[t] = f;
+    }
+  };
+  const int nt = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int w = 0; w < nt; ++w) th.emplace_back(work, T * w / nt, T * (w + 1) / nt);
+  for (auto& h : th) h.join();
+  return out;
 }
 
 void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,

@@ -148,6 +148,10 @@ struct Grid {
   std::vector<double> px, py;   // centroid coordinates per entry (centroid grid only)
 };
 void build_centroid_grid(const std::vector<double>& cx, const std::vector<double>& cy, double per_cell, Grid& G);
+// per triangle t: the squared distance from its centroid to its k-th nearest OTHER centroid (G is
+// the centroid grid of cx, cy), rounded down to fp32; +inf when there are fewer than k others
+std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy,
+                                        int k);
 // inflate > 0: each bbox grows by inflate * (its extent) + 1e-14 on every side, so a point that a
 // rounding-sensitive weight test accepts on a triangle's edge is still listed with that triangle
 void build_tri_grid(const std::vector<double>& x, const std::vector<double>& y, const std::vector<i32>& tri,

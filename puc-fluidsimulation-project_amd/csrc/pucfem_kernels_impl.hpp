@@ -496,16 +496,31 @@ __device__ __forceinline__ bool knn_less(double d, int32_t i, double bd, int32_t
 //      listed in q's cell of the inflated-bbox grid L; among those that pass, take the one with the
 //      smallest (d^2, id) key T*.  A triangle whose weights are all >= SL_MARGIN contains q with a
 //      margin no other triangle's test can reach, so the scan stops at it;
-//   2. T* is the answer iff fewer than 10 centroids have a key below T*'s (its rank is < 10):
-//      counted over the centroid-grid cells that meet the box [q - R, q + R]^2, R = sqrt(d*^2).
+//   2. T* is the answer iff fewer than 10 centroids have a key below T*'s (its rank is < 10).  Fast
+//      accept: every such centroid c has |c - c_T*| <= 2 R (R = |q - c_T*|), so 4 R^2 below the
+//      squared distance from c_T* to its 10th nearest other centroid (rho2, precomputed) bounds the
+//      rank by 9.  Otherwise they are counted over the centroid-grid cells meeting [q - R, q + R]^2.
 // Otherwise no triangle among the 10 nearest passes and the reference keeps c[n].
 struct LocDev {
   int32_t nx, ny;
   double x0, y0, hx, hy;
   const int32_t* start;  // nx*ny+1
   const int32_t* item;   // triangle ids, ascending per cell
-  const double* rec;     // per triangle: x1 y1 x2 y2 x3 y3 cx cy (64 B; cx, cy as the centroid grid's)
+  // per triangle, one 64-B record: x1 y1 x2 y2 x3 y3 (fp64), vertex ids a b d (int32), rho2 (fp32:
+  // squared distance from the centroid to the 10th nearest other centroid, rounded down)
+  const double* rec;
 };
+struct SlTri {
+  double x1, y1, x2, y2, x3, y3;
+  int32_t a, b, d;
+  float rho2;
+};
+__device__ __forceinline__ SlTri sl_tri(const LocDev& L, int32_t t) {
+  const double2* r = reinterpret_cast<const double2*>(L.rec + 8 * (int64_t)t);
+  const double2 p = r[0], q = r[1], s = r[2];
+  const int4 m = reinterpret_cast<const int4*>(r)[3];
+  return SlTri{p.x, p.y, q.x, q.y, s.x, s.y, m.x, m.y, m.z, __int_as_float(m.w)};
+}
 constexpr double SL_MARGIN = 1e-6;
 
 // -> triangle id, or -1 (no triangle among the KNN nearest centroids contains q)
@@ -514,27 +529,31 @@ __device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, 
   const int64_t cell = (int64_t)cj * L.nx + ci;
   int32_t best = 0x7fffffff;
   double bestd = INFINITY;
+  float brho2 = 0.f;
   const int32_t e1 = L.start[cell + 1];
   for (int32_t e = L.start[cell]; e < e1; ++e) {
     const int32_t t = L.item[e];
-    const double* r = L.rec + 8 * (int64_t)t;
-    const double x1 = r[0], y1 = r[1], x2 = r[2], y2 = r[3], x3 = r[4], y3 = r[5];
+    const SlTri r = sl_tri(L, t);
+    const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
     const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
     if (!(fabs(det) >= 1e-14)) continue;
     const double w1 = ((x2 - qx) * (y3 - qy) - (x3 - qx) * (y2 - qy)) / det;
     const double w2 = ((x3 - qx) * (y1 - qy) - (x1 - qx) * (y3 - qy)) / det;
     const double w3 = 1.0 - w1 - w2;
     if (w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0) {
-      const double dx = r[6] - qx, dy = r[7] - qy;
+      // centroid as StokesColor.py:321 / the centroid grid: (x1 + x2 + x3) / 3 in fp64
+      const double dx = (x1 + x2 + x3) / 3.0 - qx, dy = (y1 + y2 + y3) / 3.0 - qy;
       const double d = dx * dx + dy * dy;
       if (knn_less(d, t, bestd, best)) {
         bestd = d;
         best = t;
+        brho2 = r.rho2;
       }
       if (w1 >= SL_MARGIN && w2 >= SL_MARGIN && w3 >= SL_MARGIN) break;
     }
   }
   if (best == 0x7fffffff) return -1;
+  if (4.0 * bestd * (1.0 + 1e-9) < (double)brho2) return best;
   const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
   const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
   const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
@@ -584,9 +603,9 @@ __global__ __launch_bounds__(BS) void k_sl(MeshDev M, LocDev L, GridDev G, int64
       cn = c[g];
       nnf += 1.0;
     } else {
-      const int32_t a = M.tri[3 * found], b = M.tri[3 * found + 1], k = M.tri[3 * found + 2];
-      const double* r = L.rec + 8 * (int64_t)found;
-      const double x1 = r[0], y1 = r[1], x2 = r[2], y2 = r[3], x3 = r[4], y3 = r[5];
+      const SlTri r = sl_tri(L, found);
+      const int32_t a = r.a, b = r.b, k = r.d;
+      const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
       const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
       const double w1 = (pdx(x2, xb) * (y3 - yb) - pdx(x3, xb) * (y2 - yb)) / det;
       const double w2 = (pdx(x3, xb) * (y1 - yb) - pdx(x1, xb) * (y3 - yb)) / det;

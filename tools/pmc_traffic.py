@@ -32,7 +32,8 @@ def load(d, counter):
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
-                per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+                g = row.get("Grid_Size") or row.get("Grid_Size_X") or ""
+                per[(row["Kernel_Name"], g)].append(float(row["Counter_Value"]))
     return per
 
 
@@ -54,8 +55,9 @@ def main():
         world = int(sys.argv[sys.argv.index("--world") + 1])
     if fdir.endswith(".json"):  # re-derive from an earlier output's raw per-kernel averages
         old = json.load(open(fdir))["kernels"]
-        fetch = {k: [v["fetch_raw_avg"]] * v["dispatches_fetch"] for k, v in old.items() if v["fetch_raw_avg"] is not None}
-        write = {k: [v["write_raw_avg"]] * v["dispatches_write"] for k, v in old.items() if v["write_raw_avg"] is not None}
+        key = lambda k: tuple(k.split(" grid=")) if " grid=" in k else (k, "")
+        fetch = {key(k): [v["fetch_raw_avg"]] * v["dispatches_fetch"] for k, v in old.items() if v["fetch_raw_avg"] is not None}
+        write = {key(k): [v["write_raw_avg"]] * v["dispatches_write"] for k, v in old.items() if v["write_raw_avg"] is not None}
     else:
         fetch = load(fdir, "FETCH_SIZE")
         write = load(wdir, "WRITE_SIZE")
@@ -75,7 +77,7 @@ def main():
     res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
     fr, fw = 2.0 * 1024.0, 1.0 * 1024.0
     check = None
-    cal = [k for k in kern if short(k).endswith("k_visc_prep")]
+    cal = [k for k in kern if short(k[0]).endswith("k_visc_prep")]
     if cal and nrows and fetch.get(cal[0]) and write.get(cal[0]):
         f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
         w_avg = sum(write[cal[0]]) / len(write[cal[0]])
@@ -93,11 +95,16 @@ def main():
             e["read_bytes"] = e["fetch_raw_avg"] * fr
             e["write_bytes"] = e["write_raw_avg"] * fw
             e["hbm_bytes_per_launch"] = e["read_bytes"] + e["write_bytes"]
-        res["kernels"][short(k)] = e
-    # the bench's roofline kernels: finest-level instances (fp64 right-hand side) of k_cheb, k_cg_dir
+        res["kernels"][short(k[0]) + (f" grid={k[1]}" if k[1] else "")] = e
+    # the bench's roofline kernels, finest level only: k_cheb writing the fp64 z (last post-smoothing
+    # step) plus the k_cheb instances on the largest grid (the finest level's other steps; coarser
+    # levels run the same template on smaller grids), and the pressure CG's k_cg_dir<1>
     summary = {}
-    for key, pat in (("k_cheb", r"^k_cheb<\w+,double,"), ("k_cg_dir", r"^k_cg_dir<1,")):
-        ks = [k for k in res["kernels"] if re.match(pat, k) and "hbm_bytes_per_launch" in res["kernels"][k]]
+    cheb = [k for k in res["kernels"] if k.startswith("k_cheb<") and "hbm_bytes_per_launch" in res["kernels"][k]]
+    gmax = max((int(k.split(" grid=")[1]) for k in cheb if " grid=" in k), default=None)
+    fine = [k for k in cheb if re.match(r"^k_cheb<\w+,\w+,double,", k) or (gmax and k.endswith(f" grid={gmax}"))]
+    for key, ks in (("k_cheb", fine),
+                    ("k_cg_dir", [k for k in res["kernels"] if k.startswith("k_cg_dir<1,") and "hbm_bytes_per_launch" in res["kernels"][k]])):
         if ks:
             n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
