@@ -64,7 +64,8 @@ struct DevSell {
   int32_t* col = nullptr;
   int16_t* c16 = nullptr;  // int16 column deltas (square operators whose band fits), else null
   int64_t nslices = 0, nrows = 0, nnz = 0, padded = 0;
-  SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16}; }
+  int32_t wrap = 0;        // c16 modulus (local vector length)
+  SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16, wrap}; }
   double idx_bytes() const { return c16 ? 2.0 : 4.0; }  // per stored entry
 };
 // f(std::true_type) when A carries int16 columns, f(std::false_type) otherwise: one launch site
@@ -302,10 +303,14 @@ struct Ctx {
     if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
     return p;
   }
-  // int16 column deltas for a square operator's SELL (prm.idx32 = 0 and the band fits)
-  void attach_c16(const Sell& S, DevSell& D) {
+  // int16 column deltas for a square operator's SELL (prm.idx32 = 0 and the band fits); nloc: the
+  // local vector length (owned + ghost), the wrap modulus
+  void attach_c16(const Sell& S, i64 nloc, DevSell& D) {
     std::vector<int16_t> c16;
-    if (!prm.idx32 && sell_col16(S, c16)) D.c16 = upload(c16);
+    if (!prm.idx32 && sell_col16(S, nloc, c16)) {
+      D.c16 = upload(c16);
+      D.wrap = (int32_t)nloc;
+    }
   }
   void need_dev() const {
     if (host_only) throw Error(PUCFEM_ENODEV, "compute call on a host-only context");
@@ -1082,8 +1087,8 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
       const Sell& S = L.sA;
       sell_values_x(A, r0, S, A.val, tmp);
       L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
-                     A.rowptr[r0 + n] - A.rowptr[r0], S.padded};
-      c.attach_c16(S, L.dA);
+                     A.rowptr[r0 + n] - A.rowptr[r0], S.padded, 0};
+      c.attach_c16(S, L.nloc, L.dA);
       B.Aval = upload_as<T>(c, tmp);
       if constexpr (std::is_same<T, float>::value) B.Aval16 = upload_f16(c, tmp, false);
       L.nsend = (i64)L.lp.send_local.size();
@@ -1239,7 +1244,7 @@ void build(Ctx& c) {
     D.off = c.upload(S.slice_off);
     D.w = c.upload(S.slice_w);
     D.col = c.upload(S.col);
-    c.attach_c16(S, D);
+    c.attach_c16(S, c.nloc, D);
     D.nslices = S.nslices;
     D.nrows = S.nrows;
     D.padded = S.padded;

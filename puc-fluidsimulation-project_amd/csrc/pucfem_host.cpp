@@ -446,13 +446,15 @@ void build_sell(const Csr& A, const LocalPlan& lp, Sell& S) {
     }
 }
 
-bool sell_col16(const Sell& S, std::vector<int16_t>& out) {
+bool sell_col16(const Sell& S, i64 nloc, std::vector<int16_t>& out) {
   std::vector<int16_t> o(S.padded, 0);
   for (i64 s = 0; s < S.nslices; ++s)
     for (i64 l = 0; l < 64; ++l) {
       if (s * 64 + l >= S.nrows) continue;
       for (i64 k = 0; k < S.slice_w[s]; ++k) {
-        const i64 e = S.slice_off[s] + k * 64 + l, d = (i64)S.col[e] - s * 64;
+        const i64 e = S.slice_off[s] + k * 64 + l;
+        i64 d = (i64)S.col[e] - s * 64;
+        if (d > INT16_MAX) d -= nloc;  // decoded as base + d + nloc (base + d < 0)
         if (d < INT16_MIN || d > INT16_MAX) return false;
         o[e] = (int16_t)d;
       }

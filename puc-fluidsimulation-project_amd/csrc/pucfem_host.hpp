@@ -129,9 +129,11 @@ struct Sell {
 void build_sell(const Csr& A, const LocalPlan& lp, Sell& S);
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
                  std::vector<double>& out);
-// int16 image of a square operator's SELL columns: col - (first row of the slice); rows past nrows
-// point at the slice's first row.  false (out untouched) when some column is out of int16 range.
-bool sell_col16(const Sell& S, std::vector<int16_t>& out);
+// int16 image of a square operator's SELL columns: col - (first row of the slice), taken modulo
+// nloc (the local vector length) into [-32768, 32767], so ghost columns appended after the owned
+// rows are reached from the first rows by wrapping below 0; rows past nrows point at the slice's
+// first row.  false (out untouched) when some column is out of range.
+bool sell_col16(const Sell& S, i64 nloc, std::vector<int16_t>& out);
 // rows [r0, r0 + n) of A, columns resolved in `cols` (another level's plan)
 // pad_self: padding entries point at their own row (square operators: keeps the band, see
 // sell_col16); otherwise at column 0

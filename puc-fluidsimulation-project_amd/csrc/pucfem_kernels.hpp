@@ -27,6 +27,7 @@ struct SellDev {
   const int32_t* col;  // padded entries
   int64_t nslices, nrows;
   const int16_t* c16;  // same entries as int16 deltas from the slice's first row (band fits), or null
+  int32_t wrap;        // c16: a decoded index below 0 wraps by this (the local length; ghosts at the end)
 };
 
 template <class T>
@@ -38,7 +39,10 @@ __device__ __forceinline__ T ldnt(const T* p) {
 // strips of its row); NT: streamed with non-temporal loads (the gathered vector keeps L2 / MALL).
 template <bool C16, bool NT = true>
 __device__ __forceinline__ int32_t sell_col(const SellDev& A, int64_t e, int32_t base) {
-  if constexpr (C16) return base + (int32_t)(NT ? ldnt(A.c16 + e) : A.c16[e]);
+  if constexpr (C16) {
+    const int32_t j = base + (int32_t)(NT ? ldnt(A.c16 + e) : A.c16[e]);
+    return j + ((j >> 31) & A.wrap);
+  }
   else return NT ? ldnt(A.col + e) : A.col[e];
 }
 

@@ -61,6 +61,8 @@ def test_color_partitioned_matches_single_rank(world, precond, single, rep):
     out = run_ranks(mesh, world, "color", tol, 3, bc, 0.05)
     assert sum(o["info"]["n_own"] for o in out) == mesh.N
     assert all(o["info"]["n_ghost"] > 0 for o in out)
+    # int16 column deltas stay on with ghost columns (they wrap modulo the local vector length)
+    assert all(o["info"]["index16_P"] and o["info"]["index16_Pp"] for o in out)
     u = sum(o["u"] for o in out)  # every rank fills its owned rows
     ref = pf.StokesSimulation(mesh, bc, 0.05, "color", tol=tol)
     st = ref.step(3)
