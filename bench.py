@@ -32,8 +32,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    # defaults: the reference's StokesColor run is 5000 steps; 20 warm-up steps leave the impulsive
+    # start (whose steps are reported separately as "startup") so the timed steps are typical ones
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
     ap.add_argument("--rtol-pres", type=float, default=1e-8)
     ap.add_argument("--mg-double", action="store_true", help="fp64 V-cycle instead of the fp32 one")
@@ -44,6 +46,8 @@ def parse():
     ap.add_argument("--mg-post", type=int, default=2, help="Chebyshev post-smoothing degree")
     ap.add_argument("--mg-ratio", type=float, default=10.0, help="Chebyshev interval [lmax / ratio, lmax]")
     ap.add_argument("--mg-kind", type=int, default=1, choices=[1, 4], help="Chebyshev smoother of the first / fourth kind")
+    ap.add_argument("--proj-k", type=int, default=16,
+                    help="pressure initial guess: A-projection onto the last K solutions (0: warm start only)")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,14 +100,18 @@ def main():
     tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond, mg_single=not a.mg_double,
                         mg_f16_vals={"f16": True, "f32": False, "coarse-f16": "coarse"}[a.mg_vals],
                         index16=not a.index32, mg_degree=a.mg_pre, mg_post=a.mg_post, mg_ratio=a.mg_ratio,
-                        mg_kind=a.mg_kind)
+                        mg_kind=a.mg_kind, proj_k=a.proj_k)
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup
     log = (lambda *m: print(*m, file=sys.stderr, flush=True)) if rank == 0 else (lambda *m: None)
     log(f"[bench] setup {t_setup:.1f}s: {info}")
+    startup = []  # wall time of warm-up steps 1..3 (the impulsive start's transient; step 0 has u* = u^n)
     for k in range(a.warmup):
-        st = sim.step(1)[0]
+        t = time.perf_counter()
+        st = sim.step(1)[0]  # returns the step's stats: synchronous
+        if 1 <= k <= 3:
+            startup.append((time.perf_counter() - t, st.it_p + st.it_p2))
         log(f"[bench] warmup step {k}: CG visc/p/p2 = {st.it_visc}/{st.it_p}/{st.it_p2}")
     sim.ctx.timing(True)
     barrier()
@@ -152,6 +160,7 @@ def main():
             "dt": 0.05, "nu": 0.1, "B1": -2.0, "B2": 0.0,
             "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "pressure_precond": sim.ctx.precond,
             "mg_cheb": {"kind": a.mg_kind, "pre": a.mg_pre, "post": a.mg_post, "ratio": a.mg_ratio},
+            "pressure_guess": f"projection onto the last {a.proj_k} solutions" if a.proj_k else "previous solution",
             "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
         },
         "cg_iters_per_s": cg_iters / elapsed,
@@ -160,6 +169,9 @@ def main():
         "diagnostics": {"max_div_star": stats[-1].max_div_star, "max_final_div": stats[-1].max_final_div,
                         "mix_var": stats[-1].mix_var},
         "setup_s": t_setup,
+        "startup": {"steps": "warm-up steps 1-3 after the impulsive start (single rank timing)",
+                    "ms_per_step": [1e3 * s for s, _ in startup], "pressure_cg_iters": [i for _, i in startup]}
+        if startup else None,
     }
     # roofline of the dominant kernel: the finest-level Chebyshev smoother step (k_cheb) when the
     # pressure is multigrid-preconditioned, else the CG SpMV+direction kernel (k_cg_dir).  Algorithmic

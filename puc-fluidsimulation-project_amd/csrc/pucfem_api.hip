@@ -114,6 +114,15 @@ struct Timer {
     }
     pend.clear();
   }
+  // drop the pending samples from index k on (launches that found the solve converged and returned
+  // without work: counting them would credit their bytes to a near-zero duration)
+  void drop_from(size_t k) {
+    for (size_t i = k; i < pend.size(); ++i) {
+      pool.push_back(pend[i].a);
+      pool.push_back(pend[i].b);
+    }
+    if (k < pend.size()) pend.resize(k);
+  }
   ~Timer() {
     for (auto e : pool) (void)hipEventDestroy(e);
     for (auto& p : pend) {
@@ -172,6 +181,8 @@ struct MgLevel {
 template <typename T> MgBufs<T>& bufs(MgLevel& L);
 template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
+
+void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y);
 
 struct Ctx {
   std::string err;
@@ -273,6 +284,12 @@ struct Ctx {
   double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
   bool mg_single = false;                        // fp32 V-cycle
   double* z = nullptr;              // preconditioned residual (finest)
+  // successive right-hand sides: per pressure solve (which = 1: p, 2: p2) an A-orthonormal basis of
+  // up to proj_k solution directions, the projected guess x0 and the new direction
+  int proj_k = 0;
+  double* projX[3] = {nullptr, nullptr, nullptr};
+  int proj_m[3] = {0, 0, 0};
+  double *proj_x0 = nullptr, *proj_v = nullptr, *proj_av = nullptr, *proj_part = nullptr, *proj_c = nullptr;
   float* r32 = nullptr;             // fp32 copy of the CG residual: the fp32 V-cycle's right-hand side
 
   ~Ctx() {
@@ -668,9 +685,12 @@ struct Ctx {
     const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)dPp.nrows;  // + the fp32 r copy
     int it = 0;
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
+    std::vector<std::pair<int, size_t>> marks;  // (iteration, first timing sample of it) in this chunk
     for (;;) {
+      marks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
+        marks.push_back({it, timer.pend.size()});
         tstart(e0);
         with_c16(dPp, [&](auto c16) {
           hipLaunchKernelGGL((k_cg_dir<1, 8, true, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(),
@@ -695,7 +715,15 @@ struct Ctx {
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      if (timer.on) timer.flush();
+      if (timer.on) {
+        if (h_ctl[0])  // iterations from the converged one on launched kernels that did no work
+          for (auto& mk : marks)
+            if (mk.first >= h_ctl[1]) {
+              timer.drop_from(mk.second);
+              break;
+            }
+        timer.flush();
+      }
       if (h_ctl[0]) break;
       chunk = std::max(2, std::min(16, it / 4));
     }
@@ -754,6 +782,8 @@ struct Ctx {
                        sb.p, sb.nb, 1.0 / (double)n_free, bh);
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
+    const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
+    if (proj) project_guess(which, yst);
     int it;
     if (dense) {
       hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
@@ -762,6 +792,7 @@ struct Ctx {
       it = 0;
     } else if (use_mg) {
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
+      if (proj) project_update(which, yst);
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
@@ -772,6 +803,50 @@ struct Ctx {
     KCHK();
     halo(pout);
     return it;
+  }
+  // x0 = sum_i <X_i, b> X_i for the new right-hand side bh (A-orthonormal X: the A-projection of
+  // the solution onto span X); x0 = 0 with an empty basis, so that the first direction is the
+  // whole first solution.  Keeps x0 for the update.
+  void project_guess(int which, double* y) {
+    const i64 n = lp.n_own;
+    const int m = proj_m[which];
+    if (m == 0) {
+      HIPCHK(hipMemsetAsync(y, 0, sizeof(double) * nloc, st));
+    } else {
+      const int nb = nb_rows(n);
+      hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, bh, (const double*)nullptr,
+                         dmaster_of, proj_part);
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
+      KCHK();
+      if (world > 1) comm->allreduce(proj_c, m, false, st);
+      hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c,
+                         (const double*)nullptr, dmaster_of, 0.0, y);
+      KCHK();
+    }
+    HIPCHK(hipMemcpyAsync(proj_x0, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+  }
+  // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X.  A full
+  // basis restarts from the current solution alone (Fischer's restart: dropping old directions
+  // instead would drop the bulk of the solution, which lives in the first one).
+  void project_update(int which, const double* y) {
+    const i64 n = lp.n_own;
+    const bool restart = proj_m[which] == proj_k;
+    const int m = restart ? 0 : proj_m[which], slot = m;
+    if (restart) HIPCHK(hipMemcpyAsync(proj_v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0, proj_v);
+    KCHK();
+    halo(proj_v);
+    spmv_on(st, dPp, dKp_raw, proj_v, proj_av);
+    const int nb = nb_rows(n);
+    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, proj_av, proj_v, dmaster_of,
+                       proj_part);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m + 2, 0, proj_c);
+    KCHK();
+    if (world > 1) comm->allreduce(proj_c, m + 2, false, st);
+    hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c, proj_v,
+                       dmaster_of, 1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
+    KCHK();
+    proj_m[which] = m + 1;
   }
   void grad_proj(const double* pp, int mode) {
     const int nb = nb_for(dP.nslices);
@@ -1295,6 +1370,15 @@ void build(Ctx& c) {
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
     c.dKp_raw = c.upload(tmp);
     c.z = c.dalloc<double>(c.nloc);
+    c.proj_k = std::max(0, std::min(c.prm.proj_k, (int)PROJ_MAX));
+    if (c.proj_k > 0) {
+      for (int w = 1; w <= 2; ++w) c.projX[w] = c.dalloc<double>((i64)c.proj_k * c.nloc);
+      c.proj_x0 = c.dalloc<double>(c.nloc);
+      c.proj_v = c.dalloc<double>(c.nloc);
+      c.proj_av = c.dalloc<double>(c.nloc);
+      c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
+      c.proj_c = c.dalloc<double>(64);
+    }
     c.r32 = c.dalloc<float>(c.nloc);
     c.mg_single = c.prm.mg_single != 0;
     if (c.mg_single) mg_alloc<float>(c, tmp);

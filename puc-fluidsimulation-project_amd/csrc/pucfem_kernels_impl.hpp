@@ -249,6 +249,79 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
   }
 }
 
+// ----------------------------------------------------------------------------- solution projection
+// Successive right-hand sides (Fischer 1998): the pressure solves of consecutive steps keep an
+// A-orthonormal basis X of their recent solution directions; the initial guess is the A-orthogonal
+// projection of the new solution onto span X, x0 = sum_i <X_i, b> X_i.  X: m vectors at stride ld.
+constexpr int PROJ_MAX = 16;
+
+// partial dots <X_i, v> (i < m) and, with w, <v, w> (slot m) and the sum of w over the free
+// (non-slave) rows (slot m + 1); stride MAXB per value
+__global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict__ X, int64_t ld, int m,
+                                             const double* __restrict__ v, const double* __restrict__ w,
+                                             const int32_t* __restrict__ master_of, double* part) {
+  __shared__ double sh[4];
+  double acc[PROJ_MAX + 1], wsum = 0.0;
+#pragma unroll
+  for (int i = 0; i <= PROJ_MAX; ++i) acc[i] = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += BS) {
+    const double vr = v[r];
+#pragma unroll
+    for (int i = 0; i < PROJ_MAX; ++i)
+      if (i < m) acc[i] += X[i * ld + r] * vr;
+    if (w) {
+      acc[PROJ_MAX] += vr * w[r];
+      if (master_of[r] < 0) wsum += w[r];
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    double a = 0.0;
+#pragma unroll
+    for (int q = 0; q < PROJ_MAX; ++q)
+      if (q == i) a = acc[q];
+    const double t = block_sum(a, sh);
+    if (threadIdx.x == 0) part[(int64_t)i * MAXB + blockIdx.x] = t;
+  }
+  if (w) {
+    const double t = block_sum(acc[PROJ_MAX], sh);
+    const double u = block_sum(wsum, sh);
+    if (threadIdx.x == 0) {
+      part[(int64_t)m * MAXB + blockIdx.x] = t;
+      part[(int64_t)(m + 1) * MAXB + blockIdx.x] = u;
+    }
+  }
+}
+
+__global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) out[r] = a[r] - b[r];
+}
+
+// v == null: out = sum_i c_i X_i (the projected initial guess).
+// v != null: out = s (v - mu 1_free - sum_i c_i X_i), s = 1 / sqrt(c_m - sum_i c_i^2) -- with
+// c_i = <X_i, A v>, c_m = <v, A v> and mu = c_(m+1) / n_free (the mean of v over the free rows) this
+// is v A-orthogonalised against X, cleared of the operator's null space (constants on the free
+// rows: the V-cycle lets the CG iterate drift along it) and A-normalised; s = 0 (a null direction)
+// when v lies in span X to 1e-10 relative.  out may alias one of the X_i (element-wise update).
+__global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const double* __restrict__ c,
+                        const double* __restrict__ v, const int32_t* __restrict__ master_of, double inv_nfree,
+                        double* out) {
+  double s = 1.0, mu = 0.0;
+  if (v) {
+    mu = c[m + 1] * inv_nfree;
+    double q = 0.0;
+    for (int i = 0; i < m; ++i) q += c[i] * c[i];
+    const double den = c[m] - q;
+    s = den > 1e-10 * c[m] && den > 0.0 ? 1.0 / sqrt(den) : 0.0;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    double a = 0.0;
+    for (int i = 0; i < m; ++i) a += c[i] * X[i * ld + r];
+    out[r] = v ? s * (v[r] - (master_of[r] < 0 ? mu : 0.0) - a) : a;
+  }
+}
+
 // x = S y; slaves (master_of >= 0) take their master's value (p_s = p_m).
 __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const double* y0, const double* y1,
                          double* x0, double* x1, const int32_t* __restrict__ master_of) {

@@ -263,6 +263,21 @@ def test_mg_pressure_solve_matches_oracle(golden, single):
     sim.close()
 
 
+def test_projected_pressure_guess_same_steps():
+    """Successive-RHS projection (Fischer) only changes the pressure CG's initial guess: 24 steps with
+    a 3-vector basis (several restarts) equal the warm-started run to the CG tolerance, and once the
+    flow is steady the projected guesses need fewer iterations."""
+    mesh = pf.load_mesh("fine", refine=2)
+    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", proj_k=3))
+    b = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", proj_k=0))
+    sa, sb = a.step(24), b.step(24)
+    assert np.abs(a.u - b.u).max() < 1e-8
+    assert np.abs(a.c - b.c).max() < 1e-8
+    assert sum(x.it_p + x.it_p2 for x in sa[12:]) < sum(x.it_p + x.it_p2 for x in sb[12:])
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("single", [False, True])
 def test_mg_and_jacobi_steps_agree(single):
     """The two pressure preconditioners give the same Stokes steps (tolerance-limited)."""
