@@ -81,6 +81,7 @@ typedef struct pucfem_params {
   int32_t proj_k;      /* pressure solves (multigrid path): initial guess = A-orthogonal projection onto the
                           last proj_k solution directions of the same solve (Fischer 1998; <= 16, 0 = off,
                           warm start from the previous solution) */
+  int32_t proj_k_visc; /* the same for the two components of the viscous solve (0 = off: warm start u^n) */
   int32_t mg_kind;     /* smoother polynomial: 0/1 = Chebyshev (first kind) on [lmax / mg_ratio, lmax],
                           4 = Chebyshev of the fourth kind on [0, lmax] (Lottes 2022; no mg_ratio) */
 } pucfem_params;

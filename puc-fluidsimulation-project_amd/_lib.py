@@ -37,7 +37,7 @@ class Params(ct.Structure):
         ("center_x", ct.c_double), ("center_y", ct.c_double), ("precond", ct.c_int32),
         ("mg_degree", ct.c_int32), ("mg_ratio", ct.c_double), ("mg_post", ct.c_int32),
         ("mg_single", ct.c_int32), ("mg_rep_nodes", ct.c_int64), ("mg_f32_vals", ct.c_int32),
-        ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("mg_kind", ct.c_int32),
+        ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("proj_k_visc", ct.c_int32), ("mg_kind", ct.c_int32),
     ]
 
 

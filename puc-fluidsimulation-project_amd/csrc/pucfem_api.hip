@@ -286,10 +286,23 @@ struct Ctx {
   double* z = nullptr;              // preconditioned residual (finest)
   // successive right-hand sides: per pressure solve (which = 1: p, 2: p2) an A-orthonormal basis of
   // up to proj_k solution directions, the projected guess x0 and the new direction
-  int proj_k = 0;
-  double* projX[3] = {nullptr, nullptr, nullptr};
-  int proj_m[3] = {0, 0, 0};
-  double *proj_x0 = nullptr, *proj_v = nullptr, *proj_av = nullptr, *proj_part = nullptr, *proj_c = nullptr;
+  // (which = 3, 4: the viscous solve's x and y components, proj_k_visc directions each)
+  int proj_k = 0, proj_k_visc = 0;
+  double* projX[5] = {};
+  double* proj_x0[5] = {};
+  int proj_m[5] = {0, 0, 0, 0, 0};
+  double *proj_v = nullptr, *proj_av = nullptr, *proj_part = nullptr, *proj_c = nullptr;
+  // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
+  // space: constants on the free dofs, cleared from new directions) or the Jacobi-scaled A_visc
+  struct ProjOp {
+    const DevSell* A;
+    const double* val;
+    const int32_t* null_free;  // master_of (free rows: < 0) when the operator has the constants' null space
+    int kmax;
+  };
+  ProjOp proj_op(int which) const {
+    return which <= 2 ? ProjOp{&dPp, dKp_raw, dmaster_of, proj_k} : ProjOp{&dP, dKv, nullptr, proj_k_visc};
+  }
   float* r32 = nullptr;             // fp32 copy of the CG residual: the fp32 V-cycle's right-hand side
 
   ~Ctx() {
@@ -675,6 +688,9 @@ struct Ctx {
                          lp.n_ghost, part_a, part_b, r32o);
     });
     KCHK();
+    // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: keep r0
+    if (proj_k > 0 && (which == 1 || which == 2))
+      HIPCHK(hipMemcpyAsync(proj_av, cg_r[0], sizeof(double) * dPp.nrows, hipMemcpyDeviceToDevice, st));
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
     precondition();
@@ -754,7 +770,16 @@ struct Ctx {
     KCHK();
     double* y[2] = {yvx, yvy};
     const double* b[2] = {bvx, bvy};
+    const bool proj = proj_k_visc > 0;
+    if (proj) {  // the warm start u^n is replaced by the projection onto earlier solutions
+      project_guess(3, bvx, yvx);
+      project_guess(4, bvy, yvy);
+    }
     iters = cg<2>(dP, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    if (proj) {
+      project_update(3, yvx);
+      project_update(4, yvy);
+    }
     hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
                        (const int32_t*)nullptr);
     KCHK();
@@ -783,7 +808,7 @@ struct Ctx {
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
-    if (proj) project_guess(which, yst);
+    if (proj) project_guess(which, bh, yst);
     int it;
     if (dense) {
       hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
@@ -792,7 +817,7 @@ struct Ctx {
       it = 0;
     } else if (use_mg) {
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
-      if (proj) project_update(which, yst);
+      if (proj) project_update(which, yst, bh, cg_r[0]);
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
@@ -804,47 +829,58 @@ struct Ctx {
     halo(pout);
     return it;
   }
-  // x0 = sum_i <X_i, b> X_i for the new right-hand side bh (A-orthonormal X: the A-projection of
-  // the solution onto span X); x0 = 0 with an empty basis, so that the first direction is the
-  // whole first solution.  Keeps x0 for the update.
-  void project_guess(int which, double* y) {
+  // x0 = sum_i <X_i, b> X_i for the new right-hand side b (A-orthonormal X: the A-projection of
+  // the solution onto span X), kept for the update.  With an empty basis the solve keeps its warm
+  // start and x0 = 0, so that the first direction is the whole first solution.
+  void project_guess(int which, const double* b, double* y) {
     const i64 n = lp.n_own;
     const int m = proj_m[which];
     if (m == 0) {
-      HIPCHK(hipMemsetAsync(y, 0, sizeof(double) * nloc, st));
+      HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
+      return;
     } else {
       const int nb = nb_rows(n);
-      hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, bh, (const double*)nullptr,
-                         dmaster_of, proj_part);
+      hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, b, (const double*)nullptr,
+                         (const int32_t*)nullptr, proj_part);
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
       KCHK();
       if (world > 1) comm->allreduce(proj_c, m, false, st);
       hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c,
-                         (const double*)nullptr, dmaster_of, 0.0, y);
+                         (const double*)nullptr, (const int32_t*)nullptr, 0.0, y);
       KCHK();
     }
-    HIPCHK(hipMemcpyAsync(proj_x0, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(proj_x0[which], y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
   }
   // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X.  A full
   // basis restarts from the current solution alone (Fischer's restart: dropping old directions
   // instead would drop the bulk of the solution, which lives in the first one).
-  void project_update(int which, const double* y) {
+  // b, r_final (optional): the solve's right-hand side and final CG residual, with its initial
+  // residual r0 = b - A x0 saved in proj_av: then A v = r0 - r_final (A y = b - r_final on a
+  // restart) instead of an SpMV -- exact up to the CG recurrence's rounding drift.
+  void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr) {
     const i64 n = lp.n_own;
-    const bool restart = proj_m[which] == proj_k;
+    const ProjOp op = proj_op(which);
+    const bool restart = proj_m[which] == op.kmax;
     const int m = restart ? 0 : proj_m[which], slot = m;
     if (restart) HIPCHK(hipMemcpyAsync(proj_v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
-    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0, proj_v);
+    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], proj_v);
     KCHK();
-    halo(proj_v);
-    spmv_on(st, dPp, dKp_raw, proj_v, proj_av);
+    if (r_final) {  // x0 = 0 (first direction, restart): the CG started elsewhere, A y = b - r_final
+      const bool whole = restart || proj_m[which] == 0;
+      hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, whole ? b : proj_av, r_final, proj_av);
+      KCHK();
+    } else {
+      halo(proj_v);
+      spmv_on(st, *op.A, op.val, proj_v, proj_av);
+    }
     const int nb = nb_rows(n);
-    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, proj_av, proj_v, dmaster_of,
+    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, proj_av, proj_v, op.null_free,
                        proj_part);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m + 2, 0, proj_c);
     KCHK();
     if (world > 1) comm->allreduce(proj_c, m + 2, false, st);
     hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c, proj_v,
-                       dmaster_of, 1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
+                       op.null_free, 1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
     KCHK();
     proj_m[which] = m + 1;
   }
@@ -1370,15 +1406,7 @@ void build(Ctx& c) {
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
     c.dKp_raw = c.upload(tmp);
     c.z = c.dalloc<double>(c.nloc);
-    c.proj_k = std::max(0, std::min(c.prm.proj_k, (int)PROJ_MAX));
-    if (c.proj_k > 0) {
-      for (int w = 1; w <= 2; ++w) c.projX[w] = c.dalloc<double>((i64)c.proj_k * c.nloc);
-      c.proj_x0 = c.dalloc<double>(c.nloc);
-      c.proj_v = c.dalloc<double>(c.nloc);
-      c.proj_av = c.dalloc<double>(c.nloc);
-      c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
-      c.proj_c = c.dalloc<double>(64);
-    }
+
     c.r32 = c.dalloc<float>(c.nloc);
     c.mg_single = c.prm.mg_single != 0;
     if (c.mg_single) mg_alloc<float>(c, tmp);
@@ -1409,6 +1437,24 @@ void build(Ctx& c) {
     }
   }
   c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1;
+  // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
+  // small meshes need no better start)
+  c.proj_k = c.use_mg && !c.dense ? std::max(0, std::min(c.prm.proj_k, (int)PROJ_MAX)) : 0;
+  const bool block_visc = c.world == 1 && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
+  c.proj_k_visc = stokes && !c.dense && !block_visc ? std::max(0, std::min(c.prm.proj_k_visc, (int)PROJ_MAX)) : 0;
+  for (int w = 1; w <= 4; ++w) {
+    const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
+    if (k > 0) {
+      c.projX[w] = c.dalloc<double>((i64)k * c.nloc);
+      c.proj_x0[w] = c.dalloc<double>(c.nloc);
+    }
+  }
+  if (c.proj_k > 0 || c.proj_k_visc > 0) {
+    c.proj_v = c.dalloc<double>(c.nloc);
+    c.proj_av = c.dalloc<double>(c.nloc);
+    c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
+    c.proj_c = c.dalloc<double>(64);
+  }
   if (c.dense) {
     // A_visc^-1 and the pseudo-inverse of the merged pressure operator (constants on the free dofs
     // regularised, as for the multigrid coarse level)

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict
       if (i < m) acc[i] += X[i * ld + r] * vr;
     if (w) {
       acc[PROJ_MAX] += vr * w[r];
-      if (master_of[r] < 0) wsum += w[r];
+      if (master_of && master_of[r] < 0) wsum += w[r];
     }
   }
   for (int i = 0; i < m; ++i) {
@@ -302,7 +302,8 @@ __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __
 // v != null: out = s (v - mu 1_free - sum_i c_i X_i), s = 1 / sqrt(c_m - sum_i c_i^2) -- with
 // c_i = <X_i, A v>, c_m = <v, A v> and mu = c_(m+1) / n_free (the mean of v over the free rows) this
 // is v A-orthogonalised against X, cleared of the operator's null space (constants on the free
-// rows: the V-cycle lets the CG iterate drift along it) and A-normalised; s = 0 (a null direction)
+// rows: the V-cycle lets the CG iterate drift along it; master_of null: no null space) and
+// A-normalised; s = 0 (a null direction)
 // when v lies in span X to 1e-10 relative.  out may alias one of the X_i (element-wise update).
 __global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const double* __restrict__ c,
                         const double* __restrict__ v, const int32_t* __restrict__ master_of, double inv_nfree,
@@ -318,7 +319,7 @@ __global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const dou
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
     double a = 0.0;
     for (int i = 0; i < m; ++i) a += c[i] * X[i * ld + r];
-    out[r] = v ? s * (v[r] - (master_of[r] < 0 ? mu : 0.0) - a) : a;
+    out[r] = v ? s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - a) : a;
   }
 }
 

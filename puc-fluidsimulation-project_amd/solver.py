@@ -66,6 +66,7 @@ class Tolerances:
     index16: bool = True  # int16 column deltas where the operator band fits
     mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
     proj_k: int = 16  # pressure initial guess: A-projection onto up to proj_k solution directions (0: warm start)
+    proj_k_visc: int = 0  # the same for the viscous solve's two components (measured: no net gain at L7)
 
 
 class Context:
@@ -136,7 +137,8 @@ class Context:
                         precond=int(mg), mg_degree=tol.mg_degree, mg_ratio=tol.mg_ratio, mg_post=tol.mg_post,
                         mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes,
                         mg_f32_vals=2 if tol.mg_f16_vals == "coarse" else int(not tol.mg_f16_vals),
-                        idx32=int(not tol.index16), proj_k=tol.proj_k, mg_kind=tol.mg_kind)
+                        idx32=int(not tol.index16), proj_k=tol.proj_k, proj_k_visc=tol.proj_k_visc,
+                        mg_kind=tol.mg_kind)
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
