@@ -291,7 +291,14 @@ struct Ctx {
   double* projX[5] = {};
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
-  double *proj_v = nullptr, *proj_av = nullptr, *proj_part = nullptr, *proj_c = nullptr;
+  double *proj_part = nullptr, *proj_c = nullptr;
+  // single rank: the basis update's multi-dot and combination (m + 2 vector passes) run on a side
+  // stream, overlapping the rest of the step (the next pressure solve, the semi-Lagrangian
+  // kernel); per-solve v / A v buffers and side scratch; the next guess of the same solve waits
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_prep[5] = {}, ev_done[5] = {};
+  bool pending[5] = {false, false, false, false, false};
+  double *pv[5] = {}, *pav[5] = {}, *side_part = nullptr, *side_c = nullptr;
   // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
   // space: constants on the free dofs, cleared from new directions) or the Jacobi-scaled A_visc
   struct ProjOp {
@@ -308,6 +315,14 @@ struct Ctx {
   ~Ctx() {
     if (!host_only) {
       if (st) (void)hipStreamSynchronize(st);
+      if (st2) {
+        (void)hipStreamSynchronize(st2);
+        (void)hipStreamDestroy(st2);
+      }
+      for (int w = 0; w < 5; ++w) {
+        if (ev_prep[w]) (void)hipEventDestroy(ev_prep[w]);
+        if (ev_done[w]) (void)hipEventDestroy(ev_done[w]);
+      }
       if (gexec) (void)hipGraphExecDestroy(gexec);
       if (graph) (void)hipGraphDestroy(graph);
       for (void* a : allocs) (void)hipFree(a);
@@ -690,7 +705,7 @@ struct Ctx {
     KCHK();
     // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: keep r0
     if (proj_k > 0 && (which == 1 || which == 2))
-      HIPCHK(hipMemcpyAsync(proj_av, cg_r[0], sizeof(double) * dPp.nrows, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(pav[which], cg_r[0], sizeof(double) * dPp.nrows, hipMemcpyDeviceToDevice, st));
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
     precondition();
@@ -835,6 +850,10 @@ struct Ctx {
   void project_guess(int which, const double* b, double* y) {
     const i64 n = lp.n_own;
     const int m = proj_m[which];
+    if (pending[which]) {  // the side stream's update of this basis
+      HIPCHK(hipStreamWaitEvent(st, ev_done[which], 0));
+      pending[which] = false;
+    }
     if (m == 0) {
       HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
       return;
@@ -855,34 +874,56 @@ struct Ctx {
   // basis restarts from the current solution alone (Fischer's restart: dropping old directions
   // instead would drop the bulk of the solution, which lives in the first one).
   // b, r_final (optional): the solve's right-hand side and final CG residual, with its initial
-  // residual r0 = b - A x0 saved in proj_av: then A v = r0 - r_final (A y = b - r_final on a
+  // residual r0 = b - A x0 saved in pav[which]: then A v = r0 - r_final (A y = b - r_final on a
   // restart) instead of an SpMV -- exact up to the CG recurrence's rounding drift.
   void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     const bool restart = proj_m[which] == op.kmax;
     const int m = restart ? 0 : proj_m[which], slot = m;
-    if (restart) HIPCHK(hipMemcpyAsync(proj_v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
-    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], proj_v);
+    double *v = pv[which], *av = pav[which];
+    if (restart) HIPCHK(hipMemcpyAsync(v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
     KCHK();
     if (r_final) {  // x0 = 0 (first direction, restart): the CG started elsewhere, A y = b - r_final
       const bool whole = restart || proj_m[which] == 0;
-      hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, whole ? b : proj_av, r_final, proj_av);
+      hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, whole ? b : av, r_final, av);
       KCHK();
     } else {
-      halo(proj_v);
-      spmv_on(st, *op.A, op.val, proj_v, proj_av);
+      halo(v);
+      spmv_on(st, *op.A, op.val, v, av);
+    }
+    // multi-dot + combination: on the side stream when there is one (single rank)
+    hipStream_t s = st;
+    double *part = proj_part, *cc = proj_c;
+    if (st2) {
+      HIPCHK(hipEventRecord(ev_prep[which], st));
+      HIPCHK(hipStreamWaitEvent(st2, ev_prep[which], 0));
+      s = st2;
+      part = side_part;
+      cc = side_c;
     }
     const int nb = nb_rows(n);
-    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, proj_av, proj_v, op.null_free,
-                       proj_part);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m + 2, 0, proj_c);
+    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, s, n, projX[which], nloc, m, av, v, op.null_free, part);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, s, part, nb, MAXB, m + 2, 0, cc);
     KCHK();
-    if (world > 1) comm->allreduce(proj_c, m + 2, false, st);
-    hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c, proj_v,
-                       op.null_free, 1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
+    if (world > 1) comm->allreduce(cc, m + 2, false, s);
+    hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, s, n, projX[which], nloc, m, cc, v, op.null_free,
+                       1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
     KCHK();
+    if (st2) {
+      HIPCHK(hipEventRecord(ev_done[which], st2));
+      pending[which] = true;
+    }
     proj_m[which] = m + 1;
+  }
+  // the side stream's work is part of the step: every synchronisation point waits for it
+  void join_side() {
+    for (int w = 0; w < 5; ++w)
+      if (pending[w]) {
+        HIPCHK(hipStreamWaitEvent(st, ev_done[w], 0));
+        pending[w] = false;
+      }
   }
   void grad_proj(const double* pp, int mode) {
     const int nb = nb_for(dP.nslices);
@@ -1450,10 +1491,22 @@ void build(Ctx& c) {
     }
   }
   if (c.proj_k > 0 || c.proj_k_visc > 0) {
-    c.proj_v = c.dalloc<double>(c.nloc);
-    c.proj_av = c.dalloc<double>(c.nloc);
+    for (int w = 1; w <= 4; ++w)
+      if (c.projX[w]) {
+        c.pv[w] = c.dalloc<double>(c.nloc);
+        c.pav[w] = c.dalloc<double>(c.nloc);
+      }
     c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
     c.proj_c = c.dalloc<double>(64);
+    if (c.world == 1) {  // RCCL stays on one stream: multi-rank runs update on the main stream
+      HIPCHK(hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking));
+      for (int w = 1; w <= 4; ++w) {
+        HIPCHK(hipEventCreateWithFlags(&c.ev_prep[w], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c.ev_done[w], hipEventDisableTiming));
+      }
+      c.side_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
+      c.side_c = c.dalloc<double>(64);
+    }
   }
   if (c.dense) {
     // A_visc^-1 and the pseudo-inverse of the merged pressure operator (constants on the free dofs
@@ -2004,6 +2057,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       }
       std::vector<double> h(8 * (size_t)nsteps);
       std::vector<int> hd(3 * (size_t)nsteps);
+      c.join_side();  // a step call returns with all of its work done
       HIPCHK(hipMemcpyAsync(h.data(), rec, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipMemcpyAsync(hd.data(), dits, sizeof(int) * hd.size(), hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
@@ -2375,7 +2429,10 @@ int pucfem_timing_get(void* ctx, int32_t k, double* ms, int64_t* n, double* byte
 int pucfem_sync(void* ctx) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
-    if (!c.host_only) HIPCHK(hipStreamSynchronize(c.st));
+    if (!c.host_only) {
+      c.join_side();
+      HIPCHK(hipStreamSynchronize(c.st));
+    }
   });
 }
 
