@@ -708,17 +708,23 @@ struct Ctx {
       HIPCHK(hipMemcpyAsync(pav[which], cg_r[0], sizeof(double) * dPp.nrows, hipMemcpyDeviceToDevice, st));
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
+    const double tol2 = tol * tol;
+    // (iteration, first timing sample): samples from the converged iteration on are dropped
+    std::vector<std::pair<int, size_t>> marks;
+    hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0);
+    KCHK();
+    marks.push_back({0, timer.pend.size()});
     precondition();
     Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
     halo(z);
-    const double tol2 = tol * tol;
     const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
     const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)dPp.nrows;  // + the fp32 r copy
     int it = 0;
-    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
-    std::vector<std::pair<int, size_t>> marks;  // (iteration, first timing sample of it) in this chunk
-    for (;;) {
-      marks.clear();
+    // host convergence checks: the first after as many iterations as the last solve took (the
+    // early test in k_conv stops the work right there when the count repeats), then short chunks
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
+    for (bool first = true;; first = false) {
+      if (!first) marks.clear();  // the previous chunk's samples are flushed
       for (int k = 0; k < chunk; ++k, ++it) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         marks.push_back({it, timer.pend.size()});
@@ -739,6 +745,9 @@ struct Ctx {
         KCHK();
         tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, 1, false, 0);
+        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1);
+        KCHK();
+        marks.push_back({it + 1, timer.pend.size()});
         precondition();
         rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
         halo(z);
@@ -756,7 +765,7 @@ struct Ctx {
         timer.flush();
       }
       if (h_ctl[0]) break;
-      chunk = std::max(2, std::min(16, it / 4));
+      chunk = std::max(1, std::min(16, it / 4));
     }
     last_it[which] = h_ctl[1];
     if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "MG-PCG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");

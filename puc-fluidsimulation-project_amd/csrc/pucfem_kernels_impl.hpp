@@ -323,6 +323,16 @@ __global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const dou
   }
 }
 
+// Preconditioned CG: convergence test right after the residual update, before the preconditioner:
+// ctl = (1, it) when <r, r> <= tol2 <b, b>, so the V-cycle's kernels and the next direction kernel
+// return at once (k_cg_dir would find the same at iteration it; a NaN is left to it)
+__global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl, int it) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[0] == 0 && rr[0] <= tol2 * bb[0]) {
+    ctl[0] = 1;
+    ctl[1] = it;
+  }
+}
+
 // x = S y; slaves (master_of >= 0) take their master's value (p_s = p_m).
 __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const double* y0, const double* y1,
                          double* x0, double* x1, const int32_t* __restrict__ master_of) {

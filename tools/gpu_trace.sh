@@ -12,4 +12,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace -d /tmp/tr_$TAG -o run --output-forma
   python "$ROOT/bench.py" --no-cpu-baseline --no-secondary "$@" > "$OUT/bench.out" 2> "$OUT/bench.err"
 rc=$?; echo "rocprof rc=$rc" >&2; [ $rc -ne 0 ] && { tail -5 "$OUT/bench.err" >&2; exit $rc; }
 f=$(find /tmp/tr_$TAG -name "*kernel_trace.csv" | head -1)
-python "$ROOT/tools/trace_step.py" "$f" > "$OUT/trace_summary.txt" && cat "$OUT/trace_summary.txt" >&2
+python "$ROOT/tools/trace_step.py" "$f" ${LAST_MS:+--last-ms $LAST_MS} > "$OUT/trace_summary.txt" && cat "$OUT/trace_summary.txt" >&2

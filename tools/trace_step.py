@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-step timeline analysis of a rocprofv3 --kernel-trace CSV (bench.py run).
 
-Usage: trace_step.py KERNEL_TRACE_CSV [--last-ms 80]
-Takes the last `--window` of kernel activity (the timed steps of the bench), and prints the busy
-time per kernel name, the sum of gaps between consecutive kernels, and the wall span.
+Usage: trace_step.py KERNEL_TRACE_CSV [--last-ms T]
+Takes the kernel activity after the last gap > 50 ms (the bench's steps), or only its last T ms
+(--last-ms: the timed steps after the warm-up), and prints the busy time per kernel name, the sum
+of gaps between consecutive kernels, and the wall span.
 """
 import csv
 import sys
@@ -24,6 +25,10 @@ def main():
         if rows[i][0] - rows[i - 1][1] > 50_000_000:
             start = i
     rows = rows[start:]
+    if "--last-ms" in sys.argv:
+        tend = max(r[1] for r in rows)
+        cut = tend - float(sys.argv[sys.argv.index("--last-ms") + 1]) * 1e6
+        rows = [r for r in rows if r[0] >= cut]
     t0, t1 = rows[0][0], max(r[1] for r in rows)
     busy = defaultdict(float)
     cnt = defaultdict(int)
