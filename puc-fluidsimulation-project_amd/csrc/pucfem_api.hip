@@ -183,6 +183,16 @@ template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
 void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y);
+// k_mdot with the smallest accumulator count >= m
+void mdot_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* v, const double* w,
+             const int32_t* master_of, double* part) {
+  if (m <= 8)
+    hipLaunchKernelGGL(k_mdot<8>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
+  else if (m <= 16)
+    hipLaunchKernelGGL(k_mdot<16>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
+  else
+    hipLaunchKernelGGL(k_mdot<PROJ_MAX>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
+}
 
 struct Ctx {
   std::string err;
@@ -868,8 +878,7 @@ struct Ctx {
       return;
     } else {
       const int nb = nb_rows(n);
-      hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, st, n, projX[which], nloc, m, b, (const double*)nullptr,
-                         (const int32_t*)nullptr, proj_part);
+      mdot_on(st, nb, n, projX[which], nloc, m, b, nullptr, nullptr, proj_part);
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
       KCHK();
       if (world > 1) comm->allreduce(proj_c, m, false, st);
@@ -880,8 +889,8 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(proj_x0[which], y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
   }
   // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X.  A full
-  // basis restarts from the current solution alone (Fischer's restart: dropping old directions
-  // instead would drop the bulk of the solution, which lives in the first one).
+  // basis restarts (Fischer): a sliding window would drop the first direction, which carries the
+  // bulk of the solution.
   // b, r_final (optional): the solve's right-hand side and final CG residual, with its initial
   // residual r0 = b - A x0 saved in pav[which]: then A v = r0 - r_final (A y = b - r_final on a
   // restart) instead of an SpMV -- exact up to the CG recurrence's rounding drift.
@@ -889,6 +898,8 @@ struct Ctx {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     const bool restart = proj_m[which] == op.kmax;
+    // (measured: keeping the newest quarter of the directions across a restart does not lower the
+    // iteration counts after it)
     const int m = restart ? 0 : proj_m[which], slot = m;
     double *v = pv[which], *av = pav[which];
     if (restart) HIPCHK(hipMemcpyAsync(v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
@@ -913,7 +924,7 @@ struct Ctx {
       cc = side_c;
     }
     const int nb = nb_rows(n);
-    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BS), 0, s, n, projX[which], nloc, m, av, v, op.null_free, part);
+    mdot_on(s, nb, n, projX[which], nloc, m, av, v, op.null_free, part);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, s, part, nb, MAXB, m + 2, 0, cc);
     KCHK();
     if (world > 1) comm->allreduce(cc, m + 2, false, s);

@@ -253,39 +253,41 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
 // Successive right-hand sides (Fischer 1998): the pressure solves of consecutive steps keep an
 // A-orthonormal basis X of their recent solution directions; the initial guess is the A-orthogonal
 // projection of the new solution onto span X, x0 = sum_i <X_i, b> X_i.  X: m vectors at stride ld.
-constexpr int PROJ_MAX = 16;
+constexpr int PROJ_MAX = 32;
 
 // partial dots <X_i, v> (i < m) and, with w, <v, w> (slot m) and the sum of w over the free
 // (non-slave) rows (slot m + 1); stride MAXB per value
+// KM >= m: the accumulator count (register budget) of the instance
+template <int KM>
 __global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict__ X, int64_t ld, int m,
                                              const double* __restrict__ v, const double* __restrict__ w,
                                              const int32_t* __restrict__ master_of, double* part) {
   __shared__ double sh[4];
-  double acc[PROJ_MAX + 1], wsum = 0.0;
+  double acc[KM + 1], wsum = 0.0;
 #pragma unroll
-  for (int i = 0; i <= PROJ_MAX; ++i) acc[i] = 0.0;
+  for (int i = 0; i <= KM; ++i) acc[i] = 0.0;
   int64_t r0, r1;
   block_rows(n, r0, r1);
   for (int64_t r = r0 + threadIdx.x; r < r1; r += BS) {
     const double vr = v[r];
 #pragma unroll
-    for (int i = 0; i < PROJ_MAX; ++i)
+    for (int i = 0; i < KM; ++i)
       if (i < m) acc[i] += X[i * ld + r] * vr;
     if (w) {
-      acc[PROJ_MAX] += vr * w[r];
+      acc[KM] += vr * w[r];
       if (master_of && master_of[r] < 0) wsum += w[r];
     }
   }
   for (int i = 0; i < m; ++i) {
     double a = 0.0;
 #pragma unroll
-    for (int q = 0; q < PROJ_MAX; ++q)
+    for (int q = 0; q < KM; ++q)
       if (q == i) a = acc[q];
     const double t = block_sum(a, sh);
     if (threadIdx.x == 0) part[(int64_t)i * MAXB + blockIdx.x] = t;
   }
   if (w) {
-    const double t = block_sum(acc[PROJ_MAX], sh);
+    const double t = block_sum(acc[KM], sh);
     const double u = block_sum(wsum, sh);
     if (threadIdx.x == 0) {
       part[(int64_t)m * MAXB + blockIdx.x] = t;

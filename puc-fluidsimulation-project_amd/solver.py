@@ -65,7 +65,7 @@ class Tolerances:
     mg_f16_vals: bool | str = False
     index16: bool = True  # int16 column deltas where the operator band fits
     mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
-    proj_k: int = 16  # pressure initial guess: A-projection onto up to proj_k solution directions (0: warm start)
+    proj_k: int = 24  # pressure initial guess: A-projection onto up to proj_k solution directions (0: warm start)
     proj_k_visc: int = 0  # the same for the viscous solve's two components (measured: no net gain at L7)
 
 
