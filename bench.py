@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="time the steps without per-launch kernel events (no roofline block)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--fine-steps", type=int, default=200)
     return ap.parse_args()
@@ -114,7 +116,7 @@ def main():
         if 1 <= k <= 3:
             startup.append((time.perf_counter() - t, st.it_p + st.it_p2))
         log(f"[bench] warmup step {k}: CG visc/p/p2 = {st.it_visc}/{st.it_p}/{st.it_p2}")
-    sim.ctx.timing(True)
+    sim.ctx.timing(not a.no_kernel_timing)
     barrier()
     sim.ctx.sync()
     t0 = time.perf_counter()
@@ -134,6 +136,19 @@ def main():
             ktab[nm] = {"launches_timed": n, "avg_launch_ms": ms / n, "bytes_per_launch": b,
                         "achieved_GBps": b / (ms / n * 1e-3) / 1e9}
     sim.ctx.timing(False)
+    # the same kernels launched back to back outside the step (pucfem_bench_kernel): per-launch time
+    # of a batch between two events, and the average of per-launch dispatch events
+    batch = {}
+    if sim.ctx.precond == "mg" and not a.mg_double:
+        import ctypes as ct
+
+        for kid, nm in ((0, "k_cheb"), (1, "k_resid"), (2, "k_cg_dir"), (16 * 8, "k_cheb+8 coarse launches"),
+                        (256, "k_cheb, idle GPU at each launch")):
+            mb, me, by = ct.c_double(), ct.c_double(), ct.c_double()
+            L.check(L.lib().pucfem_bench_kernel(sim.ctx.h, kid, 20, ct.byref(mb), ct.byref(me), ct.byref(by)),
+                    sim.ctx.h)
+            batch[nm] = {"ms_batch": mb.value, "ms_each_event": me.value, "bytes": by.value,
+                         "GBps_batch": by.value / (mb.value * 1e-3) / 1e9}
     cg_iters = sum(2 * s.it_visc + s.it_p + s.it_p2 for s in stats)  # viscous CG is 2-RHS
     cg_iter_launches = sum(s.it_visc + s.it_p + s.it_p2 for s in stats)
     steps_per_s = a.steps / elapsed
@@ -197,6 +212,7 @@ def main():
                            "traffic": traffic, "bytes_per_launch": kd["bytes_per_launch"],
                            "avg_launch_ms": kd["avg_launch_ms"], "launches_timed": kd["launches_timed"]}
     rec["kernels"] = ktab
+    rec["kernel_batch"] = batch
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats)
     if rank == 0 and world == 1 and not a.no_secondary:

@@ -194,6 +194,13 @@ int pucfem_sync(void* ctx);
 /* micro-benchmark of the dominant kernel (k_cg_dir) variants on the pressure operator:
    variant 0 plain loop, 1 unrolled, 2 non-temporal, 3 unrolled + non-temporal; average ms/launch */
 int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters, double* ms_out);
+/* timing of one kernel on the context's finest-level data (bench.py's roofline cross-check):
+   kernel 0 = k_cheb general step (fp32 V-cycle), 1 = k_resid, 2 = k_cg_dir<1> of the pressure CG.
+   ms_batch: `iters` back-to-back launches between two events, per launch; ms_each: the average of
+   per-launch dispatch events (hipExtLaunchKernelGGL); bytes: algorithmic bytes per launch.
+   kernel + 16*F: F untimed launches of a coarse level's smoother follow every timed launch
+   (ms_batch then includes them; ms_each still times the kernel's own launches) */
+int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_batch, double* ms_each, double* bytes);
 /* sizes of the internal operators: out[0]=N, [1]=T, [2]=nnz(P), [3]=nnz(Pp), [4]=n_own,
    [5]=n_ghost, [6]=padded SELL entries (P), [7]=padded SELL entries (Pp), [8]=n_pairs, [9]=n_dirichlet,
    [10]=storage flags (bit 0: P has int16 columns, bit 1: Pp has int16 columns, bit 2: the finest

@@ -82,6 +82,7 @@ SIGNATURES = {
     "pucfem_timing_get": ([_P, ct.c_int32, _D, _I64, _D], ct.c_int),
     "pucfem_sync": ([_P], ct.c_int),
     "pucfem_bench_dir": ([_P, ct.c_int32, ct.c_int32, ct.c_int32, _D], ct.c_int),
+    "pucfem_bench_kernel": ([_P, ct.c_int32, ct.c_int32, _D, _D, _D], ct.c_int),
     "pucfem_info": ([_P, _I64], ct.c_int),
     "pucfem_refine": ([ct.c_int64, _D, _I32, ct.c_int64, _I32, ct.c_int32, _I64, _I64, _D, _I32, _I32], ct.c_int),
     "pucfem_host_get_csr": ([_P, ct.c_int32, _I64, _I64, _I64, _I64, _D], ct.c_int),

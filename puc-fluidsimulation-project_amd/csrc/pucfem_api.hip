@@ -2,10 +2,12 @@
 // all-reduce, and the Stokes / heat / Poisson step loops.  One HIP stream per context; every
 // kernel of a step is enqueued back to back and the host synchronises only to poll CG
 // convergence (once per chunk of iterations) and to return results.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -14,6 +16,7 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "pucfem.h"
@@ -183,15 +186,23 @@ template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
 void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y);
-// k_mdot with the smallest accumulator count >= m
+// k_mdot for basis size m (0..PROJ_MAX): one instance per size
+template <int M>
+void mdot_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* v, const double* w,
+                 const int32_t* master_of, double* part) {
+  hipLaunchKernelGGL(k_mdot<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, v, w, master_of, part);
+}
+using MdotFn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
+                        const int32_t*, double*);
+template <int... M>
+constexpr std::array<MdotFn, sizeof...(M)> mdot_table(std::integer_sequence<int, M...>) {
+  return {&mdot_launch<M>...};
+}
 void mdot_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* v, const double* w,
              const int32_t* master_of, double* part) {
-  if (m <= 8)
-    hipLaunchKernelGGL(k_mdot<8>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
-  else if (m <= 16)
-    hipLaunchKernelGGL(k_mdot<16>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
-  else
-    hipLaunchKernelGGL(k_mdot<PROJ_MAX>, dim3(nb), dim3(BS), 0, s, n, X, ld, m, v, w, master_of, part);
+  static constexpr auto tab = mdot_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
+  if (m < 0 || m > PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
+  tab[m](s, nb, n, X, ld, v, w, master_of, part);
 }
 
 struct Ctx {
@@ -237,6 +248,7 @@ struct Ctx {
   int32_t *dcdst = nullptr, *dcsrc = nullptr, *ddnode = nullptr;
   double *ddval = nullptr, *dbctmp = nullptr;
   int ncopy = 0, ndir = 0;
+  bool bc_gather = true;  // some copy source is also written: k_bc_gather saves the sources first
   int32_t* dsend = nullptr;
   double* dsendbuf = nullptr;
   i64 nsend = 0;
@@ -384,18 +396,18 @@ struct Ctx {
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
   // ------------------------------------------------------------------ timing helpers
-  void tstart(hipEvent_t& a) {
-    if (timer.on) {
-      a = timer.get();
-      HIPCHK(hipEventRecord(a, st));
-    }
-  }
-  void tstop(int cls, hipEvent_t a, double bytes) {
-    if (timer.on) {
-      hipEvent_t b = timer.get();
-      HIPCHK(hipEventRecord(b, st));
-      timer.pend.push_back({cls, a, b, bytes});
+  // Launch on the library stream.  When timing (cls >= 0), the start / stop events are taken by the
+  // kernel's dispatch itself (hipExtLaunchKernelGGL): the sample is the kernel's own duration, as
+  // rocprofv3 reports it, without the command-processor gap a separately recorded event adds.
+  template <typename... KArgs, typename... Args>
+  void klaunch(int cls, double bytes, void (*kernel)(KArgs...), dim3 g, dim3 b, Args... args) {
+    if (timer.on && cls >= 0) {
+      hipEvent_t a = timer.get(), e = timer.get();
+      hipExtLaunchKernelGGL(kernel, g, b, 0, st, a, e, 0, args...);
+      timer.pend.push_back({cls, a, e, bytes});
       if (timer.pend.size() > 4096) timer.flush();  // bounded number of live events
+    } else {
+      hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
     }
   }
 
@@ -506,27 +518,26 @@ struct Ctx {
     const double bytes_dir = (8.0 + A.idx_bytes()) * (double)A.nnz + 32.0 * NR * (double)A.nrows;
     const double bytes_upd = 48.0 * NR * (double)A.nrows;
     int it = 0;
-    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 2 ? last_it[which] - 1 : 4));
+    // host convergence checks: the first after as many iterations as the last solve took (k_conv
+    // after each update lets the check see convergence without a further direction launch)
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
     for (;;) {
       for (int k = 0; k < chunk; ++k, ++it) {
-        hipEvent_t e0 = nullptr, e1 = nullptr;
         // HIP-event timing samples every 8th iteration (bounded event count for long solves)
         const bool samp = (it & 7) == 0;
-        if (samp) tstart(e0);
         with_c16(A, [&](auto c16) {
-          hipLaunchKernelGGL((k_cg_dir<NR, 8, true, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), val, v,
-                             lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
-                             part_c);
+          klaunch(samp ? 1 : -1, bytes_dir, k_cg_dir<NR, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(),
+                  val, v, lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
+                  part_c, (const double*)nullptr, 0, 0);
         });
         KCHK();
-        if (samp) tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, NR, false, 2);
-        if (samp) tstart(e1);
-        hipLaunchKernelGGL((k_cg_upd<NR>), dim3(nb), dim3(BS), 0, st, v, A.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
-                           part_a);
+        klaunch(samp ? 2 : -1, bytes_upd, k_cg_upd<NR>, dim3(nb), dim3(BS), v, A.nrows, pq.p, pq.nb, pq.stride,
+                (const double*)scal, (const int*)ctl, part_a, (float*)nullptr);
         KCHK();
-        if (samp) tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, NR, false, 0);
+        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, NR);
+        KCHK();
         if (NR == 2) halo(cg_r[0], cg_r[1]);
         else halo(cg_r[0]);
         for (int c = 0; c < NR; ++c) std::swap(v.po[c], v.pn[c]);
@@ -535,7 +546,7 @@ struct Ctx {
       HIPCHK(hipStreamSynchronize(st));
       if (timer.on) timer.flush();
       if (h_ctl[0]) break;
-      chunk = std::max(4, std::min(64, it / 8));
+      chunk = std::max(1, std::min(64, it / 8));
     }
     last_it[which] = h_ctl[1];
     if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "CG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");
@@ -584,32 +595,31 @@ struct Ctx {
       if (mode == 1) mg_halo(L, cur);
       const bool last = k == deg - 1;
       const bool timed = finest && mode != 0;
-      hipEvent_t e0 = nullptr;
-      if (timed) tstart(e0);
       const double* rd = last ? rdot : nullptr;
       const bool toz = last && zout;
       const int nb = rd ? nb_for(A.nslices) : nb_mg(A.nslices);
       const T* xi = mode == 1 ? cur : nullptr;
+      // algorithmic bytes: matrix (value + column) per entry; per row x_in (mode 1) or b and dinv
+      // (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r
+      const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
+      const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
+      const double bytes = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row);
       B.with_vals([&](auto* val) {
         using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
         with_c16(A, [&](auto c16) {
           constexpr bool C = decltype(c16)::value;
           if (toz)
-            hipLaunchKernelGGL((k_cheb<T, TB, double, VT, C>), dim3(nb), dim3(BS), 0, st, A.view(), val, B.dinv, b, xi,
-                               zout, B.d, c1, c2, c20, mode, ctl, rd, part);
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, double, VT, C, 1>, dim3(nb), dim3(BS), A.view(), val,
+                    (const T*)B.dinv, b, xi, zout, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+          else if (finest)
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), val,
+                    (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
           else
-            hipLaunchKernelGGL((k_cheb<T, TB, T, VT, C>), dim3(nb), dim3(BS), 0, st, A.view(), val, B.dinv, b, xi, out,
-                               B.d, c1, c2, c20, mode, ctl, rd, part);
+            klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), val, (const T*)B.dinv, b, xi,
+                    out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
         });
       });
       KCHK();
-      // algorithmic bytes: matrix (value + int32 column) per entry; per row x_in (mode 1) or b and
-      // dinv (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r
-      if (timed) {
-        const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
-        const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
-        tstop(0, e0, (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row));
-      }
       cur = toz ? nullptr : out;
     }
     return cur;
@@ -642,30 +652,32 @@ struct Ctx {
     }
     T* x = mg_smooth<T, TB>(L, A, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, prm.mg_degree);
     mg_halo(L, x);
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    if (finest) tstart(e0);
+    // residual: matrix entries, x gathered once, b read, res written
+    const double bytes_res =
+        (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB));
     B.with_vals([&](auto* val) {
       using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
       with_c16(A, [&](auto c16) {
-        hipLaunchKernelGGL((k_resid<T, TB, VT, decltype(c16)::value>), dim3(nb_mg(A.nslices)), dim3(BS), 0, st,
-                           A.view(), val, b, x, B.res, ctl);
+        if (finest)
+          klaunch(5, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 1>, dim3(nb_mg(A.nslices)), dim3(BS),
+                  A.view(), val, b, (const T*)x, B.res, (const int*)ctl);
+        else
+          klaunch(-1, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 0>, dim3(nb_mg(A.nslices)), dim3(BS),
+                  A.view(), val, b, (const T*)x, B.res, (const int*)ctl);
       });
     });
     KCHK();
-    // matrix entries, x gathered once, b read, res written
-    if (finest)
-      tstop(5, e0, (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB)));
     mg_halo(L, B.res);
     MgLevel& C = mg[l - 1];
     MgBufs<T>& CB = bufs<T>(C);
-    if (finest) tstart(e1);
     const bool gather = C.rep && !L.rep && world > 1;  // into the finest replicated level
     T* cb = gather ? CB.b + L.r_r0 : CB.b;
-    hipLaunchKernelGGL(k_transfer<T>, dim3(nb_mg(L.dR.nslices)), dim3(BS), 0, st, L.dR.view(), B.Rval, B.res, cb, 0,
-                       ctl);
-    KCHK();
     // restriction: entries (value + column), fine residual read once, coarse rhs written
-    if (finest) tstop(6, e1, (double)(sizeof(T) + 4) * (double)L.dR.nnz + (double)sizeof(T) * (double)(A.nrows + L.dR.nrows));
+    klaunch(finest ? 6 : -1,
+            (double)(sizeof(T) + 4) * (double)L.dR.nnz + (double)sizeof(T) * (double)(A.nrows + L.dR.nrows),
+            k_transfer<T>, dim3(nb_mg(L.dR.nslices)), dim3(BS), L.dR.view(), (const T*)B.Rval, (const T*)B.res, cb, 0,
+            (const int*)ctl);
+    KCHK();
     if (gather) {
       comm->group_start();
       for (int r = 0; r < world; ++r) comm->bcast(CB.b + C.rs[r], C.rs[r + 1] - C.rs[r], r, st);
@@ -673,12 +685,12 @@ struct Ctx {
     }
     T* xc = vcycle<T, T>(l - 1, CB.b, nullptr, nullptr);
     mg_halo(C, xc);
-    if (finest) tstart(e2);
-    hipLaunchKernelGGL(k_transfer<T>, dim3(nb_mg(L.dPr.nslices)), dim3(BS), 0, st, L.dPr.view(), B.Prval, xc, x, 1,
-                       ctl);
-    KCHK();
     // prolongation: entries, coarse x read once, fine x read + written
-    if (finest) tstop(7, e2, (double)(sizeof(T) + 4) * (double)L.dPr.nnz + (double)sizeof(T) * (double)(2 * A.nrows + L.dR.nrows));
+    klaunch(finest ? 7 : -1,
+            (double)(sizeof(T) + 4) * (double)L.dPr.nnz + (double)sizeof(T) * (double)(2 * A.nrows + L.dR.nrows),
+            k_transfer<T>, dim3(nb_mg(L.dPr.nslices)), dim3(BS), L.dPr.view(), (const T*)B.Prval, (const T*)xc, x, 1,
+            (const int*)ctl);
+    KCHK();
     T* other = (x == xa) ? xb : xa;
     return mg_smooth<T, TB>(L, A, B, b, x, x, other, finest ? z : nullptr, rdot, part,
                             prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
@@ -721,46 +733,38 @@ struct Ctx {
     const double tol2 = tol * tol;
     // (iteration, first timing sample): samples from the converged iteration on are dropped
     std::vector<std::pair<int, size_t>> marks;
-    hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0);
+    hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
     KCHK();
-    marks.push_back({0, timer.pend.size()});
-    precondition();
-    Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-    halo(z);
     const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
     const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)dPp.nrows;  // + the fp32 r copy
     int it = 0;
-    // host convergence checks: the first after as many iterations as the last solve took (the
-    // early test in k_conv stops the work right there when the count repeats), then short chunks
-    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
+    // an iteration = V-cycle, direction, update, convergence test (k_conv): the host checks right
+    // after a test, so a solve that converges at a check launches no V-cycle after it.  The first
+    // check comes one iteration before the last solve's count (a no-op iteration costs more than a
+    // check's round trip), then every iteration while the solve is short.
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 1 ? last_it[which] - 1 : (last_it[which] ? 1 : 4)));
     for (bool first = true;; first = false) {
       if (!first) marks.clear();  // the previous chunk's samples are flushed
       for (int k = 0; k < chunk; ++k, ++it) {
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        marks.push_back({it, timer.pend.size()});
-        tstart(e0);
+        marks.push_back({it, timer.pend.size()});  // this iteration's V-cycle works iff not converged at it
+        precondition();
+        Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
+        halo(z);
         with_c16(dPp, [&](auto c16) {
-          hipLaunchKernelGGL((k_cg_dir<1, 8, true, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(),
-                             dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it,
-                             maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+          klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(),
+                  (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it,
+                  maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
         });
         KCHK();
-        tstop(1, e0, bytes_dir);
         Red pq = reduce_global(part_c, nb, 1, false, 2);
-        tstart(e1);
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
-        hipLaunchKernelGGL((k_cg_upd<1>), dim3(nb), dim3(BS), 0, st, vu, dPp.nrows, pq.p, pq.nb, pq.stride, scal, ctl,
-                           part_a, r32o);
+        klaunch(2, bytes_upd, k_cg_upd<1>, dim3(nb), dim3(BS), vu, dPp.nrows, pq.p, pq.nb, pq.stride,
+                (const double*)scal, (const int*)ctl, part_a, r32o);
         KCHK();
-        tstop(2, e1, bytes_upd);
         rr = reduce_global(part_a, nb, 1, false, 0);
-        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1);
+        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, 1);
         KCHK();
-        marks.push_back({it + 1, timer.pend.size()});
-        precondition();
-        rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-        halo(z);
         std::swap(v.po[0], v.pn[0]);
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -775,7 +779,7 @@ struct Ctx {
         timer.flush();
       }
       if (h_ctl[0]) break;
-      chunk = std::max(1, std::min(16, it / 4));
+      chunk = it < 8 ? 1 : std::min(16, it / 4);
     }
     last_it[which] = h_ctl[1];
     if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "MG-PCG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");
@@ -786,8 +790,14 @@ struct Ctx {
   // ------------------------------------------------------------------ building blocks of the step
   void bc(double* a, double* b) {  // makePerBCU + makeDirBCU on owned rows
     if (ncopy == 0 && ndir == 0) return;
-    hipLaunchKernelGGL(k_bc, dim3(1), dim3(1024), 0, st, ncopy, dcdst, dcsrc, dbctmp, ndir, ddnode, ddval,
-                       dir_ncomp, a, b);
+    const int nb = (int)std::min<i64>(1024, std::max<i64>(1, (ncopy + ndir + BS - 1) / BS));
+    if (bc_gather && ncopy > 0) {
+      hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcsrc,
+                         dbctmp, dir_ncomp, a, b);
+      KCHK();
+    }
+    hipLaunchKernelGGL(k_bc_apply, dim3(nb), dim3(BS), 0, st, ncopy, dcdst, dcsrc,
+                       bc_gather ? (const double*)dbctmp : nullptr, ndir, ddnode, ddval, dir_ncomp, a, b);
     KCHK();
   }
   int viscous(int& iters) {  // StokesColor.py:540-547
@@ -823,14 +833,12 @@ struct Ctx {
   }
   void div(const double* ax, const double* ay, double* out, bool rhs) {
     const int nb = nb_for(dP.nslices);
-    hipEvent_t e = nullptr;
-    tstart(e);
     with_c16(dP, [&](auto c16) {
-      hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, ax, ay, das1,
-                         out, dmp, -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
+      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own, k_div<decltype(c16)::value>,
+              dim3(nb), dim3(BS), dP.view(), (const double*)dGx, (const double*)dGy, ax, ay, (const double*)das1, out,
+              (const double*)dmp, -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
     });
     KCHK();
-    tstop(3, e, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own);
   }
   int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
     const int nb = nb_for(dP.nslices);
@@ -877,7 +885,7 @@ struct Ctx {
       HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
       return;
     } else {
-      const int nb = nb_rows(n);
+      const int nb = grid_ew(n);
       mdot_on(st, nb, n, projX[which], nloc, m, b, nullptr, nullptr, proj_part);
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
       KCHK();
@@ -923,7 +931,7 @@ struct Ctx {
       part = side_part;
       cc = side_c;
     }
-    const int nb = nb_rows(n);
+    const int nb = grid_ew(n);
     mdot_on(s, nb, n, projX[which], nloc, m, av, v, op.null_free, part);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, s, part, nb, MAXB, m + 2, 0, cc);
     KCHK();
@@ -947,14 +955,13 @@ struct Ctx {
   }
   void grad_proj(const double* pp, int mode) {
     const int nb = nb_for(dP.nslices);
-    hipEvent_t e = nullptr;
-    tstart(e);
     with_c16(dP, [&](auto c16) {
-      hipLaunchKernelGGL(k_grad_proj<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, dP.view(), dGx, dGy, pp, das1,
-                         prm.dt, mode, ddir, usx, usy, ux, uy);
+      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own,
+              k_grad_proj<decltype(c16)::value>, dim3(nb), dim3(BS), dP.view(), (const double*)dGx,
+              (const double*)dGy, pp, (const double*)das1, prm.dt, mode, (const uint8_t*)ddir, (const double*)usx,
+              (const double*)usy, ux, uy);
     });
     KCHK();
-    tstop(3, e, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own);
   }
 
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
@@ -975,12 +982,10 @@ struct Ctx {
     reduce_into(part_d, nb_for(dP.nslices), 1, true, 1);  // max |final div|
     if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
-      hipEvent_t e = nullptr;
-      tstart(e);
-      hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, lgrid, cgrid, lp.r0, lp.n_own,
-                         ux, uy, prm.dt, c_full, c_new, dwmix, (int32_t*)nullptr, part_sl);
+      klaunch(4, 8.0 * 6 * (double)lp.n_own, k_sl, dim3(nb), dim3(BS), MeshDev{mx, my, mtri, mesh.T}, lgrid, cgrid,
+              lp.r0, lp.n_own, (const double*)ux, (const double*)uy, prm.dt, (const double*)c_full, c_new,
+              (const double*)dwmix, (int32_t*)nullptr, part_sl);
       KCHK();
-      tstop(4, e, 8.0 * 6 * (double)lp.n_own);
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
       } else {
@@ -1518,7 +1523,9 @@ void build(Ctx& c) {
       }
     c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
     c.proj_c = c.dalloc<double>(64);
-    if (c.world == 1) {  // RCCL stays on one stream: multi-rank runs update on the main stream
+    // RCCL stays on one stream: multi-rank runs update on the main stream (PUCFEM_NO_SIDE_STREAM:
+    // single-rank runs too, a measurement knob)
+    if (c.world == 1 && !std::getenv("PUCFEM_NO_SIDE_STREAM")) {
       HIPCHK(hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking));
       for (int w = 1; w <= 4; ++w) {
         HIPCHK(hipEventCreateWithFlags(&c.ev_prep[w], hipEventDisableTiming));
@@ -1605,6 +1612,23 @@ void build(Ctx& c) {
       if (g < lp.r0 || g >= lp.r1) continue;
       dn.push_back((i32)(g - lp.r0));
       for (int q = 0; q < c.dir_ncomp; ++q) dv.push_back(c.dir_vals[c.dir_ncomp * k + q]);
+    }
+    // a copy into a Dirichlet node is overwritten by its Dirichlet value: drop it, so the write sets
+    // are disjoint
+    {
+      std::vector<char> written(no, 0);
+      for (i32 d : dn) written[d] = 1;
+      std::vector<i32> cd2, cs2;
+      for (size_t k = 0; k < cd.size(); ++k)
+        if (!written[cd[k]]) {
+          cd2.push_back(cd[k]);
+          cs2.push_back(cs[k]);
+        }
+      cd.swap(cd2);
+      cs.swap(cs2);
+      for (i32 d : cd) written[d] = 1;
+      c.bc_gather = false;
+      for (i32 sidx : cs) c.bc_gather = c.bc_gather || written[sidx];
     }
     c.ncopy = (int)cd.size();
     c.ndir = (int)dn.size();
@@ -2666,6 +2690,116 @@ int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters,
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *ms_out = ms / iters;
+  });
+}
+
+int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_batch, double* ms_each, double* bytes) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.use_mg && c.mg_single && iters > 0, "bench_kernel needs a multigrid context with the fp32 V-cycle");
+    MgLevel& L = c.mg.back();
+    MgBufs<float>& B = L.f32;
+    const DevSell& A = c.dPp;
+    // kernel / 16 = untimed launches of a coarse level's smoother between the timed launches (how the
+    // per-launch events behave when other kernels run in between, as inside a step)
+    // kernel / 256 = 1: the host waits for every launch before it submits the next (the GPU is idle
+    // when each launch's packet arrives)
+    const bool idle = (kernel / 256) & 1;
+    kernel %= 256;
+    const int nfill = kernel / 16;
+    kernel %= 16;
+    const int nb_mg = c.nb_mg(A.nslices), nb = Ctx::nb_for(A.nslices);
+    CgVecs<1> v;
+    v.y[0] = c.yp;
+    v.b[0] = c.bh;
+    v.r[0] = c.z;
+    v.po[0] = c.cg_pa[0];
+    v.pn[0] = c.cg_pb[0];
+    v.q[0] = c.cg_q[0];
+    double by = 0.0;
+    // scalar state of k_cg_dir: beta = 1, never converged
+    const double sc[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+    double* one = c.redbuf + 8 * 60;
+    HIPCHK(hipMemcpyAsync(c.scal, sc, sizeof(sc), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(one, sc, sizeof(double), hipMemcpyHostToDevice, c.st));
+    int* ctl0 = reinterpret_cast<int*>(c.redbuf + 8 * 61);
+    HIPCHK(hipMemsetAsync(ctl0, 0, 4 * sizeof(int), c.st));
+    auto launch = [&](hipEvent_t a, hipEvent_t e) {
+      with_c16(A, [&](auto c16) {
+        constexpr bool C16 = decltype(c16)::value;
+        switch (kernel) {
+          case 0:
+            hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0,
+                                  A.view(), (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
+                                  (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
+                                  (const double*)nullptr, (double*)nullptr);
+            break;
+          case 1:
+            hipExtLaunchKernelGGL(k_resid<float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0, A.view(),
+                                  (const float*)B.Aval, (const float*)c.r32, (const float*)B.x, B.res,
+                                  (const int*)nullptr);
+            break;
+          default:
+            hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(nb), dim3(BS), 0, c.st, a, e, 0, A.view(),
+                                  (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
+                                  (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
+                                  (const double*)nullptr, 0, 0);
+        }
+      });
+      KCHK();
+    };
+    switch (kernel) {
+      case 0: by = (4.0 + A.idx_bytes()) * (double)A.nnz + 28.0 * (double)A.nrows; break;
+      case 1: by = (4.0 + A.idx_bytes()) * (double)A.nnz + 12.0 * (double)A.nrows; break;
+      default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + 32.0 * (double)A.nrows;
+    }
+    MgLevel& Lc = c.mg[c.mg.size() >= 3 ? c.mg.size() - 3 : 0];
+    auto fill = [&] {
+      for (int f = 0; f < nfill; ++f) {
+        with_c16(Lc.dA, [&](auto c16) {
+          constexpr bool C16 = decltype(c16)::value;
+          hipLaunchKernelGGL((k_cheb<float, float, float, float, C16, 0>), dim3(c.nb_mg(Lc.dA.nslices)), dim3(BS), 0,
+                             c.st, Lc.dA.view(), (const float*)Lc.f32.Aval, (const float*)Lc.f32.dinv,
+                             (const float*)Lc.f32.b, (const float*)nullptr, Lc.f32.x2, Lc.f32.d, 0.3, 0.7, 0.0, 2,
+                             (const int*)nullptr, (const double*)nullptr, (double*)nullptr);
+        });
+        KCHK();
+      }
+    };
+    launch(nullptr, nullptr);
+    hipEvent_t ea, eb;
+    HIPCHK(hipEventCreate(&ea));
+    HIPCHK(hipEventCreate(&eb));
+    HIPCHK(hipEventRecord(ea, c.st));
+    for (int k = 0; k < iters; ++k) {
+      launch(nullptr, nullptr);
+      fill();
+    }
+    HIPCHK(hipEventRecord(eb, c.st));
+    HIPCHK(hipEventSynchronize(eb));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ea, eb));
+    *ms_batch = ms / iters;
+    std::vector<hipEvent_t> ev(2 * (size_t)iters);
+    for (auto& x : ev) HIPCHK(hipEventCreate(&x));
+    for (int k = 0; k < iters; ++k) {
+      launch(ev[2 * k], ev[2 * k + 1]);
+      fill();
+      if (idle) HIPCHK(hipStreamSynchronize(c.st));
+    }
+    HIPCHK(hipEventSynchronize(ev.back()));
+    double tot = 0.0;
+    for (int k = 0; k < iters; ++k) {
+      HIPCHK(hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]));
+      tot += ms;
+    }
+    *ms_each = tot / iters;
+    for (auto& x : ev) (void)hipEventDestroy(x);
+    (void)hipEventDestroy(ea);
+    (void)hipEventDestroy(eb);
+    *bytes = by;
   });
 }
 

@@ -255,45 +255,53 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
 // projection of the new solution onto span X, x0 = sum_i <X_i, b> X_i.  X: m vectors at stride ld.
 constexpr int PROJ_MAX = 32;
 
-// partial dots <X_i, v> (i < m) and, with w, <v, w> (slot m) and the sum of w over the free
-// (non-slave) rows (slot m + 1); stride MAXB per value
-// KM >= m: the accumulator count (register budget) of the instance
-template <int KM>
-__global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict__ X, int64_t ld, int m,
+// partial dots <X_i, v> (i < M) and, with w, <v, w> (slot M) and the sum of w over the free
+// (non-slave) rows (slot M + 1); stride MAXB per value.  One instance per basis size M: the M loads
+// of a row are unconditional, so they are all in flight together (a runtime count puts each load
+// behind a branch and serialises them: 2 TB/s).
+template <int M>
+__global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict__ X, int64_t ld,
                                              const double* __restrict__ v, const double* __restrict__ w,
                                              const int32_t* __restrict__ master_of, double* part) {
-  __shared__ double sh[4];
-  double acc[KM + 1], wsum = 0.0;
+  constexpr int NA = M + 2;
+  __shared__ double sh[NA][4];
+  double acc[NA];
 #pragma unroll
-  for (int i = 0; i <= KM; ++i) acc[i] = 0.0;
-  int64_t r0, r1;
-  block_rows(n, r0, r1);
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += BS) {
-    const double vr = v[r];
-#pragma unroll
-    for (int i = 0; i < KM; ++i)
-      if (i < m) acc[i] += X[i * ld + r] * vr;
-    if (w) {
-      acc[KM] += vr * w[r];
-      if (master_of && master_of[r] < 0) wsum += w[r];
-    }
-  }
-  for (int i = 0; i < m; ++i) {
-    double a = 0.0;
-#pragma unroll
-    for (int q = 0; q < KM; ++q)
-      if (q == i) a = acc[q];
-    const double t = block_sum(a, sh);
-    if (threadIdx.x == 0) part[(int64_t)i * MAXB + blockIdx.x] = t;
-  }
+  for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+  // grid-stride rows: the resident waves read one compact window of every basis vector (contiguous
+  // per-block chunks spread them over the whole of each vector, TLB-bound)
+  const int64_t step = (int64_t)gridDim.x * BS;
   if (w) {
-    const double t = block_sum(acc[KM], sh);
-    const double u = block_sum(wsum, sh);
-    if (threadIdx.x == 0) {
-      part[(int64_t)m * MAXB + blockIdx.x] = t;
-      part[(int64_t)(m + 1) * MAXB + blockIdx.x] = u;
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+      const double vr = v[r], wr = w[r];
+      double x[M > 0 ? M : 1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+#pragma unroll
+      for (int i = 0; i < M; ++i) acc[i] += x[i] * vr;
+      acc[M] += vr * wr;
+      if (master_of && master_of[r] < 0) acc[M + 1] += wr;
+    }
+  } else {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+      const double vr = v[r];
+      double x[M > 0 ? M : 1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+#pragma unroll
+      for (int i = 0; i < M; ++i) acc[i] += x[i] * vr;
     }
   }
+  const int nv = w ? NA : M;
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+    if (i < nv) {
+      const double t = wave_sum(acc[i]);
+      if ((threadIdx.x & 63) == 0) sh[i][threadIdx.x >> 6] = t;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nv; i += BS)
+    part[(int64_t)i * MAXB + blockIdx.x] = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
 }
 
 __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
@@ -325,13 +333,18 @@ __global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const dou
   }
 }
 
-// Preconditioned CG: convergence test right after the residual update, before the preconditioner:
-// ctl = (1, it) when <r, r> <= tol2 <b, b>, so the V-cycle's kernels and the next direction kernel
-// return at once (k_cg_dir would find the same at iteration it; a NaN is left to it)
-__global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl, int it) {
-  if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[0] == 0 && rr[0] <= tol2 * bb[0]) {
-    ctl[0] = 1;
-    ctl[1] = it;
+// CG convergence test right after the residual update: ctl = (1, it) when <r_c, r_c> <= tol2 <b_c, b_c>
+// for every right-hand side c < nr, so the host's check after an iteration sees it (and a V-cycle
+// or direction kernel launched after it returns at once).  k_cg_dir would find the same at
+// iteration it; a NaN is left to it.
+__global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl, int it, int nr) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[0] == 0) {
+    bool conv = true;
+    for (int c = 0; c < nr; ++c) conv = conv && rr[c] <= tol2 * bb[c];
+    if (conv) {
+      ctl[0] = 1;
+      ctl[1] = it;
+    }
   }
 }
 
@@ -528,24 +541,34 @@ __global__ __launch_bounds__(BS) void k_grad(SellDev A, const double* __restrict
 
 // ----------------------------------------------------------------------------- boundary conditions
 // makePerBCU then makeDirBCU (StokesColor.py:405-431) / reapply_periodic_u + reapply_dirchlect_u
-// (heatEq.py:282-301).  One block: copies are two-phase (gather all sources, then write), which
-// realises the host-resolved sequential semantics; Dirichlet values are written after.
-__global__ __launch_bounds__(1024) void k_bc(int ncopy, const int32_t* __restrict__ cdst, const int32_t* __restrict__ csrc,
-                                             double* tmp, int ndir, const int32_t* __restrict__ dnode,
-                                             const double* __restrict__ dval, int ncomp, double* u0, double* u1) {
-  for (int k = threadIdx.x; k < ncopy; k += blockDim.x) {
+// (heatEq.py:282-301).
+// Boundary conditions on owned rows, multi-block: copies u[dst] = u_old[src] (makePerBCU, sources
+// resolved to pre-copy values on the host), then Dirichlet values (makeDirBCU).  The host drops the
+// copies whose destination is a Dirichlet node (the Dirichlet value wins), so the two write sets are
+// disjoint; when a source is also written, k_bc_gather first saves the sources in tmp (a separate
+// launch orders every read before any write), else tmp is null and k_bc_apply reads u directly.
+__global__ void k_bc_gather(int ncopy, const int32_t* __restrict__ csrc, double* __restrict__ tmp, int ncomp,
+                            const double* __restrict__ u0, const double* __restrict__ u1) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ncopy; k += gridDim.x * blockDim.x) {
     tmp[2 * k] = u0[csrc[k]];
     if (ncomp > 1) tmp[2 * k + 1] = u1[csrc[k]];
   }
-  __syncthreads();
-  for (int k = threadIdx.x; k < ncopy; k += blockDim.x) {
-    u0[cdst[k]] = tmp[2 * k];
-    if (ncomp > 1) u1[cdst[k]] = tmp[2 * k + 1];
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < ndir; k += blockDim.x) {
-    u0[dnode[k]] = dval[ncomp * k];
-    if (ncomp > 1) u1[dnode[k]] = dval[ncomp * k + 1];
+}
+__global__ void k_bc_apply(int ncopy, const int32_t* __restrict__ cdst, const int32_t* __restrict__ csrc,
+                           const double* tmp, int ndir, const int32_t* __restrict__ dnode,
+                           const double* __restrict__ dval, int ncomp, double* u0, double* u1) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ncopy + ndir; k += gridDim.x * blockDim.x) {
+    if (k < ncopy) {
+      const int d = cdst[k];
+      const double a = tmp ? tmp[2 * k] : u0[csrc[k]];
+      const double b = ncomp > 1 ? (tmp ? tmp[2 * k + 1] : u1[csrc[k]]) : 0.0;
+      u0[d] = a;
+      if (ncomp > 1) u1[d] = b;
+    } else {
+      const int j = k - ncopy, d = dnode[j];
+      u0[d] = dval[ncomp * j];
+      if (ncomp > 1) u1[d] = dval[ncomp * j + 1];
+    }
   }
 }
 
@@ -987,7 +1010,9 @@ __device__ __forceinline__ T sell_row_dot(const SellDev& A, const VT* __restrict
 // T: the V-cycle's storage/arithmetic type (float in the mixed-precision cycle, double otherwise);
 // TB: the right-hand side (the CG residual, double, on the finest level); TO: the output (double
 // for the final step that writes the preconditioned residual z).
-template <typename T, typename TB, typename TO, typename VT, bool C16>
+// LV: a level tag with no effect on the code (1: the finest level, 2: pucfem_bench_kernel), so that
+// profilers report the finest level's launches apart from the coarser levels' ones.
+template <typename T, typename TB, typename TO, typename VT, bool C16, int LV = 0>
 __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const VT* __restrict__ val, const T* __restrict__ dinv,
                                              const TB* __restrict__ b, const T* __restrict__ xin,
                                              TO* __restrict__ xout, T* __restrict__ d, double c1, double c2,
@@ -1029,7 +1054,7 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const VT* __restrict__ v
 }
 
 // res = b - A x
-template <typename T, typename TB, typename VT, bool C16>
+template <typename T, typename TB, typename VT, bool C16, int LV = 0>
 __global__ __launch_bounds__(BS) void k_resid(SellDev A, const VT* __restrict__ val, const TB* __restrict__ b,
                                               const T* __restrict__ x, T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;

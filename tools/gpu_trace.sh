@@ -13,3 +13,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace -d /tmp/tr_$TAG -o run --output-forma
 rc=$?; echo "rocprof rc=$rc" >&2; [ $rc -ne 0 ] && { tail -5 "$OUT/bench.err" >&2; exit $rc; }
 f=$(find /tmp/tr_$TAG -name "*kernel_trace.csv" | head -1)
 python "$ROOT/tools/trace_step.py" "$f" ${LAST_MS:+--last-ms $LAST_MS} > "$OUT/trace_summary.txt" && cat "$OUT/trace_summary.txt" >&2
+for p in "k_cheb<float, float, float, float, true, 1>" "k_cheb<float, float, double, float, true, 1>" \
+         "k_resid<float, float, float, true, 1>" "k_cg_dir<1" "k_reduce" "k_bc_apply" "k_cg_upd<1>"; do
+  python "$ROOT/tools/trace_launch.py" "$f" "$p" ${LAST_MS:+--last-ms $LAST_MS} >> "$OUT/trace_launch.txt"
+done
+cat "$OUT/trace_launch.txt" >&2
