@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <numeric>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -313,6 +314,19 @@ struct Ctx {
   double* projX[5] = {};
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
+  // full-basis re-seeding (proj_reseed): the guess's coefficients (h_alpha) and the update's
+  // reduction values (h_cc), pinned; per basis the coordinates of the last solutions.
+  // PUCFEM_PROJ_KEEP (measurement knob, default 8, 0: Fischer's restart) seeds kept
+  double *h_alpha = nullptr, *h_cc = nullptr;
+  double* projXalt[5] = {};
+  struct ProjHist {
+    std::vector<std::vector<double>> sols;
+    std::vector<double> alpha;
+    int m = 0;
+    bool pending = false;
+  } proj_hist[5];
+  int proj_keep = std::getenv("PUCFEM_PROJ_KEEP") ? std::max(0, std::min(PROJ_KEEP_MAX, std::atoi(std::getenv("PUCFEM_PROJ_KEEP"))))
+                                                   : 8;
   double *proj_part = nullptr, *proj_c = nullptr;
   // single rank: the basis update's multi-dot and combination (m + 2 vector passes) run on a side
   // stream, overlapping the rest of the step (the next pressure solve, the semi-Lagrangian
@@ -349,6 +363,8 @@ struct Ctx {
       if (graph) (void)hipGraphDestroy(graph);
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
+      if (h_alpha) (void)hipHostFree(h_alpha);
+      if (h_cc) (void)hipHostFree(h_cc);
       if (h_pinned) (void)hipHostFree(h_pinned);
       comm.reset();
       if (st) (void)hipStreamDestroy(st);
@@ -890,25 +906,96 @@ struct Ctx {
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
       KCHK();
       if (world > 1) comm->allreduce(proj_c, m, false, st);
+      HIPCHK(hipMemcpyAsync(h_alpha + which * PROJ_MAX, proj_c, sizeof(double) * m, hipMemcpyDeviceToHost, st));
       hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c,
                          (const double*)nullptr, (const int32_t*)nullptr, 0.0, y);
       KCHK();
     }
     HIPCHK(hipMemcpyAsync(proj_x0[which], y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
   }
-  // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X.  A full
-  // basis restarts (Fischer): a sliding window would drop the first direction, which carries the
-  // bulk of the solution.
+  // coordinates of the last solve's solution in the basis (lazily: its update's reduction values
+  // reach h_cc asynchronously; read here, after a host synchronisation that follows them):
+  // y = x0 + v = sum_i (a_i + c_i) X_i + sqrt(den) X_new (+ a null-space constant)
+  void proj_finish_coords(int which) {
+    ProjHist& H = proj_hist[which];
+    if (!H.pending) return;
+    const int m = H.m;
+    const double* cc = h_cc + which * (PROJ_MAX + 2);
+    std::vector<double> y(m + 1, 0.0);
+    double q = 0.0;
+    for (int i = 0; i < m; ++i) {
+      y[i] = H.alpha[i] + cc[i];
+      q += cc[i] * cc[i];
+    }
+    const double den = cc[m] - q;
+    y[m] = den > 1e-10 * cc[m] && den > 0.0 ? std::sqrt(den) : 0.0;  // as k_mcomb's null test
+    H.sols.push_back(std::move(y));
+    if ((int)H.sols.size() > PROJ_KEEP_MAX) H.sols.erase(H.sols.begin());
+    H.pending = false;
+  }
+  // Full basis: re-seed it with the span of the last keep - 1 solutions and this solve's guess x0
+  // (coordinates in the A-orthonormal basis: A-inner products are coordinate dot products, so a
+  // Gram-Schmidt of the coordinate rows gives the new basis' coefficients Q, X' = Q X).  The new
+  // direction of this solve then lies outside span X' only by v, so the next guesses still see the
+  // recent solutions, where Fischer's restart (keep = 0) drops everything: a few solves of 4-7
+  // iterations where the full basis gives 1-2.  Returns the new basis size; `alpha` becomes x0's
+  // coordinates in the new basis.
+  int proj_reseed(int which, int m, std::vector<double>& alpha, hipStream_t s) {
+    ProjHist& H = proj_hist[which];
+    std::vector<std::vector<double>> seeds;
+    const int cap = std::min(proj_keep, m - 1);  // <= m - 1 directions: room for this solve's one
+    const int nh = std::min<int>((int)H.sols.size(), cap - 1);
+    for (int k = (int)H.sols.size() - nh; k < (int)H.sols.size(); ++k) seeds.push_back(H.sols[k]);
+    seeds.push_back(alpha);
+    for (auto& v : seeds) v.resize(m, 0.0);
+    // modified Gram-Schmidt on the coordinate rows, two passes (successive solutions are nearly
+    // parallel: one pass leaves Q orthogonal only to eps / |residual|, and a basis that is not
+    // A-orthonormal makes the projection formula wrong, not just weaker): seeds[a] = sum_b R[a][b] Q[b];
+    // seeds within 1e-6 of the span of the earlier ones add nothing but their coordinates' noise
+    std::vector<std::vector<double>> Q, R(seeds.size());
+    for (size_t a = 0; a < seeds.size(); ++a) {
+      std::vector<double> w = seeds[a];
+      const double n0 = std::sqrt(std::inner_product(w.begin(), w.end(), w.begin(), 0.0));
+      R[a].assign(PROJ_KEEP_MAX, 0.0);
+      for (int pass = 0; pass < 2; ++pass)
+        for (size_t b2 = 0; b2 < Q.size(); ++b2) {
+          const double d = std::inner_product(w.begin(), w.end(), Q[b2].begin(), 0.0);
+          R[a][b2] += d;
+          for (int j = 0; j < m; ++j) w[j] -= d * Q[b2][j];
+        }
+      const double nw = std::sqrt(std::inner_product(w.begin(), w.end(), w.begin(), 0.0));
+      if (nw > 1e-6 * n0 && nw > 0.0 && (int)Q.size() < cap) {
+        R[a][Q.size()] = nw;
+        for (double& x : w) x /= nw;
+        Q.push_back(std::move(w));
+      }
+    }
+    const int kq = (int)Q.size();
+    QMat qm{};
+    for (int i = 0; i < kq; ++i)
+      for (int j = 0; j < m; ++j) qm.q[i][j] = Q[i][j];
+    const i64 n = lp.n_own;
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, s, n, (const double*)projX[which], nloc, m, qm, kq,
+                       projXalt[which]);
+    KCHK();
+    std::swap(projX[which], projXalt[which]);
+    H.sols.clear();
+    for (int a = 0; a + 1 < (int)seeds.size(); ++a) H.sols.emplace_back(R[a].begin(), R[a].begin() + kq);
+    alpha.assign(R.back().begin(), R.back().begin() + kq);
+    return kq;
+  }
+  // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X; a full
+  // basis is re-seeded first (proj_reseed).
   // b, r_final (optional): the solve's right-hand side and final CG residual, with its initial
   // residual r0 = b - A x0 saved in pav[which]: then A v = r0 - r_final (A y = b - r_final on a
   // restart) instead of an SpMV -- exact up to the CG recurrence's rounding drift.
   void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
-    const bool restart = proj_m[which] == op.kmax;
-    // (measured: keeping the newest quarter of the directions across a restart does not lower the
-    // iteration counts after it)
-    const int m = restart ? 0 : proj_m[which], slot = m;
+    proj_finish_coords(which);
+    const bool full = proj_m[which] == op.kmax, restart = full && (proj_keep == 0 || op.kmax < 2);
+    int m = restart ? 0 : proj_m[which];
+    std::vector<double> alpha(h_alpha + which * PROJ_MAX, h_alpha + which * PROJ_MAX + m);
     double *v = pv[which], *av = pav[which];
     if (restart) HIPCHK(hipMemcpyAsync(v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
@@ -931,13 +1018,22 @@ struct Ctx {
       part = side_part;
       cc = side_c;
     }
+    if (restart) proj_hist[which].sols.clear();
+    if (full && !restart) m = proj_reseed(which, m, alpha, s);
     const int nb = grid_ew(n);
     mdot_on(s, nb, n, projX[which], nloc, m, av, v, op.null_free, part);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, s, part, nb, MAXB, m + 2, 0, cc);
     KCHK();
     if (world > 1) comm->allreduce(cc, m + 2, false, s);
+    if (proj_keep > 0) {
+      HIPCHK(hipMemcpyAsync(h_cc + which * (PROJ_MAX + 2), cc, sizeof(double) * (m + 2), hipMemcpyDeviceToHost, s));
+      ProjHist& H = proj_hist[which];
+      H.alpha = alpha;
+      H.m = m;
+      H.pending = true;
+    }
     hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, s, n, projX[which], nloc, m, cc, v, op.null_free,
-                       1.0 / (double)n_free, projX[which] + (i64)slot * nloc);
+                       1.0 / (double)n_free, projX[which] + (i64)m * nloc);
     KCHK();
     if (st2) {
       HIPCHK(hipEventRecord(ev_done[which], st2));
@@ -1513,6 +1609,7 @@ void build(Ctx& c) {
     if (k > 0) {
       c.projX[w] = c.dalloc<double>((i64)k * c.nloc);
       c.proj_x0[w] = c.dalloc<double>(c.nloc);
+      if (c.proj_keep > 0) c.projXalt[w] = c.dalloc<double>((i64)k * c.nloc);  // re-seeding target
     }
   }
   if (c.proj_k > 0 || c.proj_k_visc > 0) {
@@ -1767,6 +1864,8 @@ int pucfem_ctx_create(int32_t device, void** out) {
       HIPCHK(hipSetDevice(device));
       HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
       HIPCHK(hipHostMalloc((void**)&c->h_ctl, 4 * sizeof(int), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->h_alpha, 5 * PROJ_MAX * sizeof(double), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->h_cc, 5 * (PROJ_MAX + 2) * sizeof(double), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64 * sizeof(double), hipHostMallocDefault));
     }
     *out = c.release();

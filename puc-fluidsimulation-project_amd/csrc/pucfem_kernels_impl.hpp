@@ -304,6 +304,28 @@ __global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict
     part[(int64_t)i * MAXB + blockIdx.x] = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
 }
 
+// basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X
+constexpr int PROJ_KEEP_MAX = 8;
+struct QMat {
+  double q[PROJ_KEEP_MAX][PROJ_MAX];
+};
+__global__ __launch_bounds__(BS) void k_reseed(int64_t n, const double* __restrict__ X, int64_t ld, int m, QMat Q,
+                                               int kq, double* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    double acc[PROJ_KEEP_MAX];
+#pragma unroll
+    for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] = 0.0;
+    for (int j = 0; j < m; ++j) {
+      const double x = X[j * ld + r];
+#pragma unroll
+      for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] += Q.q[i][j] * x;
+    }
+#pragma unroll
+    for (int i = 0; i < PROJ_KEEP_MAX; ++i)
+      if (i < kq) out[i * ld + r] = acc[i];
+  }
+}
+
 __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) out[r] = a[r] - b[r];
 }
