@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="pressure CG preconditioner: geometric multigrid over the refinement levels, or Jacobi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-table", action="store_true",
+                    help="per-launch events on every kernel class (default: the roofline kernel only)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="time the steps without per-launch kernel events (no roofline block)")
     ap.add_argument("--no-secondary", action="store_true")
@@ -116,7 +118,9 @@ def main():
         if 1 <= k <= 3:
             startup.append((time.perf_counter() - t, st.it_p + st.it_p2))
         log(f"[bench] warmup step {k}: CG visc/p/p2 = {st.it_visc}/{st.it_p}/{st.it_p2}")
-    sim.ctx.timing(not a.no_kernel_timing)
+    # per-launch events on the roofline kernel only (each timed launch costs a few us of dispatch);
+    # --kernel-table times every kernel class of the table below
+    sim.ctx.timing(0 if a.no_kernel_timing else (1 if a.kernel_table or a.precond != "mg" else 2))
     barrier()
     sim.ctx.sync()
     t0 = time.perf_counter()

@@ -182,7 +182,8 @@ int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps);
 int pucfem_mixing_index(void* ctx, const double* c, double* out3);
 
 /* ---- measurement ------------------------------------------------------------------ */
-/* HIP-event timing of each kernel class on the context's stream (bench.py roofline). */
+/* HIP-event timing of each kernel class on the context's stream (bench.py roofline).
+   on: 0 off, 1 every class, 2 class 0 only (the finest-level smoother: the roofline kernel) */
 int pucfem_timing_enable(void* ctx, int32_t on);
 /* kernel classes: 0 = multigrid Chebyshev smoother on the finest level (k_cheb), 1 = CG SpMV+direction
    (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl),

@@ -88,6 +88,7 @@ struct Red {  // a (possibly globally reduced) partial array
 
 struct Timer {
   bool on = false;
+  uint32_t mask = ~0u;  // timed kernel classes
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
@@ -417,7 +418,7 @@ struct Ctx {
   // rocprofv3 reports it, without the command-processor gap a separately recorded event adds.
   template <typename... KArgs, typename... Args>
   void klaunch(int cls, double bytes, void (*kernel)(KArgs...), dim3 g, dim3 b, Args... args) {
-    if (timer.on && cls >= 0) {
+    if (timer.on && cls >= 0 && ((timer.mask >> cls) & 1u)) {
       hipEvent_t a = timer.get(), e = timer.get();
       hipExtLaunchKernelGGL(kernel, g, b, 0, st, a, e, 0, args...);
       timer.pend.push_back({cls, a, e, bytes});
@@ -2546,7 +2547,9 @@ int pucfem_timing_enable(void* ctx, int32_t on) {
     c.need_dev();
     HIPCHK(hipStreamSynchronize(c.st));
     c.timer.flush();
+    require(on >= 0 && on <= 2, "timing mode");
     c.timer.on = on != 0;
+    c.timer.mask = on == 2 ? 1u : ~0u;
     for (int k = 0; k < Timer::NCLS; ++k) {
       c.timer.ms[k] = 0;
       c.timer.bytes[k] = 0;

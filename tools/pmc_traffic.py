@@ -96,13 +96,12 @@ def main():
             e["write_bytes"] = e["write_raw_avg"] * fw
             e["hbm_bytes_per_launch"] = e["read_bytes"] + e["write_bytes"]
         res["kernels"][short(k[0]) + (f" grid={k[1]}" if k[1] else "")] = e
-    # the bench's roofline kernels, finest level only: k_cheb writing the fp64 z (last post-smoothing
-    # step) plus the k_cheb instances on the largest grid (the finest level's other steps; coarser
-    # levels run the same template on smaller grids), and the pressure CG's k_cg_dir<1>
+    # the bench's roofline kernels, finest level only: the k_cheb instances with level tag 1 (the
+    # finest level's smoothing steps; tag 0 = coarser levels, 2 = pucfem_bench_kernel's batch), and
+    # the pressure CG's k_cg_dir<1>
     summary = {}
     cheb = [k for k in res["kernels"] if k.startswith("k_cheb<") and "hbm_bytes_per_launch" in res["kernels"][k]]
-    gmax = max((int(k.split(" grid=")[1]) for k in cheb if " grid=" in k), default=None)
-    fine = [k for k in cheb if re.match(r"^k_cheb<\w+,\w+,double,", k) or (gmax and k.endswith(f" grid={gmax}"))]
+    fine = [k for k in cheb if re.match(r"^k_cheb<[^>]*,1> grid=", k)]
     for key, ks in (("k_cheb", fine),
                     ("k_cg_dir", [k for k in res["kernels"] if k.startswith("k_cg_dir<1,") and "hbm_bytes_per_launch" in res["kernels"][k]])):
         if ks:
