@@ -1802,20 +1802,39 @@ void build(Ctx& c) {
       // semi-Lagrangian point location: inflated-bbox grid (~1 triangle per cell) + packed records
       Grid LG;
       build_tri_grid(X, Y, tri, 1.0, LG, 1e-6);
+      const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
+      // records in node order: position p holds triangle p2t[p], sorted by smallest vertex id
+      std::vector<i32> p2t(m.T), t2p(m.T), vmin(m.T);
+      for (i64 t = 0; t < m.T; ++t) {
+        p2t[t] = (i32)t;
+        vmin[t] = std::min(tri[3 * t], std::min(tri[3 * t + 1], tri[3 * t + 2]));
+      }
+      std::stable_sort(p2t.begin(), p2t.end(), [&](i32 a, i32 b) { return vmin[a] < vmin[b]; });
+      for (i64 p = 0; p < m.T; ++p) t2p[p2t[p]] = (i32)p;
+      std::vector<int32_t> rec(4 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
+      std::vector<float> rho2p(m.T);
+      for (i64 p = 0; p < m.T; ++p) {
+        const i64 t = p2t[p];
+        for (int v = 0; v < 3; ++v) rec[4 * p + v] = tri[3 * t + v];
+        rec[4 * p + 3] = (int32_t)t;
+        rho2p[p] = rho2[t];
+      }
+      std::vector<double> xy(2 * (size_t)N);
+      for (i64 i = 0; i < N; ++i) {
+        xy[2 * i] = X[i];
+        xy[2 * i + 1] = Y[i];
+      }
+      for (i64 cl = 0; cl + 1 < (i64)LG.cell_start.size(); ++cl) {
+        auto b0 = LG.item.begin() + LG.cell_start[cl], b1 = LG.item.begin() + LG.cell_start[cl + 1];
+        for (auto it = b0; it != b1; ++it) *it = t2p[*it];
+        std::sort(b0, b1);
+      }
       GridDev lg{};
       dgrid(LG, lg, false);
-      const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
-      std::vector<double> rec(8 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
-      for (i64 t = 0; t < m.T; ++t) {
-        for (int v = 0; v < 3; ++v) {
-          rec[8 * t + 2 * v] = X[tri[3 * t + v]];
-          rec[8 * t + 2 * v + 1] = Y[tri[3 * t + v]];
-        }
-        int32_t tail[4] = {tri[3 * t], tri[3 * t + 1], tri[3 * t + 2], 0};
-        std::memcpy(&tail[3], &rho2[t], sizeof(float));
-        std::memcpy(&rec[8 * t + 6], tail, sizeof(tail));
-      }
-      c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item, c.upload(rec)};
+      c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item,
+                       reinterpret_cast<const int4*>(c.upload(rec)), reinterpret_cast<const double2*>(c.upload(xy)),
+                       c.upload(rho2p),
+                       std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0};
     }
     c.c_full = c.dalloc<double>(N);
     c.c_new = c.dalloc<double>(N);

@@ -632,39 +632,43 @@ __device__ __forceinline__ bool knn_less(double d, int32_t i, double bd, int32_t
 //      squared distance from c_T* to its 10th nearest other centroid (rho2, precomputed) bounds the
 //      rank by 9.  Otherwise they are counted over the centroid-grid cells meeting [q - R, q + R]^2.
 // Otherwise no triangle among the 10 nearest passes and the reference keeps c[n].
+// Records are stored in node order (triangles sorted by their smallest vertex id), not in the
+// mesh's triangle order, and hold vertex ids only (16 B: a, b, d and the mesh's triangle id, which
+// the (distance, id) keys keep); the vertex coordinates come from one interleaved (x, y) array in
+// node order, which neighbouring triangles share.  Cells list record positions.
 struct LocDev {
   int32_t nx, ny;
   double x0, y0, hx, hy;
   const int32_t* start;  // nx*ny+1
-  const int32_t* item;   // triangle ids, ascending per cell
-  // per triangle, one 64-B record: x1 y1 x2 y2 x3 y3 (fp64), vertex ids a b d (int32), rho2 (fp32:
-  // squared distance from the centroid to the 10th nearest other centroid, rounded down)
-  const double* rec;
+  const int32_t* item;   // record positions, ascending per cell
+  const int4* rec;       // per position: vertex ids a b d, triangle id
+  const double2* xy;     // node coordinates (internal numbering)
+  // per position: squared distance from the centroid to the 10th nearest other centroid (rounded down)
+  const float* rho2;
+  int32_t probe;  // measurement knob (PUCFEM_SL_PROBE): 1 = accept T* without the rank count
 };
 struct SlTri {
   double x1, y1, x2, y2, x3, y3;
-  int32_t a, b, d;
-  float rho2;
+  int32_t a, b, d, id;
 };
-__device__ __forceinline__ SlTri sl_tri(const LocDev& L, int32_t t) {
-  const double2* r = reinterpret_cast<const double2*>(L.rec + 8 * (int64_t)t);
-  const double2 p = r[0], q = r[1], s = r[2];
-  const int4 m = reinterpret_cast<const int4*>(r)[3];
-  return SlTri{p.x, p.y, q.x, q.y, s.x, s.y, m.x, m.y, m.z, __int_as_float(m.w)};
+__device__ __forceinline__ SlTri sl_tri(const LocDev& L, int32_t pos) {
+  const int4 m = L.rec[pos];
+  const double2 p = L.xy[m.x], q = L.xy[m.y], s = L.xy[m.z];
+  return SlTri{p.x, p.y, q.x, q.y, s.x, s.y, m.x, m.y, m.z, m.w};
 }
 constexpr double SL_MARGIN = 1e-6;
 
-// -> triangle id, or -1 (no triangle among the KNN nearest centroids contains q)
+// -> record position of the triangle, or -1 (no triangle among the KNN nearest centroids contains q)
 __device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, double qx, double qy) {
   const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
   const int64_t cell = (int64_t)cj * L.nx + ci;
-  int32_t best = 0x7fffffff;
+  int32_t best = 0x7fffffff, bpos = -1;
   double bestd = INFINITY;
-  float brho2 = 0.f;
   const int32_t e1 = L.start[cell + 1];
   for (int32_t e = L.start[cell]; e < e1; ++e) {
-    const int32_t t = L.item[e];
-    const SlTri r = sl_tri(L, t);
+    const int32_t pos = L.item[e];
+    const SlTri r = sl_tri(L, pos);
+    const int32_t t = r.id;
     const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
     const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
     if (!(fabs(det) >= 1e-14)) continue;
@@ -678,13 +682,13 @@ __device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, 
       if (knn_less(d, t, bestd, best)) {
         bestd = d;
         best = t;
-        brho2 = r.rho2;
+        bpos = pos;
       }
       if (w1 >= SL_MARGIN && w2 >= SL_MARGIN && w3 >= SL_MARGIN) break;
     }
   }
-  if (best == 0x7fffffff) return -1;
-  if (4.0 * bestd * (1.0 + 1e-9) < (double)brho2) return best;
+  if (bpos < 0) return -1;
+  if (4.0 * bestd * (1.0 + 1e-9) < (double)L.rho2[bpos] || (L.probe & 1)) return bpos;
   const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
   const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
   const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
@@ -697,7 +701,7 @@ __device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, 
       if (knn_less(d, G.item[e], bestd, best) && ++cnt >= KNN) return -1;
     }
   }
-  return best;
+  return bpos;
 }
 
 __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:353-357
