@@ -188,23 +188,40 @@ template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
 void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y);
-// k_mdot for basis size m (0..PROJ_MAX): one instance per size
+// k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size
 template <int M>
-void mdot_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* v, const double* w,
-                 const int32_t* master_of, double* part) {
-  hipLaunchKernelGGL(k_mdot<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, v, w, master_of, part);
+void mdot2_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* b, const double* av,
+                  const double* v, const int32_t* master_of, double* part) {
+  hipLaunchKernelGGL(k_mdot2<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, b, av, v, master_of, part);
 }
-using MdotFn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
-                        const int32_t*, double*);
+using Mdot2Fn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
+                         const double*, const int32_t*, double*);
 template <int... M>
-constexpr std::array<MdotFn, sizeof...(M)> mdot_table(std::integer_sequence<int, M...>) {
-  return {&mdot_launch<M>...};
+constexpr std::array<Mdot2Fn, sizeof...(M)> mdot2_table(std::integer_sequence<int, M...>) {
+  return {&mdot2_launch<M>...};
 }
-void mdot_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* v, const double* w,
-             const int32_t* master_of, double* part) {
-  static constexpr auto tab = mdot_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
+void mdot2_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* b, const double* av,
+              const double* v, const int32_t* master_of, double* part) {
+  static constexpr auto tab = mdot2_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
   if (m < 0 || m > PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
-  tab[m](s, nb, n, X, ld, v, w, master_of, part);
+  tab[m](s, nb, n, X, ld, b, av, v, master_of, part);
+}
+template <int M>
+void pcomb_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* K, const double* v,
+                  const int32_t* master_of, double* xm, double* y, double* x0) {
+  hipLaunchKernelGGL(k_pcomb<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, K, v, master_of, xm, y, x0);
+}
+using PcombFn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
+                         const int32_t*, double*, double*, double*);
+template <int... M>
+constexpr std::array<PcombFn, sizeof...(M)> pcomb_table(std::integer_sequence<int, M...>) {
+  return {&pcomb_launch<M>...};
+}
+void pcomb_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* K, const double* v,
+              const int32_t* master_of, double* xm, double* y, double* x0) {
+  static constexpr auto tab = pcomb_table(std::make_integer_sequence<int, PROJ_MAX>{});
+  if (m < 0 || m >= PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
+  tab[m](s, nb, n, X, ld, K, v, master_of, xm, y, x0);
 }
 
 struct Ctx {
@@ -315,27 +332,26 @@ struct Ctx {
   double* projX[5] = {};
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
-  // full-basis re-seeding (proj_reseed): the guess's coefficients (h_alpha) and the update's
-  // reduction values (h_cc), pinned; per basis the coordinates of the last solutions.
-  // PUCFEM_PROJ_KEEP (measurement knob, default 8, 0: Fischer's restart) seeds kept
-  double *h_alpha = nullptr, *h_cc = nullptr;
+  // Deferred update (project_guess): after a solve only v = y - x0 and A v are formed; the next
+  // guess of the same solve orthogonalises v against X, appends it and projects the new right-hand
+  // side in one multi-dot and one combination pass over X.  h_coef (pinned) receives each guess's
+  // coefficients, read at the next guess to track the coordinates of the recent solutions in the
+  // basis (re-seeding a full basis, proj_reseed).  PUCFEM_PROJ_KEEP (measurement knob, 2..8,
+  // default 8): seeds kept.
+  static constexpr int NCOEF = 2 * PROJ_MAX + 4;
+  double* h_coef = nullptr;
   double* projXalt[5] = {};
   struct ProjHist {
-    std::vector<std::vector<double>> sols;
-    std::vector<double> alpha;
-    int m = 0;
-    bool pending = false;
+    std::vector<std::vector<double>> sols;  // coordinates of the last solutions
+    std::vector<double> gamma;              // coordinates of the last guess x0
+    int coef_m = -1;                        // h_coef holds a guess over coef_m directions (-1: none)
   } proj_hist[5];
-  int proj_keep = std::getenv("PUCFEM_PROJ_KEEP") ? std::max(0, std::min(PROJ_KEEP_MAX, std::atoi(std::getenv("PUCFEM_PROJ_KEEP"))))
-                                                   : 8;
-  double *proj_part = nullptr, *proj_c = nullptr;
-  // single rank: the basis update's multi-dot and combination (m + 2 vector passes) run on a side
-  // stream, overlapping the rest of the step (the next pressure solve, the semi-Lagrangian
-  // kernel); per-solve v / A v buffers and side scratch; the next guess of the same solve waits
-  hipStream_t st2 = nullptr;
-  hipEvent_t ev_prep[5] = {}, ev_done[5] = {};
-  bool pending[5] = {false, false, false, false, false};
-  double *pv[5] = {}, *pav[5] = {}, *side_part = nullptr, *side_c = nullptr;
+  int proj_keep = std::getenv("PUCFEM_PROJ_KEEP")
+                      ? std::max(2, std::min(PROJ_KEEP_MAX, std::atoi(std::getenv("PUCFEM_PROJ_KEEP"))))
+                      : 8;
+  double *proj_part = nullptr, *proj_d = nullptr, *proj_coef = nullptr;
+  bool proj_pend[5] = {false, false, false, false, false};  // v / A v wait for the next guess
+  double *pv[5] = {}, *pav[5] = {};
   // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
   // space: constants on the free dofs, cleared from new directions) or the Jacobi-scaled A_visc
   struct ProjOp {
@@ -352,20 +368,11 @@ struct Ctx {
   ~Ctx() {
     if (!host_only) {
       if (st) (void)hipStreamSynchronize(st);
-      if (st2) {
-        (void)hipStreamSynchronize(st2);
-        (void)hipStreamDestroy(st2);
-      }
-      for (int w = 0; w < 5; ++w) {
-        if (ev_prep[w]) (void)hipEventDestroy(ev_prep[w]);
-        if (ev_done[w]) (void)hipEventDestroy(ev_done[w]);
-      }
       if (gexec) (void)hipGraphExecDestroy(gexec);
       if (graph) (void)hipGraphDestroy(graph);
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
-      if (h_alpha) (void)hipHostFree(h_alpha);
-      if (h_cc) (void)hipHostFree(h_cc);
+      if (h_coef) (void)hipHostFree(h_coef);
       if (h_pinned) (void)hipHostFree(h_pinned);
       comm.reset();
       if (st) (void)hipStreamDestroy(st);
@@ -888,71 +895,79 @@ struct Ctx {
     halo(pout);
     return it;
   }
-  // x0 = sum_i <X_i, b> X_i for the new right-hand side b (A-orthonormal X: the A-projection of
-  // the solution onto span X), kept for the update.  With an empty basis the solve keeps its warm
-  // start and x0 = 0, so that the first direction is the whole first solution.
+  // Successive right-hand sides (Fischer 1998) with a deferred update.
+  // Guess for the right-hand side b: x0 = sum_i <X_i, b> X_i, the A-projection of the new solution
+  // onto span X (X A-orthonormal).  Before it, the last solve's direction v = y - x0 (with A v) is
+  // A-orthogonalised against X, cleared of the operator's null space and appended:
+  //   X_m = s (v - mu 1_free - sum_i c_i X_i),  c_i = <X_i, A v>,  s = (<v, A v> - |c|^2)^-1/2,
+  //   <X_m, b> = s (<v, b> - mu sum_free b - sum_i c_i <X_i, b>),
+  // so one multi-dot pass over X (dots with b and A v, k_mdot2) and one combination pass (X_m and
+  // x0 together, k_pcomb) do both: 2m + 9 vector passes per solve where a separate update took
+  // 4m + 15.  A full basis is re-seeded first (proj_reseed).  With an empty basis the solve keeps
+  // its warm start (x0 = 0).
   void project_guess(int which, const double* b, double* y) {
     const i64 n = lp.n_own;
-    const int m = proj_m[which];
-    if (pending[which]) {  // the side stream's update of this basis
-      HIPCHK(hipStreamWaitEvent(st, ev_done[which], 0));
-      pending[which] = false;
-    }
-    if (m == 0) {
-      HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
-      return;
-    } else {
-      const int nb = grid_ew(n);
-      mdot_on(st, nb, n, projX[which], nloc, m, b, nullptr, nullptr, proj_part);
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, m, 0, proj_c);
-      KCHK();
-      if (world > 1) comm->allreduce(proj_c, m, false, st);
-      HIPCHK(hipMemcpyAsync(h_alpha + which * PROJ_MAX, proj_c, sizeof(double) * m, hipMemcpyDeviceToHost, st));
-      hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, st, n, projX[which], nloc, m, proj_c,
-                         (const double*)nullptr, (const int32_t*)nullptr, 0.0, y);
-      KCHK();
-    }
-    HIPCHK(hipMemcpyAsync(proj_x0[which], y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
-  }
-  // coordinates of the last solve's solution in the basis (lazily: its update's reduction values
-  // reach h_cc asynchronously; read here, after a host synchronisation that follows them):
-  // y = x0 + v = sum_i (a_i + c_i) X_i + sqrt(den) X_new (+ a null-space constant)
-  void proj_finish_coords(int which) {
+    const ProjOp op = proj_op(which);
     ProjHist& H = proj_hist[which];
-    if (!H.pending) return;
-    const int m = H.m;
-    const double* cc = h_cc + which * (PROJ_MAX + 2);
-    std::vector<double> y(m + 1, 0.0);
-    double q = 0.0;
-    for (int i = 0; i < m; ++i) {
-      y[i] = H.alpha[i] + cc[i];
-      q += cc[i] * cc[i];
+    proj_coords(which);
+    int m = proj_m[which];
+    if (!proj_pend[which]) {  // first solve: no direction yet
+      HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
+      H.gamma.clear();
+      return;
     }
-    const double den = cc[m] - q;
-    y[m] = den > 1e-10 * cc[m] && den > 0.0 ? std::sqrt(den) : 0.0;  // as k_mcomb's null test
+    const int nb = grid_ew(n);
+    mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, 2 * m + 4, 0, proj_d);
+    KCHK();
+    if (world > 1) comm->allreduce(proj_d, 2 * m + 4, false, st);
+    QMat qm{};
+    int kq = m;
+    if (m == op.kmax) kq = proj_reseed(which, m, qm);  // full: X' = Q X, the dots follow as Q a, Q c
+    hipLaunchKernelGGL(k_pcoef, dim3(1), dim3(64), 0, st, (const double*)proj_d, m, qm, m == op.kmax ? kq : -1,
+                       1.0 / (double)n_free, proj_coef);
+    KCHK();
+    HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
+    pcomb_on(st, nb, n, projX[which], nloc, kq, proj_coef, pv[which], op.null_free, projX[which] + (i64)kq * nloc, y,
+             proj_x0[which]);
+    H.coef_m = kq;
+    proj_m[which] = kq + 1;
+    proj_pend[which] = false;
+  }
+  // coordinates bookkeeping: the last guess's coefficients (h_coef, copied with it; read after the
+  // solve's host synchronisation) give the last solution y = x0 + v in the basis,
+  // [gamma_i + c_i, 1 / s], and the last guess x0, [a_i, alpha_new]
+  void proj_coords(int which) {
+    ProjHist& H = proj_hist[which];
+    if (H.coef_m < 0) return;
+    const int m = H.coef_m;
+    const double* K = h_coef + which * NCOEF;  // a (m), c (m), s, mu, alpha_new
+    std::vector<double> y(m + 1, 0.0);
+    for (int i = 0; i < m; ++i) y[i] = (i < (int)H.gamma.size() ? H.gamma[i] : 0.0) + K[m + i];
+    y[m] = K[2 * m] > 0.0 ? 1.0 / K[2 * m] : 0.0;
     H.sols.push_back(std::move(y));
     if ((int)H.sols.size() > PROJ_KEEP_MAX) H.sols.erase(H.sols.begin());
-    H.pending = false;
+    H.gamma.assign(K, K + m);
+    H.gamma.push_back(K[2 * m + 2]);
+    H.coef_m = -1;
   }
-  // Full basis: re-seed it with the span of the last keep - 1 solutions and this solve's guess x0
-  // (coordinates in the A-orthonormal basis: A-inner products are coordinate dot products, so a
-  // Gram-Schmidt of the coordinate rows gives the new basis' coefficients Q, X' = Q X).  The new
-  // direction of this solve then lies outside span X' only by v, so the next guesses still see the
-  // recent solutions, where Fischer's restart (keep = 0) drops everything: a few solves of 4-7
-  // iterations where the full basis gives 1-2.  Returns the new basis size; `alpha` becomes x0's
-  // coordinates in the new basis.
-  int proj_reseed(int which, int m, std::vector<double>& alpha, hipStream_t s) {
+  // Full basis: re-seed it with the span of the last solutions and the last guess x0 (the pending
+  // direction v then completes the span of the last solution).  In an A-orthonormal basis A-inner
+  // products are coordinate dot products, so a Gram-Schmidt of the coordinate rows gives the new
+  // basis' coefficients Q, X' = Q X (k_reseed, one pass over X).  Two Gram-Schmidt passes:
+  // successive solutions are nearly parallel, one pass leaves Q orthogonal only to eps / |residual|,
+  // and a basis that is not A-orthonormal makes the projection formula wrong, not just weaker;
+  // seeds within 1e-6 of the span of the earlier ones add only their coordinates' noise.  Fischer's
+  // restart (drop everything) costs a run of solves of 7, 5, 4, 3 iterations where the full basis
+  // gives 1-2.  Returns the new basis size (<= kmax - 1).
+  int proj_reseed(int which, int m, QMat& qm) {
     ProjHist& H = proj_hist[which];
+    const int cap = std::min(proj_keep, m - 1);
     std::vector<std::vector<double>> seeds;
-    const int cap = std::min(proj_keep, m - 1);  // <= m - 1 directions: room for this solve's one
     const int nh = std::min<int>((int)H.sols.size(), cap - 1);
     for (int k = (int)H.sols.size() - nh; k < (int)H.sols.size(); ++k) seeds.push_back(H.sols[k]);
-    seeds.push_back(alpha);
+    seeds.push_back(H.gamma);
     for (auto& v : seeds) v.resize(m, 0.0);
-    // modified Gram-Schmidt on the coordinate rows, two passes (successive solutions are nearly
-    // parallel: one pass leaves Q orthogonal only to eps / |residual|, and a basis that is not
-    // A-orthonormal makes the projection formula wrong, not just weaker): seeds[a] = sum_b R[a][b] Q[b];
-    // seeds within 1e-6 of the span of the earlier ones add nothing but their coordinates' noise
     std::vector<std::vector<double>> Q, R(seeds.size());
     for (size_t a = 0; a < seeds.size(); ++a) {
       std::vector<double> w = seeds[a];
@@ -972,83 +987,38 @@ struct Ctx {
       }
     }
     const int kq = (int)Q.size();
-    QMat qm{};
     for (int i = 0; i < kq; ++i)
       for (int j = 0; j < m; ++j) qm.q[i][j] = Q[i][j];
     const i64 n = lp.n_own;
-    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, s, n, (const double*)projX[which], nloc, m, qm, kq,
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const double*)projX[which], nloc, m, qm, kq,
                        projXalt[which]);
     KCHK();
     std::swap(projX[which], projXalt[which]);
     H.sols.clear();
     for (int a = 0; a + 1 < (int)seeds.size(); ++a) H.sols.emplace_back(R[a].begin(), R[a].begin() + kq);
-    alpha.assign(R.back().begin(), R.back().begin() + kq);
+    H.gamma.assign(R.back().begin(), R.back().begin() + kq);
     return kq;
   }
-  // new direction v = y - x0, A-orthogonalised against X and A-normalised, appended to X; a full
-  // basis is re-seeded first (proj_reseed).
-  // b, r_final (optional): the solve's right-hand side and final CG residual, with its initial
-  // residual r0 = b - A x0 saved in pav[which]: then A v = r0 - r_final (A y = b - r_final on a
-  // restart) instead of an SpMV -- exact up to the CG recurrence's rounding drift.
+  // after a solve: the new direction v = y - x0 and A v, for the next guess.  b, r_final (optional):
+  // the solve's right-hand side and final CG residual, with its initial residual r0 = b - A x0 saved
+  // in pav[which]: then A v = r0 - r_final (A y = b - r_final for the first direction, whose solve
+  // started from the warm start with x0 = 0) instead of an SpMV -- exact up to the CG recurrence's
+  // rounding drift.
   void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
-    proj_finish_coords(which);
-    const bool full = proj_m[which] == op.kmax, restart = full && (proj_keep == 0 || op.kmax < 2);
-    int m = restart ? 0 : proj_m[which];
-    std::vector<double> alpha(h_alpha + which * PROJ_MAX, h_alpha + which * PROJ_MAX + m);
     double *v = pv[which], *av = pav[which];
-    if (restart) HIPCHK(hipMemcpyAsync(v, y, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
-    else hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
+    hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
     KCHK();
-    if (r_final) {  // x0 = 0 (first direction, restart): the CG started elsewhere, A y = b - r_final
-      const bool whole = restart || proj_m[which] == 0;
+    if (r_final) {
+      const bool whole = proj_m[which] == 0;
       hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, whole ? b : av, r_final, av);
       KCHK();
     } else {
       halo(v);
       spmv_on(st, *op.A, op.val, v, av);
     }
-    // multi-dot + combination: on the side stream when there is one (single rank)
-    hipStream_t s = st;
-    double *part = proj_part, *cc = proj_c;
-    if (st2) {
-      HIPCHK(hipEventRecord(ev_prep[which], st));
-      HIPCHK(hipStreamWaitEvent(st2, ev_prep[which], 0));
-      s = st2;
-      part = side_part;
-      cc = side_c;
-    }
-    if (restart) proj_hist[which].sols.clear();
-    if (full && !restart) m = proj_reseed(which, m, alpha, s);
-    const int nb = grid_ew(n);
-    mdot_on(s, nb, n, projX[which], nloc, m, av, v, op.null_free, part);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, s, part, nb, MAXB, m + 2, 0, cc);
-    KCHK();
-    if (world > 1) comm->allreduce(cc, m + 2, false, s);
-    if (proj_keep > 0) {
-      HIPCHK(hipMemcpyAsync(h_cc + which * (PROJ_MAX + 2), cc, sizeof(double) * (m + 2), hipMemcpyDeviceToHost, s));
-      ProjHist& H = proj_hist[which];
-      H.alpha = alpha;
-      H.m = m;
-      H.pending = true;
-    }
-    hipLaunchKernelGGL(k_mcomb, dim3(grid_ew(n)), dim3(BS), 0, s, n, projX[which], nloc, m, cc, v, op.null_free,
-                       1.0 / (double)n_free, projX[which] + (i64)m * nloc);
-    KCHK();
-    if (st2) {
-      HIPCHK(hipEventRecord(ev_done[which], st2));
-      pending[which] = true;
-    }
-    proj_m[which] = m + 1;
-  }
-  // the side stream's work is part of the step: every synchronisation point waits for it
-  void join_side() {
-    for (int w = 0; w < 5; ++w)
-      if (pending[w]) {
-        HIPCHK(hipStreamWaitEvent(st, ev_done[w], 0));
-        pending[w] = false;
-      }
+    proj_pend[which] = true;
   }
   void grad_proj(const double* pp, int mode) {
     const int nb = nb_for(dP.nslices);
@@ -1602,15 +1572,17 @@ void build(Ctx& c) {
   c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1;
   // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
   // small meshes need no better start)
-  c.proj_k = c.use_mg && !c.dense ? std::max(0, std::min(c.prm.proj_k, (int)PROJ_MAX)) : 0;
+  // (a basis needs room for the re-seeded span and one new direction: at least 3)
+  auto proj_size = [](int k) { return k <= 0 ? 0 : std::max(3, std::min(k, (int)PROJ_MAX)); };
+  c.proj_k = c.use_mg && !c.dense ? proj_size(c.prm.proj_k) : 0;
   const bool block_visc = c.world == 1 && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
-  c.proj_k_visc = stokes && !c.dense && !block_visc ? std::max(0, std::min(c.prm.proj_k_visc, (int)PROJ_MAX)) : 0;
+  c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
   for (int w = 1; w <= 4; ++w) {
     const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
     if (k > 0) {
       c.projX[w] = c.dalloc<double>((i64)k * c.nloc);
       c.proj_x0[w] = c.dalloc<double>(c.nloc);
-      if (c.proj_keep > 0) c.projXalt[w] = c.dalloc<double>((i64)k * c.nloc);  // re-seeding target
+      c.projXalt[w] = c.dalloc<double>((i64)k * c.nloc);  // re-seeding target
     }
   }
   if (c.proj_k > 0 || c.proj_k_visc > 0) {
@@ -1619,19 +1591,9 @@ void build(Ctx& c) {
         c.pv[w] = c.dalloc<double>(c.nloc);
         c.pav[w] = c.dalloc<double>(c.nloc);
       }
-    c.proj_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
-    c.proj_c = c.dalloc<double>(64);
-    // RCCL stays on one stream: multi-rank runs update on the main stream (PUCFEM_NO_SIDE_STREAM:
-    // single-rank runs too, a measurement knob)
-    if (c.world == 1 && !std::getenv("PUCFEM_NO_SIDE_STREAM")) {
-      HIPCHK(hipStreamCreateWithFlags(&c.st2, hipStreamNonBlocking));
-      for (int w = 1; w <= 4; ++w) {
-        HIPCHK(hipEventCreateWithFlags(&c.ev_prep[w], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c.ev_done[w], hipEventDisableTiming));
-      }
-      c.side_part = c.dalloc<double>((i64)(PROJ_MAX + 2) * MAXB);
-      c.side_c = c.dalloc<double>(64);
-    }
+    c.proj_part = c.dalloc<double>((i64)Ctx::NCOEF * MAXB);
+    c.proj_d = c.dalloc<double>(Ctx::NCOEF);
+    c.proj_coef = c.dalloc<double>(Ctx::NCOEF);
   }
   if (c.dense) {
     // A_visc^-1 and the pseudo-inverse of the merged pressure operator (constants on the free dofs
@@ -1884,8 +1846,7 @@ int pucfem_ctx_create(int32_t device, void** out) {
       HIPCHK(hipSetDevice(device));
       HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
       HIPCHK(hipHostMalloc((void**)&c->h_ctl, 4 * sizeof(int), hipHostMallocDefault));
-      HIPCHK(hipHostMalloc((void**)&c->h_alpha, 5 * PROJ_MAX * sizeof(double), hipHostMallocDefault));
-      HIPCHK(hipHostMalloc((void**)&c->h_cc, 5 * (PROJ_MAX + 2) * sizeof(double), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->h_coef, 5 * Ctx::NCOEF * sizeof(double), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64 * sizeof(double), hipHostMallocDefault));
     }
     *out = c.release();
@@ -2220,7 +2181,6 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       }
       std::vector<double> h(8 * (size_t)nsteps);
       std::vector<int> hd(3 * (size_t)nsteps);
-      c.join_side();  // a step call returns with all of its work done
       HIPCHK(hipMemcpyAsync(h.data(), rec, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipMemcpyAsync(hd.data(), dits, sizeof(int) * hd.size(), hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
@@ -2595,7 +2555,6 @@ int pucfem_sync(void* ctx) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
     if (!c.host_only) {
-      c.join_side();
       HIPCHK(hipStreamSynchronize(c.st));
     }
   });

@@ -255,55 +255,6 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
 // projection of the new solution onto span X, x0 = sum_i <X_i, b> X_i.  X: m vectors at stride ld.
 constexpr int PROJ_MAX = 32;
 
-// partial dots <X_i, v> (i < M) and, with w, <v, w> (slot M) and the sum of w over the free
-// (non-slave) rows (slot M + 1); stride MAXB per value.  One instance per basis size M: the M loads
-// of a row are unconditional, so they are all in flight together (a runtime count puts each load
-// behind a branch and serialises them: 2 TB/s).
-template <int M>
-__global__ __launch_bounds__(BS) void k_mdot(int64_t n, const double* __restrict__ X, int64_t ld,
-                                             const double* __restrict__ v, const double* __restrict__ w,
-                                             const int32_t* __restrict__ master_of, double* part) {
-  constexpr int NA = M + 2;
-  __shared__ double sh[NA][4];
-  double acc[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) acc[i] = 0.0;
-  // grid-stride rows: the resident waves read one compact window of every basis vector (contiguous
-  // per-block chunks spread them over the whole of each vector, TLB-bound)
-  const int64_t step = (int64_t)gridDim.x * BS;
-  if (w) {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
-      const double vr = v[r], wr = w[r];
-      double x[M > 0 ? M : 1];
-#pragma unroll
-      for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
-#pragma unroll
-      for (int i = 0; i < M; ++i) acc[i] += x[i] * vr;
-      acc[M] += vr * wr;
-      if (master_of && master_of[r] < 0) acc[M + 1] += wr;
-    }
-  } else {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
-      const double vr = v[r];
-      double x[M > 0 ? M : 1];
-#pragma unroll
-      for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
-#pragma unroll
-      for (int i = 0; i < M; ++i) acc[i] += x[i] * vr;
-    }
-  }
-  const int nv = w ? NA : M;
-#pragma unroll
-  for (int i = 0; i < NA; ++i)
-    if (i < nv) {
-      const double t = wave_sum(acc[i]);
-      if ((threadIdx.x & 63) == 0) sh[i][threadIdx.x >> 6] = t;
-    }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nv; i += BS)
-    part[(int64_t)i * MAXB + blockIdx.x] = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
-}
-
 // basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X
 constexpr int PROJ_KEEP_MAX = 8;
 struct QMat {
@@ -326,33 +277,118 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const double* __restri
   }
 }
 
-__global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
-  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) out[r] = a[r] - b[r];
+// deferred projection update + guess (Ctx::project_guess), pass 1: partial dots of the M basis
+// vectors with b and A v, and <v, b>, <v, A v>, the sums of v and b over the free (non-slave) rows
+// (master_of null: no null space, zero); stride MAXB per value, order
+// [<X_i, b> (M), <X_i, A v> (M), <v, b>, <v, A v>, sum_free v, sum_free b].  One instance per M:
+// the M loads of a row are unconditional (all in flight together); grid-stride rows keep the
+// resident waves on one compact window of every vector.
+template <int M>
+__global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const double* __restrict__ X, int64_t ld,
+                                              const double* __restrict__ b, const double* __restrict__ av,
+                                              const double* __restrict__ v, const int32_t* __restrict__ master_of,
+                                              double* part) {
+  constexpr int NA = 2 * M + 4;
+  __shared__ double sh[NA][4];
+  double acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+  const int64_t step = (int64_t)gridDim.x * BS;
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+    const double br = b[r], ar = av[r], vr = v[r];
+    double x[M > 0 ? M : 1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      acc[i] += x[i] * br;
+      acc[M + i] += x[i] * ar;
+    }
+    acc[2 * M] += vr * br;
+    acc[2 * M + 1] += vr * ar;
+    if (master_of && master_of[r] < 0) {
+      acc[2 * M + 2] += vr;
+      acc[2 * M + 3] += br;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const double t = wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) sh[i][threadIdx.x >> 6] = t;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NA; i += BS)
+    part[(int64_t)i * MAXB + blockIdx.x] = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
 }
 
-// v == null: out = sum_i c_i X_i (the projected initial guess).
-// v != null: out = s (v - mu 1_free - sum_i c_i X_i), s = 1 / sqrt(c_m - sum_i c_i^2) -- with
-// c_i = <X_i, A v>, c_m = <v, A v> and mu = c_(m+1) / n_free (the mean of v over the free rows) this
-// is v A-orthogonalised against X, cleared of the operator's null space (constants on the free
-// rows: the V-cycle lets the CG iterate drift along it; master_of null: no null space) and
-// A-normalised; s = 0 (a null direction)
-// when v lies in span X to 1e-10 relative.  out may alias one of the X_i (element-wise update).
-__global__ void k_mcomb(int64_t n, const double* X, int64_t ld, int m, const double* __restrict__ c,
-                        const double* __restrict__ v, const int32_t* __restrict__ master_of, double inv_nfree,
-                        double* out) {
-  double s = 1.0, mu = 0.0;
-  if (v) {
-    mu = c[m + 1] * inv_nfree;
-    double q = 0.0;
-    for (int i = 0; i < m; ++i) q += c[i] * c[i];
-    const double den = c[m] - q;
-    s = den > 1e-10 * c[m] && den > 0.0 ? 1.0 / sqrt(den) : 0.0;
+// pass 1 -> coefficients (one thread).  D: the reduced dots of k_mdot2 over m vectors; kq >= 0: the
+// basis was re-seeded, X' = Q X (kq rows), so <X'_i, .> = Q <X, .>.  Out (m' = kq or m):
+// [a (m'), c (m'), s, mu, alpha] with a_i = <X_i, b>, c_i = <X_i, A v>,
+// s = (<v, A v> - |c|^2)^-1/2 (0 when v lies in span X to 1e-10 relative: a null direction),
+// mu = sum_free v / n_free, alpha = <X_m, b> = s (<v, b> - mu sum_free b - <c, a>).
+__global__ void k_pcoef(const double* __restrict__ D, int m, QMat Q, int kq, double inv_nfree, double* K) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int mp = kq >= 0 ? kq : m;
+  double q = 0.0, ca = 0.0;
+  for (int i = 0; i < mp; ++i) {
+    double a = 0.0, c = 0.0;
+    if (kq >= 0) {
+      for (int j = 0; j < m; ++j) {
+        a += Q.q[i][j] * D[j];
+        c += Q.q[i][j] * D[m + j];
+      }
+    } else {
+      a = D[i];
+      c = D[m + i];
+    }
+    K[i] = a;
+    K[mp + i] = c;
+    q += c * c;
+    ca += c * a;
   }
+  const double vb = D[2 * m], vav = D[2 * m + 1], vs = D[2 * m + 2], bs = D[2 * m + 3];
+  const double den = vav - q;
+  const double s = den > 1e-10 * vav && den > 0.0 ? 1.0 / sqrt(den) : 0.0;
+  const double mu = vs * inv_nfree;
+  K[2 * mp] = s;
+  K[2 * mp + 1] = mu;
+  K[2 * mp + 2] = s * (vb - mu * bs - ca);
+}
+
+// pass 2: the new direction X_M = s (v - mu 1_free - sum_i c_i X_i) and the guess
+// x0 = sum_i a_i X_i + alpha X_M (written to y and x0), one pass over the M basis vectors
+template <int M>
+__global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const double* __restrict__ X, int64_t ld,
+                                              const double* __restrict__ K, const double* __restrict__ v,
+                                              const int32_t* __restrict__ master_of, double* __restrict__ xm_out,
+                                              double* __restrict__ y, double* __restrict__ x0) {
+  double ka[M > 0 ? M : 1], kc[M > 0 ? M : 1];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    ka[i] = K[i];
+    kc[i] = K[M + i];
+  }
+  const double s = K[2 * M], mu = K[2 * M + 1], alpha = K[2 * M + 2];
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
-    double a = 0.0;
-    for (int i = 0; i < m; ++i) a += c[i] * X[i * ld + r];
-    out[r] = v ? s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - a) : a;
+    double x[M > 0 ? M : 1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    double sa = 0.0, sc = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      sa += ka[i] * x[i];
+      sc += kc[i] * x[i];
+    }
+    const double xm = s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
+    const double g = sa + alpha * xm;
+    xm_out[r] = xm;
+    y[r] = g;
+    x0[r] = g;
   }
+}
+
+__global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) out[r] = a[r] - b[r];
 }
 
 // CG convergence test right after the residual update: ctl = (1, it) when <r_c, r_c> <= tol2 <b_c, b_c>
