@@ -352,6 +352,13 @@ struct Ctx {
   double *proj_part = nullptr, *proj_d = nullptr, *proj_coef = nullptr;
   bool proj_pend[5] = {false, false, false, false, false};  // v / A v wait for the next guess
   double *pv[5] = {}, *pav[5] = {};
+  // viscous warm start u^n + a polynomial extrapolation of the increments u* - u of the last steps:
+  // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that;
+  // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. 3, default 3 (L7, 40 steps: viscous
+  // iterations per step 5 / 4 / 3 / 2-3 for orders 0-3, 17.47 / 16.82 / 16.12 / 15.75 ms per step)
+  double* dvinc[6] = {};
+  int have_vinc = 0;
+  int visc_extrap = std::getenv("PUCFEM_VISC_EXTRAP") ? std::max(0, std::min(3, std::atoi(std::getenv("PUCFEM_VISC_EXTRAP")))) : 3;
   // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
   // space: constants on the free dofs, cleared from new directions) or the Jacobi-scaled A_visc
   struct ProjOp {
@@ -834,7 +841,11 @@ struct Ctx {
       bc(usx, usy);
       return 0;
     }
-    hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy);
+    const bool ext = dvinc[0] != nullptr && !proj_k_visc;
+    VincDev vd{};
+    vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
+    for (int k = 0; k < 6; ++k) vd.d[k] = dvinc[k];
+    hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
     KCHK();
     double* y[2] = {yvx, yvy};
     const double* b[2] = {bvx, bvy};
@@ -848,8 +859,19 @@ struct Ctx {
       project_update(3, yvx);
       project_update(4, yvy);
     }
-    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
-                       (const int32_t*)nullptr);
+    if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
+      const int last = 2 * (visc_extrap - 1);
+      hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yvx, yvy, ux, uy, usx, usy,
+                         dvinc[last], dvinc[last + 1]);
+      for (int k = last; k >= 2; k -= 2) {
+        std::swap(dvinc[k], dvinc[k - 2]);
+        std::swap(dvinc[k + 1], dvinc[k - 1]);
+      }
+      have_vinc = std::min(have_vinc + 1, visc_extrap);
+    } else {
+      hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
+                         (const int32_t*)nullptr);
+    }
     KCHK();
     bc(usx, usy);
     halo(usx, usy);
@@ -1585,6 +1607,8 @@ void build(Ctx& c) {
       c.projXalt[w] = c.dalloc<double>((i64)k * c.nloc);  // re-seeding target
     }
   }
+  if (stokes && !c.dense && !block_visc && c.proj_k_visc == 0 && c.visc_extrap > 0)
+    for (int k = 0; k < 2 * c.visc_extrap; ++k) c.dvinc[k] = c.dalloc<double>(c.nloc);
   if (c.proj_k > 0 || c.proj_k_visc > 0) {
     for (int w = 1; w <= 4; ++w)
       if (c.projX[w]) {
@@ -2026,7 +2050,10 @@ int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count)
       c.halo(a);
     };
     switch (field) {
-      case PUCFEM_F_U: own2(c.ux, c.uy); break;
+      case PUCFEM_F_U:
+        own2(c.ux, c.uy);
+        c.have_vinc = 0;  // a new state: no last viscous increment
+        break;
       case PUCFEM_F_USTAR: own2(c.usx, c.usy); break;
       case PUCFEM_F_SCALAR: own1(c.scalar); break;
       case PUCFEM_F_C: {
@@ -2358,8 +2385,9 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
       }
       HIPCHK(hipMemcpyAsync(c.ux, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
       HIPCHK(hipMemcpyAsync(c.uy, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      c.have_vinc = 0;  // u now holds this solve's right-hand side
       hipLaunchKernelGGL(k_visc_prep, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, c.ux, c.uy, c.bvx,
-                         c.bvy, c.yvx, c.yvy);
+                         c.bvy, c.yvx, c.yvy, VincDev{});
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
       const double* bb[2] = {c.bvx, c.bvy};

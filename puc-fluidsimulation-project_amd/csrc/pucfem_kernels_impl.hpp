@@ -419,14 +419,46 @@ __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const 
 }
 
 // viscous preparation: b^ = S u (rhs), y0 = S^-1 u (warm start x0 = u^n), StokesColor.py:540-545
+// warm start u^n + a polynomial extrapolation of the viscous increment u* - u from the last steps
+// (it changes smoothly from step to step): d = (d_1x, d_1y, d_2x, ...) the last `order` increments,
+// newest first; u^n + d_1 (order 1), + 2 d_1 - d_2 (2), + 3 d_1 - 3 d_2 + d_3 (3)
+struct VincDev {
+  const double* d[6];
+  int order;
+};
 __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
-                            const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy) {
+                            const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy,
+                            VincDev D) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
     bx[i] = s[i] * a;
     by[i] = s[i] * b;
-    yx[i] = sq[i] * a;
-    yy[i] = sq[i] * b;
+    double ga = a, gb = b;
+    if (D.order == 1) {
+      ga += D.d[0][i];
+      gb += D.d[1][i];
+    } else if (D.order == 2) {
+      ga += 2.0 * D.d[0][i] - D.d[2][i];
+      gb += 2.0 * D.d[1][i] - D.d[3][i];
+    } else if (D.order == 3) {
+      ga += 3.0 * (D.d[0][i] - D.d[2][i]) + D.d[4][i];
+      gb += 3.0 * (D.d[1][i] - D.d[3][i]) + D.d[5][i];
+    }
+    yx[i] = sq[i] * ga;
+    yy[i] = sq[i] * gb;
+  }
+}
+// u* = S y (both components) and the increment u* - u for the next step's warm start
+__global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double* __restrict__ yx,
+                           const double* __restrict__ yy, const double* __restrict__ ux, const double* __restrict__ uy,
+                           double* __restrict__ usx, double* __restrict__ usy, double* __restrict__ dx,
+                           double* __restrict__ dy) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    const double a = s[i] * yx[i], b = s[i] * yy[i];
+    usx[i] = a;
+    usy[i] = b;
+    dx[i] = a - ux[i];
+    dy[i] = b - uy[i];
   }
 }
 
