@@ -78,10 +78,12 @@ typedef struct pucfem_params {
                           (arithmetic stays fp32), 1 = all stored in fp32, 2 = the finest in fp32 and
                           the coarser levels in fp16 */
   int32_t idx32;       /* 0 = int16 column deltas for square operators whose band fits, 1 = int32 columns */
-  int32_t proj_k;      /* pressure solves (multigrid path): initial guess = A-orthogonal projection onto the
-                          last proj_k solution directions of the same solve (Fischer 1998; <= 32, 0 = off,
-                          warm start from the previous solution) */
-  int32_t proj_k_visc; /* the same for the two components of the viscous solve (0 = off: warm start u^n) */
+  int32_t proj_k;      /* pressure solves (multigrid path): initial guess = A-orthogonal projection onto a
+                          basis of up to proj_k directions spanning the recent solutions of the same solve
+                          (Fischer 1998, deferred basis update, re-seeded when full; 3..32, 0 = off: warm
+                          start from the previous solution) */
+  int32_t proj_k_visc; /* the same for the two components of the viscous solve (0 = off: warm start u^n
+                          plus an extrapolation of the last viscous increments) */
   int32_t mg_kind;     /* smoother polynomial: 0/1 = Chebyshev (first kind) on [lmax / mg_ratio, lmax],
                           4 = Chebyshev of the fourth kind on [0, lmax] (Lottes 2022; no mg_ratio) */
 } pucfem_params;

@@ -263,6 +263,22 @@ def test_mg_pressure_solve_matches_oracle(golden, single):
     sim.close()
 
 
+def test_viscous_extrapolated_start_same_steps(monkeypatch):
+    """The viscous CG starts from u^n plus a third-order extrapolation of the last viscous increments
+    instead of u^n: only the start changes, so 16 steps equal the plain warm-started run to the CG
+    tolerance (rtol 1e-12), with fewer viscous iterations once three increments exist."""
+    mesh = pf.load_mesh("fine", refine=2)
+    a = stokes(mesh)
+    monkeypatch.setenv("PUCFEM_VISC_EXTRAP", "0")  # read when a context is created
+    b = stokes(mesh)
+    sa, sb = a.step(16), b.step(16)
+    assert np.abs(a.u - b.u).max() < 1e-9
+    assert np.abs(a.c - b.c).max() < 1e-9
+    assert sum(x.it_visc for x in sa[4:]) < sum(x.it_visc for x in sb[4:])
+    a.close()
+    b.close()
+
+
 def test_projected_pressure_guess_same_steps():
     """Successive-RHS projection (Fischer) only changes the pressure CG's initial guess: 24 steps with
     a 3-vector basis (several restarts) equal the warm-started run to the CG tolerance, and once the
