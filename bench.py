@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--level", type=int, default=7, help="red refinements of mesh_fine (7 -> 14.2M nodes)")
-    ap.add_argument("--rtol-pres", type=float, default=1e-8)
+    ap.add_argument("--rtol-pres", type=float, default=None,
+                    help="pressure CG rtol (default: Tolerances.production(), checked by tests/test_gpu_production.py)")
     ap.add_argument("--mg-double", action="store_true", help="fp64 V-cycle instead of the fp32 one")
     ap.add_argument("--mg-vals", default="f32", choices=["f16", "f32", "coarse-f16"],
                     help="fp32 V-cycle operator storage: fp16 on every level, fp32, or fp16 below the finest level")
@@ -102,10 +103,15 @@ def main():
 
     t_setup = time.time()
     mesh = pf.load_mesh("fine", refine=a.level)
-    tol = pf.Tolerances(rtol_visc=1e-12, rtol_pres=a.rtol_pres, precond=a.precond, mg_single=not a.mg_double,
-                        mg_f16_vals={"f16": True, "f32": False, "coarse-f16": "coarse"}[a.mg_vals],
-                        index16=not a.index32, mg_degree=a.mg_pre, mg_post=a.mg_post, mg_ratio=a.mg_ratio,
-                        mg_kind=a.mg_kind, proj_k=a.proj_k, proj_k_visc=a.proj_k_visc)
+    # the production settings (the configuration tests/test_gpu_production.py checks against the
+    # oracle), with the measurement knobs below overriding single fields
+    tol = pf.Tolerances.production(precond=a.precond, mg_single=not a.mg_double,
+                                   mg_f16_vals={"f16": True, "f32": False, "coarse-f16": "coarse"}[a.mg_vals],
+                                   index16=not a.index32, mg_degree=a.mg_pre, mg_post=a.mg_post, mg_ratio=a.mg_ratio,
+                                   mg_kind=a.mg_kind, proj_k=a.proj_k, proj_k_visc=a.proj_k_visc)
+    if a.rtol_pres is not None:
+        tol.rtol_pres = a.rtol_pres
+    a.rtol_pres = tol.rtol_pres
     sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", device=local, tol=tol, dist=dist)
     info = sim.ctx.info()
     t_setup = time.time() - t_setup

@@ -86,6 +86,8 @@ typedef struct pucfem_params {
                           plus an extrapolation of the last viscous increments) */
   int32_t mg_kind;     /* smoother polynomial: 0/1 = Chebyshev (first kind) on [lmax / mg_ratio, lmax],
                           4 = Chebyshev of the fourth kind on [0, lmax] (Lottes 2022; no mg_ratio) */
+  int32_t solver_path; /* 0 = auto; 1 = multi-kernel iterative solves on every mesh (no dense inverses and no
+                          one-workgroup CG on small meshes: the large-mesh code path, for parity tests) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -209,6 +211,12 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
    [10]=storage flags (bit 0: P has int16 columns, bit 1: Pp has int16 columns, bit 2: the finest
    V-cycle operator is stored in fp16), [11]=multigrid levels (0: none) */
 int pucfem_info(void* ctx, int64_t* out12);
+/* which code path the step runs (for tests of the production path): out[0] viscous solve (0 dense inverse,
+   1 one-workgroup CG, 2 multi-kernel CG), [1] pressure solve (0 dense, 1 one-workgroup CG, 2 multi-kernel
+   Jacobi CG, 3 multigrid-preconditioned CG), [2] projection bases re-seeded so far, [3] / [4] current
+   basis sizes of the two pressure solves, [5] extrapolation order of the viscous warm start in use,
+   [6] projection basis capacity (0: off), [7] reserved */
+int pucfem_path_info(void* ctx, int64_t* out8);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

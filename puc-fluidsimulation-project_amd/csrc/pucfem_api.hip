@@ -302,7 +302,11 @@ struct Ctx {
   int32_t* dnotfound = nullptr;
   int32_t ntr = 0;
   double *trx = nullptr, *try_ = nullptr, *trs = nullptr, *d_eaten = nullptr;
-  int last_it[3] = {0, 0, 0};
+  // iteration count of the last solve per `which` slot (the next solve's first host check): 0 viscous,
+  // 1 / 2 the two pressure solves of a step, 3 / 4 standalone viscous / pressure solves (pucfem_solve)
+  int last_it[6] = {0, 0, 0, 0, 0, 0};
+  bool lds_attr[3] = {false, false, false};  // k_cg_block<NR>: dynamic-LDS attribute set on this device
+  double* solve_tmp = nullptr;  // pucfem_solve scratch (4 x nloc): standalone solves never touch the step state
   int* dits = nullptr;  // per-step iteration counts written by single-workgroup solves (no host sync)
   int cur_step = 0;
   bool block_cg = true;  // small operators: whole CG in one workgroup
@@ -505,11 +509,12 @@ struct Ctx {
       const size_t mat = (size_t)A.padded * (sizeof(double) + sizeof(int32_t));
       const bool mat_lds = vec + mat <= (size_t)150 * 1024;
       const size_t lds = vec + (mat_lds ? mat : 0);
-      static bool attr[3] = {false, false, false};
-      if (!attr[NR]) {
+      // the attribute is per device and function: set it once per context (a context is bound to one
+      // device; a second context on the same device sets it again, which is harmless)
+      if (!lds_attr[NR]) {
         HIPCHK(hipFuncSetAttribute((const void*)k_cg_block<NR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    150 * 1024));
-        attr[NR] = true;
+        lds_attr[NR] = true;
       }
       int* slot = dits ? dits + 3 * cur_step + which : nullptr;
       hipLaunchKernelGGL((k_cg_block<NR>), dim3(1), dim3(CGB_THREADS), lds, st, A.view(), val, y[0],
@@ -982,8 +987,10 @@ struct Ctx {
   // seeds within 1e-6 of the span of the earlier ones add only their coordinates' noise.  Fischer's
   // restart (drop everything) costs a run of solves of 7, 5, 4, 3 iterations where the full basis
   // gives 1-2.  Returns the new basis size (<= kmax - 1).
+  int64_t n_reseed = 0;  // full bases re-seeded so far (pucfem_path_info)
   int proj_reseed(int which, int m, QMat& qm) {
     ProjHist& H = proj_hist[which];
+    ++n_reseed;
     const int cap = std::min(proj_keep, m - 1);
     std::vector<std::vector<double>> seeds;
     const int nh = std::min<int>((int)H.sols.size(), cap - 1);
@@ -1591,7 +1598,8 @@ void build(Ctx& c) {
       c.dAinv = c.upload(D);
     }
   }
-  c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1;
+  c.block_cg = c.prm.solver_path != 1;
+  c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1 && c.prm.solver_path != 1;
   // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
   // small meshes need no better start)
   // (a basis needs room for the re-seeded span and one new direction: at least 3)
@@ -2376,6 +2384,10 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
     require(c.world == 1, "pucfem_solve is single-rank");
     const i64 N = c.mesh.N;
     int it = 0;
+    // standalone solves run on scratch buffers with their own iteration-hint slots (3, 4) and no
+    // projection basis: a context that is stepping keeps u, p, the warm starts and the bases intact
+    if (!c.solve_tmp) c.solve_tmp = c.dalloc<double>(4 * c.nloc);
+    double *s0 = c.solve_tmp, *s1 = s0 + c.nloc, *s2 = s1 + c.nloc, *s3 = s2 + c.nloc;
     if (op == PUCFEM_OP_VISC) {
       // rhs = b (as u^n, initial guess b): the viscous CG without BCs
       std::vector<double> bx(N), by(N);
@@ -2383,30 +2395,29 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
         bx[g] = b[2 * c.ord.new2old[g]];
         by[g] = b[2 * c.ord.new2old[g] + 1];
       }
-      HIPCHK(hipMemcpyAsync(c.ux, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-      HIPCHK(hipMemcpyAsync(c.uy, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-      c.have_vinc = 0;  // u now holds this solve's right-hand side
-      hipLaunchKernelGGL(k_visc_prep, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, c.ux, c.uy, c.bvx,
+      HIPCHK(hipMemcpyAsync(s0, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipMemcpyAsync(s1, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+      hipLaunchKernelGGL(k_visc_prep, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s1, c.bvx,
                          c.bvy, c.yvx, c.yvy, VincDev{});
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
       const double* bb[2] = {c.bvx, c.bvy};
-      it = c.cg<2>(c.dP, c.dKv, y, bb, rtol, maxit, 0);
-      hipLaunchKernelGGL(k_cg_fin, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, 2, c.dsv, c.yvx, c.yvy, c.usx, c.usy,
+      it = c.cg<2>(c.dP, c.dKv, y, bb, rtol, maxit, 3);
+      hipLaunchKernelGGL(k_cg_fin, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, 2, c.dsv, c.yvx, c.yvy, s2, s3,
                          (const int32_t*)nullptr);
       KCHK();
       std::vector<double> ox(N), oy(N);
-      HIPCHK(hipMemcpyAsync(ox.data(), c.usx, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
-      HIPCHK(hipMemcpyAsync(oy.data(), c.usy, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(ox.data(), s2, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(oy.data(), s3, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
       for (i64 g = 0; g < N; ++g) {
         x[2 * c.ord.new2old[g]] = ox[g];
         x[2 * c.ord.new2old[g] + 1] = oy[g];
       }
     } else if (op == PUCFEM_OP_PRES) {
-      require(c.dKp, "no pressure operator");
-      // b = b_p: braw = (M + 1e-12) * b_p, then the same path as the step
-      std::vector<double> mp(N), bp(N), br(N);
+      require(c.dKp || c.dKp_raw, "no pressure operator");
+      // b = b_p: braw = (M + 1e-12) * b_p, then the same path as the step (slot 4: no projection)
+      std::vector<double> mp(N), br(N);
       HIPCHK(hipMemcpyAsync(mp.data(), c.dmp, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
       double sum = 0.0;
@@ -2419,19 +2430,19 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
       part[MAXB] = sum;
       HIPCHK(hipMemcpyAsync(c.part_d, part.data(), sizeof(double) * part.size(), hipMemcpyHostToDevice, c.st));
       // pressure() reduces part_d + MAXB over nb_for(dP) blocks: only entry 0 is non-zero
-      HIPCHK(hipMemsetAsync(c.yp, 0, sizeof(double) * c.nloc, c.st));
+      HIPCHK(hipMemsetAsync(s0, 0, sizeof(double) * c.nloc, c.st));
       pucfem_params save = c.prm;
       c.prm.rtol_pres = rtol;
       c.prm.maxit_pres = maxit;
       try {
-        it = c.pressure(c.yp, c.p, 1);
+        it = c.pressure(s0, s1, 4);
       } catch (...) {
         c.prm = save;
         throw;
       }
       c.prm = save;
       std::vector<double> o(N);
-      HIPCHK(hipMemcpyAsync(o.data(), c.p, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+      HIPCHK(hipMemcpyAsync(o.data(), s1, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
       for (i64 g = 0; g < N; ++g) x[c.ord.new2old[g]] = o[g];
     } else if (op == PUCFEM_OP_LIT) {
@@ -2604,6 +2615,24 @@ int pucfem_info(void* ctx, int64_t* o) {
     o[9] = (int64_t)c.dir_nodes.size();
     o[10] = (c.dP.c16 ? 1 : 0) | (c.dPp.c16 ? 2 : 0) | (!c.mg.empty() && c.mg.back().f32.Aval16 ? 4 : 0);
     o[11] = (int64_t)c.mg.size();
+  });
+}
+
+int pucfem_path_info(void* ctx, int64_t* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    for (int k = 0; k < 8; ++k) o[k] = 0;
+    const bool stokes = c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD;
+    if (!stokes) return;
+    const bool block = c.world == 1 && c.block_cg && c.lp.n_own <= (i64)CGB_THREADS * CGB_MAXR;
+    o[0] = c.dense ? 0 : (block ? 1 : 2);
+    o[1] = c.dense ? 0 : (c.use_mg ? 3 : (block ? 1 : 2));
+    o[2] = c.n_reseed;
+    o[3] = c.proj_m[1];
+    o[4] = c.proj_m[2];
+    o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
+    o[6] = c.proj_k;
   });
 }
 

@@ -117,7 +117,8 @@ struct LocalComm : Comm {
   std::shared_ptr<LocalShared> S;
   int rank, world;
   std::vector<LocalShared::Op> pending;
-  double* tmp = nullptr;  // reduction output, up to 64 values
+  static constexpr size_t MAXRED = 128;  // >= 2 * PROJ_MAX + 4 (the projection's multi-dot)
+  double* tmp = nullptr;  // reduction output, up to MAXRED values
   double** dptrs = nullptr;
 
   LocalComm(const std::string& key, int w, int r) : rank(r), world(w) {
@@ -133,7 +134,7 @@ struct LocalComm : Comm {
     if (S->world != w) throw std::runtime_error("LocalComm world mismatch");
     if (hipEventCreateWithFlags(&S->ready[r], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S->done[r], hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&tmp, 64 * sizeof(double)) != hipSuccess || hipMalloc(&dptrs, 64 * sizeof(double*)) != hipSuccess)
+        hipMalloc(&tmp, MAXRED * sizeof(double)) != hipSuccess || hipMalloc(&dptrs, 64 * sizeof(double*)) != hipSuccess)
       throw std::runtime_error("LocalComm: HIP allocation failed");
     S->barrier();  // every rank has created its events
   }
@@ -145,7 +146,8 @@ struct LocalComm : Comm {
     if (e != hipSuccess) throw std::runtime_error(std::string("LocalComm HIP: ") + hipGetErrorString(e));
   }
   void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) override {
-    if (n > 64) throw std::runtime_error("LocalComm allreduce supports <= 64 values");
+    if (n > MAXRED) throw std::runtime_error("LocalComm allreduce supports <= 128 values");
+    if (world > 64) throw std::runtime_error("LocalComm supports <= 64 ranks");
     chk(hipEventRecord(S->ready[rank], st));
     S->red[rank] = buf;
     S->barrier();

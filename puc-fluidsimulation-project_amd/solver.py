@@ -67,6 +67,25 @@ class Tolerances:
     mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
     proj_k: int = 24  # pressure initial guess: A-projection onto up to proj_k solution directions (0: warm start)
     proj_k_visc: int = 0  # the same for the viscous solve's two components (measured: no net gain at L7)
+    # "auto": small meshes (<= 1500 nodes, one rank) solve with precomputed dense inverses and meshes of
+    # <= 4096 nodes with a one-workgroup CG; "iterative": the large-mesh multi-kernel CG path on every mesh
+    solver_path: str = "auto"
+
+    @classmethod
+    def production(cls, **kw):
+        """The settings bench.py measures (and the production-path parity tests check): multigrid-
+        preconditioned pressure CG with the fp32 V-cycle, the 24-direction projected pressure guess,
+        int16 column deltas, the extrapolated viscous start, pressure rtol PRODUCTION_RTOL_PRES."""
+        base = dict(rtol_visc=1e-12, rtol_pres=PRODUCTION_RTOL_PRES, precond="mg", mg_single=True,
+                    mg_f16_vals=False, index16=True, mg_degree=2, mg_post=2, mg_ratio=10.0, mg_kind=1,
+                    proj_k=24, proj_k_visc=0)
+        base.update(kw)
+        return cls(**base)
+
+
+# pressure CG tolerance of the measured configuration (bench.py); tests/test_gpu_production.py checks
+# that it keeps every step within 1e-6 of the oracle's exact solves
+PRODUCTION_RTOL_PRES = 1e-8
 
 
 class Context:
@@ -138,7 +157,7 @@ class Context:
                         mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes,
                         mg_f32_vals=2 if tol.mg_f16_vals == "coarse" else int(not tol.mg_f16_vals),
                         idx32=int(not tol.index16), proj_k=tol.proj_k, proj_k_visc=tol.proj_k_visc,
-                        mg_kind=tol.mg_kind)
+                        mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path])
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
@@ -178,6 +197,15 @@ class Context:
         d["index16_P"], d["index16_Pp"], d["mg_f16_vals"] = bool(o[10] & 1), bool(o[10] & 2), bool(o[10] & 4)
         d["mg_levels"] = o[11]
         return d
+
+    def path_info(self):
+        """The code path of the step (pucfem_path_info)."""
+        o = (ct.c_int64 * 8)()
+        self._c(self.L.pucfem_path_info(self.h, o))
+        visc = {0: "dense", 1: "block", 2: "multi-kernel"}
+        pres = {0: "dense", 1: "block", 2: "jacobi-cg", 3: "mg-pcg"}
+        return dict(viscous=visc[o[0]], pressure=pres[o[1]], reseeds=o[2], basis_p=o[3], basis_p2=o[4],
+                    visc_extrap_order=o[5], proj_k=o[6])
 
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))
@@ -257,7 +285,9 @@ class StokesSimulation:
             from .tracers import tracer_init
 
             pts = tracer_init(self.bc.squirmer_radius, self.bc.center) if tracers is None else tracers
+            pts = np.asarray(pts, dtype=np.float64).reshape(-1, 2)
             self.ctx.set_field(_lib.F_TRACERS, pts)
+            self.n_tracers = len(pts)
 
     def step(self, n=1):
         st = self.ctx.step(n)
@@ -294,9 +324,7 @@ class StokesSimulation:
         return self.ctx.get_field(_lib.F_STATUS, (self._ntr(),)).astype(np.int64)
 
     def _ntr(self):
-        from .tracers import tracer_init
-
-        return len(tracer_init(self.bc.squirmer_radius, self.bc.center))
+        return getattr(self, "n_tracers", 0)
 
     def close(self):
         self.ctx.close()

@@ -1,0 +1,86 @@
+"""End-to-end outcomes of the reference's full runs, through the GPU path (SURVEY.md §8c contract iii).
+
+The reference's own 6000-step mesh.1 runs (captured by tests/golden/gen_golden.py into
+long_mesh1.npz) and its published food-capture outcomes (README.md:43-45, StokesFood.py:494-505:
+eaten 228 / 482 / 486 of 488 for the neutral / pusher / puller squirmer), and the mesh_fine
+5000-step StokesColor run of BASELINE configs[2] (mixing progress 0.443 @ step 99,
+0.977 @ 999, 0.969 @ 2999, 0.959 @ 4999).  The reference's pressure is rounding-determined (§0), so
+these are compared at its noise floor: progress +-0.01, eaten +-2 %.  (The oracle's CPU runs of the
+same restated formulation land on 228 / 482 / 486 exactly and within 7e-4 of the progress trace.)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, has_gpu, load_pkg
+
+pytestmark = pytest.mark.gpu
+
+pf = load_pkg()
+from importlib import import_module  # noqa: E402
+
+S = import_module("puc-fluidsimulation-project_amd.solver")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not has_gpu():
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+
+
+@pytest.fixture(scope="module")
+def long_ref():
+    return dict(np.load(os.path.join(GOLDEN, "long_mesh1.npz")))
+
+
+def progress_trace(mesh, steps, tol=None):
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol or S.Tolerances())
+    _, _, var0 = S._mixing0(mesh, sim)
+    st = sim.step(steps)
+    sim.close()
+    return np.array([1.0 - s.mix_var / (var0 + 1e-16) for s in st]), st
+
+
+def test_color_mesh1_6000_steps_progress_trace(long_ref):
+    """StokesColor.py (mesh.1, 6000 steps): mixing progress within 0.01 of the reference's printed
+    trace at every 100th step (StokesColor.py:583-586), max div(u*) within 2 % at every step."""
+    mesh = pf.load_mesh("mesh1")
+    prog, st = progress_trace(mesh, 6000)
+    ref = long_ref["color_mesh1_progress"]
+    d = np.abs(prog - ref)
+    assert d[99::100].max() < 0.01, d[99::100].max()
+    assert d.max() < 0.01
+    assert abs(prog[-1] - 0.955) < 0.01
+    ds = np.array([s.max_div_star for s in st])
+    rd = long_ref["color_mesh1_divstar"]
+    # printed with 3 significant digits ("%.2e", StokesColor.py:586): 2 % per step
+    assert (np.abs(ds - rd) <= 0.02 * rd).all(), (np.abs(ds - rd) / rd).max()
+
+
+@pytest.mark.parametrize("name,B2,eaten", [("neutral", 0.0, 228), ("pusher", -5.0, 482), ("puller", 5.0, 486)])
+def test_food_mesh1_6000_steps_eaten(long_ref, name, B2, eaten):
+    """StokesFood.py (mesh.1, nu=1, DT=0.01, 6000 steps): eaten count within 2 % of the reference's
+    228 / 482 / 486 (README.md:43-45) and of its trace along the run."""
+    mesh = pf.load_mesh("mesh1")
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(B2=B2, nu=1.0), 0.01, "food", 0)
+    st = sim.step(6000)
+    e = np.array([s.eaten for s in st])
+    status = sim.tracer_status
+    sim.close()
+    assert abs(e[-1] - eaten) <= 0.02 * eaten, (e[-1], eaten)
+    assert e[-1] == status.sum()
+    assert np.all(np.diff(e) >= 0)  # capture is sticky
+    ref = long_ref[f"food_mesh1_{name}_eaten"]
+    assert np.abs(e - ref).max() <= max(3, 0.02 * eaten), np.abs(e - ref).max()
+
+
+def test_color_mesh_fine_5000_steps_config2():
+    """BASELINE configs[2]: StokesColor neutral squirmer on mesh_fine, 5000 steps."""
+    mesh = pf.load_mesh("fine")
+    prog, st = progress_trace(mesh, 5000)
+    for step, val in ((99, 0.443), (999, 0.977), (2999, 0.969), (4999, 0.959)):
+        assert abs(prog[step] - val) < 0.01, (step, prog[step], val)
+    # the printed max|div u*| and max|final div| of the last step (11.5 and 11.6)
+    assert abs(st[-1].max_div_star - 11.5) < 0.05 * 11.5
+    assert abs(st[-1].max_final_div - 11.6) < 0.05 * 11.6

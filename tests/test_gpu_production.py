@@ -1,0 +1,145 @@
+"""Parity of the PRODUCTION (large-mesh) code path against the oracle, step by step.
+
+bench.py measures Tolerances.production(): the multi-kernel Jacobi-scaled viscous CG<2> with the
+extrapolated warm start, the multigrid-preconditioned pressure CG with the fp32 V-cycle, the
+24-direction projected pressure guess (re-seeded when full), int16 SELL column deltas and the
+locate-then-rank semi-Lagrangian kernel.  mesh_fine itself takes the small-mesh direct path, so these
+tests run refined meshes (L2 = 17k, L3 = 69k nodes) where none of the small-mesh shortcuts apply, and
+compare against oracle.StokesRef (exact sparse solves of the same pressure restatement) along
+independent trajectories: contract (ii) of SURVEY.md §8c, |u - u_oracle| < 1e-6 and
+|c - c_oracle| < 1e-6 at every step.  A solver_path knob forces the same multi-kernel solvers on
+mesh_fine / mesh.1 so the large-mesh kernels are also checked against the reference's own goldens.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import has_gpu, load_pkg
+
+pytestmark = pytest.mark.gpu
+
+pf = load_pkg()
+from importlib import import_module  # noqa: E402
+
+L = import_module("puc-fluidsimulation-project_amd._lib")
+S = import_module("puc-fluidsimulation-project_amd.solver")
+
+TOL_STEP = 1e-6  # north_star: < 1e-6 per Stokes step vs the reference formulation
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not has_gpu():
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+
+
+def test_production_color_L3_every_step_vs_oracle():
+    """48 StokesColor steps on mesh_fine x3 (69,632 nodes) with the bench's exact settings: the
+    projection bases fill (24 directions per pressure solve) and are re-seeded at least twice."""
+    mesh = pf.load_mesh("fine", refine=3)
+    tol = S.Tolerances.production()
+    assert tol.rtol_pres == S.PRODUCTION_RTOL_PRES
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    info = sim.ctx.info()
+    assert info["mg_levels"] == 4 and info["index16_P"] and info["index16_Pp"], info
+    ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.05, 0.1, -2.0, 0.0, "color")
+    u, c = ref.initial()
+    worst_u = worst_c = 0.0
+    for k in range(48):
+        st = sim.step(1)[0]
+        out = ref.step(u, c)
+        u, c = out["u"], out["c"]
+        du = np.abs(sim.u - u).max()
+        dc = np.abs(sim.c - c).max()
+        worst_u, worst_c = max(worst_u, du), max(worst_c, dc)
+        assert du < TOL_STEP and dc < TOL_STEP, (k, du, dc)
+        assert abs(st.max_div_star - np.abs(out["div_u_star"]).max()) <= 1e-6 * np.abs(out["div_u_star"]).max(), k
+        assert abs(st.mix_var - out["mixing"][2]) < 1e-9, k
+    path = sim.ctx.path_info()
+    assert path["viscous"] == "multi-kernel" and path["pressure"] == "mg-pcg", path
+    assert path["proj_k"] == 24 and path["reseeds"] >= 2, path
+    assert path["visc_extrap_order"] == 3, path
+    print(f"L3 production path, 48 steps: max |u - oracle| = {worst_u:.2e}, max |c - oracle| = {worst_c:.2e}")
+    sim.close()
+
+
+def test_production_food_pusher_L2_vs_oracle():
+    """StokesFood pusher (B1=-2, B2=-5, nu=1, DT=0.01) on mesh_fine x2 (17,536 nodes), production
+    settings, 30 steps: velocity, tracer positions, NaN mask and capture status against the oracle."""
+    mesh = pf.load_mesh("fine", refine=2)
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(B2=-5.0, nu=1.0), 0.01, "food", 0, S.Tolerances.production())
+    ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.01, 1.0, -2.0, -5.0, "food")
+    u, _ = ref.initial()
+    pts = O.tracer_init()
+    status = np.zeros(len(pts), dtype=int)
+    for k in range(30):
+        st = sim.step(1)[0]
+        out = ref.step(u, tracers=pts, status=status)
+        u, pts, status = out["u"], out["tracers"], out["status"]
+        assert np.abs(sim.u - u).max() < TOL_STEP, k
+        got = sim.tracers
+        assert np.array_equal(np.isnan(got), np.isnan(pts)), k
+        ok = ~np.isnan(pts)
+        assert np.abs(got[ok] - pts[ok]).max() < TOL_STEP, k
+        assert np.array_equal(sim.tracer_status, status), k
+        assert st.eaten == status.sum()
+    assert sim.ctx.path_info()["pressure"] == "mg-pcg"
+    sim.close()
+
+
+@pytest.mark.parametrize("m", ["mesh1", "fine"])
+def test_forced_multikernel_path_vs_goldens(m, golden):
+    """The large-mesh solvers (multi-kernel Jacobi CG for both solves) forced onto the reference's own
+    meshes: 3 steps against the oracle (<= 1e-6) and the literal reference (its 1e-2 noise floor)."""
+    g = golden(m)
+    mesh = pf.load_mesh(m)
+    tol = S.Tolerances(rtol_visc=1e-14, rtol_pres=1e-13, solver_path="iterative")
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    path = sim.ctx.path_info()
+    assert path["viscous"] == "multi-kernel" and path["pressure"] == "jacobi-cg", path
+    ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.05, 0.1, -2.0, 0.0, "color")
+    u, c = ref.initial()
+    for k in range(3):
+        st = sim.step(1)[0]
+        out = ref.step(u, c)
+        u, c = out["u"], out["c"]
+        assert np.abs(sim.u - u).max() < TOL_STEP, k
+        assert np.abs(sim.c - c).max() < TOL_STEP, k
+        if k == 0:  # same u^n as the reference: u* = A_visc^-1 u^n is comparable to its LU solve
+            np.testing.assert_allclose(sim.field(L.F_USTAR, 2), g["color_s0_u_star"], rtol=0, atol=1e-10)
+        assert np.abs(sim.u - g[f"color_s{k}_u"]).max() < 1e-2
+        assert st.it_p > 0 and (k == 0 or st.it_visc > 0)
+    sim.close()
+
+
+def test_standalone_solves_leave_the_step_state_alone():
+    """pucfem_solve on a context that is stepping runs on scratch buffers: u, p, the warm starts and
+    the projection bases are untouched, so the next steps equal those of an undisturbed run."""
+    mesh = pf.load_mesh("fine", refine=2)
+    tol = S.Tolerances.production()
+    a = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    b = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    a.step(6)
+    b.step(6)
+    rng = np.random.default_rng(5)
+    u_before, p_before = b.u, b.field(L.F_P)
+    b.ctx.solve(L.OP_VISC, rng.standard_normal((mesh.N, 2)), rtol=1e-12)
+    b.ctx.solve(L.OP_PRES, rng.standard_normal(mesh.N), rtol=1e-10)
+    np.testing.assert_array_equal(b.u, u_before)
+    np.testing.assert_array_equal(b.field(L.F_P), p_before)
+    sa, sb = a.step(4), b.step(4)
+    np.testing.assert_array_equal(a.u, b.u)
+    assert [(x.it_visc, x.it_p, x.it_p2) for x in sa] == [(x.it_visc, x.it_p, x.it_p2) for x in sb]
+    a.close()
+    b.close()
+
+
+def test_custom_tracers_shape():
+    """StokesSimulation(tracers=...) reports the given tracer count through the getters."""
+    mesh = pf.load_mesh("fine")
+    pts = np.array([[0.1, 0.1], [0.9, 0.2], [0.3, 0.8]])
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(nu=1.0), 0.01, "food", 0, tracers=pts)
+    assert sim.tracers.shape == (3, 2) and sim.tracer_status.shape == (3,)
+    sim.step(2)
+    assert sim.tracers.shape == (3, 2)
+    sim.close()
