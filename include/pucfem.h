@@ -88,6 +88,10 @@ typedef struct pucfem_params {
                           4 = Chebyshev of the fourth kind on [0, lmax] (Lottes 2022; no mg_ratio) */
   int32_t solver_path; /* 0 = auto; 1 = multi-kernel iterative solves on every mesh (no dense inverses and no
                           one-workgroup CG on small meshes: the large-mesh code path, for parity tests) */
+  int32_t assembled;   /* 0 = auto: with a multigrid hierarchy of >= 2 levels, the rows of nodes inside the
+                          coarse mesh's triangles are matrix-free lattice stencils (per-face constants) and only
+                          the nodes on coarse edges / vertices keep stored SELL rows; 1 = stored SELL operators
+                          for every row */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -215,7 +219,8 @@ int pucfem_info(void* ctx, int64_t* out12);
    1 one-workgroup CG, 2 multi-kernel CG), [1] pressure solve (0 dense, 1 one-workgroup CG, 2 multi-kernel
    Jacobi CG, 3 multigrid-preconditioned CG), [2] projection bases re-seeded so far, [3] / [4] current
    basis sizes of the two pressure solves, [5] extrapolation order of the viscous warm start in use,
-   [6] projection basis capacity (0: off), [7] reserved */
+   [6] projection basis capacity (0: off), [7] 1 when the operators are lattice stencils on the face
+   interiors (pucfem_params.assembled = 0 with a hierarchy), 0 when every row is a stored SELL row */
 int pucfem_path_info(void* ctx, int64_t* out8);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
@@ -227,6 +232,13 @@ int pucfem_refine(int64_t n_nodes, const double* xy, const int32_t* markers, int
    global column ids).  Call with col == NULL to get nnz.  For CPU tests of the assembly. */
 int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, int64_t* rowptr,
                         int64_t* col, double* val);
+/* Host reference of the lattice face stencils (CPU tests of the index arithmetic and the per-face
+   coefficients; single-rank contexts with lattice operators).  Rows of face-interior nodes of the output
+   level are written, every other entry of y is NaN.  kind 0: K x, 1: Gx x0 + Gy x1 (x is (N, 2), the
+   divergence numerator), 2: S A_visc S x, 3: the level's periodic-merged pressure operator (any level),
+   5: prolongation from level-1 into level (x on level-1), 6: restriction from level into level-1.
+   Vectors in the caller numbering of their level (level = the multigrid level, 0 = the coarse mesh). */
+int pucfem_host_lattice_apply(void* ctx, int32_t level, int32_t kind, const double* x, double* y);
 /* Partition plan for (rank, world) computed on a host-only context (pucfem_ctx_create(-1)):
    owned rows (caller numbering) in internal order, then the ghost ids; send lists per peer.
    Sizes first (arrays NULL), then contents. */

@@ -38,7 +38,7 @@ class Params(ct.Structure):
         ("mg_degree", ct.c_int32), ("mg_ratio", ct.c_double), ("mg_post", ct.c_int32),
         ("mg_single", ct.c_int32), ("mg_rep_nodes", ct.c_int64), ("mg_f32_vals", ct.c_int32),
         ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("proj_k_visc", ct.c_int32), ("mg_kind", ct.c_int32),
-        ("solver_path", ct.c_int32),
+        ("solver_path", ct.c_int32), ("assembled", ct.c_int32),
     ]
 
 
@@ -88,6 +88,7 @@ SIGNATURES = {
     "pucfem_path_info": ([_P, _I64], ct.c_int),
     "pucfem_refine": ([ct.c_int64, _D, _I32, ct.c_int64, _I32, ct.c_int32, _I64, _I64, _D, _I32, _I32], ct.c_int),
     "pucfem_host_get_csr": ([_P, ct.c_int32, _I64, _I64, _I64, _I64, _D], ct.c_int),
+    "pucfem_host_lattice_apply": ([_P, ct.c_int32, ct.c_int32, _D, _D], ct.c_int),
     "pucfem_host_partition": ([_P, ct.c_int32, ct.c_int32, _I64, _I64, _I64, _I64, _I32, _I64, _I64, _I32], ct.c_int),
 }
 

@@ -69,8 +69,32 @@ struct DevSell {
   int16_t* c16 = nullptr;  // int16 column deltas (square operators whose band fits), else null
   int64_t nslices = 0, nrows = 0, nnz = 0, padded = 0;
   int32_t wrap = 0;        // c16 modulus (local vector length)
-  SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16, wrap}; }
+  int32_t* rows = nullptr; // row list (lattice operators: the skeleton rows), else null
+  int64_t n_own = 0;       // owned rows of the vector space (0: nrows)
+  SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16, wrap, rows, n_own ? n_own : nrows}; }
   double idx_bytes() const { return c16 ? 2.0 : 4.0; }  // per stored entry
+  double row_bytes() const { return rows ? 4.0 : 0.0; }  // per row (the row list)
+  int64_t own() const { return n_own ? n_own : nrows; }   // rows of the vector space
+};
+
+// A lattice operator's face part on the host (pucfem_lattice.hpp): the FaceDev image and its work
+// items.  Partial-producing launches cap the face blocks (the partial arrays hold MAXB blocks in all),
+// the others give every item a block.
+constexpr int32_t FACE_PART_BLOCKS = 4096;
+struct HFace {
+  FaceDev d{};
+  int32_t items = 0;
+  int64_t rows = 0;  // face-interior rows (algorithmic bytes)
+  FaceDev part() const {
+    FaceDev f = d;
+    f.nb = std::min(items, FACE_PART_BLOCKS);
+    return f;
+  }
+  FaceDev full() const {
+    FaceDev f = d;
+    f.nb = items;
+    return f;
+  }
 };
 // f(std::true_type) when A carries int16 columns, f(std::false_type) otherwise: one launch site
 // instantiates both SpMV variants
@@ -182,12 +206,22 @@ struct MgLevel {
   bool rep = false;
   i64 r_r0 = 0;  // first row of this level's restriction operator (rows live on level l-1)
   i64 own0(int rank) const { return rep ? 0 : rs[rank]; }
+  // lattice face parts (Ctx::lattice): the faces whose interiors are this rank's rows of this level,
+  // their tables (plain: K / G / A_visc; merged: the periodic-merged pressure operator) and records;
+  // the prolongation into this level gathers the same faces on level l-1 (pr_tab2, merged), the
+  // restriction into level l-1 writes the faces of its rows [r_r0, r_r0 + nr) (r_tab, bases from
+  // r_r0) from this level's nodes (r_tab2, plain)
+  LatticeLevel latl;
+  std::vector<i32> lf_faces, r_faces;
+  std::vector<lat::FaceTab> lf_plain, lf_merged, pr_tab2, r_tab, r_tab2;
+  std::vector<double> lf_coef;
+  HFace hA, hPr, hR;  // level operator (merged), prolongation into / restriction from this level
 };
 template <typename T> MgBufs<T>& bufs(MgLevel& L);
 template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
-void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y);
+void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* val, const double* x, double* y);
 // k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size
 template <int M>
 void mdot2_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* b, const double* av,
@@ -320,6 +354,14 @@ struct Ctx {
   hipGraph_t graph = nullptr;
   double* gstats = nullptr;
 
+  // ---- lattice operators (pucfem_lattice.hpp): multigrid hierarchies with faces of interior nodes
+  bool lattice = false;
+  Macro macro;
+  LatticeLevel lat_fine;  // the finest level's layout until build_mg_host moves it into mg.back()
+  HFace fK, fVisc, fP;  // finest level: K / Gx / Gy (plain table), scaled A_visc (plain), pressure (merged)
+  double* dwsk = nullptr;  // scaled A_visc skeleton column weights
+  static FaceDev nof() { return FaceDev{}; }
+
   // ---- multigrid
   HostMesh coarse;
   int mg_levels = 0;  // refinements from `coarse` to `mesh` (0: no hierarchy given)
@@ -370,9 +412,11 @@ struct Ctx {
     const double* val;
     const int32_t* null_free;  // master_of (free rows: < 0) when the operator has the constants' null space
     int kmax;
+    FaceDev fc;
   };
   ProjOp proj_op(int which) const {
-    return which <= 2 ? ProjOp{&dPp, dKp_raw, dmaster_of, proj_k} : ProjOp{&dP, dKv, nullptr, proj_k_visc};
+    return which <= 2 ? ProjOp{&dPp, dKp_raw, dmaster_of, proj_k, fP.full()}
+                      : ProjOp{&dP, dKv, nullptr, proj_k_visc, fVisc.full()};
   }
   float* r32 = nullptr;             // fp32 copy of the CG residual: the fp32 V-cycle's right-hand side
 
@@ -408,6 +452,7 @@ struct Ctx {
   // int16 column deltas for a square operator's SELL (prm.idx32 = 0 and the band fits); nloc: the
   // local vector length (owned + ghost), the wrap modulus
   void attach_c16(const Sell& S, i64 nloc, DevSell& D) {
+    if (!S.rows.empty()) return;  // row lists (lattice skeleton rows): int32 columns
     std::vector<int16_t> c16;
     if (!prm.idx32 && sell_col16(S, nloc, c16)) {
       D.c16 = upload(c16);
@@ -502,9 +547,9 @@ struct Ctx {
 
   // ------------------------------------------------------------------ CG
   template <int NR>
-  int cg(const DevSell& A, const double* val, double* const y[NR], const double* const b[NR], double tol,
-         int maxit, int which) {
-    if (world == 1 && block_cg && A.nrows <= (int64_t)CGB_THREADS * CGB_MAXR) {
+  int cg(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
+         double tol, int maxit, int which) {
+    if (world == 1 && block_cg && !hf.items && A.nrows <= (int64_t)CGB_THREADS * CGB_MAXR) {
       const size_t vec = (size_t)NR * A.nrows * sizeof(double);
       const size_t mat = (size_t)A.padded * (sizeof(double) + sizeof(int32_t));
       const bool mat_lds = vec + mat <= (size_t)150 * 1024;
@@ -528,7 +573,8 @@ struct Ctx {
       if (h_ctl[0] != 1) throw Error(PUCFEM_ENOCONV, "CG did not converge within maxit=" + std::to_string(maxit));
       return h_ctl[1];
     }
-    const int nb = nb_for(A.nslices);
+    const FaceDev fc = hf.part();
+    const int nb = fc.nb + std::min(nb_for(A.nslices), MAXB - fc.nb);
     CgVecs<NR> v;
     for (int c = 0; c < NR; ++c) {
       v.y[c] = y[c];
@@ -541,8 +587,8 @@ struct Ctx {
     if (NR == 2) halo(y[0], y[1]);
     else halo(y[0]);
     with_c16(A, [&](auto c16) {
-      hipLaunchKernelGGL((k_cg_init<NR, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), val, v, lp.n_ghost,
-                         part_a, part_b);
+      hipLaunchKernelGGL((k_cg_init<NR, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), fc, val, v,
+                         lp.n_ghost, part_a, part_b);
     });
     KCHK();
     Red rr = reduce_global(part_a, nb, NR, false, 0);
@@ -551,8 +597,9 @@ struct Ctx {
     if (NR == 2) halo(cg_r[0], cg_r[1]);
     else halo(cg_r[0]);
     const double tol2 = tol * tol;
-    const double bytes_dir = (8.0 + A.idx_bytes()) * (double)A.nnz + 32.0 * NR * (double)A.nrows;
-    const double bytes_upd = 48.0 * NR * (double)A.nrows;
+    const double bytes_dir =
+        (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 32.0 * NR * (double)A.own();
+    const double bytes_upd = 48.0 * NR * (double)A.own();
     int it = 0;
     // host convergence checks: the first after as many iterations as the last solve took (k_conv
     // after each update lets the check see convergence without a further direction launch)
@@ -563,15 +610,15 @@ struct Ctx {
         const bool samp = (it & 7) == 0;
         with_c16(A, [&](auto c16) {
           klaunch(samp ? 1 : -1, bytes_dir, k_cg_dir<NR, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(),
-                  val, v, lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
+                  fc, val, v, lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
                   part_c, (const double*)nullptr, 0, 0);
         });
         KCHK();
         Red pq = reduce_global(part_c, nb, NR, false, 2);
-        klaunch(samp ? 2 : -1, bytes_upd, k_cg_upd<NR>, dim3(nb), dim3(BS), v, A.nrows, pq.p, pq.nb, pq.stride,
-                (const double*)scal, (const int*)ctl, part_a, (float*)nullptr);
+        klaunch(samp ? 2 : -1, bytes_upd, k_cg_upd<NR>, dim3(nb_rows(A.own())), dim3(BS), v, A.own(), pq.p, pq.nb,
+                pq.stride, (const double*)scal, (const int*)ctl, part_a, (float*)nullptr);
         KCHK();
-        rr = reduce_global(part_a, nb, NR, false, 0);
+        rr = reduce_global(part_a, nb_rows(A.own()), NR, false, 0);
         hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, NR);
         KCHK();
         if (NR == 2) halo(cg_r[0], cg_r[1]);
@@ -598,9 +645,14 @@ struct Ctx {
   // x += d with step-dependent scalars.
   // x_in (nullable: zero initial guess) -> returns the buffer holding the result; with zout the
   // last step writes its result (in fp64) to zout instead and nullptr is returned.
+  // launch grids of a lattice operator: its face blocks, then the SELL blocks (launches that write
+  // partials stay within MAXB blocks)
+  static int grid_part(const FaceDev& f, const DevSell& A) { return f.nb + std::min(nb_for(A.nslices), MAXB - f.nb); }
+  int grid_full(const FaceDev& f, const DevSell& A) const { return f.nb + nb_mg(A.nslices); }
+
   template <typename T, typename TB>
-  T* mg_smooth(MgLevel& L, const DevSell& A, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb, double* zout,
-               const double* rdot, double* part, int deg) {
+  T* mg_smooth(MgLevel& L, const DevSell& A, const HFace& hf, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb,
+               double* zout, const double* rdot, double* part, int deg) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
@@ -633,26 +685,30 @@ struct Ctx {
       const bool timed = finest && mode != 0;
       const double* rd = last ? rdot : nullptr;
       const bool toz = last && zout;
-      const int nb = rd ? nb_for(A.nslices) : nb_mg(A.nslices);
+      const FaceDev fc = rd ? hf.part() : hf.full();
+      const int nb = rd ? grid_part(fc, A) : grid_full(fc, A);
       const T* xi = mode == 1 ? cur : nullptr;
       // algorithmic bytes: matrix (value + column) per entry; per row x_in (mode 1) or b and dinv
-      // (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r
+      // (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r; face rows
+      // read no matrix and no dinv (per-face constants)
       const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
+      const double rd_face = (mode == 1 ? 2.0 * sizeof(T) : 0.0) + sizeof(TB) + (rd ? 8.0 : 0.0);
       const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
-      const double bytes = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (rd_row + wr_row);
+      const double bytes = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz +
+                           (double)A.nrows * (rd_row + wr_row + A.row_bytes()) + (double)hf.rows * (rd_face + wr_row);
       B.with_vals([&](auto* val) {
         using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
         with_c16(A, [&](auto c16) {
           constexpr bool C = decltype(c16)::value;
           if (toz)
-            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, double, VT, C, 1>, dim3(nb), dim3(BS), A.view(), val,
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, double, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
                     (const T*)B.dinv, b, xi, zout, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
           else if (finest)
-            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), val,
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
                     (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
           else
-            klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), val, (const T*)B.dinv, b, xi,
-                    out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+            klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), fc, val, (const T*)B.dinv, b,
+                    xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
         });
       });
       KCHK();
@@ -668,6 +724,7 @@ struct Ctx {
     MgBufs<T>& B = bufs<T>(L);
     const bool finest = l == (int)mg.size() - 1;
     const DevSell& A = finest ? dPp : L.dA;
+    const HFace& hf = finest ? fP : L.hA;
     T* xa = B.x;
     T* xb = B.x2;
     if (l == 0) {
@@ -686,20 +743,21 @@ struct Ctx {
       // coarse levels: the fused first smoothing step reads b at ghost columns
       if (prm.mg_degree >= 2) mg_halo(L, const_cast<T*>(b));
     }
-    T* x = mg_smooth<T, TB>(L, A, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, prm.mg_degree);
+    T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, prm.mg_degree);
     mg_halo(L, x);
     // residual: matrix entries, x gathered once, b read, res written
-    const double bytes_res =
-        (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + (double)A.nrows * (2.0 * sizeof(T) + sizeof(TB));
+    const double bytes_res = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
+                             (double)A.own() * (2.0 * sizeof(T) + sizeof(TB));
+    const FaceDev fr = hf.full();
     B.with_vals([&](auto* val) {
       using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
       with_c16(A, [&](auto c16) {
         if (finest)
-          klaunch(5, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 1>, dim3(nb_mg(A.nslices)), dim3(BS),
-                  A.view(), val, b, (const T*)x, B.res, (const int*)ctl);
+          klaunch(5, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 1>, dim3(grid_full(fr, A)), dim3(BS),
+                  A.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
         else
-          klaunch(-1, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 0>, dim3(nb_mg(A.nslices)), dim3(BS),
-                  A.view(), val, b, (const T*)x, B.res, (const int*)ctl);
+          klaunch(-1, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 0>, dim3(grid_full(fr, A)), dim3(BS),
+                  A.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
       });
     });
     KCHK();
@@ -709,10 +767,12 @@ struct Ctx {
     const bool gather = C.rep && !L.rep && world > 1;  // into the finest replicated level
     T* cb = gather ? CB.b + L.r_r0 : CB.b;
     // restriction: entries (value + column), fine residual read once, coarse rhs written
+    const FaceDev frs = L.hR.full(), fpr = L.hPr.full();
     klaunch(finest ? 6 : -1,
-            (double)(sizeof(T) + 4) * (double)L.dR.nnz + (double)sizeof(T) * (double)(A.nrows + L.dR.nrows),
-            k_transfer<T>, dim3(nb_mg(L.dR.nslices)), dim3(BS), L.dR.view(), (const T*)B.Rval, (const T*)B.res, cb, 0,
-            (const int*)ctl);
+            (double)(sizeof(T) + 4) * (double)L.dR.nnz + L.dR.row_bytes() * (double)L.dR.nrows +
+                (double)sizeof(T) * (double)(A.own() + L.dR.nrows + L.hR.rows),
+            k_transfer<T>, dim3(grid_full(frs, L.dR)), dim3(BS), L.dR.view(), frs, (const T*)B.Rval, (const T*)B.res,
+            cb, 0, (const int*)ctl);
     KCHK();
     if (gather) {
       comm->group_start();
@@ -723,12 +783,13 @@ struct Ctx {
     mg_halo(C, xc);
     // prolongation: entries, coarse x read once, fine x read + written
     klaunch(finest ? 7 : -1,
-            (double)(sizeof(T) + 4) * (double)L.dPr.nnz + (double)sizeof(T) * (double)(2 * A.nrows + L.dR.nrows),
-            k_transfer<T>, dim3(nb_mg(L.dPr.nslices)), dim3(BS), L.dPr.view(), (const T*)B.Prval, (const T*)xc, x, 1,
-            (const int*)ctl);
+            (double)(sizeof(T) + 4) * (double)L.dPr.nnz + L.dPr.row_bytes() * (double)L.dPr.nrows +
+                (double)sizeof(T) * (double)(2 * A.own() + L.dR.nrows + L.hR.rows),
+            k_transfer<T>, dim3(grid_full(fpr, L.dPr)), dim3(BS), L.dPr.view(), fpr, (const T*)B.Prval, (const T*)xc,
+            x, 1, (const int*)ctl);
     KCHK();
     T* other = (x == xa) ? xb : xa;
-    return mg_smooth<T, TB>(L, A, B, b, x, x, other, finest ? z : nullptr, rdot, part,
+    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest ? z : nullptr, rdot, part,
                             prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
@@ -743,7 +804,10 @@ struct Ctx {
   }
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
-    const int nb = nb_for(dPp.nslices);
+    const FaceDev fc = fP.part();
+    const int nb = grid_part(fc, dPp);  // also the grid of the V-cycle's last smoothing step (<r, z> partials)
+    const i64 n = dPp.own();
+    const int nbu = nb_rows(n);
     CgVecs<1> v;
     v.y[0] = y;
     v.b[0] = b;
@@ -757,13 +821,13 @@ struct Ctx {
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
     float* r32o = mg_single ? r32 : nullptr;
     with_c16(dPp, [&](auto c16) {
-      hipLaunchKernelGGL((k_cg_init<1, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(), dKp_raw, vi,
+      hipLaunchKernelGGL((k_cg_init<1, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(), fc, dKp_raw, vi,
                          lp.n_ghost, part_a, part_b, r32o);
     });
     KCHK();
     // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: keep r0
     if (proj_k > 0 && (which == 1 || which == 2))
-      HIPCHK(hipMemcpyAsync(pav[which], cg_r[0], sizeof(double) * dPp.nrows, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(pav[which], cg_r[0], sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
     const double tol2 = tol * tol;
@@ -771,8 +835,9 @@ struct Ctx {
     std::vector<std::pair<int, size_t>> marks;
     hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
     KCHK();
-    const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + 32.0 * (double)dPp.nrows;
-    const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)dPp.nrows;  // + the fp32 r copy
+    const double bytes_dir =
+        (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows + 32.0 * (double)n;
+    const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)n;  // + the fp32 r copy
     int it = 0;
     // an iteration = V-cycle, direction, update, convergence test (k_conv): the host checks right
     // after a test, so a solve that converges at a check launches no V-cycle after it.  The first
@@ -787,7 +852,7 @@ struct Ctx {
         Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
         halo(z);
         with_c16(dPp, [&](auto c16) {
-          klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(),
+          klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(), fc,
                   (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it,
                   maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
         });
@@ -795,10 +860,10 @@ struct Ctx {
         Red pq = reduce_global(part_c, nb, 1, false, 2);
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
-        klaunch(2, bytes_upd, k_cg_upd<1>, dim3(nb), dim3(BS), vu, dPp.nrows, pq.p, pq.nb, pq.stride,
+        klaunch(2, bytes_upd, k_cg_upd<1>, dim3(nbu), dim3(BS), vu, n, pq.p, pq.nb, pq.stride,
                 (const double*)scal, (const int*)ctl, part_a, r32o);
         KCHK();
-        rr = reduce_global(part_a, nb, 1, false, 0);
+        rr = reduce_global(part_a, nbu, 1, false, 0);
         hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, 1);
         KCHK();
         std::swap(v.po[0], v.pn[0]);
@@ -859,7 +924,7 @@ struct Ctx {
       project_guess(3, bvx, yvx);
       project_guess(4, bvy, yvy);
     }
-    iters = cg<2>(dP, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
     if (proj) {
       project_update(3, yvx);
       project_update(4, yvy);
@@ -882,17 +947,20 @@ struct Ctx {
     halo(usx, usy);
     return 0;
   }
+  // grid of k_div (its partials: max |div|, sum braw)
+  int div_grid() const { return grid_part(fK.part(), dP); }
   void div(const double* ax, const double* ay, double* out, bool rhs) {
-    const int nb = nb_for(dP.nslices);
+    const FaceDev fc = fK.part();
     with_c16(dP, [&](auto c16) {
-      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 4 * (double)lp.n_own, k_div<decltype(c16)::value>,
-              dim3(nb), dim3(BS), dP.view(), (const double*)dGx, (const double*)dGy, ax, ay, (const double*)das1, out,
-              (const double*)dmp, -(1.0 / prm.dt), rhs ? braw : (double*)nullptr, part_d);
+      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
+              k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
+              (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
+              rhs ? braw : (double*)nullptr, part_d);
     });
     KCHK();
   }
   int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
-    const int nb = nb_for(dP.nslices);
+    const int nb = div_grid();
     Red sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
     const i64 n = lp.n_own;
     const double* sc = (use_mg || dense) ? nullptr : dsp;  // MG and dense paths solve the unscaled system
@@ -914,7 +982,7 @@ struct Ctx {
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
-      it = cg<1>(dPp, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
+      it = cg<1>(dPp, HFace{}, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
     }
     hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
                        (double*)nullptr, dmaster_of);
@@ -1045,15 +1113,15 @@ struct Ctx {
       KCHK();
     } else {
       halo(v);
-      spmv_on(st, *op.A, op.val, v, av);
+      spmv_on(st, *op.A, op.fc, op.val, v, av);
     }
     proj_pend[which] = true;
   }
   void grad_proj(const double* pp, int mode) {
-    const int nb = nb_for(dP.nslices);
+    const FaceDev fc = fK.full();
     with_c16(dP, [&](auto c16) {
-      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + 8.0 * 6 * (double)lp.n_own,
-              k_grad_proj<decltype(c16)::value>, dim3(nb), dim3(BS), dP.view(), (const double*)dGx,
+      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 40.0 * (double)lp.n_own,
+              k_grad_proj<decltype(c16)::value>, dim3(grid_full(fc, dP)), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, pp, (const double*)das1, prm.dt, mode, (const uint8_t*)ddir, (const double*)usx,
               (const double*)usy, ux, uy);
     });
@@ -1065,7 +1133,7 @@ struct Ctx {
     int itv = 0;
     viscous(itv);
     div(usx, usy, div_star, true);
-    reduce_into(part_d, nb_for(dP.nslices), 1, true, 0);  // max |div u*|
+    reduce_into(part_d, div_grid(), 1, true, 0);  // max |div u*|
     const int itp = pressure(yp, p, 1);
     grad_proj(p, 0);
     bc(ux, uy);
@@ -1075,7 +1143,7 @@ struct Ctx {
     grad_proj(p2, 1);
     halo(ux, uy);
     div(ux, uy, final_div, false);
-    reduce_into(part_d, nb_for(dP.nslices), 1, true, 1);  // max |final div|
+    reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       klaunch(4, 8.0 * 6 * (double)lp.n_own, k_sl, dim3(nb), dim3(BS), MeshDev{mx, my, mtri, mesh.T}, lgrid, cgrid,
@@ -1131,8 +1199,8 @@ struct Ctx {
            *sh = litw[7];
     auto spmv = [&](const double* in, double* out) {
       with_c16(dLit, [&](auto c16) {
-        hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), dLitv,
-                           in, out);
+        hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), nof(),
+                           dLitv, in, out);
       });
       KCHK();
     };
@@ -1182,10 +1250,10 @@ struct Ctx {
 
 Ctx* C(void* p) { return static_cast<Ctx*>(p); }
 
-void spmv_on(hipStream_t st, const DevSell& A, const double* val, const double* x, double* y) {
+void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* val, const double* x, double* y) {
   with_c16(A, [&](auto c16) {
-    hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(Ctx::nb_for(A.nslices)), dim3(BS), 0, st, A.view(), val, x,
-                       y);
+    hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(fc.nb + Ctx::nb_for(A.nslices)), dim3(BS), 0, st, A.view(),
+                       fc, val, x, y);
   });
 }
 
@@ -1261,7 +1329,8 @@ void build_mg_host(Ctx& c) {
   }
   for (int l = 0; l < Lv; ++l) {
     MgLevel& L = c.mg[l];
-    make_ordering_cuts(L.mesh, c.ord.cuts, L.ord);
+    if (c.lattice) lattice_ordering(L.mesh, c.macro, l, L.ord, L.latl);
+    else make_ordering_cuts(L.mesh, c.ord.cuts, L.ord);
     build_pattern(L.mesh, L.ord, L.P);
     Assembly A;
     assemble_stokes(L.mesh, L.ord, L.P, A);
@@ -1283,6 +1352,7 @@ void build_mg_host(Ctx& c) {
   }
   MgLevel& F = c.mg[Lv];
   F.ord = c.ord;
+  if (c.lattice) F.latl = std::move(c.lat_fine);
   F.dof = c.dof;
   F.master_of = c.master_of;
   for (int l = 1; l <= Lv; ++l) {
@@ -1360,7 +1430,9 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
       const Sell& S = L.sA;
       sell_values_x(A, r0, S, A.val, tmp);
       L.dA = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
-                     A.rowptr[r0 + n] - A.rowptr[r0], S.padded, 0};
+                     S.rows.empty() ? A.rowptr[r0 + n] - A.rowptr[r0] : S.nnz, S.padded, 0};
+      if (!S.rows.empty()) L.dA.rows = c.upload(S.rows);
+      L.dA.n_own = n;
       c.attach_c16(S, L.nloc, L.dA);
       B.Aval = upload_as<T>(c, tmp);
       if constexpr (std::is_same<T, float>::value) B.Aval16 = upload_f16(c, tmp, false);
@@ -1380,12 +1452,14 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
       const Sell& S = L.sPr;
       sell_values_x(L.Pr, r0, S, L.Pr.val, tmp);
       L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
-                      L.Pr.rowptr[r0 + n] - L.Pr.rowptr[r0], S.padded};
+                      S.rows.empty() ? L.Pr.rowptr[r0 + n] - L.Pr.rowptr[r0] : S.nnz, S.padded};
+      if (!S.rows.empty()) L.dPr.rows = c.upload(S.rows);
       B.Prval = upload_as<T>(c, tmp);
       const Sell& R = L.sR;
       sell_values_x(L.R, L.r_r0, R, L.R.val, tmp);
       L.dR = DevSell{c.upload(R.slice_off), c.upload(R.slice_w), c.upload(R.col), nullptr, R.nslices, R.nrows,
-                     L.R.rowptr[L.r_r0 + R.nrows] - L.R.rowptr[L.r_r0], R.padded};
+                     R.rows.empty() ? L.R.rowptr[L.r_r0 + R.nrows] - L.R.rowptr[L.r_r0] : R.nnz, R.padded};
+      if (!R.rows.empty()) L.dR.rows = c.upload(R.rows);
       B.Rval = upload_as<T>(c, tmp);
     }
     for (T** f : {&B.x, &B.x2, &B.b, &B.d, &B.res}) *f = c.dalloc<T>(L.nloc);
@@ -1402,7 +1476,14 @@ void build(Ctx& c) {
   require(!(literal && c.world > 1), "heat / Poisson literal operators run on one rank");
   require(!stokes || prm.sl_k == KNN, "sl_k must be 10 (PointLocator.find default)");
   HostMesh& m = c.mesh;
-  make_ordering(m, prm.nstrips, c.ord);
+  // lattice operators: a multigrid hierarchy of >= 2 red refinements (face interiors exist)
+  c.lattice = stokes && prm.precond == 1 && c.mg_levels >= 2 && prm.assembled == 0;
+  if (c.lattice) {
+    build_macro(c.coarse, prm.nstrips, c.mg_levels, c.macro);
+    lattice_ordering(m, c.macro, c.mg_levels, c.ord, c.lat_fine);
+  } else {
+    make_ordering(m, prm.nstrips, c.ord);
+  }
   build_pattern(m, c.ord, c.P);
   assemble_stokes(m, c.ord, c.P, c.as);
   const i64 N = m.N;
@@ -1480,23 +1561,65 @@ void build(Ctx& c) {
       make_local_plan2(pr, L.rs, c.rank, L.lp);
     }
     c.lp = c.mg[Lv].lp;
+    // lattice operators: SELL rows for the skeleton (macro edge / vertex nodes) only
+    auto skel = [&](const LatticeLevel& LL, i64 r0, i64 n) {
+      std::vector<i32> rows;
+      for (i64 i = 0; i < n; ++i)
+        if (LL.type[r0 + i] != 0) rows.push_back((i32)i);
+      return rows;
+    };
     for (int l = 0; l <= Lv; ++l) {  // host SELL images; resolving every column validates the plans
       MgLevel& L = c.mg[l];
-      if (l < Lv) build_sell_x(L.Pp, L.own0(c.rank), L.lp.n_own, L.lp, L.sA, true);
+      const i64 o0 = L.own0(c.rank);
+      if (l < Lv) {
+        if (c.lattice) build_sell_rows(L.Pp, o0, skel(L.latl, o0, L.lp.n_own), L.lp, L.sA);
+        else build_sell_x(L.Pp, o0, L.lp.n_own, L.lp, L.sA, true);
+      }
       if (l >= 1) {
         const MgLevel& C = c.mg[l - 1];
-        build_sell_x(L.Pr, L.own0(c.rank), L.lp.n_own, C.lp, L.sPr);
+        if (c.lattice) build_sell_rows(L.Pr, o0, skel(L.latl, o0, L.lp.n_own), C.lp, L.sPr);
+        else build_sell_x(L.Pr, o0, L.lp.n_own, C.lp, L.sPr);
         // restriction rows: the coarse level's owned rows; into a replicated level from a
         // distributed one, this rank's strip rows of it (completed by the all-gather)
         const bool gather = C.rep && !L.rep;
         L.r_r0 = gather ? C.rs[c.rank] : C.own0(c.rank);
         const i64 nr = gather ? C.rs[c.rank + 1] - C.rs[c.rank] : C.lp.n_own;
-        build_sell_x(L.R, L.r_r0, nr, L.lp, L.sR);
+        if (c.lattice) build_sell_rows(L.R, L.r_r0, skel(C.latl, L.r_r0, nr), L.lp, L.sR);
+        else build_sell_x(L.R, L.r_r0, nr, L.lp, L.sR);
+      }
+    }
+    if (c.lattice) {  // face tables and coefficient records of every level (pucfem_lattice.hpp)
+      const double dtnu = prm.dt * prm.nu;
+      for (int l = 0; l <= Lv; ++l) {
+        MgLevel& L = c.mg[l];
+        const i64 o0 = L.own0(c.rank);
+        L.lf_faces = lattice_faces(c.macro, L.latl, o0, L.lp.n_own);
+        lattice_tabs(c.macro, L.latl, L.lf_faces, -1, L.lp, nullptr, L.lf_plain);
+        lattice_tabs(c.macro, L.latl, L.lf_faces, -1, L.lp, &L.dof, L.lf_merged);
+        lattice_coefs(c.macro, L.lf_faces, l, dtnu, L.lf_coef);
+        if (l >= 1) {
+          MgLevel& C = c.mg[l - 1];
+          lattice_tabs(c.macro, C.latl, L.lf_faces, -1, C.lp, &C.dof, L.pr_tab2);
+          const bool gather = C.rep && !L.rep;
+          const i64 nr = gather ? C.rs[c.rank + 1] - C.rs[c.rank] : C.lp.n_own;
+          L.r_faces = lattice_faces(c.macro, C.latl, L.r_r0, nr);
+          lattice_tabs(c.macro, C.latl, L.r_faces, L.r_r0, C.lp, nullptr, L.r_tab);
+          lattice_tabs(c.macro, L.latl, L.r_faces, -1, L.lp, nullptr, L.r_tab2);
+        }
       }
     }
   }
-  build_sell(c.P, c.lp, c.sP);
-  if (stokes) build_sell(c.Pp, c.lp, c.sPp);
+  if (c.lattice) {
+    const LatticeLevel& LL = c.mg.back().latl;
+    std::vector<i32> rows;
+    for (i64 i = 0; i < c.lp.n_own; ++i)
+      if (LL.type[c.lp.r0 + i] != 0) rows.push_back((i32)i);
+    build_sell_rows(c.P, c.lp.r0, rows, c.lp, c.sP);
+    build_sell_rows(c.Pp, c.lp.r0, rows, c.lp, c.sPp);
+  } else {
+    build_sell(c.P, c.lp, c.sP);
+    if (stokes) build_sell(c.Pp, c.lp, c.sPp);
+  }
   if (literal) build_sell(c.Lit, c.lp, c.sLit);
   c.built = true;
   // tooling hook (tools/spmv_lab.hip --real): the pressure operator's SELL image
@@ -1521,7 +1644,9 @@ void build(Ctx& c) {
     D.nslices = S.nslices;
     D.nrows = S.nrows;
     D.padded = S.padded;
-    D.nnz = A.rowptr[lp.r1] - A.rowptr[lp.r0];
+    D.nnz = S.rows.empty() ? A.rowptr[lp.r1] - A.rowptr[lp.r0] : S.nnz;
+    if (!S.rows.empty()) D.rows = c.upload(S.rows);
+    D.n_own = lp.n_own;
   };
   std::vector<double> tmp;
   dsell(c.sP, c.P, c.dP);
@@ -1555,6 +1680,14 @@ void build(Ctx& c) {
     std::vector<double> sq(N);
     for (i64 g = 0; g < N; ++g) sq[g] = 1.0 / sg[g];
     c.dsqv = c.upload(local_vec(sq));
+    if (c.lattice) {  // scaled A_visc, skeleton columns: s_j, 0 for Dirichlet columns (StokesColor.py:473-475)
+      std::vector<double> w = local_vec(sg);
+      for (i64 i = 0; i < no; ++i)
+        if (isdir[lp.r0 + i]) w[i] = 0.0;
+      for (i64 k = 0; k < lp.n_ghost; ++k)
+        if (isdir[lp.ghost_global[k]]) w[no + k] = 0.0;
+      c.dwsk = c.upload(w);
+    }
   }
   if (stokes) {
     dsell(c.sPp, c.Pp, c.dPp);
@@ -1573,6 +1706,47 @@ void build(Ctx& c) {
     c.mg_single = c.prm.mg_single != 0;
     if (c.mg_single) mg_alloc<float>(c, tmp);
     else mg_alloc<double>(c, tmp);
+    if (c.lattice) {  // the face parts of every lattice operator (pucfem_lattice.hpp)
+      auto mkface = [&](const std::vector<lat::FaceTab>& tab, const std::vector<lat::FaceTab>* tab2, const double* coef,
+                        const float* coef32, int l, int l2, int op) {
+        HFace h;
+        const i32 n = 1 << l, F = lat::interior_count(n);
+        if (tab.empty() || F == 0) return h;
+        h.d.tab = c.upload(tab);
+        h.d.tab2 = tab2 ? c.upload(*tab2) : nullptr;
+        h.d.coef = coef;
+        h.d.coef32 = coef32;
+        h.d.wsk = op == 1 ? c.dwsk : nullptr;
+        h.d.nf = (int32_t)tab.size();
+        h.d.n = n;
+        h.d.F = F;
+        h.d.cpf = (F + BS - 1) / BS;
+        h.d.n2 = l2 >= 0 ? 1 << l2 : 0;
+        h.d.rinv = 1.0f / (float)(n - 1);
+        h.d.nb = 0;
+        h.d.op = op;
+        h.items = h.d.nf * h.d.cpf;
+        h.rows = (i64)h.d.nf * F;
+        return h;
+      };
+      const int Lv = c.mg_levels;
+      for (int l = 0; l <= Lv; ++l) {
+        MgLevel& L = c.mg[l];
+        const double* coef = c.upload(L.lf_coef);
+        const float* coef32 = c.upload(std::vector<float>(L.lf_coef.begin(), L.lf_coef.end()));
+        if (l < Lv) {
+          L.hA = mkface(L.lf_merged, nullptr, coef, coef32, l, -1, 0);
+        } else {
+          c.fP = mkface(L.lf_merged, nullptr, coef, coef32, l, -1, 0);
+          c.fK = mkface(L.lf_plain, nullptr, coef, coef32, l, -1, 0);
+          c.fVisc = mkface(L.lf_plain, nullptr, coef, coef32, l, -1, 1);
+        }
+        if (l >= 1) {
+          L.hPr = mkface(L.lf_plain, &L.pr_tab2, nullptr, nullptr, l, l - 1, 0);
+          L.hR = mkface(L.r_tab, &L.r_tab2, nullptr, nullptr, l - 1, l, 0);
+        }
+      }
+    }
     // coarsest: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
     {
       MgLevel& L0 = c.mg[0];
@@ -2306,14 +2480,22 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_GX:
       case PUCFEM_OP_GY: {
         perm_in(x, 1, t0, nullptr);
+        require(op == PUCFEM_OP_K || !c.lattice, "Gx / Gy alone are not applied on lattice operators (use DIV / GRAD)");
         const double* v = op == PUCFEM_OP_K ? c.dK : op == PUCFEM_OP_GX ? c.dGx : c.dGy;
-        spmv_on(c.st, c.dP, v, t0, o0);
+        spmv_on(c.st, c.dP, c.fK.full(), v, t0, o0);
         KCHK();
         perm_out(y, 1, o0, nullptr);
         break;
       }
       case PUCFEM_OP_PRES: {
         require(c.dKp, "no pressure operator (scheme is not Stokes)");
+        if (c.lattice) {  // the unscaled merged operator (the multigrid path's)
+          perm_in(x, 1, t0, nullptr);
+          spmv_on(c.st, c.dPp, c.fP.full(), c.dKp_raw, t0, o0);
+          KCHK();
+          perm_out(y, 1, o0, nullptr);
+          break;
+        }
         perm_in(x, 1, t0, nullptr);
         // unscaled action: S^-1 A^ S^-1 x
         std::vector<double> s(N);
@@ -2322,7 +2504,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         std::vector<double> a(N), xs(N);
         for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
         HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-        spmv_on(c.st, c.dPp, c.dKp, t0, o0);
+        spmv_on(c.st, c.dPp, FaceDev{}, c.dKp, t0, o0);
         KCHK();
         HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipStreamSynchronize(c.st));
@@ -2332,7 +2514,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_LIT: {
         require(c.dLitv, "no literal operator (scheme is Stokes)");
         perm_in(x, 1, t0, nullptr);
-        spmv_on(c.st, c.dLit, c.dLitv, t0, o0);
+        spmv_on(c.st, c.dLit, FaceDev{}, c.dLitv, t0, o0);
         KCHK();
         perm_out(y, 1, o0, nullptr);
         break;
@@ -2340,8 +2522,8 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_DIV: {
         perm_in(x, 2, t0, t1);
         with_c16(c.dP, [&](auto c16) {
-          hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st,
-                             c.dP.view(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
+          hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(c.div_grid()), dim3(BS), 0, c.st, c.dP.view(),
+                             c.fK.part(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
         });
         KCHK();
         perm_out(y, 1, o0, nullptr);
@@ -2350,8 +2532,8 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_GRAD: {
         perm_in(x, 1, t0, nullptr);
         with_c16(c.dP, [&](auto c16) {
-          hipLaunchKernelGGL(k_grad<decltype(c16)::value>, dim3(Ctx::nb_for(c.dP.nslices)), dim3(BS), 0, c.st,
-                             c.dP.view(), c.dGx, c.dGy, t0, c.das1, o0, o1);
+          hipLaunchKernelGGL(k_grad<decltype(c16)::value>, dim3(c.grid_full(c.fK.full(), c.dP)), dim3(BS), 0, c.st,
+                             c.dP.view(), c.fK.full(), c.dGx, c.dGy, t0, c.das1, o0, o1);
         });
         KCHK();
         perm_out(y, 2, o0, o1);
@@ -2364,7 +2546,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         HIPCHK(hipStreamSynchronize(c.st));
         for (i64 g = 0; g < N; ++g) xs[g] = x[c.ord.new2old[g]] / s[g];
         HIPCHK(hipMemcpyAsync(t0, xs.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-        spmv_on(c.st, c.dP, c.dKv, t0, o0);
+        spmv_on(c.st, c.dP, c.fVisc.full(), c.dKv, t0, o0);
         KCHK();
         HIPCHK(hipMemcpyAsync(a.data(), o0, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipStreamSynchronize(c.st));
@@ -2402,7 +2584,7 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
       const double* bb[2] = {c.bvx, c.bvy};
-      it = c.cg<2>(c.dP, c.dKv, y, bb, rtol, maxit, 3);
+      it = c.cg<2>(c.dP, c.fVisc, c.dKv, y, bb, rtol, maxit, 3);
       hipLaunchKernelGGL(k_cg_fin, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, 2, c.dsv, c.yvx, c.yvy, s2, s3,
                          (const int32_t*)nullptr);
       KCHK();
@@ -2633,6 +2815,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[4] = c.proj_m[2];
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
+    o[7] = c.lattice ? 1 : 0;
   });
 }
 
@@ -2748,6 +2931,50 @@ int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, in
   });
 }
 
+int pucfem_host_lattice_apply(void* ctx, int32_t level, int32_t kind, const double* x, double* y) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    require(c.lattice && c.world == 1, "needs a single-rank context with lattice operators");
+    const int Lv = c.mg_levels;
+    require(level >= 0 && level <= Lv, "level out of range");
+    require(kind >= 0 && kind <= 6 && kind != 4, "kind");
+    require(kind >= 3 || level == Lv, "kinds 0-2 are finest-level operators");
+    require(kind < 5 || level >= 1, "transfers need level >= 1");
+    MgLevel& L = c.mg[level];
+    const int in_l = kind == 5 ? level - 1 : level, out_l = kind == 6 ? level - 1 : level;
+    const Ordering& oin = c.mg[in_l].ord;
+    const Ordering& oout = c.mg[out_l].ord;
+    const i64 nin = (i64)oin.new2old.size(), nout = (i64)oout.new2old.size();
+    const int ncomp = kind == 1 ? 2 : 1;
+    std::vector<double> x0(nin), x1(ncomp > 1 ? nin : 0), yv(nout, NAN);
+    for (i64 g = 0; g < nin; ++g) {
+      const i64 o = oin.new2old[g];
+      x0[g] = x[ncomp * o];
+      if (ncomp > 1) x1[g] = x[ncomp * o + 1];
+    }
+    const int n = 1 << level;
+    std::vector<double> wsk;
+    if (kind == 2) {
+      std::vector<uint8_t> isdir(c.mesh.N, 0);
+      for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
+      wsk.resize(c.mesh.N);
+      for (i64 g = 0; g < c.mesh.N; ++g) wsk[g] = isdir[g] ? 0.0 : 1.0 / std::sqrt(diag_of(c.P, c.Kv, g));
+    }
+    if (kind <= 2) {
+      lattice_apply_host(kind, n, L.lf_plain, L.lf_coef, x0.data(), ncomp > 1 ? x1.data() : nullptr,
+                         kind == 2 ? wsk.data() : nullptr, yv.data());
+    } else if (kind == 3) {
+      lattice_apply_host(0, n, L.lf_merged, L.lf_coef, x0.data(), nullptr, nullptr, yv.data());
+    } else if (kind == 5) {
+      lattice_apply_host(3, n, L.lf_plain, L.lf_coef, x0.data(), nullptr, nullptr, yv.data(), &L.pr_tab2, n / 2);
+    } else {
+      lattice_apply_host(4, n / 2, L.r_tab, L.lf_coef, x0.data(), nullptr, nullptr, yv.data(), &L.r_tab2, n);
+    }
+    for (i64 g = 0; g < nout; ++g) y[oout.new2old[g]] = yv[g];
+  });
+}
+
 int pucfem_host_partition(void* ctx, int32_t rank, int32_t world, int64_t* n_own, int64_t* n_ghost, int64_t* owned,
                           int64_t* ghosts, int32_t* ghost_owner, int64_t* n_send, int64_t* send_ids,
                           int32_t* send_peer) {
@@ -2786,7 +3013,7 @@ int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters,
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.dKp, "needs a Stokes context");
+    require(c.dKp && !c.lattice, "needs a Stokes context with SELL operators");
     const DevSell& A = c.dPp;
     const int nb = nblocks > 0 ? std::min(nblocks, MAXB) : Ctx::nb_for(A.nslices);
     CgVecs<1> v;
@@ -2805,12 +3032,12 @@ int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters,
     HIPCHK(hipMemsetAsync(c.ctl, 0, 2 * sizeof(int), c.st));
     auto launch = [&]() {
       switch (variant) {
-        case 0: hipLaunchKernelGGL((k_cg_dir<1, 0, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        case 1: hipLaunchKernelGGL((k_cg_dir<1, 8, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        case 2: hipLaunchKernelGGL((k_cg_dir<1, 0, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
-        case 3: hipLaunchKernelGGL((k_cg_dir<1, 8, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 0: hipLaunchKernelGGL((k_cg_dir<1, 0, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), FaceDev{}, c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 1: hipLaunchKernelGGL((k_cg_dir<1, 8, false, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), FaceDev{}, c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 2: hipLaunchKernelGGL((k_cg_dir<1, 0, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), FaceDev{}, c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+        case 3: hipLaunchKernelGGL((k_cg_dir<1, 8, true, false>), dim3(nb), dim3(BS), 0, c.st, A.view(), FaceDev{}, c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
         default: require(A.c16 != nullptr, "variant 4 needs int16 columns");
-                 hipLaunchKernelGGL((k_cg_dir<1, 8, true, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
+                 hipLaunchKernelGGL((k_cg_dir<1, 8, true, true>), dim3(nb), dim3(BS), 0, c.st, A.view(), FaceDev{}, c.dKp, v, (int64_t)0, c.part_a, 1, 1, c.part_a, 1, 1, c.scal, c.ctl, 1, 1 << 30, 0.0, c.part_c); break;
       }
       KCHK();
     };
@@ -2847,7 +3074,8 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
     kernel %= 256;
     const int nfill = kernel / 16;
     kernel %= 16;
-    const int nb_mg = c.nb_mg(A.nslices), nb = Ctx::nb_for(A.nslices);
+    const FaceDev ff = c.fP.full(), fpt = c.fP.part();
+    const int nb_mg = c.grid_full(ff, A), nb = Ctx::grid_part(fpt, A);
     CgVecs<1> v;
     v.y[0] = c.yp;
     v.b[0] = c.bh;
@@ -2869,17 +3097,17 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
         switch (kernel) {
           case 0:
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0,
-                                  A.view(), (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
+                                  A.view(), ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
                                   (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
                                   (const double*)nullptr, (double*)nullptr);
             break;
           case 1:
             hipExtLaunchKernelGGL(k_resid<float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0, A.view(),
-                                  (const float*)B.Aval, (const float*)c.r32, (const float*)B.x, B.res,
+                                  ff, (const float*)B.Aval, (const float*)c.r32, (const float*)B.x, B.res,
                                   (const int*)nullptr);
             break;
           default:
-            hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(nb), dim3(BS), 0, c.st, a, e, 0, A.view(),
+            hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(nb), dim3(BS), 0, c.st, a, e, 0, A.view(), fpt,
                                   (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
                                   (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
                                   (const double*)nullptr, 0, 0);
@@ -2887,18 +3115,20 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
       });
       KCHK();
     };
+    // face rows read no matrix (and the smoother no dinv: 24 B instead of 28)
+    const double fr = (double)c.fP.rows, sk = (double)A.nrows, rb = A.row_bytes();
     switch (kernel) {
-      case 0: by = (4.0 + A.idx_bytes()) * (double)A.nnz + 28.0 * (double)A.nrows; break;
-      case 1: by = (4.0 + A.idx_bytes()) * (double)A.nnz + 12.0 * (double)A.nrows; break;
-      default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + 32.0 * (double)A.nrows;
+      case 0: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (28.0 + rb) * sk + 24.0 * fr; break;
+      case 1: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (12.0 + rb) * sk + 12.0 * fr; break;
+      default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk + 32.0 * fr;
     }
     MgLevel& Lc = c.mg[c.mg.size() >= 3 ? c.mg.size() - 3 : 0];
     auto fill = [&] {
       for (int f = 0; f < nfill; ++f) {
         with_c16(Lc.dA, [&](auto c16) {
           constexpr bool C16 = decltype(c16)::value;
-          hipLaunchKernelGGL((k_cheb<float, float, float, float, C16, 0>), dim3(c.nb_mg(Lc.dA.nslices)), dim3(BS), 0,
-                             c.st, Lc.dA.view(), (const float*)Lc.f32.Aval, (const float*)Lc.f32.dinv,
+          hipLaunchKernelGGL((k_cheb<float, float, float, float, C16, 0>), dim3(c.grid_full(Lc.hA.full(), Lc.dA)), dim3(BS),
+                             0, c.st, Lc.dA.view(), Lc.hA.full(), (const float*)Lc.f32.Aval, (const float*)Lc.f32.dinv,
                              (const float*)Lc.f32.b, (const float*)nullptr, Lc.f32.x2, Lc.f32.d, 0.3, 0.7, 0.0, 2,
                              (const int*)nullptr, (const double*)nullptr, (double*)nullptr);
         });

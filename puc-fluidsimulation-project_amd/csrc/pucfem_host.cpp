@@ -7,6 +7,7 @@
 #include <map>
 #include <numeric>
 #include <stdexcept>
+#include <mutex>
 #include <thread>
 
 namespace pucfem {
@@ -465,6 +466,7 @@ bool sell_col16(const Sell& S, i64 nloc, std::vector<int16_t>& out) {
 
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,
                  std::vector<double>& out) {
+  if (!S.rows.empty()) return sell_values_rows(A, lp.r0, S, val, out);
   out.assign(S.padded, 0.0);
   for (i64 s = 0; s < S.nslices; ++s)
     for (i64 l = 0; l < 64; ++l) {
@@ -808,6 +810,7 @@ void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S, b
 }
 
 void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out) {
+  if (!S.rows.empty()) return sell_values_rows(A, r0, S, val, out);
   out.assign(S.padded, 0.0);
   for (i64 s = 0; s < S.nslices; ++s)
     for (i64 l = 0; l < 64; ++l) {
@@ -816,6 +819,397 @@ void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double
       const i64 b = A.rowptr[r0 + r], len = A.rowptr[r0 + r + 1] - b;
       for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
     }
+}
+
+}  // namespace pucfem
+
+// ============================================================================= lattice layout
+namespace pucfem {
+
+void build_sell_rows(const Csr& A, i64 r0, const std::vector<i32>& rows, const LocalPlan& cols, Sell& S) {
+  const i64 n = (i64)rows.size();
+  S.nrows = n;
+  S.nslices = (n + 63) / 64;
+  S.slice_off.assign(S.nslices + 1, 0);
+  S.slice_w.assign(S.nslices, 0);
+  S.rows.assign(S.nslices * 64, -1);
+  for (i64 s = 0; s < S.nslices; ++s) {
+    i64 w = 0;
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 k = s * 64 + l;
+      if (k < n) {
+        const i64 r = r0 + rows[k];
+        w = std::max(w, A.rowptr[r + 1] - A.rowptr[r]);
+        S.rows[k] = rows[k];
+      }
+    }
+    S.slice_w[s] = (i32)w;
+    S.slice_off[s + 1] = S.slice_off[s] + w * 64;
+  }
+  S.padded = S.slice_off[S.nslices];
+  S.nnz = 0;
+  for (i64 k = 0; k < n; ++k) S.nnz += A.rowptr[r0 + rows[k] + 1] - A.rowptr[r0 + rows[k]];
+  S.col.assign(S.padded, 0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 k = s * 64 + l;
+      const i64 r = k < n ? r0 + rows[k] : -1;
+      const i64 len = k < n ? A.rowptr[r + 1] - A.rowptr[r] : 0;
+      // padding entries of a listed row gather the row's first column again (value 0, in cache)
+      const i32 first = len > 0 ? to_local(cols, A.col[A.rowptr[r]]) : 0;
+      for (i64 e = 0; e < S.slice_w[s]; ++e)
+        S.col[S.slice_off[s] + e * 64 + l] = e < len ? to_local(cols, A.col[A.rowptr[r] + e]) : first;
+    }
+}
+
+void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out) {
+  out.assign(S.padded, 0.0);
+  for (i64 s = 0; s < S.nslices; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 k = s * 64 + l;
+      if (k >= S.nrows) continue;
+      const i64 r = r0 + S.rows[k];
+      const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
+      for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = val[b + e];
+    }
+}
+
+namespace {
+template <class F>
+void parallel_for(i64 n, F&& f) {
+  const int nt = (int)std::max<i64>(1, std::min<i64>({64, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
+  if (nt == 1) {
+    f((i64)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int w = 0; w < nt; ++w) th.emplace_back([&, w] { f(n * w / nt, n * (w + 1) / nt); });
+  for (auto& h : th) h.join();
+}
+}  // namespace
+
+void build_macro(const HostMesh& c, int strips, int lw, Macro& M) {
+  M.nv = c.N;
+  M.nf = c.T;
+  M.x = c.x;
+  M.y = c.y;
+  M.tri = c.tri;
+  std::vector<std::pair<i32, i32>> es;
+  es.reserve(3 * c.T);
+  for (i64 t = 0; t < c.T; ++t)
+    for (int e = 0; e < 3; ++e) {
+      const i32 a = c.tri[3 * t + e], b = c.tri[3 * t + (e + 1) % 3];
+      es.push_back({std::min(a, b), std::max(a, b)});
+    }
+  std::sort(es.begin(), es.end());
+  es.erase(std::unique(es.begin(), es.end()), es.end());
+  M.ne = (i64)es.size();
+  M.ev.resize(2 * M.ne);
+  for (i64 e = 0; e < M.ne; ++e) {
+    M.ev[2 * e] = es[e].first;
+    M.ev[2 * e + 1] = es[e].second;
+  }
+  auto eid = [&](i32 a, i32 b) {
+    const std::pair<i32, i32> k{std::min(a, b), std::max(a, b)};
+    return (i32)(std::lower_bound(es.begin(), es.end(), k) - es.begin());
+  };
+  M.fe.resize(3 * M.nf);
+  for (i64 f = 0; f < M.nf; ++f) {
+    const i32 A = c.tri[3 * f], B = c.tri[3 * f + 1], C = c.tri[3 * f + 2];
+    M.fe[3 * f] = eid(A, B);
+    M.fe[3 * f + 1] = eid(A, C);
+    M.fe[3 * f + 2] = eid(B, C);
+  }
+  // strip keys (y) and x keys of every primitive; weights = nodes at level lw
+  const i32 n = 1 << lw;
+  const double wF = lat::interior_count(n), wE = std::max(0, n - 1), wV = 1.0;
+  struct Item {
+    double ky, kx, w;
+    int kind;
+    i32 id;
+  };
+  std::vector<Item> it;
+  it.reserve(M.nf + M.ne + M.nv);
+  for (i64 f = 0; f < M.nf; ++f) {
+    const i32 A = c.tri[3 * f], B = c.tri[3 * f + 1], C = c.tri[3 * f + 2];
+    it.push_back({(c.y[A] + c.y[B] + c.y[C]) / 3.0, (c.x[A] + c.x[B] + c.x[C]) / 3.0, wF, 0, (i32)f});
+  }
+  for (i64 e = 0; e < M.ne; ++e) {
+    const i32 a = M.ev[2 * e], b = M.ev[2 * e + 1];
+    it.push_back({(c.y[a] + c.y[b]) * 0.5, (c.x[a] + c.x[b]) * 0.5, wE, 1, (i32)e});
+  }
+  for (i64 v = 0; v < M.nv; ++v) it.push_back({c.y[v], c.x[v], wV, 2, (i32)v});
+  std::vector<Item> byy = it;
+  std::stable_sort(byy.begin(), byy.end(), [](const Item& a, const Item& b) { return a.ky < b.ky; });
+  double W = 0.0;
+  for (auto& q : byy) W += q.w;
+  // auto: strips of about 16 faces (the rank partition's granularity), at most 64
+  const int S = strips > 0 ? strips : (int)std::max<i64>(1, std::min<i64>(64, M.nf / 16));
+  M.cuts.clear();
+  double acc = 0.0;
+  size_t k = 0;
+  for (int s = 1; s < S; ++s) {
+    const double target = W * s / S;
+    while (k < byy.size() && acc + byy[k].w <= target) acc += byy[k++].w;
+    // move to a key boundary (equal keys -- periodic partners -- share a strip)
+    while (k > 0 && k < byy.size() && byy[k].ky == byy[k - 1].ky) acc += byy[k++].w;
+    if (k == 0 || k >= byy.size()) continue;
+    const double cut = 0.5 * (byy[k - 1].ky + byy[k].ky);
+    if (M.cuts.empty() || cut > M.cuts.back()) M.cuts.push_back(cut);
+  }
+  M.S = (int)M.cuts.size() + 1;
+  auto strip_of = [&](double ky) { return (i32)(std::upper_bound(M.cuts.begin(), M.cuts.end(), ky) - M.cuts.begin()); };
+  for (int kind = 0; kind < 3; ++kind) {
+    std::vector<Item> v;
+    for (auto& q : it)
+      if (q.kind == kind) v.push_back(q);
+    std::sort(v.begin(), v.end(), [&](const Item& a, const Item& b) {
+      const i32 sa = strip_of(a.ky), sb = strip_of(b.ky);
+      if (sa != sb) return sa < sb;
+      if (a.kx != b.kx) return a.kx < b.kx;
+      return a.id < b.id;
+    });
+    std::vector<i32>& ord = kind == 0 ? M.order_f : kind == 1 ? M.order_e : M.order_v;
+    std::vector<i32>& sp = kind == 0 ? M.strip_f : kind == 1 ? M.strip_e : M.strip_v;
+    ord.resize(v.size());
+    sp.assign(M.S + 1, 0);
+    for (size_t q = 0; q < v.size(); ++q) {
+      ord[q] = v[q].id;
+      sp[strip_of(v[q].ky) + 1]++;
+    }
+    for (int s = 0; s < M.S; ++s) sp[s + 1] += sp[s];
+  }
+}
+
+void lattice_ordering(const HostMesh& ml, const Macro& M, int l, Ordering& ord, LatticeLevel& LL) {
+  const i32 n = 1 << l;
+  LL.l = l;
+  LL.n = n;
+  LL.F = lat::interior_count(n);
+  LL.face_start.assign(M.nf, -1);
+  LL.edge_start.assign(M.ne, -1);
+  LL.vert_start.assign(M.nv, -1);
+  ord.strip_ptr.assign(M.S + 1, 0);
+  i64 pos = 0;
+  for (int s = 0; s < M.S; ++s) {
+    for (i32 q = M.strip_f[s]; q < M.strip_f[s + 1]; ++q) {
+      LL.face_start[M.order_f[q]] = pos;
+      pos += LL.F;
+    }
+    for (i32 q = M.strip_e[s]; q < M.strip_e[s + 1]; ++q) {
+      LL.edge_start[M.order_e[q]] = pos;
+      pos += n - 1;
+    }
+    for (i32 q = M.strip_v[s]; q < M.strip_v[s + 1]; ++q) LL.vert_start[M.order_v[q]] = pos++;
+    ord.strip_ptr[s + 1] = pos;
+  }
+  if (pos != ml.N || ml.T != M.nf * ((i64)1 << (2 * l)))
+    throw std::runtime_error("lattice ordering: the mesh is not the coarse mesh refined " + std::to_string(l) + " times");
+  // a triangle containing each node (the first one), then the node's lattice position in that
+  // triangle's ancestor face (ancestor of fine triangle t = t >> 2l: red_refine numbers the children
+  // of t as 4t .. 4t+3)
+  std::vector<i64> n2t(ml.N, -1);
+  for (i64 t = 0; t < ml.T; ++t)
+    for (int v = 0; v < 3; ++v)
+      if (n2t[ml.tri[3 * t + v]] < 0) n2t[ml.tri[3 * t + v]] = t;
+  ord.new2old.assign(ml.N, -1);
+  ord.old2new.assign(ml.N, -1);
+  LL.type.assign(ml.N, 0);
+  std::vector<int> bad(1, 0);
+  std::mutex mx;
+  parallel_for(ml.N, [&](i64 v0, i64 v1) {
+    for (i64 v = v0; v < v1; ++v) {
+      const i64 t = n2t[v];
+      if (t < 0) {
+        std::lock_guard<std::mutex> lk(mx);
+        bad[0] = 1;
+        continue;
+      }
+      const i64 f = t >> (2 * l);
+      const i32 A = M.tri[3 * f], B = M.tri[3 * f + 1], C = M.tri[3 * f + 2];
+      const double xa = M.x[A], ya = M.y[A];
+      const double ex = M.x[B] - xa, ey = M.y[B] - ya, fx = M.x[C] - xa, fy = M.y[C] - ya;
+      const double det = ex * fy - fx * ey;
+      const double px = ml.x[v] - xa, py = ml.y[v] - ya;
+      const double li = n * ((px * fy - fx * py) / det), lj = n * ((ex * py - px * ey) / det);
+      const i64 i = std::llround(li), j = std::llround(lj);
+      if (std::fabs(li - i) > 1e-4 || std::fabs(lj - j) > 1e-4 || i < 0 || j < 0 || i + j > n) {
+        std::lock_guard<std::mutex> lk(mx);
+        bad[0] = 2;
+        continue;
+      }
+      i64 id;
+      uint8_t ty;
+      if (i >= 1 && j >= 1 && i + j <= n - 1) {
+        id = LL.face_start[f] + lat::rowbase((i32)j - 1, n) + (i - 1);
+        ty = 0;
+      } else if ((i == 0 && j == 0) || (i == n && j == 0) || (i == 0 && j == n)) {
+        id = LL.vert_start[i == n ? B : (j == n ? C : A)];
+        ty = 2;
+      } else {
+        i32 e, from;
+        i64 p;
+        if (j == 0) {
+          e = M.fe[3 * f], from = A, p = i;
+        } else if (i == 0) {
+          e = M.fe[3 * f + 1], from = A, p = j;
+        } else {
+          e = M.fe[3 * f + 2], from = B, p = j;
+        }
+        const i64 kk = M.ev[2 * e] == from ? p : n - p;
+        id = LL.edge_node(e, (i32)kk);
+        ty = 1;
+      }
+      ord.old2new[v] = (i32)id;
+      LL.type[id] = ty;
+    }
+  });
+  if (bad[0]) throw std::runtime_error("lattice ordering: a node is not on its macro face's lattice");
+  for (i64 v = 0; v < ml.N; ++v) {
+    const i32 g = ord.old2new[v];
+    if (g < 0 || ord.new2old[g] >= 0) throw std::runtime_error("lattice ordering is not a bijection");
+    ord.new2old[g] = (i32)v;
+  }
+  ord.cuts = M.cuts;
+}
+
+std::vector<i32> lattice_faces(const Macro& M, const LatticeLevel& LL, i64 r0, i64 nrows) {
+  std::vector<std::pair<i64, i32>> v;
+  if (LL.F > 0)
+    for (i64 f = 0; f < M.nf; ++f)
+      if (LL.face_start[f] >= r0 && LL.face_start[f] < r0 + nrows) v.push_back({LL.face_start[f], (i32)f});
+  std::sort(v.begin(), v.end());
+  std::vector<i32> out;
+  for (auto& p : v) out.push_back(p.second);
+  return out;
+}
+
+void lattice_tabs(const Macro& M, const LatticeLevel& LL, const std::vector<i32>& faces, i64 row0,
+                  const LocalPlan& lp, const std::vector<i32>* dof, std::vector<lat::FaceTab>& out) {
+  const i32 n = LL.n;
+  out.resize(faces.size());
+  auto loc = [&](i64 g) -> i32 { return to_local(lp, dof ? (*dof)[g] : (i32)g); };
+  for (size_t q = 0; q < faces.size(); ++q) {
+    const i32 f = faces[q];
+    const i32 A = M.tri[3 * f], B = M.tri[3 * f + 1];
+    lat::FaceTab& T = out[q];
+    T.base = row0 >= 0 ? (i32)(LL.face_start[f] - row0) : to_local(lp, (i32)LL.face_start[f]);
+    T.rec = (i32)q;
+    const i32 es[3] = {M.fe[3 * f], M.fe[3 * f + 1], M.fe[3 * f + 2]};
+    const i32 from[3] = {A, A, B};
+    int32_t* dst[3][2] = {{&T.ab0, &T.abs}, {&T.ac0, &T.acs}, {&T.bc0, &T.bcs}};
+    for (int k = 0; k < 3; ++k) {
+      const i32 e = es[k];
+      auto node = [&](i32 p) { return LL.edge_node(e, M.ev[2 * e] == from[k] ? p : n - p); };
+      const i32 a1 = loc(node(1)), a2 = n >= 3 ? loc(node(2)) : a1 + 1;
+      const i32 st = a2 - a1;
+      if (st != 1 && st != -1) throw std::runtime_error("lattice table: edge nodes are not contiguous");
+      for (i32 p = 1; p <= n - 1; ++p)
+        if (loc(node(p)) != a1 + st * (p - 1)) throw std::runtime_error("lattice table: edge nodes are not contiguous");
+      *dst[k][0] = a1 - st;
+      *dst[k][1] = st;
+    }
+  }
+}
+
+void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double dtnu, std::vector<double>& out) {
+  out.assign(faces.size() * (size_t)lat::NCOEF, 0.0);
+  for (size_t q = 0; q < faces.size(); ++q) {
+    const i32 f = faces[q];
+    const i32 o[3] = {M.tri[3 * f], M.tri[3 * f + 1], M.tri[3 * f + 2]};
+    const double x1 = M.x[o[0]], y1 = M.y[o[0]], x2 = M.x[o[1]], y2 = M.y[o[1]], x3 = M.x[o[2]], y3 = M.y[o[2]];
+    // the reference's element formulas (StokesColor.py:98-128, :130-165): K_T is scale-invariant,
+    // so every small triangle of the face has the macro triangle's element matrix
+    const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
+    const double yd[3] = {y2 - y3, y3 - y1, y1 - y2};
+    const double xd[3] = {x3 - x2, x1 - x3, x2 - x1};
+    const double den = 2 * std::fabs(det);
+    auto KT = [&](int p, int r) { return (yd[p] * yd[r] + xd[p] * xd[r]) / den; };
+    double* c = out.data() + q * lat::NCOEF;
+    // each lattice edge is shared by an "up" triangle (the face's orientation) and a "down" one (its
+    // point reflection), both contributing the same element entry
+    c[lat::C_KAB] = 2.0 * KT(0, 1);
+    c[lat::C_KAC] = 2.0 * KT(0, 2);
+    c[lat::C_KBC] = 2.0 * KT(1, 2);
+    c[lat::C_KD] = 2.0 * (KT(0, 0) + KT(1, 1) + KT(2, 2));
+    // level-l small triangle: det / 4^l, hat gradients 2^l (yd, xd) / det, area / 3 = |det| / (6 4^l)
+    const double s4 = std::ldexp(1.0, -2 * l), s2 = std::ldexp(1.0, l);
+    const double a3 = 0.5 * std::fabs(det) * s4 / 3.0;
+    double gx[3], gy[3];
+    for (int p = 0; p < 3; ++p) {
+      gx[p] = yd[p] * s2 / det;
+      gy[p] = xd[p] * s2 / det;
+    }
+    // G row of an interior node: a3 (g_col(up) - g_col(down)) per direction (the down triangle's
+    // hat gradients are the up triangle's, negated)
+    c[lat::C_G1X] = a3 * (gx[1] - gx[0]);
+    c[lat::C_G1Y] = a3 * (gy[1] - gy[0]);
+    c[lat::C_G2X] = a3 * (gx[2] - gx[0]);
+    c[lat::C_G2Y] = a3 * (gy[2] - gy[0]);
+    c[lat::C_G3X] = a3 * (gx[2] - gx[1]);
+    c[lat::C_G3Y] = a3 * (gy[2] - gy[1]);
+    c[lat::C_AS1] = 6.0 * a3 + 1e-12;
+    c[lat::C_VD] = 1.0 + dtnu * c[lat::C_KD];
+    c[lat::C_VS] = 1.0 / std::sqrt(c[lat::C_VD]);
+    c[lat::C_DTNU] = dtnu;
+    c[lat::C_DINV] = 1.0 / c[lat::C_KD];
+  }
+}
+
+void lattice_apply_host(int kind, int n, const std::vector<lat::FaceTab>& tab, const std::vector<double>& coef,
+                        const double* x0, const double* x1, const double* wsk, double* y,
+                        const std::vector<lat::FaceTab>* tab2, int n2) {
+  const i32 F = lat::interior_count(n);
+  const float rinv = 1.0f / (float)(n - 1);
+  for (size_t q = 0; q < tab.size(); ++q) {
+    const lat::FaceTab& T = tab[q];
+    if (kind >= 3) {  // transfers (pucfem_kernels_impl.hpp k_transfer)
+      const lat::FaceTab& G = (*tab2)[q];
+      for (i32 t = 0; t < F; ++t) {
+        int32_t i, j;
+        lat::coords(t, n, rinv, i, j);
+        double v;
+        if (kind == 3) {
+          const i32 i0 = i >> 1, i1 = (i + 1) >> 1, j0 = j >> 1, j1 = (j + 1) >> 1;
+          if (!(i & 1) && !(j & 1)) v = x0[lat::point(G, n2, i0, j0)];
+          else if (!(j & 1)) v = 0.5 * (x0[lat::point(G, n2, i0, j0)] + x0[lat::point(G, n2, i1, j0)]);
+          else if (!(i & 1)) v = 0.5 * (x0[lat::point(G, n2, i0, j0)] + x0[lat::point(G, n2, i0, j1)]);
+          else v = 0.5 * (x0[lat::point(G, n2, i0, j1)] + x0[lat::point(G, n2, i1, j0)]);
+        } else {
+          const i32 I = 2 * i, J = 2 * j;
+          v = x0[lat::point(G, n2, I, J)] +
+              0.5 * (x0[lat::point(G, n2, I - 1, J)] + x0[lat::point(G, n2, I + 1, J)] + x0[lat::point(G, n2, I, J - 1)] +
+                     x0[lat::point(G, n2, I, J + 1)] + x0[lat::point(G, n2, I + 1, J - 1)] +
+                     x0[lat::point(G, n2, I - 1, J + 1)]);
+        }
+        y[T.base + t] = v;
+      }
+      continue;
+    }
+    const double* c = coef.data() + (size_t)T.rec * lat::NCOEF;
+    for (i32 t = 0; t < F; ++t) {
+      int32_t i, j, nb[6];
+      bool in[6];
+      lat::coords(t, n, rinv, i, j);
+      lat::neighbours(T, n, t, i, j, nb, in);
+      const i32 r = T.base + t;
+      if (kind == 0) {
+        y[r] = c[lat::C_KD] * x0[r] + c[lat::C_KAB] * (x0[nb[0]] + x0[nb[1]]) + c[lat::C_KAC] * (x0[nb[2]] + x0[nb[3]]) +
+               c[lat::C_KBC] * (x0[nb[4]] + x0[nb[5]]);
+      } else if (kind == 1) {
+        y[r] = c[lat::C_G1X] * (x0[nb[1]] - x0[nb[0]]) + c[lat::C_G2X] * (x0[nb[2]] - x0[nb[3]]) +
+               c[lat::C_G3X] * (x0[nb[4]] - x0[nb[5]]) + c[lat::C_G1Y] * (x1[nb[1]] - x1[nb[0]]) +
+               c[lat::C_G2Y] * (x1[nb[2]] - x1[nb[3]]) + c[lat::C_G3Y] * (x1[nb[4]] - x1[nb[5]]);
+      } else {
+        const double vs = c[lat::C_VS];
+        double w[6];
+        for (int k = 0; k < 6; ++k) w[k] = (in[k] ? vs : wsk[nb[k]]) * x0[nb[k]];
+        y[r] = vs * (c[lat::C_VD] * vs * x0[r] +
+                     c[lat::C_DTNU] * (c[lat::C_KAB] * (w[0] + w[1]) + c[lat::C_KAC] * (w[2] + w[3]) +
+                                       c[lat::C_KBC] * (w[4] + w[5])));
+      }
+    }
+  }
 }
 
 }  // namespace pucfem

@@ -6,6 +6,8 @@
 #include <string>
 #include <vector>
 
+#include "pucfem_lattice.hpp"
+
 namespace pucfem {
 
 using i32 = int32_t;
@@ -124,7 +126,66 @@ struct Sell {
   std::vector<i64> slice_off;  // nslices+1, entry offsets
   std::vector<i32> slice_w;
   std::vector<i32> col;        // local column ids
+  // row list (lattice operators: the skeleton rows only), local output indices, padded to nslices*64
+  // with -1; empty: slice s holds rows s*64 .. s*64+63
+  std::vector<i32> rows;
+  i64 nnz = 0;  // stored (unpadded) entries of the listed rows (build_sell_rows)
 };
+// SELL of the rows `rows` (offsets from r0 into A's rows; they are also the local output indices),
+// columns resolved in `cols`; int32 columns only (rows are not contiguous)
+void build_sell_rows(const Csr& A, i64 r0, const std::vector<i32>& rows, const LocalPlan& cols, Sell& S);
+void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
+
+// ----------------------------------------------------------------------------- lattice layout
+// Macro primitives (the coarse mesh of a red-refinement hierarchy: faces, edges, vertices), their
+// strips and their order (pucfem_lattice.hpp).
+struct Macro {
+  i64 nv = 0, ne = 0, nf = 0;
+  std::vector<double> x, y;     // coarse coordinates
+  std::vector<i32> tri;         // 3 nf: A, B, C of every face (the coarse mesh's triangles, CCW)
+  std::vector<i32> ev;          // 2 ne: edge endpoints (lo < hi)
+  std::vector<i32> fe;          // 3 nf: edge ids of AB, AC, BC
+  int S = 1;                    // strips
+  std::vector<double> cuts;     // S - 1 increasing y values
+  // strip-major order: per strip its faces, then its edges, then its vertices (x-sorted); pos_* the
+  // position of a primitive in its kind's order, strip_* the first position of each strip (S + 1)
+  std::vector<i32> order_f, order_e, order_v;
+  std::vector<i32> strip_f, strip_e, strip_v;
+};
+// strips: 0 = auto; weights of the strip balance: interior / edge nodes at level `lw`
+void build_macro(const HostMesh& coarse, int strips, int lw, Macro& M);
+
+struct LatticeLevel {
+  int l = 0;
+  i32 n = 1, F = 0;               // segments per macro edge, interior nodes per face
+  std::vector<i64> face_start;    // per face id: internal id of its first interior node
+  std::vector<i64> edge_start;    // per edge id: internal id of its node k = 1 (from the lo endpoint)
+  std::vector<i64> vert_start;    // per vertex id
+  std::vector<uint8_t> type;      // per internal id: 0 face interior, 1 macro edge, 2 macro vertex
+  // global internal id of point k (1..n-1, from the lo endpoint) of edge e
+  i64 edge_node(i32 e, i32 k) const { return edge_start[e] + k - 1; }
+};
+// The internal ordering of level l of the hierarchy (ml = the coarse mesh red-refined l times):
+// strip-major; in a strip the face interiors (lattice layout), the edges, the vertices.  Fills
+// ord (new2old, old2new, strip_ptr, cuts) and LL.  Throws if a node is not on the lattice.
+void lattice_ordering(const HostMesh& ml, const Macro& M, int l, Ordering& ord, LatticeLevel& LL);
+
+// Face tables of one rank at one level: faces whose interiors are rows [r0, r0 + nrows) of the level
+// (internal ids), local indices through the plan `lp` (owned + ghosts); dof: the periodic master map
+// of the level (internal ids; null: the plain, unmerged table).  Returns the local face list (face ids).
+std::vector<i32> lattice_faces(const Macro& M, const LatticeLevel& LL, i64 r0, i64 nrows);
+void lattice_tabs(const Macro& M, const LatticeLevel& LL, const std::vector<i32>& faces, i64 row0,
+                  const LocalPlan& lp, const std::vector<i32>* dof, std::vector<lat::FaceTab>& out);
+// Coefficient records (lat::NCOEF doubles per face of `faces`) at level l
+void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double dtnu, std::vector<double>& out);
+// Host reference of the face stencils (CPU tests of the index arithmetic and the coefficients):
+// kind 0 y = K x (K-type stencil), 1 = the lumped divergence numerator Gx ux + Gy uy (x: 2 vectors,
+// x0 and x1), 2 = A_visc scaled (wsk: skeleton weights), 3 = prolongation rows (x0 on the coarse level
+// through tab2, n2 = n / 2), 4 = restriction rows (x0 on the fine level through tab2, n2 = 2 n); writes
+// the face rows of y only.
+void lattice_apply_host(int kind, int n, const std::vector<lat::FaceTab>& tab, const std::vector<double>& coef,
+                        const double* x0, const double* x1, const double* wsk, double* y,
+                        const std::vector<lat::FaceTab>* tab2 = nullptr, int n2 = 0);
 // rows [r0, r1) of `A` (global internal ids) -> local SELL; values extracted with sell_values().
 void build_sell(const Csr& A, const LocalPlan& lp, Sell& S);
 void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::vector<double>& val,

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pucfem_lattice.hpp"
+
 namespace pucfem {
 namespace dev {
 
@@ -28,6 +30,33 @@ struct SellDev {
   int64_t nslices, nrows;
   const int16_t* c16;  // same entries as int16 deltas from the slice's first row (band fits), or null
   int32_t wrap;        // c16: a decoded index below 0 wraps by this (the local length; ghosts at the end)
+  // row list (lattice operators: the skeleton rows), nslices * 64 local output indices, -1 padded;
+  // null: slice s holds rows s * 64 .. s * 64 + 63 (< nrows)
+  const int32_t* rows;
+  int64_t n_own;       // owned rows of the vectors the operator acts on (their ghosts follow)
+};
+// output row of lane `lane` of slice s, or -1
+__device__ __forceinline__ int64_t sell_row(const SellDev& A, int64_t s, int lane) {
+  const int64_t r = s * 64 + lane;
+  if (A.rows) return A.rows[r];
+  return r < A.nrows ? r : -1;
+}
+
+// The face-interior part of a lattice operator (pucfem_lattice.hpp): the first `nb` blocks of a launch
+// run the interior rows of the rank's faces (chunks of BS consecutive rows of one face, so a
+// block's face table entry and coefficients are uniform: scalar loads), the remaining blocks run the
+// skeleton rows through the SELL.  nb = 0: no face part (plain SELL operators).
+struct FaceDev {
+  const lat::FaceTab* tab;   // row side: one entry per face
+  const lat::FaceTab* tab2;  // transfers: the same faces on the other level (the gathered vector)
+  const double* coef;        // lat::NCOEF doubles per record
+  const float* coef32;
+  const double* wsk;         // viscous (op 1): skeleton column weights s_j (0: Dirichlet column)
+  int32_t nf, n, F, cpf;     // faces, lattice size, interior nodes per face, BS-row chunks per face
+  int32_t n2;                // transfers: lattice size of the gathered level
+  float rinv;                // 1 / (n - 1)
+  int32_t nb;                // blocks on the face part
+  int32_t op;                // 0 = stiffness-type stencil (K, merged pressure, level operators), 1 = scaled A_visc
 };
 
 template <class T>
@@ -110,6 +139,11 @@ __device__ __forceinline__ void by_width(int w, F&& f) {
 // slice range of this block
 __device__ __forceinline__ void block_slices(int64_t nslices, int64_t& s0, int64_t& s1) {
   const int64_t nb = gridDim.x, b = blockIdx.x;
+  s0 = (nslices * b) / nb;
+  s1 = (nslices * (b + 1)) / nb;
+}
+// slice range of block b of the nb blocks that run the SELL rows
+__device__ __forceinline__ void block_slices_n(int64_t nslices, int64_t nb, int64_t b, int64_t& s0, int64_t& s1) {
   s0 = (nslices * b) / nb;
   s1 = (nslices * (b + 1)) / nb;
 }

@@ -6,25 +6,95 @@
 namespace pucfem {
 namespace dev {
 
+// ----------------------------------------------------------------------------- lattice face rows
+// fn(F, lf, t, i, j) for the interior rows of the face part that block b of nbf runs (work items: chunks
+// of BS consecutive rows of one face; the item index is block-uniform, so the face table entry and
+// the coefficient record are scalar loads)
+template <class Fn>
+__device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
+  const int32_t items = fc.nf * fc.cpf;
+  for (int32_t it = b; it < items; it += nbf) {
+    const int32_t lf = it / fc.cpf;
+    const int32_t t = (it - lf * fc.cpf) * BS + (int32_t)threadIdx.x;
+    const lat::FaceTab F = fc.tab[lf];
+    if (t < fc.F) {
+      int32_t i, j;
+      lat::coords(t, fc.n, fc.rinv, i, j);
+      fn(F, lf, t, i, j);
+    }
+  }
+}
+
+// entries of an interior row of a stiffness-type face operator: a[0] the row's own, a[1 + k] its
+// neighbour k (lat::neighbours order).  op 0: K (every level's operator, the merged pressure
+// operator with the merged table); op 1: the Jacobi-scaled A_visc, S A S with s_f inside the face
+// and the skeleton columns' s_j (0 for Dirichlet columns, StokesColor.py:473-475) from fc.wsk
+template <typename T>
+__device__ __forceinline__ void face_kcoefs(const FaceDev& fc, const lat::FaceTab& F, const int32_t (&nb)[6],
+                                            const bool (&in)[6], T (&a)[7]) {
+  if constexpr (std::is_same<T, float>::value) {
+    const float* c = fc.coef32 + F.rec * lat::NCOEF;
+    a[0] = c[lat::C_KD];
+    a[1] = a[2] = c[lat::C_KAB];
+    a[3] = a[4] = c[lat::C_KAC];
+    a[5] = a[6] = c[lat::C_KBC];
+  } else {
+    const double* c = fc.coef + F.rec * lat::NCOEF;
+    const double k3[3] = {c[lat::C_KAB], c[lat::C_KAC], c[lat::C_KBC]};
+    if (fc.op == 1) {
+      const double vs = c[lat::C_VS], g = vs * c[lat::C_DTNU];
+      a[0] = vs * c[lat::C_VD] * vs;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a[1 + k] = (g * k3[k >> 1]) * (in[k] ? vs : fc.wsk[nb[k]]);
+    } else {
+      a[0] = c[lat::C_KD];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a[1 + k] = k3[k >> 1];
+    }
+  }
+}
+
+// the lumped gradient stencil of an interior row applied to x: (sum_j Gx_ij x_j, sum_j Gy_ij x_j)
+__device__ __forceinline__ void face_grad(const double* c, const int32_t (&nb)[6], const double* __restrict__ x,
+                                          double& gx, double& gy) {
+  const double d1 = x[nb[1]] - x[nb[0]], d2 = x[nb[2]] - x[nb[3]], d3 = x[nb[4]] - x[nb[5]];
+  gx = c[lat::C_G1X] * d1 + c[lat::C_G2X] * d2 + c[lat::C_G3X] * d3;
+  gy = c[lat::C_G1Y] * d1 + c[lat::C_G2Y] * d2 + c[lat::C_G3Y] * d3;
+}
+
 // ----------------------------------------------------------------------------- SpMV
 // y = A x over owned rows (generic; unit `pucfem_apply`, residuals).
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_spmv(SellDev A, const double* __restrict__ val,
+__global__ __launch_bounds__(BS) void k_spmv(SellDev A, FaceDev fc, const double* __restrict__ val,
                                              const double* __restrict__ x, double* __restrict__ y) {
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      double a[7];
+      face_kcoefs(fc, F, nb, in, a);
+      double acc = a[0] * x[F.base + t];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc += a[1 + k] * x[nb[k]];
+      y[F.base + t] = acc;
+    });
+    return;
+  }
   int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
+    const int64_t row = sell_row(A, s, lane);
     const int32_t base = (int32_t)(s * 64);
     double acc = 0.0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
       acc += val[e] * x[sell_col<C16, false>(A, e, base)];
     }
-    if (row < A.nrows) y[row] = acc;
+    if (row >= 0) y[row] = acc;
   }
 }
 
@@ -49,46 +119,66 @@ struct CgVecs {
 // r32 (optional): fp32 copy of r for the mixed-precision V-cycle, whose right-hand side is only
 // ever used in fp32 (bit-identical to converting inside the cycle, at half the bytes per read)
 template <int NR, bool C16>
-__global__ __launch_bounds__(BS) void k_cg_init(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
+__global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                 int64_t n_ghost, double* part_rr, double* part_bb,
                                                 float* __restrict__ r32 = nullptr) {
   __shared__ double sh[4];
-  int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = wave_id();
   double rr[NR], bb[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t off = A.off[s];
-    const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
-    const int32_t base = (int32_t)(s * 64);
-    double acc[NR];
+  auto finish = [&](int64_t row, const double (&acc)[NR]) {
 #pragma unroll
-    for (int c = 0; c < NR; ++c) acc[c] = 0.0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      const double a = val[e];
-      const int32_t j = sell_col<C16, false>(A, e, base);
-#pragma unroll
-      for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
+    for (int c = 0; c < NR; ++c) {
+      const double b = v.b[c][row];
+      const double r = b - acc[c];
+      v.r[c][row] = r;
+      if (r32) r32[row] = (float)r;
+      v.po[c][row] = 0.0;
+      rr[c] += r * r;
+      bb[c] += b * b;
     }
-    if (row < A.nrows) {
+  };
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      double a[7];
+      face_kcoefs(fc, F, nb, in, a);
+      const int64_t row = F.base + t;
+      double acc[NR];
 #pragma unroll
       for (int c = 0; c < NR; ++c) {
-        const double b = v.b[c][row];
-        const double r = b - acc[c];
-        v.r[c][row] = r;
-        if (r32) r32[row] = (float)r;
-        v.po[c][row] = 0.0;
-        rr[c] += r * r;
-        bb[c] += b * b;
+        acc[c] = a[0] * v.y[c][row];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) acc[c] += a[1 + k] * v.y[c][nb[k]];
       }
+      finish(row, acc);
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t off = A.off[s];
+      const int w = A.w[s];
+      const int64_t row = sell_row(A, s, lane);
+      const int32_t base = (int32_t)(s * 64);
+      double acc[NR];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+      for (int k = 0; k < w; ++k) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        const double a = val[e];
+        const int32_t j = sell_col<C16, false>(A, e, base);
+#pragma unroll
+        for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
+      }
+      if (row >= 0) finish(row, acc);
     }
   }
   // zero the ghost part of p_old (ghost r arrives by halo exchange)
-  for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
+  for (int64_t g = A.n_own + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.n_own + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) v.po[c][g] = 0.0;
@@ -112,7 +202,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
                                           const double (&beta)[NR], int64_t s, int lane, double (&pq)[NR]) {
   const int64_t off = A.off[s];
   const int w = A.w[s];
-  const int64_t row = s * 64 + lane;
+  const int64_t row = sell_row(A, s, lane);
   const int32_t base = (int32_t)(s * 64);
   double acc[NR];
 #pragma unroll
@@ -150,7 +240,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
   } else {
     generic();
   }
-  if (row < A.nrows) {
+  if (row >= 0) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
       const double p = v.r[c][row] + beta[c] * v.po[c][row];
@@ -162,7 +252,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 }
 
 template <int NR, int WMAX, bool NT, bool C16>
-__global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restrict__ val, CgVecs<NR> v,
+__global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
                                                int* ctl, int it, int maxit, double tol2, double* part_pq,
@@ -198,14 +288,40 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, const double* __restri
       if (it == 0) scal[8 + c] = bb[c];
     }
   }
-  int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = wave_id();
   double pq[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, s, lane, pq);
-  for (int64_t g = A.nrows + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.nrows + n_ghost;
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      double a[7];
+      face_kcoefs(fc, F, nb, in, a);
+      const int64_t row = F.base + t;
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        const double* r = v.r[c];
+        const double* po = v.po[c];
+        double g[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) g[k] = r[nb[k]] + beta[c] * po[nb[k]];
+        const double p = r[row] + beta[c] * po[row];
+        double q = a[0] * p;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) q += a[1 + k] * g[k];
+        v.pn[c][row] = p;
+        v.q[c][row] = q;
+        pq[c] += p * q;
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, s, lane, pq);
+  }
+  for (int64_t g = A.n_own + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.n_own + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) v.pn[c][g] = v.r[c][g] + beta[c] * v.po[c][g];
@@ -467,52 +583,75 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double
 // Optionally the pressure RHS of the row-scaled system: braw = (M + 1e-12) * (-(1/DT) * div)
 // (StokesColor.py:554 with A_pressure = K / (M + 1e-12)).  Partials: [0] max|div|, [1] sum(braw).
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_div(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
-                                            const double* __restrict__ ux, const double* __restrict__ uy,
-                                            const double* __restrict__ as1, double* __restrict__ div,
-                                            const double* __restrict__ mp, double negidt, double* __restrict__ braw,
-                                            double* part) {
+__global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double* __restrict__ gx,
+                                            const double* __restrict__ gy, const double* __restrict__ ux,
+                                            const double* __restrict__ uy, const double* __restrict__ as1,
+                                            double* __restrict__ div, const double* __restrict__ mp, double negidt,
+                                            double* __restrict__ braw, double* part) {
   __shared__ double sh[4];
-  int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = wave_id();
   double mx = 0.0, sb = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t off = A.off[s];
-    const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
-    const int32_t base = (int32_t)(s * 64);
-    double acc = 0.0;
-    by_width(w, [&](auto wc) {
-      constexpr int WN = decltype(wc)::value;
-      if constexpr (WN > 0) {
-        int32_t cj[WN];
-        double ax[WN], ay[WN];
-#pragma unroll
-        for (int k = 0; k < WN; ++k) {
-          const int64_t e = off + (int64_t)k * 64 + lane;
-          cj[k] = sell_col<C16>(A, e, base);
-          ax[k] = ldnt(gx + e);
-          ay[k] = ldnt(gy + e);
-        }
-#pragma unroll
-        for (int k = 0; k < WN; ++k) acc += ax[k] * ux[cj[k]] + ay[k] * uy[cj[k]];
-      } else {
-        for (int k = 0; k < w; ++k) {
-          const int64_t e = off + (int64_t)k * 64 + lane;
-          const int32_t j = sell_col<C16>(A, e, base);
-          acc += ldnt(gx + e) * ux[j] + ldnt(gy + e) * uy[j];
-        }
-      }
-    });
-    if (row < A.nrows) {
-      const double d = acc / as1[row];
+  if ((int32_t)blockIdx.x < fc.nb) {
+    // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      const double* c = fc.coef + F.rec * lat::NCOEF;
+      double ax, ay, bx, by;
+      face_grad(c, nb, ux, ax, ay);
+      face_grad(c, nb, uy, bx, by);
+      const int64_t row = F.base + t;
+      const double as = c[lat::C_AS1];
+      const double d = (ax + by) / as;
       div[row] = d;
       mx = fmax(mx, fabs(d));
       if (braw) {
-        const double b = mp[row] * (negidt * d);
+        const double b = as * (negidt * d);
         braw[row] = b;
         sb += b;
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t off = A.off[s];
+      const int w = A.w[s];
+      const int64_t row = sell_row(A, s, lane);
+      const int32_t base = (int32_t)(s * 64);
+      double acc = 0.0;
+      by_width(w, [&](auto wc) {
+        constexpr int WN = decltype(wc)::value;
+        if constexpr (WN > 0) {
+          int32_t cj[WN];
+          double ax[WN], ay[WN];
+#pragma unroll
+          for (int k = 0; k < WN; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            cj[k] = sell_col<C16>(A, e, base);
+            ax[k] = ldnt(gx + e);
+            ay[k] = ldnt(gy + e);
+          }
+#pragma unroll
+          for (int k = 0; k < WN; ++k) acc += ax[k] * ux[cj[k]] + ay[k] * uy[cj[k]];
+        } else {
+          for (int k = 0; k < w; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            const int32_t j = sell_col<C16>(A, e, base);
+            acc += ldnt(gx + e) * ux[j] + ldnt(gy + e) * uy[j];
+          }
+        }
+      });
+      if (row >= 0) {
+        const double d = acc / as1[row];
+        div[row] = d;
+        mx = fmax(mx, fabs(d));
+        if (braw) {
+          const double b = mp[row] * (negidt * d);
+          braw[row] = b;
+          sb += b;
+        }
       }
     }
   }
@@ -547,18 +686,41 @@ __global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int
 // projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
 // projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __restrict__ gx,
+__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const double* __restrict__ gx,
                                                   const double* __restrict__ gy, const double* __restrict__ p,
                                                   const double* __restrict__ as1, double dt, int mode,
                                                   const uint8_t* __restrict__ dirflag, const double* usx,
                                                   const double* usy, double* ux, double* uy) {
+  auto finish = [&](int64_t row, double gpx, double gpy, bool dirichlet) {
+    if (mode == 0) {
+      ux[row] = usx[row] - dt * gpx;
+      uy[row] = usy[row] - dt * gpy;
+    } else if (!dirichlet) {
+      ux[row] = ux[row] - dt * gpx;
+      uy[row] = uy[row] - dt * gpy;
+    }
+  };
+  if ((int32_t)blockIdx.x < fc.nb) {
+    // interior rows are never Dirichlet nodes
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      const double* c = fc.coef + F.rec * lat::NCOEF;
+      double ax, ay;
+      face_grad(c, nb, p, ax, ay);
+      const double d = c[lat::C_AS1];
+      finish(F.base + t, ax / d, ay / d, false);
+    });
+    return;
+  }
   int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
+    const int64_t row = sell_row(A, s, lane);
     const int32_t base = (int32_t)(s * 64);
     double ax = 0.0, ay = 0.0;
     by_width(w, [&](auto wc) {
@@ -588,32 +750,38 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, const double* __res
         }
       }
     });
-    if (row < A.nrows) {
+    if (row >= 0) {
       const double d = as1[row];
-      const double gpx = ax / d, gpy = ay / d;
-      if (mode == 0) {
-        ux[row] = usx[row] - dt * gpx;
-        uy[row] = usy[row] - dt * gpy;
-      } else if (!dirflag[row]) {
-        ux[row] = ux[row] - dt * gpx;
-        uy[row] = uy[row] - dt * gpy;
-      }
+      finish(row, ax / d, ay / d, dirflag[row] != 0);
     }
   }
 }
 
 // gradient only (calculate_gradiant, StokesColor.py:224-263) for the unit op
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_grad(SellDev A, const double* __restrict__ gx, const double* __restrict__ gy,
-                                             const double* __restrict__ p, const double* __restrict__ as1,
-                                             double* outx, double* outy) {
+__global__ __launch_bounds__(BS) void k_grad(SellDev A, FaceDev fc, const double* __restrict__ gx,
+                                             const double* __restrict__ gy, const double* __restrict__ p,
+                                             const double* __restrict__ as1, double* outx, double* outy) {
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      const double* c = fc.coef + F.rec * lat::NCOEF;
+      double ax, ay;
+      face_grad(c, nb, p, ax, ay);
+      outx[F.base + t] = ax / c[lat::C_AS1];
+      outy[F.base + t] = ay / c[lat::C_AS1];
+    });
+    return;
+  }
   int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
     const int w = A.w[s];
-    const int64_t row = s * 64 + lane;
+    const int64_t row = sell_row(A, s, lane);
     const int32_t base = (int32_t)(s * 64);
     double ax = 0.0, ay = 0.0;
     for (int k = 0; k < w; ++k) {
@@ -622,7 +790,7 @@ __global__ __launch_bounds__(BS) void k_grad(SellDev A, const double* __restrict
       ax += gx[e] * pj;
       ay += gy[e] * pj;
     }
-    if (row < A.nrows) {
+    if (row >= 0) {
       outx[row] = ax / as1[row];
       outy[row] = ay / as1[row];
     }
@@ -1107,38 +1275,64 @@ __device__ __forceinline__ T sell_row_dot(const SellDev& A, const VT* __restrict
 // LV: a level tag with no effect on the code (1: the finest level, 2: pucfem_bench_kernel), so that
 // profilers report the finest level's launches apart from the coarser levels' ones.
 template <typename T, typename TB, typename TO, typename VT, bool C16, int LV = 0>
-__global__ __launch_bounds__(BS) void k_cheb(SellDev A, const VT* __restrict__ val, const T* __restrict__ dinv,
-                                             const TB* __restrict__ b, const T* __restrict__ xin,
-                                             TO* __restrict__ xout, T* __restrict__ d, double c1, double c2,
-                                             double c20, int mode, const int* ctl, const double* __restrict__ rdot,
-                                             double* part) {
+__global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __restrict__ val,
+                                             const T* __restrict__ dinv, const TB* __restrict__ b,
+                                             const T* __restrict__ xin, TO* __restrict__ xout, T* __restrict__ d,
+                                             double c1, double c2, double c20, int mode, const int* ctl,
+                                             const double* __restrict__ rdot, double* part) {
   __shared__ double sh[4];
   if (ctl && ctl[0]) return;
-  int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
-  const int lane = threadIdx.x & 63, wv = wave_id();
   const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
   double acc_rz = 0.0;
-  for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t row = s * 64 + lane;
-    T ax = 0;
-    if (mode == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
-    else if (mode == 2)
-      ax = sell_row_dot_g<C16, T>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
-    if (row < A.nrows) {
-      T dn, xo;
-      if (mode == 0) {
-        dn = tc2 * dinv[row] * (T)b[row];
-        xo = dn;
-      } else {
-        const T x1 = mode == 2 ? tc20 * dinv[row] * (T)b[row] : xin[row];
-        const T d1 = mode == 2 ? x1 : d[row];
-        dn = tc1 * d1 + tc2 * dinv[row] * ((T)b[row] - ax);
-        xo = x1 + dn;
+  // the step's row update from A x (ax), the row's 1 / diag and the fused first step's x1
+  auto finish = [&](int64_t row, T ax, T di) {
+    T dn, xo;
+    if (mode == 0) {
+      dn = tc2 * di * (T)b[row];
+      xo = dn;
+    } else {
+      const T x1 = mode == 2 ? tc20 * di * (T)b[row] : xin[row];
+      const T d1 = mode == 2 ? x1 : d[row];
+      dn = tc1 * d1 + tc2 * di * ((T)b[row] - ax);
+      xo = x1 + dn;
+    }
+    d[row] = dn;
+    xout[row] = (TO)xo;
+    if (rdot) acc_rz += rdot[row] * (double)xo;
+  };
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      T a[7];
+      face_kcoefs(fc, F, nb, in, a);
+      const T di = std::is_same<T, float>::value ? (T)fc.coef32[F.rec * lat::NCOEF + lat::C_DINV]
+                                                 : (T)fc.coef[F.rec * lat::NCOEF + lat::C_DINV];
+      const int64_t row = F.base + t;
+      T ax = 0;
+      if (mode == 1) {
+        ax = a[0] * xin[row];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ax += a[1 + k] * xin[nb[k]];
+      } else if (mode == 2) {  // x1 = c20 Dinv b at the gathered columns (skeleton columns: their own dinv)
+        ax = a[0] * (tc20 * di * (T)b[row]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ax += a[1 + k] * (tc20 * (in[k] ? di : dinv[nb[k]]) * (T)b[nb[k]]);
       }
-      d[row] = dn;
-      xout[row] = (TO)xo;
-      if (rdot) acc_rz += rdot[row] * (double)xo;
+      finish(row, ax, di);
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t row = sell_row(A, s, lane);
+      T ax = 0;
+      if (mode == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
+      else if (mode == 2)
+        ax = sell_row_dot_g<C16, T>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
+      if (row >= 0) finish(row, ax, dinv[row]);
     }
   }
   if (rdot) {
@@ -1149,37 +1343,80 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, const VT* __restrict__ v
 
 // res = b - A x
 template <typename T, typename TB, typename VT, bool C16, int LV = 0>
-__global__ __launch_bounds__(BS) void k_resid(SellDev A, const VT* __restrict__ val, const TB* __restrict__ b,
-                                              const T* __restrict__ x, T* __restrict__ res, const int* ctl) {
+__global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* __restrict__ val,
+                                              const TB* __restrict__ b, const T* __restrict__ x,
+                                              T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
+  if ((int32_t)blockIdx.x < fc.nb) {
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      int32_t nb[6];
+      bool in[6];
+      lat::neighbours(F, fc.n, t, i, j, nb, in);
+      T a[7];
+      face_kcoefs(fc, F, nb, in, a);
+      const int64_t row = F.base + t;
+      T ax = a[0] * x[row];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) ax += a[1 + k] * x[nb[k]];
+      res[row] = (T)b[row] - ax;
+    });
+    return;
+  }
   int64_t s0, s1;
-  block_slices(A.nslices, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
-    const int64_t row = s * 64 + lane;
+    const int64_t row = sell_row(A, s, lane);
     const T ax = sell_row_dot<C16>(A, val, x, s, lane);
-    if (row < A.nrows) res[row] = (T)b[row] - ax;
+    if (row >= 0) res[row] = (T)b[row] - ax;
   }
 }
 
-// y = T x (restriction) or y += T x (prolongation, add = 1)
+// y = T x (restriction) or y += T x (prolongation, add = 1).  Face part: prolongation rows are the
+// fine level's interior nodes (linear interpolation from the coarse lattice, fc.tab2 = the coarse
+// level's merged table); restriction rows the coarse level's interior nodes (the transpose: the
+// fine node on top with weight 1 and its six midpoint neighbours with 1/2, all fine interior nodes).
 template <typename T>
-__global__ __launch_bounds__(BS) void k_transfer(SellDev M, const T* __restrict__ val, const T* __restrict__ x,
-                                                 T* __restrict__ y, int add, const int* ctl) {
+__global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T* __restrict__ val,
+                                                 const T* __restrict__ x, T* __restrict__ y, int add, const int* ctl) {
   if (ctl && ctl[0]) return;
+  if ((int32_t)blockIdx.x < fc.nb) {
+    const int32_t n2 = fc.n2;
+    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+      const lat::FaceTab G = fc.tab2[lf];
+      const int64_t row = F.base + t;
+      if (add) {
+        const int32_t i0 = i >> 1, i1 = (i + 1) >> 1, j0 = j >> 1, j1 = (j + 1) >> 1;
+        T v;
+        if (!(i & 1) && !(j & 1)) v = x[lat::point(G, n2, i0, j0)];
+        else if (!(j & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i1, j0)]);
+        else if (!(i & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i0, j1)]);
+        else v = (T)0.5 * (x[lat::point(G, n2, i0, j1)] + x[lat::point(G, n2, i1, j0)]);
+        y[row] = y[row] + v;
+      } else {
+        const int32_t I = 2 * i, J = 2 * j;
+        const T c = x[lat::point(G, n2, I, J)];
+        const T h = x[lat::point(G, n2, I - 1, J)] + x[lat::point(G, n2, I + 1, J)] + x[lat::point(G, n2, I, J - 1)] +
+                    x[lat::point(G, n2, I, J + 1)] + x[lat::point(G, n2, I + 1, J - 1)] +
+                    x[lat::point(G, n2, I - 1, J + 1)];
+        y[row] = c + (T)0.5 * h;
+      }
+    });
+    return;
+  }
   int64_t s0, s1;
-  block_slices(M.nslices, s0, s1);
+  block_slices_n(M.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = M.off[s];
     const int w = M.w[s];
-    const int64_t row = s * 64 + lane;
+    const int64_t row = sell_row(M, s, lane);
     T acc = 0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
       acc += val[e] * x[M.col[e]];
     }
-    if (row < M.nrows) y[row] = add ? y[row] + acc : acc;
+    if (row >= 0) y[row] = add ? y[row] + acc : acc;
   }
 }
 

@@ -70,6 +70,9 @@ class Tolerances:
     # "auto": small meshes (<= 1500 nodes, one rank) solve with precomputed dense inverses and meshes of
     # <= 4096 nodes with a one-workgroup CG; "iterative": the large-mesh multi-kernel CG path on every mesh
     solver_path: str = "auto"
+    # "auto": on multigrid hierarchies (>= 2 levels) the rows of the nodes inside the coarse triangles are
+    # matrix-free lattice stencils; "assembled": stored SELL rows everywhere
+    operators: str = "auto"
 
     @classmethod
     def production(cls, **kw):
@@ -157,7 +160,8 @@ class Context:
                         mg_single=int(tol.mg_single), mg_rep_nodes=tol.mg_rep_nodes,
                         mg_f32_vals=2 if tol.mg_f16_vals == "coarse" else int(not tol.mg_f16_vals),
                         idx32=int(not tol.index16), proj_k=tol.proj_k, proj_k_visc=tol.proj_k_visc,
-                        mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path])
+                        mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path],
+                        assembled={"auto": 0, "assembled": 1}[tol.operators])
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
@@ -205,7 +209,7 @@ class Context:
         visc = {0: "dense", 1: "block", 2: "multi-kernel"}
         pres = {0: "dense", 1: "block", 2: "jacobi-cg", 3: "mg-pcg"}
         return dict(viscous=visc[o[0]], pressure=pres[o[1]], reseeds=o[2], basis_p=o[3], basis_p2=o[4],
-                    visc_extrap_order=o[5], proj_k=o[6])
+                    visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7]))
 
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))

@@ -29,7 +29,7 @@ def run_ranks(mesh, world, scheme, tol, steps, bc, dt):
         try:
             sim = pf.StokesSimulation(mesh, bc, dt, scheme, device=0, tol=tol, dist=(r, world, uid))
             st = sim.step(steps)
-            res = {"u": sim.u, "info": sim.ctx.info(), "stats": st}
+            res = {"u": sim.u, "info": sim.ctx.info(), "stats": st, "lattice": sim.ctx.path_info()["lattice"]}
             if scheme == "color":
                 res["c"] = sim.c
             else:
@@ -57,12 +57,17 @@ def run_ranks(mesh, world, scheme, tol, steps, bc, dt):
 def test_color_partitioned_matches_single_rank(world, precond, single, rep):
     mesh = pf.load_mesh("fine", refine=3)
     tol = pf.Tolerances(rtol_pres=1e-12, rtol_visc=1e-13, precond=precond, mg_single=single, mg_rep_nodes=rep)
+    lattice = precond == "mg"
     bc = pf.SquirmerBC()
     out = run_ranks(mesh, world, "color", tol, 3, bc, 0.05)
     assert sum(o["info"]["n_own"] for o in out) == mesh.N
     assert all(o["info"]["n_ghost"] > 0 for o in out)
-    # int16 column deltas stay on with ghost columns (they wrap modulo the local vector length)
-    assert all(o["info"]["index16_P"] and o["info"]["index16_Pp"] for o in out)
+    # the lattice operators (matrix-free face stencils, SELL skeleton rows) on every rank; with the
+    # Jacobi-preconditioned pressure the stored SELL operators, whose int16 column deltas stay on with
+    # ghost columns (they wrap modulo the local vector length)
+    assert all(o["lattice"] == lattice for o in out)
+    if not lattice:
+        assert all(o["info"]["index16_P"] and o["info"]["index16_Pp"] for o in out)
     u = sum(o["u"] for o in out)  # every rank fills its owned rows
     ref = pf.StokesSimulation(mesh, bc, 0.05, "color", tol=tol)
     st = ref.step(3)

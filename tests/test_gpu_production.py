@@ -33,15 +33,22 @@ def _need_gpu():
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
 
 
-def test_production_color_L3_every_step_vs_oracle():
+@pytest.mark.parametrize("operators", ["auto", "assembled"])
+def test_production_color_L3_every_step_vs_oracle(operators):
     """48 StokesColor steps on mesh_fine x3 (69,632 nodes) with the bench's exact settings: the
-    projection bases fill (24 directions per pressure solve) and are re-seeded at least twice."""
+    projection bases fill (24 directions per pressure solve) and are re-seeded at least twice.
+    operators 'auto' is the production path (matrix-free lattice stencils on the face interiors,
+    SELL rows on the skeleton); 'assembled' the stored SELL operators (int16 column deltas) for every row."""
     mesh = pf.load_mesh("fine", refine=3)
-    tol = S.Tolerances.production()
+    tol = S.Tolerances.production(operators=operators)
     assert tol.rtol_pres == S.PRODUCTION_RTOL_PRES
     sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
     info = sim.ctx.info()
-    assert info["mg_levels"] == 4 and info["index16_P"] and info["index16_Pp"], info
+    assert info["mg_levels"] == 4, info
+    if operators == "auto":
+        assert sim.ctx.path_info()["lattice"]
+    else:
+        assert info["index16_P"] and info["index16_Pp"] and not sim.ctx.path_info()["lattice"], info
     ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.05, 0.1, -2.0, 0.0, "color")
     u, c = ref.initial()
     worst_u = worst_c = 0.0
@@ -59,7 +66,8 @@ def test_production_color_L3_every_step_vs_oracle():
     assert path["viscous"] == "multi-kernel" and path["pressure"] == "mg-pcg", path
     assert path["proj_k"] == 24 and path["reseeds"] >= 2, path
     assert path["visc_extrap_order"] == 3, path
-    print(f"L3 production path, 48 steps: max |u - oracle| = {worst_u:.2e}, max |c - oracle| = {worst_c:.2e}")
+    print(f"L3 production path ({operators}), 48 steps: max |u - oracle| = {worst_u:.2e}, "
+          f"max |c - oracle| = {worst_c:.2e}")
     sim.close()
 
 
@@ -83,7 +91,7 @@ def test_production_food_pusher_L2_vs_oracle():
         assert np.abs(got[ok] - pts[ok]).max() < TOL_STEP, k
         assert np.array_equal(sim.tracer_status, status), k
         assert st.eaten == status.sum()
-    assert sim.ctx.path_info()["pressure"] == "mg-pcg"
+    assert sim.ctx.path_info()["pressure"] == "mg-pcg" and sim.ctx.path_info()["lattice"]
     sim.close()
 
 
