@@ -574,7 +574,7 @@ struct Ctx {
       return h_ctl[1];
     }
     const FaceDev fc = hf.part();
-    const int nb = fc.nb + std::min(nb_for(A.nslices), MAXB - fc.nb);
+    const int nb = grid_part(fc, A);
     CgVecs<NR> v;
     for (int c = 0; c < NR; ++c) {
       v.y[c] = y[c];
@@ -647,8 +647,16 @@ struct Ctx {
   // last step writes its result (in fp64) to zout instead and nullptr is returned.
   // launch grids of a lattice operator: its face blocks, then the SELL blocks (launches that write
   // partials stay within MAXB blocks)
-  static int grid_part(const FaceDev& f, const DevSell& A) { return f.nb + std::min(nb_for(A.nslices), MAXB - f.nb); }
-  int grid_full(const FaceDev& f, const DevSell& A) const { return f.nb + nb_mg(A.nslices); }
+  // The SELL blocks come first and their count is a multiple of 8, so the face blocks' hardware ids
+  // keep their XCD (id % 8) for the XCD-aware item order of face_rows.
+  static int sell_blocks(int nb, const FaceDev& f) {
+    if (!f.nb) return nb;
+    return std::min((nb + 7) & ~7, (MAXB - f.nb) & ~7);
+  }
+  static int grid_part(const FaceDev& f, const DevSell& A) { return f.nb + sell_blocks(nb_for(A.nslices), f); }
+  int grid_full(const FaceDev& f, const DevSell& A) const {
+    return f.nb + (f.nb ? (nb_mg(A.nslices) + 7) & ~7 : nb_mg(A.nslices));
+  }
 
   template <typename T, typename TB>
   T* mg_smooth(MgLevel& L, const DevSell& A, const HFace& hf, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb,
@@ -1252,7 +1260,7 @@ Ctx* C(void* p) { return static_cast<Ctx*>(p); }
 
 void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* val, const double* x, double* y) {
   with_c16(A, [&](auto c16) {
-    hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(fc.nb + Ctx::nb_for(A.nslices)), dim3(BS), 0, st, A.view(),
+    hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(Ctx::grid_part(fc, A)), dim3(BS), 0, st, A.view(),
                        fc, val, x, y);
   });
 }
@@ -1720,7 +1728,7 @@ void build(Ctx& c) {
         h.d.nf = (int32_t)tab.size();
         h.d.n = n;
         h.d.F = F;
-        h.d.cpf = (F + BS - 1) / BS;
+        h.d.cpf = (F + BS * FACE_RPT - 1) / (BS * FACE_RPT);
         h.d.n2 = l2 >= 0 ? 1 << l2 : 0;
         h.d.rinv = 1.0f / (float)(n - 1);
         h.d.nb = 0;
@@ -3094,7 +3102,33 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
     auto launch = [&](hipEvent_t a, hipEvent_t e) {
       with_c16(A, [&](auto c16) {
         constexpr bool C16 = decltype(c16)::value;
+        SellDev none = A.view();
+        none.nslices = 0;
         switch (kernel) {
+          case 3:  // the face part alone
+            hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(ff.nb + 8), dim3(BS), 0, c.st, a, e, 0,
+                                  none, ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
+                                  (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
+                                  (const double*)nullptr, (double*)nullptr);
+            break;
+          case 4:  // the SELL (skeleton) part alone
+            hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(c.nb_mg(A.nslices)), dim3(BS), 0, c.st,
+                                  a, e, 0, A.view(), FaceDev{}, (const float*)B.Aval, (const float*)B.dinv,
+                                  (const float*)c.r32, (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1,
+                                  (const int*)nullptr, (const double*)nullptr, (double*)nullptr);
+            break;
+          case 5:  // k_cg_dir, the face part alone
+            hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(fpt.nb + 8), dim3(BS), 0, c.st, a, e, 0, none, fpt,
+                                  (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
+                                  (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
+                                  (const double*)nullptr, 0, 0);
+            break;
+          case 6:  // k_cg_dir, the SELL (skeleton) part alone
+            hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(Ctx::nb_for(A.nslices)), dim3(BS), 0, c.st, a, e, 0,
+                                  A.view(), FaceDev{}, (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one,
+                                  1, 1, (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
+                                  (const double*)nullptr, 0, 0);
+            break;
           case 0:
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0,
                                   A.view(), ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
@@ -3119,6 +3153,10 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
     const double fr = (double)c.fP.rows, sk = (double)A.nrows, rb = A.row_bytes();
     switch (kernel) {
       case 0: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (28.0 + rb) * sk + 24.0 * fr; break;
+      case 3: by = 24.0 * fr; break;
+      case 4: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (28.0 + rb) * sk; break;
+      case 5: by = 32.0 * fr; break;
+      case 6: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk; break;
       case 1: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (12.0 + rb) * sk + 12.0 * fr; break;
       default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk + 32.0 * fr;
     }

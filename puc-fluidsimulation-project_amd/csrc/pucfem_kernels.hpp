@@ -22,6 +22,7 @@ constexpr int BS = 256;     // threads per block
 constexpr int MAXB = 8192;  // max blocks of a partial-producing launch (= partial stride)
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
 constexpr int SLB = 4096;   // max blocks (= partial stride) of the semi-Lagrangian kernel
+constexpr int FACE_RPT = 4; // face-interior rows per thread of a lattice work item (BS * FACE_RPT rows of one face)
 
 struct SellDev {
   const int64_t* off;  // nslices+1
@@ -42,17 +43,18 @@ __device__ __forceinline__ int64_t sell_row(const SellDev& A, int64_t s, int lan
   return r < A.nrows ? r : -1;
 }
 
-// The face-interior part of a lattice operator (pucfem_lattice.hpp): the first `nb` blocks of a launch
-// run the interior rows of the rank's faces (chunks of BS consecutive rows of one face, so a
-// block's face table entry and coefficients are uniform: scalar loads), the remaining blocks run the
-// skeleton rows through the SELL.  nb = 0: no face part (plain SELL operators).
+// The face-interior part of a lattice operator (pucfem_lattice.hpp): the last `nb` blocks of a launch
+// run the interior rows of the rank's faces (chunks of BS * FACE_RPT consecutive rows of one face, so a
+// block's face table entry and coefficients are uniform: scalar loads), the first blocks run the
+// skeleton rows through the SELL (dispatched first: their rows are longer and their gathers slower, so
+// they overlap the face blocks instead of trailing them).  nb = 0: no face part (plain SELL operators).
 struct FaceDev {
   const lat::FaceTab* tab;   // row side: one entry per face
   const lat::FaceTab* tab2;  // transfers: the same faces on the other level (the gathered vector)
   const double* coef;        // lat::NCOEF doubles per record
   const float* coef32;
   const double* wsk;         // viscous (op 1): skeleton column weights s_j (0: Dirichlet column)
-  int32_t nf, n, F, cpf;     // faces, lattice size, interior nodes per face, BS-row chunks per face
+  int32_t nf, n, F, cpf;     // faces, lattice size, interior nodes per face, BS * FACE_RPT-row chunks per face
   int32_t n2;                // transfers: lattice size of the gathered level
   float rinv;                // 1 / (n - 1)
   int32_t nb;                // blocks on the face part
@@ -62,6 +64,14 @@ struct FaceDev {
 template <class T>
 __device__ __forceinline__ T ldnt(const T* p) {
   return __builtin_nontemporal_load(p);
+}
+// Non-temporal (streaming) store of a kernel's output vector: the lattice kernels' gathers keep the
+// L2 busy with the input vectors, and ordinary stores of the outputs allocate L2 lines that then have
+// to be written back; the streaming store halves the time of a gather kernel with two fp64 outputs
+// (tools/face_lab.hip: 119 -> 61 us for the 14M-row direction kernel, the same bytes as a pure copy).
+template <class T>
+__device__ __forceinline__ void stnt(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
 }
 // column of entry e of the slice whose first row is `base`.  C16: the operator's band fits int16, so
 // the index stream is 2 B/entry instead of 4 (strip ordering keeps every neighbour within a few

@@ -13,14 +13,27 @@ namespace dev {
 template <class Fn>
 __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
   const int32_t items = fc.nf * fc.cpf;
+  // one block per item (launches without partials): consecutive chunks of a face run on one XCD
+  // (blocks are dealt round-robin over the 8 XCDs), so the rows a chunk shares with its neighbours
+  // stay in that XCD's L2
+  if (nbf == items && items >= 8 * 64) {
+    // XCD x = b % 8 runs blocks x, x + 8, ...: K_x = items / 8 (+1 for x < items % 8) of them, which
+    // take the x-th contiguous range of items (a bijection of [0, items))
+    const int32_t x = b & 7, q = items >> 3, rem = items & 7;
+    b = x * q + (x < rem ? x : rem) + (b >> 3);
+    nbf = items + 1;  // one item, no further iteration
+  }
   for (int32_t it = b; it < items; it += nbf) {
     const int32_t lf = it / fc.cpf;
-    const int32_t t = (it - lf * fc.cpf) * BS + (int32_t)threadIdx.x;
+    const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT) + (int32_t)threadIdx.x;
     const lat::FaceTab F = fc.tab[lf];
-    if (t < fc.F) {
-      int32_t i, j;
-      lat::coords(t, fc.n, fc.rinv, i, j);
-      fn(F, lf, t, i, j);
+    for (int32_t r = 0; r < FACE_RPT; ++r) {
+      const int32_t t = t0 + r * BS;
+      if (t < fc.F) {
+        int32_t i, j;
+        lat::coords(t, fc.n, fc.rinv, i, j);
+        fn(F, lf, t, i, j);
+      }
     }
   }
 }
@@ -30,16 +43,16 @@ __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t 
 // operator with the merged table); op 1: the Jacobi-scaled A_visc, S A S with s_f inside the face
 // and the skeleton columns' s_j (0 for Dirichlet columns, StokesColor.py:473-475) from fc.wsk
 template <typename T>
-__device__ __forceinline__ void face_kcoefs(const FaceDev& fc, const lat::FaceTab& F, const int32_t (&nb)[6],
+__device__ __forceinline__ void face_kcoefs(const FaceDev& fc, int32_t lf, const int32_t (&nb)[6],
                                             const bool (&in)[6], T (&a)[7]) {
   if constexpr (std::is_same<T, float>::value) {
-    const float* c = fc.coef32 + F.rec * lat::NCOEF;
+    const float* c = fc.coef32 + lf * lat::NCOEF;
     a[0] = c[lat::C_KD];
     a[1] = a[2] = c[lat::C_KAB];
     a[3] = a[4] = c[lat::C_KAC];
     a[5] = a[6] = c[lat::C_KBC];
   } else {
-    const double* c = fc.coef + F.rec * lat::NCOEF;
+    const double* c = fc.coef + lf * lat::NCOEF;
     const double k3[3] = {c[lat::C_KAB], c[lat::C_KAC], c[lat::C_KBC]};
     if (fc.op == 1) {
       const double vs = c[lat::C_VS], g = vs * c[lat::C_DTNU];
@@ -67,22 +80,22 @@ __device__ __forceinline__ void face_grad(const double* c, const int32_t (&nb)[6
 template <bool C16>
 __global__ __launch_bounds__(BS) void k_spmv(SellDev A, FaceDev fc, const double* __restrict__ val,
                                              const double* __restrict__ x, double* __restrict__ y) {
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
       double a[7];
-      face_kcoefs(fc, F, nb, in, a);
+      face_kcoefs(fc, lf, nb, in, a);
       double acc = a[0] * x[F.base + t];
 #pragma unroll
       for (int k = 0; k < 6; ++k) acc += a[1 + k] * x[nb[k]];
-      y[F.base + t] = acc;
+      stnt(y + F.base + t, acc);
     });
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -94,7 +107,7 @@ __global__ __launch_bounds__(BS) void k_spmv(SellDev A, FaceDev fc, const double
       const int64_t e = off + (int64_t)k * 64 + lane;
       acc += val[e] * x[sell_col<C16, false>(A, e, base)];
     }
-    if (row >= 0) y[row] = acc;
+    if (row >= 0) stnt(y + row, acc);
   }
 }
 
@@ -131,20 +144,20 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
     for (int c = 0; c < NR; ++c) {
       const double b = v.b[c][row];
       const double r = b - acc[c];
-      v.r[c][row] = r;
-      if (r32) r32[row] = (float)r;
-      v.po[c][row] = 0.0;
+      stnt(v.r[c] + row, r);
+      if (r32) stnt(r32 + row, (float)r);
+      stnt(v.po[c] + row, 0.0);
       rr[c] += r * r;
       bb[c] += b * b;
     }
   };
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
       double a[7];
-      face_kcoefs(fc, F, nb, in, a);
+      face_kcoefs(fc, lf, nb, in, a);
       const int64_t row = F.base + t;
       double acc[NR];
 #pragma unroll
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t off = A.off[s];
@@ -244,8 +257,8 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
       const double p = v.r[c][row] + beta[c] * v.po[c][row];
-      v.pn[c][row] = p;
-      v.q[c][row] = acc[c];
+      stnt(v.pn[c] + row, p);
+      stnt(v.q[c] + row, acc[c]);
       pq[c] += p * acc[c];
     }
   }
@@ -291,13 +304,13 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
   double pq[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
       double a[7];
-      face_kcoefs(fc, F, nb, in, a);
+      face_kcoefs(fc, lf, nb, in, a);
       const int64_t row = F.base + t;
 #pragma unroll
       for (int c = 0; c < NR; ++c) {
@@ -310,14 +323,14 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
         double q = a[0] * p;
 #pragma unroll
         for (int k = 0; k < 6; ++k) q += a[1 + k] * g[k];
-        v.pn[c][row] = p;
-        v.q[c][row] = q;
+        stnt(v.pn[c] + row, p);
+        stnt(v.q[c] + row, q);
         pq[c] += p * q;
       }
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, s, lane, pq);
   }
@@ -351,10 +364,10 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
   for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
-      v.y[c][i] += alpha[c] * v.pn[c][i];
+      stnt(v.y[c] + i, v.y[c][i] + alpha[c] * v.pn[c][i]);
       const double r = v.r[c][i] - alpha[c] * v.q[c][i];
-      v.r[c][i] = r;
-      if (NR == 1 && r32) r32[i] = (float)r;
+      stnt(v.r[c] + i, r);
+      if (NR == 1 && r32) stnt(r32 + i, (float)r);
       rr[c] += r * r;
     }
   }
@@ -497,14 +510,14 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const double* __restric
     }
     const double xm = s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
     const double g = sa + alpha * xm;
-    xm_out[r] = xm;
-    y[r] = g;
-    x0[r] = g;
+    stnt(xm_out + r, xm);
+    stnt(y + r, g);
+    stnt(x0 + r, g);
   }
 }
 
 __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
-  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) out[r] = a[r] - b[r];
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) stnt(out + r, a[r] - b[r]);
 }
 
 // CG convergence test right after the residual update: ctl = (1, it) when <r_c, r_c> <= tol2 <b_c, b_c>
@@ -547,8 +560,8 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
                             VincDev D) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
-    bx[i] = s[i] * a;
-    by[i] = s[i] * b;
+    stnt(bx + i, s[i] * a);
+    stnt(by + i, s[i] * b);
     double ga = a, gb = b;
     if (D.order == 1) {
       ga += D.d[0][i];
@@ -560,8 +573,8 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
       ga += 3.0 * (D.d[0][i] - D.d[2][i]) + D.d[4][i];
       gb += 3.0 * (D.d[1][i] - D.d[3][i]) + D.d[5][i];
     }
-    yx[i] = sq[i] * ga;
-    yy[i] = sq[i] * gb;
+    stnt(yx + i, sq[i] * ga);
+    stnt(yy + i, sq[i] * gb);
   }
 }
 // u* = S y (both components) and the increment u* - u for the next step's warm start
@@ -571,10 +584,10 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double
                            double* __restrict__ dy) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = s[i] * yx[i], b = s[i] * yy[i];
-    usx[i] = a;
-    usy[i] = b;
-    dx[i] = a - ux[i];
-    dy[i] = b - uy[i];
+    stnt(usx + i, a);
+    stnt(usy + i, b);
+    stnt(dx + i, a - ux[i]);
+    stnt(dy + i, b - uy[i]);
   }
 }
 
@@ -590,30 +603,30 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
                                             double* __restrict__ braw, double* part) {
   __shared__ double sh[4];
   double mx = 0.0, sb = 0.0;
-  if ((int32_t)blockIdx.x < fc.nb) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
-      const double* c = fc.coef + F.rec * lat::NCOEF;
+      const double* c = fc.coef + lf * lat::NCOEF;
       double ax, ay, bx, by;
       face_grad(c, nb, ux, ax, ay);
       face_grad(c, nb, uy, bx, by);
       const int64_t row = F.base + t;
       const double as = c[lat::C_AS1];
       const double d = (ax + by) / as;
-      div[row] = d;
+      stnt(div + row, d);
       mx = fmax(mx, fabs(d));
       if (braw) {
         const double b = as * (negidt * d);
-        braw[row] = b;
+        stnt(braw + row, b);
         sb += b;
       }
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t off = A.off[s];
@@ -645,11 +658,11 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
       });
       if (row >= 0) {
         const double d = acc / as1[row];
-        div[row] = d;
+        stnt(div + row, d);
         mx = fmax(mx, fabs(d));
         if (braw) {
           const double b = mp[row] * (negidt * d);
-          braw[row] = b;
+          stnt(braw + row, b);
           sb += b;
         }
       }
@@ -679,7 +692,7 @@ __global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int
       if (slave_of[i] >= 0) b += braw[slave_of[i]];
       b = s ? s[i] * (b - mean) : (b - mean);
     }
-    bh[i] = b;
+    stnt(bh + i, b);
   }
 }
 
@@ -693,20 +706,20 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const d
                                                   const double* usy, double* ux, double* uy) {
   auto finish = [&](int64_t row, double gpx, double gpy, bool dirichlet) {
     if (mode == 0) {
-      ux[row] = usx[row] - dt * gpx;
-      uy[row] = usy[row] - dt * gpy;
+      stnt(ux + row, usx[row] - dt * gpx);
+      stnt(uy + row, usy[row] - dt * gpy);
     } else if (!dirichlet) {
-      ux[row] = ux[row] - dt * gpx;
-      uy[row] = uy[row] - dt * gpy;
+      stnt(ux + row, ux[row] - dt * gpx);
+      stnt(uy + row, uy[row] - dt * gpy);
     }
   };
-  if ((int32_t)blockIdx.x < fc.nb) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows are never Dirichlet nodes
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
-      const double* c = fc.coef + F.rec * lat::NCOEF;
+      const double* c = fc.coef + lf * lat::NCOEF;
       double ax, ay;
       face_grad(c, nb, p, ax, ay);
       const double d = c[lat::C_AS1];
@@ -715,7 +728,7 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const d
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -762,21 +775,21 @@ template <bool C16>
 __global__ __launch_bounds__(BS) void k_grad(SellDev A, FaceDev fc, const double* __restrict__ gx,
                                              const double* __restrict__ gy, const double* __restrict__ p,
                                              const double* __restrict__ as1, double* outx, double* outy) {
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
-      const double* c = fc.coef + F.rec * lat::NCOEF;
+      const double* c = fc.coef + lf * lat::NCOEF;
       double ax, ay;
       face_grad(c, nb, p, ax, ay);
-      outx[F.base + t] = ax / c[lat::C_AS1];
-      outy[F.base + t] = ay / c[lat::C_AS1];
+      stnt(outx + F.base + t, ax / c[lat::C_AS1]);
+      stnt(outy + F.base + t, ay / c[lat::C_AS1]);
     });
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -1296,19 +1309,19 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
       dn = tc1 * d1 + tc2 * di * ((T)b[row] - ax);
       xo = x1 + dn;
     }
-    d[row] = dn;
-    xout[row] = (TO)xo;
+    stnt(d + row, dn);
+    stnt(xout + row, (TO)xo);
     if (rdot) acc_rz += rdot[row] * (double)xo;
   };
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
       T a[7];
-      face_kcoefs(fc, F, nb, in, a);
-      const T di = std::is_same<T, float>::value ? (T)fc.coef32[F.rec * lat::NCOEF + lat::C_DINV]
-                                                 : (T)fc.coef[F.rec * lat::NCOEF + lat::C_DINV];
+      face_kcoefs(fc, lf, nb, in, a);
+      const T di = std::is_same<T, float>::value ? (T)fc.coef32[lf * lat::NCOEF + lat::C_DINV]
+                                                 : (T)fc.coef[lf * lat::NCOEF + lat::C_DINV];
       const int64_t row = F.base + t;
       T ax = 0;
       if (mode == 1) {
@@ -1324,7 +1337,7 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t row = sell_row(A, s, lane);
@@ -1347,28 +1360,28 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
                                               const TB* __restrict__ b, const T* __restrict__ x,
                                               T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
-  if ((int32_t)blockIdx.x < fc.nb) {
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
       T a[7];
-      face_kcoefs(fc, F, nb, in, a);
+      face_kcoefs(fc, lf, nb, in, a);
       const int64_t row = F.base + t;
       T ax = a[0] * x[row];
 #pragma unroll
       for (int k = 0; k < 6; ++k) ax += a[1 + k] * x[nb[k]];
-      res[row] = (T)b[row] - ax;
+      stnt(res + row, (T)b[row] - ax);
     });
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = sell_row(A, s, lane);
     const T ax = sell_row_dot<C16>(A, val, x, s, lane);
-    if (row >= 0) res[row] = (T)b[row] - ax;
+    if (row >= 0) stnt(res + row, (T)b[row] - ax);
   }
 }
 
@@ -1380,9 +1393,9 @@ template <typename T>
 __global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T* __restrict__ val,
                                                  const T* __restrict__ x, T* __restrict__ y, int add, const int* ctl) {
   if (ctl && ctl[0]) return;
-  if ((int32_t)blockIdx.x < fc.nb) {
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     const int32_t n2 = fc.n2;
-    face_rows(fc, blockIdx.x, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       const lat::FaceTab G = fc.tab2[lf];
       const int64_t row = F.base + t;
       if (add) {
@@ -1392,20 +1405,20 @@ __global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T*
         else if (!(j & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i1, j0)]);
         else if (!(i & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i0, j1)]);
         else v = (T)0.5 * (x[lat::point(G, n2, i0, j1)] + x[lat::point(G, n2, i1, j0)]);
-        y[row] = y[row] + v;
+        stnt(y + row, y[row] + v);
       } else {
         const int32_t I = 2 * i, J = 2 * j;
         const T c = x[lat::point(G, n2, I, J)];
         const T h = x[lat::point(G, n2, I - 1, J)] + x[lat::point(G, n2, I + 1, J)] + x[lat::point(G, n2, I, J - 1)] +
                     x[lat::point(G, n2, I, J + 1)] + x[lat::point(G, n2, I + 1, J - 1)] +
                     x[lat::point(G, n2, I - 1, J + 1)];
-        y[row] = c + (T)0.5 * h;
+        stnt(y + row, c + (T)0.5 * h);
       }
     });
     return;
   }
   int64_t s0, s1;
-  block_slices_n(M.nslices, gridDim.x - fc.nb, blockIdx.x - fc.nb, s0, s1);
+  block_slices_n(M.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = M.off[s];
@@ -1416,7 +1429,7 @@ __global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T*
       const int64_t e = off + (int64_t)k * 64 + lane;
       acc += val[e] * x[M.col[e]];
     }
-    if (row >= 0) y[row] = add ? y[row] + acc : acc;
+    if (row >= 0) stnt(y + row, add ? y[row] + acc : acc);
   }
 }
 
