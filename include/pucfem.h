@@ -196,7 +196,7 @@ int pucfem_timing_enable(void* ctx, int32_t on);
 /* kernel classes: 0 = multigrid Chebyshev smoother on the finest level (k_cheb), 1 = CG SpMV+direction
    (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl),
    5 = multigrid residual on the finest level (k_resid), 6 = restriction from the finest level,
-   7 = prolongation to the finest level (k_transfer) */
+   7 = prolongation to the finest level (k_transfer), 8 = the semi-Lagrangian rank-count pass (k_sl_rank) */
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);
@@ -219,8 +219,9 @@ int pucfem_info(void* ctx, int64_t* out12);
    1 one-workgroup CG, 2 multi-kernel CG), [1] pressure solve (0 dense, 1 one-workgroup CG, 2 multi-kernel
    Jacobi CG, 3 multigrid-preconditioned CG), [2] projection bases re-seeded so far, [3] / [4] current
    basis sizes of the two pressure solves, [5] extrapolation order of the viscous warm start in use,
-   [6] projection basis capacity (0: off), [7] 1 when the operators are lattice stencils on the face
-   interiors (pucfem_params.assembled = 0 with a hierarchy), 0 when every row is a stored SELL row */
+   [6] projection basis capacity (0: off), [7] bit 0: the operators are lattice stencils on the face
+   interiors (pucfem_params.assembled = 0 with a hierarchy; clear: every row is a stored SELL row),
+   bit 1: the semi-Lagrangian point location uses the lattice locator (else per-triangle records) */
 int pucfem_path_info(void* ctx, int64_t* out8);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */

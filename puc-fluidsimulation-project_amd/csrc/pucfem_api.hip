@@ -116,7 +116,7 @@ struct Timer {
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
-  static constexpr int NCLS = 8;
+  static constexpr int NCLS = 9;
   double ms[NCLS] = {};
   double bytes[NCLS] = {};
   int64_t n[NCLS] = {};
@@ -330,7 +330,11 @@ struct Ctx {
   int32_t* mtri = nullptr;
   GridDev cgrid{}, tgrid{};
   LocDev lgrid{};
+  LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
+  bool lat_sl = false;
   double* part_sl = nullptr;  // k_sl partials, 3 x SLB
+  int2* sl_queue = nullptr;   // k_sl -> k_sl_rank: points whose rank needs the centroid count (mesh.N)
+  int32_t* sl_qcnt = nullptr; // per wave of k_sl: queued entries (SLB * BS / 64)
   bool has_cgrid = false, has_tgrid = false;
   double *c_full = nullptr, *c_new = nullptr, *ufx = nullptr, *ufy = nullptr;
   int32_t* dnotfound = nullptr;
@@ -490,6 +494,20 @@ struct Ctx {
       hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
     }
   }
+  // k_sl over rows [row0, row0 + n) of the full replica c (cout: the new values), either locator
+  void sl_launch(int nb, i64 row0, i64 n, const double* vx, const double* vy, double dt, const double* cf, double* cn,
+                 const double* w, int32_t* nf) {
+    const MeshDev M{mx, my, mtri, mesh.T};
+    if (lat_sl)
+      klaunch(4, 8.0 * 6 * (double)n, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n,
+              vx, vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
+    else
+      klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx,
+              vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
+    klaunch(8, 0.0, k_sl_rank, dim3(nb), dim3(BS), M, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt, cf, cn, w, nf,
+            part_sl, (const int2*)sl_queue, (const int32_t*)sl_qcnt);
+  }
+
 
   // ------------------------------------------------------------------ communication
   // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
@@ -1154,9 +1172,7 @@ struct Ctx {
     reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
-      klaunch(4, 8.0 * 6 * (double)lp.n_own, k_sl, dim3(nb), dim3(BS), MeshDev{mx, my, mtri, mesh.T}, lgrid, cgrid,
-              lp.r0, lp.n_own, (const double*)ux, (const double*)uy, prm.dt, (const double*)c_full, c_new,
-              (const double*)dwmix, (int32_t*)nullptr, part_sl);
+      sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
       KCHK();
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
@@ -1928,6 +1944,10 @@ void build(Ctx& c) {
   }
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
+  if (stokes) {
+    c.sl_queue = c.dalloc<int2>(m.N);
+    c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
+  }
   c.scal = c.dalloc<double>(32);
   c.ctl = c.dalloc<int>(4);
   c.redbuf = c.dalloc<double>(8 * 64);
@@ -1975,42 +1995,65 @@ void build(Ctx& c) {
       build_tri_grid(X, Y, tri, 4.0, TG);
       dgrid(TG, c.tgrid, false);
       c.has_tgrid = true;
-      // semi-Lagrangian point location: inflated-bbox grid (~1 triangle per cell) + packed records
-      Grid LG;
-      build_tri_grid(X, Y, tri, 1.0, LG, 1e-6);
       const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
-      // records in node order: position p holds triangle p2t[p], sorted by smallest vertex id
-      std::vector<i32> p2t(m.T), t2p(m.T), vmin(m.T);
-      for (i64 t = 0; t < m.T; ++t) {
-        p2t[t] = (i32)t;
-        vmin[t] = std::min(tri[3 * t], std::min(tri[3 * t + 1], tri[3 * t + 2]));
-      }
-      std::stable_sort(p2t.begin(), p2t.end(), [&](i32 a, i32 b) { return vmin[a] < vmin[b]; });
-      for (i64 p = 0; p < m.T; ++p) t2p[p2t[p]] = (i32)p;
-      std::vector<int32_t> rec(4 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
-      std::vector<float> rho2p(m.T);
-      for (i64 p = 0; p < m.T; ++p) {
-        const i64 t = p2t[p];
-        for (int v = 0; v < 3; ++v) rec[4 * p + v] = tri[3 * t + v];
-        rec[4 * p + 3] = (int32_t)t;
-        rho2p[p] = rho2[t];
-      }
+      const float* drv2 = c.upload(knn_radius2(G, X, Y, KNN + 1, false));
       std::vector<double> xy(2 * (size_t)N);
       for (i64 i = 0; i < N; ++i) {
         xy[2 * i] = X[i];
         xy[2 * i + 1] = Y[i];
       }
-      for (i64 cl = 0; cl + 1 < (i64)LG.cell_start.size(); ++cl) {
-        auto b0 = LG.item.begin() + LG.cell_start[cl], b1 = LG.item.begin() + LG.cell_start[cl + 1];
-        for (auto it = b0; it != b1; ++it) *it = t2p[*it];
-        std::sort(b0, b1);
+      const double2* dxy = reinterpret_cast<const double2*>(c.upload(xy));
+      const int probe = std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0;
+      // semi-Lagrangian point location: on a lattice hierarchy the lattice locator (no per-triangle
+      // records); PUCFEM_SL_RECORDS=1 forces the record locator (measurement / cross-check knob)
+      std::vector<lat::SlFace> sf;
+      std::vector<uint32_t> cells;
+      c.lat_sl = c.lattice && !c.mg.empty() && !(std::getenv("PUCFEM_SL_RECORDS") && std::atoi(std::getenv("PUCFEM_SL_RECORDS")));
+      if (c.lat_sl) {
+        try {
+          lattice_locator(c.macro, c.mg.back().latl, m, c.ord, sf, cells);
+        } catch (const std::exception&) {
+          c.lat_sl = false;  // a hierarchy not numbered face by face: the record locator below
+        }
       }
-      GridDev lg{};
-      dgrid(LG, lg, false);
-      c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item,
-                       reinterpret_cast<const int4*>(c.upload(rec)), reinterpret_cast<const double2*>(c.upload(xy)),
-                       c.upload(rho2p),
-                       std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0};
+      if (c.lat_sl) {
+        Grid MG;
+        build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.5, MG, 1e-6);
+        GridDev mg{};
+        dgrid(MG, mg, false);
+        c.llgrid = LatLocDev{mg.nx, mg.ny, mg.x0, mg.y0, mg.hx, mg.hy, mg.start, mg.item,
+                             reinterpret_cast<const lat::SlFace*>(c.upload(sf)), c.upload(cells), dxy,
+                             c.upload(rho2), drv2, c.mg.back().latl.n, probe};
+      } else {
+        // inflated-bbox grid (~1 triangle per cell) + packed records
+        Grid LG;
+        build_tri_grid(X, Y, tri, 1.0, LG, 1e-6);
+        // records in node order: position p holds triangle p2t[p], sorted by smallest vertex id
+        std::vector<i32> p2t(m.T), t2p(m.T), vmin(m.T);
+        for (i64 t = 0; t < m.T; ++t) {
+          p2t[t] = (i32)t;
+          vmin[t] = std::min(tri[3 * t], std::min(tri[3 * t + 1], tri[3 * t + 2]));
+        }
+        std::stable_sort(p2t.begin(), p2t.end(), [&](i32 a, i32 b) { return vmin[a] < vmin[b]; });
+        for (i64 p = 0; p < m.T; ++p) t2p[p2t[p]] = (i32)p;
+        std::vector<int32_t> rec(4 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
+        std::vector<float> rho2p(m.T);
+        for (i64 p = 0; p < m.T; ++p) {
+          const i64 t = p2t[p];
+          for (int v = 0; v < 3; ++v) rec[4 * p + v] = tri[3 * t + v];
+          rec[4 * p + 3] = (int32_t)t;
+          rho2p[p] = rho2[t];
+        }
+        for (i64 cl = 0; cl + 1 < (i64)LG.cell_start.size(); ++cl) {
+          auto b0 = LG.item.begin() + LG.cell_start[cl], b1 = LG.item.begin() + LG.cell_start[cl + 1];
+          for (auto it = b0; it != b1; ++it) *it = t2p[*it];
+          std::sort(b0, b1);
+        }
+        GridDev lg{};
+        dgrid(LG, lg, false);
+        c.lgrid = LocDev{lg.nx, lg.ny, lg.x0, lg.y0, lg.hx, lg.hy, lg.start, lg.item,
+                         reinterpret_cast<const int4*>(c.upload(rec)), dxy, c.upload(rho2p), drv2, probe};
+      }
     }
     c.c_full = c.dalloc<double>(N);
     c.c_new = c.dalloc<double>(N);
@@ -2675,8 +2718,7 @@ int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, d
     HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
     HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
     const int nb = c.nb_sl(N);
-    hipLaunchKernelGGL(k_sl, dim3(nb), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, c.mesh.T}, c.lgrid, c.cgrid,
-                       (int64_t)0, N, tx, ty, dt, cf, cn, c.dwmix, c.dnotfound, c.part_sl);
+    c.sl_launch(nb, 0, N, tx, ty, dt, cf, cn, c.dwmix, c.dnotfound);
     KCHK();
     std::vector<double> o(N);
     std::vector<int32_t> nf(N);
@@ -2823,7 +2865,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[4] = c.proj_m[2];
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
-    o[7] = c.lattice ? 1 : 0;
+    o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0);
   });
 }
 

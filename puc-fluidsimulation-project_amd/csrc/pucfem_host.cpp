@@ -523,9 +523,15 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
 
 std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy,
                                         int k) {
+  return knn_radius2(G, cx, cy, k, true);
+}
+
+std::vector<float> knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy, int k,
+                               bool self) {
+  const i64 ncent = (i64)G.item.size();
   const i64 T = (i64)cx.size();
   std::vector<float> out(T, INFINITY);
-  if (T <= k) return out;
+  if (ncent - (self ? 1 : 0) < k) return out;
   auto work = [&](i64 t0, i64 t1) {
     std::vector<double> best(k);
     for (i64 t = t0; t < t1; ++t) {
@@ -540,7 +546,7 @@ std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>
             if (i < 0 || i >= G.nx) continue;
             const i64 c = (i64)j * G.nx + i;
             for (i32 e = G.cell_start[c]; e < G.cell_start[c + 1]; ++e) {
-              if (G.item[e] == (i32)t) continue;
+              if (self && G.item[e] == (i32)t) continue;
               const double dx = G.px[e] - qx, dy = G.py[e] - qy, d = dx * dx + dy * dy;
               if (d >= best[k - 1]) continue;
               int p = k - 1;
@@ -1154,6 +1160,106 @@ void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double 
     c[lat::C_DTNU] = dtnu;
     c[lat::C_DINV] = 1.0 / c[lat::C_KD];
   }
+}
+
+void lattice_locator(const Macro& M, const LatticeLevel& LL, const HostMesh& m, const Ordering& ord,
+                     std::vector<lat::SlFace>& faces, std::vector<uint32_t>& cells) {
+  const int l = LL.l;
+  const i32 n = LL.n;
+  const i64 per = (i64)1 << (2 * l);  // fine triangles per face
+  if (n < 4 || m.T != M.nf * per) throw std::runtime_error("lattice locator: needs >= 2 refinement levels");
+  LocalPlan gp;  // identity plan: global internal ids
+  gp.r0 = 0;
+  gp.r1 = m.N;
+  gp.n_own = m.N;
+  std::vector<i32> all(M.nf);
+  std::iota(all.begin(), all.end(), 0);
+  std::vector<lat::FaceTab> tabs;
+  lattice_tabs(M, LL, all, -1, gp, nullptr, tabs);
+  faces.assign(M.nf, lat::SlFace{});
+  for (i64 f = 0; f < M.nf; ++f) {
+    const i32 A = M.tri[3 * f], B = M.tri[3 * f + 1], C = M.tri[3 * f + 2];
+    const double ex = M.x[B] - M.x[A], ey = M.y[B] - M.y[A], fx = M.x[C] - M.x[A], fy = M.y[C] - M.y[A];
+    const double det = ex * fy - fx * ey;
+    lat::SlFace& S = faces[f];
+    S.ax = M.x[A];
+    S.ay = M.y[A];
+    S.m00 = fy / det;
+    S.m01 = -fx / det;
+    S.m10 = -ey / det;
+    S.m11 = ex / det;
+    S.tab = tabs[f];
+    S.va = (i32)LL.vert_start[A];
+    S.vb = (i32)LL.vert_start[B];
+    S.vc = (i32)LL.vert_start[C];
+    S.t0 = f * per;
+  }
+  // cell table from face 0: lattice coordinates of the stored vertices of its fine triangles
+  cells.assign((size_t)2 * n * n, 0xffffffffu);
+  const lat::SlFace& S0 = faces[0];
+  auto latpt = [&](i32 v, i32& i, i32& j) {
+    const double dx = m.x[v] - S0.ax, dy = m.y[v] - S0.ay;
+    const double u = n * (S0.m00 * dx + S0.m01 * dy), w = n * (S0.m10 * dx + S0.m11 * dy);
+    i = (i32)std::llround(u);
+    j = (i32)std::llround(w);
+    if (std::fabs(u - i) > 1e-4 || std::fabs(w - j) > 1e-4) throw std::runtime_error("lattice locator: off-lattice vertex");
+  };
+  for (i64 t = 0; t < per; ++t) {
+    i32 pi[3], pj[3];
+    for (int k = 0; k < 3; ++k) latpt(m.tri[3 * t + k], pi[k], pj[k]);
+    const i32 i = std::min({pi[0], pi[1], pi[2]}), j = std::min({pj[0], pj[1], pj[2]});
+    bool has00 = false;
+    for (int k = 0; k < 3; ++k) has00 = has00 || (pi[k] == i && pj[k] == j);
+    const i32 sflag = has00 ? 0 : 1;
+    i32 ci[3], cj[3];
+    lat::cell_vertices(i, j, sflag, ci, cj);
+    int rot = -1;
+    for (int r = 0; r < 3; ++r) {
+      bool ok = true;
+      for (int k = 0; k < 3; ++k) ok = ok && ci[(r + k) % 3] == pi[k] && cj[(r + k) % 3] == pj[k];
+      if (ok) rot = r;
+    }
+    if (rot < 0) throw std::runtime_error("lattice locator: a fine triangle is not a rotation of its cell");
+    const i64 ce = lat::cell_index(n, i, j, sflag);
+    if (cells[ce] != 0xffffffffu) throw std::runtime_error("lattice locator: two triangles in one cell");
+    cells[ce] = ((uint32_t)t << 2) | (uint32_t)rot;
+  }
+  // every face: the same local numbering (red_refine's recursion is the same for every face)
+  struct Ent {
+    i32 i, j, s;
+    uint32_t e;
+  };
+  std::vector<Ent> ents;
+  for (i32 j = 0; j < n; ++j)
+    for (i32 i = 0; i + j <= n - 1; ++i)
+      for (i32 sflag = 0; sflag < 2; ++sflag) {
+        if (i + j > n - 1 - sflag) continue;
+        const uint32_t e = cells[lat::cell_index(n, i, j, sflag)];
+        if (e == 0xffffffffu) throw std::runtime_error("lattice locator: empty cell");
+        ents.push_back({i, j, sflag, e});
+      }
+  if ((i64)ents.size() != per) throw std::runtime_error("lattice locator: cell count");
+  std::vector<int> bad(1, 0);
+  std::mutex mx;
+  parallel_for(M.nf, [&](i64 f0, i64 f1) {
+    for (i64 f = f0; f < f1; ++f) {
+      const lat::SlFace& S = faces[f];
+      for (const Ent& E : ents) {
+        i32 ci[3], cj[3];
+        lat::cell_vertices(E.i, E.j, E.s, ci, cj);
+        const int rot = (int)(E.e & 3);
+        const i64 t = S.t0 + (i64)(E.e >> 2);
+        for (int k = 0; k < 3; ++k) {
+          const i32 want = lat::vertex(S.tab, S.va, S.vb, S.vc, n, ci[(rot + k) % 3], cj[(rot + k) % 3]);
+          if (ord.old2new[m.tri[3 * t + k]] != want) {
+            std::lock_guard<std::mutex> lk(mx);
+            bad[0] = 1;
+          }
+        }
+      }
+    }
+  });
+  if (bad[0]) throw std::runtime_error("lattice locator: a face's fine triangles do not follow face 0's numbering");
 }
 
 void lattice_apply_host(int kind, int n, const std::vector<lat::FaceTab>& tab, const std::vector<double>& coef,

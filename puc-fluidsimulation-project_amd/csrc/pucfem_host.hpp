@@ -178,6 +178,13 @@ void lattice_tabs(const Macro& M, const LatticeLevel& LL, const std::vector<i32>
                   const LocalPlan& lp, const std::vector<i32>* dof, std::vector<lat::FaceTab>& out);
 // Coefficient records (lat::NCOEF doubles per face of `faces`) at level l
 void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double dtnu, std::vector<double>& out);
+// Point location on the finest level of a lattice hierarchy (the semi-Lagrangian step): one SlFace per
+// macro face (frame, face table in global internal ids of `ord`, corners, first fine triangle) and the
+// cell table, per cell (i, j, s) of a face (lat::cell_index) the fine triangle's offset in its face
+// and the rotation of its stored vertex order: (offset << 2) | rotation.  Built from face 0 and checked
+// against the mesh's triangles on every face (throws if a face is numbered differently).
+void lattice_locator(const Macro& M, const LatticeLevel& LL, const HostMesh& m, const Ordering& ord,
+                     std::vector<lat::SlFace>& faces, std::vector<uint32_t>& cells);
 // Host reference of the face stencils (CPU tests of the index arithmetic and the coefficients):
 // kind 0 y = K x (K-type stencil), 1 = the lumped divergence numerator Gx ux + Gy uy (x: 2 vectors,
 // x0 and x1), 2 = A_visc scaled (wsk: skeleton weights), 3 = prolongation rows (x0 on the coarse level
@@ -211,6 +218,11 @@ struct Grid {
   std::vector<double> px, py;   // centroid coordinates per entry (centroid grid only)
 };
 void build_centroid_grid(const std::vector<double>& cx, const std::vector<double>& cy, double per_cell, Grid& G);
+// per query point i: the squared distance to its k-th nearest centroid of the centroid grid G (self:
+// the points are G's own centroids, and item i itself is skipped), rounded down to fp32; +inf when
+// there are fewer than k
+std::vector<float> knn_radius2(const Grid& G, const std::vector<double>& qx, const std::vector<double>& qy, int k,
+                               bool self);
 // per triangle t: the squared distance from its centroid to its k-th nearest OTHER centroid (G is
 // the centroid grid of cx, cy), rounded down to fp32; +inf when there are fewer than k others
 std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy,

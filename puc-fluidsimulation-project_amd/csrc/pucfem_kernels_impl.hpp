@@ -894,6 +894,7 @@ struct LocDev {
   const double2* xy;     // node coordinates (internal numbering)
   // per position: squared distance from the centroid to the 10th nearest other centroid (rounded down)
   const float* rho2;
+  const float* rv2;  // per node: squared distance to its (KNN + 1)-th nearest centroid (rounded down)
   int32_t probe;  // measurement knob (PUCFEM_SL_PROBE): 1 = accept T* without the rank count
 };
 struct SlTri {
@@ -907,37 +908,11 @@ __device__ __forceinline__ SlTri sl_tri(const LocDev& L, int32_t pos) {
 }
 constexpr double SL_MARGIN = 1e-6;
 
-// -> record position of the triangle, or -1 (no triangle among the KNN nearest centroids contains q)
-__device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, double qx, double qy) {
-  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
-  const int64_t cell = (int64_t)cj * L.nx + ci;
-  int32_t best = 0x7fffffff, bpos = -1;
-  double bestd = INFINITY;
-  const int32_t e1 = L.start[cell + 1];
-  for (int32_t e = L.start[cell]; e < e1; ++e) {
-    const int32_t pos = L.item[e];
-    const SlTri r = sl_tri(L, pos);
-    const int32_t t = r.id;
-    const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
-    const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
-    if (!(fabs(det) >= 1e-14)) continue;
-    const double w1 = ((x2 - qx) * (y3 - qy) - (x3 - qx) * (y2 - qy)) / det;
-    const double w2 = ((x3 - qx) * (y1 - qy) - (x1 - qx) * (y3 - qy)) / det;
-    const double w3 = 1.0 - w1 - w2;
-    if (w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0) {
-      // centroid as StokesColor.py:321 / the centroid grid: (x1 + x2 + x3) / 3 in fp64
-      const double dx = (x1 + x2 + x3) / 3.0 - qx, dy = (y1 + y2 + y3) / 3.0 - qy;
-      const double d = dx * dx + dy * dy;
-      if (knn_less(d, t, bestd, best)) {
-        bestd = d;
-        best = t;
-        bpos = pos;
-      }
-      if (w1 >= SL_MARGIN && w2 >= SL_MARGIN && w3 >= SL_MARGIN) break;
-    }
-  }
-  if (bpos < 0) return -1;
-  if (4.0 * bestd * (1.0 + 1e-9) < (double)L.rho2[bpos] || (L.probe & 1)) return bpos;
+// rank test of the best passing triangle (id best, squared centroid distance bestd, fast-accept
+// radius rho2): true iff fewer than KNN centroids have a (d^2, id) key below it
+__device__ __forceinline__ bool sl_rank_ok(const GridDev& G, double qx, double qy, double bestd, int32_t best,
+                                           float rho2, int32_t probe) {
+  if (4.0 * bestd * (1.0 + 1e-9) < (double)rho2 || (probe & 1)) return true;
   const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
   const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
   const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
@@ -947,10 +922,155 @@ __device__ __forceinline__ int32_t sl_locate(const LocDev& L, const GridDev& G, 
     for (int32_t e = f0; e < f1; ++e) {  // cells i0..i1 of row j are one contiguous entry range
       const double dx = G.px[e] - qx, dy = G.py[e] - qy;
       const double d = dx * dx + dy * dy;
-      if (knn_less(d, G.item[e], bestd, best) && ++cnt >= KNN) return -1;
+      if (knn_less(d, G.item[e], bestd, best) && ++cnt >= KNN) return false;
     }
   }
-  return bpos;
+  return true;
+}
+
+// the reference's weight test (StokesColor.py:325-333) and centroid distance of one candidate
+__device__ __forceinline__ bool sl_test(const SlTri& r, double qx, double qy, double& d, bool& margin) {
+  const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
+  const double det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
+  if (!(fabs(det) >= 1e-14)) return false;
+  const double w1 = ((x2 - qx) * (y3 - qy) - (x3 - qx) * (y2 - qy)) / det;
+  const double w2 = ((x3 - qx) * (y1 - qy) - (x1 - qx) * (y3 - qy)) / det;
+  const double w3 = 1.0 - w1 - w2;
+  if (!(w1 >= 0.0 && w2 >= 0.0 && w3 >= 0.0)) return false;
+  // centroid as StokesColor.py:321 / the centroid grid: (x1 + x2 + x3) / 3 in fp64
+  const double dx = (x1 + x2 + x3) / 3.0 - qx, dy = (y1 + y2 + y3) / 3.0 - qy;
+  d = dx * dx + dy * dy;
+  margin = w1 >= SL_MARGIN && w2 >= SL_MARGIN && w3 >= SL_MARGIN;
+  return true;
+}
+
+// Locate step (the rank test follows in k_sl / k_sl_rank): the passing triangle with the smallest
+// (d^2, id) key (false: none passes), its d^2 and its fast-accept radius.
+// Record locator: the records listed in q's cell of the inflated-bbox grid.
+__device__ __forceinline__ bool sl_best(const LocDev& L, double qx, double qy, SlTri& out, double& bestd, float& rho2) {
+  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
+  const int64_t cell = (int64_t)cj * L.nx + ci;
+  int32_t best = 0x7fffffff, bpos = -1;
+  bestd = INFINITY;
+  const int32_t e1 = L.start[cell + 1];
+  for (int32_t e = L.start[cell]; e < e1; ++e) {
+    const int32_t pos = L.item[e];
+    const SlTri r = sl_tri(L, pos);
+    double d;
+    bool margin;
+    if (sl_test(r, qx, qy, d, margin)) {
+      if (knn_less(d, r.id, bestd, best)) {
+        bestd = d;
+        best = r.id;
+        bpos = pos;
+        out = r;
+      }
+      if (margin) break;
+    }
+  }
+  if (bpos < 0) return false;
+  rho2 = L.rho2[bpos];
+  return true;
+}
+
+// Lattice locator (Ctx::lattice): the finest mesh is the coarse mesh red-refined L times, so the
+// candidates of the weight test are found arithmetically instead of from per-triangle records: the
+// macro faces listed in q's cell of a grid over the coarse triangles (inflated bboxes), q's lattice
+// coordinates (u, v) = n M (q - A) in each, and the cells (i, j, s) whose closure holds (u, v) up to
+// SL_LDEL lattice units (one cell away from edges, more only within 1e-7 of a lattice line, where the
+// reference's weight test can pass in several triangles).  The rotation stored in the cell table
+// gives the triangle's vertices in the mesh's own order, so the weight test and the (d^2, id) keys
+// are the record locator's, bit for bit.
+struct LatLocDev {
+  int32_t nx, ny;
+  double x0, y0, hx, hy;
+  const int32_t* start;          // macro grid cells -> face ids
+  const int32_t* item;
+  const lat::SlFace* face;
+  const uint32_t* cell;          // per lattice cell (lat::cell_index): (offset in face << 2) | rotation
+  const double2* xy;             // node coordinates (internal numbering)
+  const float* rho2;             // per triangle id
+  const float* rv2;              // per node, as LocDev::rv2
+  int32_t n, probe;
+};
+constexpr double SL_LDEL = 1e-7;
+
+// one lattice cell of face S as an SlTri (vertices in the mesh's stored order)
+__device__ __forceinline__ SlTri sl_cell(const LatLocDev& L, const lat::SlFace& S, int32_t i, int32_t j, int32_t s) {
+  const uint32_t ent = L.cell[lat::cell_index(L.n, i, j, s)];
+  const int32_t rot = (int32_t)(ent & 3u);
+  int32_t pi[3], pj[3], vid[3];
+  lat::cell_vertices(i, j, s, pi, pj);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int32_t kk = (rot + k) % 3;
+    vid[k] = lat::vertex(S.tab, S.va, S.vb, S.vc, L.n, pi[kk], pj[kk]);
+  }
+  const double2 p = L.xy[vid[0]], q = L.xy[vid[1]], w = L.xy[vid[2]];
+  return SlTri{p.x, p.y, q.x, q.y, w.x, w.y, vid[0], vid[1], vid[2], (int32_t)(S.t0 + (int64_t)(ent >> 2))};
+}
+
+// Lattice locator.  Common case: q lies inside a macro face and inside one lattice cell by more than
+// SL_LDEL, so no other triangle can pass the weight test: that cell alone is tested.  Otherwise every
+// cell of every candidate face whose closure holds q up to SL_LDEL is tested, as the record locator
+// tests every record of its grid cell.
+__device__ __forceinline__ bool sl_best(const LatLocDev& L, double qx, double qy, SlTri& out, double& bestd,
+                                        float& rho2) {
+  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
+  const int64_t gc = (int64_t)cj * L.nx + ci;
+  const int32_t n = L.n;
+  const double dn = (double)n;
+  int32_t best = 0x7fffffff;
+  bestd = INFINITY;
+  bool done = false;
+  const int32_t e1 = L.start[gc + 1];
+  for (int32_t e = L.start[gc]; e < e1 && !done; ++e) {
+    const lat::SlFace& S = L.face[L.item[e]];
+    const double dx = qx - S.ax, dy = qy - S.ay;
+    const double u = dn * (S.m00 * dx + S.m01 * dy), v = dn * (S.m10 * dx + S.m11 * dy);
+    if (!(u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL)) continue;
+    const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
+    {
+      const double a = u - i0, b = v - j0;
+      const int32_t s = a + b > 1.0 ? 1 : 0;
+      const bool inner = s == 0 ? (a >= SL_LDEL && b >= SL_LDEL && a + b <= 1.0 - SL_LDEL)
+                                : (a <= 1.0 - SL_LDEL && b <= 1.0 - SL_LDEL && a + b >= 1.0 + SL_LDEL);
+      if (inner && i0 + j0 <= n - 1 - s) {  // q strictly inside this cell (hence inside the face)
+        const SlTri r = sl_cell(L, S, i0, j0, s);
+        double d;
+        bool margin;
+        if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, bestd, best)) {
+          bestd = d;
+          best = r.id;
+          out = r;
+        }
+        break;
+      }
+    }
+    for (int32_t j = max(j0 - 1, 0); j <= j0 + 1 && !done; ++j)
+      for (int32_t i = max(i0 - 1, 0); i <= i0 + 1 && i + j <= n - 1 && !done; ++i) {
+        const double a = u - i, b = v - j;
+        for (int32_t s = 0; s < 2 && !done; ++s) {
+          const bool near = s == 0 ? (a >= -SL_LDEL && b >= -SL_LDEL && a + b <= 1.0 + SL_LDEL)
+                                   : (i + j <= n - 2 && a <= 1.0 + SL_LDEL && b <= 1.0 + SL_LDEL && a + b >= 1.0 - SL_LDEL);
+          if (!near) continue;
+          const SlTri r = sl_cell(L, S, i, j, s);
+          double d;
+          bool margin;
+          if (sl_test(r, qx, qy, d, margin)) {
+            if (knn_less(d, r.id, bestd, best)) {
+              bestd = d;
+              best = r.id;
+              out = r;
+            }
+            done = margin;
+          }
+        }
+      }
+  }
+  if (best == 0x7fffffff) return false;
+  rho2 = L.rho2[best];
+  return true;
 }
 
 __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:353-357
@@ -960,53 +1080,141 @@ __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:3
   return d;
 }
 
-// advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
-// nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
-// Partials: [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
+// back-traced point of row i (StokesColor.py:361-372): x mod 1, y clamped into (0, 1)
+__device__ __forceinline__ void sl_point(const MeshDev& M, int64_t g, double vx, double vy, double dt, double& xb,
+                                         double& yb) {
+  xb = py_mod(M.x[g] - dt * vx * 1.0, 1.0);
+  yb = M.y[g] - dt * vy * 1.0;
+  if (yb < 0.0) yb = 1e-12;
+  if (yb > 1.0) yb = 1.0 - 1e-12;
+}
+// interpolation in the located triangle with periodic x differences (StokesColor.py:374-386)
+__device__ __forceinline__ double sl_value(const SlTri& r, double xb, double yb, const double* __restrict__ c) {
+  const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
+  const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
+  const double w1 = (pdx(x2, xb) * (y3 - yb) - pdx(x3, xb) * (y2 - yb)) / det;
+  const double w2 = (pdx(x3, xb) * (y1 - yb) - pdx(x1, xb) * (y3 - yb)) / det;
+  const double w3 = 1.0 - w1 - w2;
+  return w1 * c[r.a] + w2 * c[r.b] + w3 * c[r.d];
+}
+
 // advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
 // nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
 // Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
-__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LocDev L, GridDev G, int64_t row0, int64_t n,
+// Two passes.  k_sl locates every point and finishes those whose rank the fast accept settles (or
+// that no triangle holds); the rest, which need the centroid count, are queued and finished by
+// k_sl_rank, so the count's long loop runs on dense waves instead of stalling 63 finished lanes.
+// The queue is per wave and deterministic: wave w of block b writes its k-th entry into slot
+// k % 64 of the (k / 64)-th 64-row slice it processed (entries never outrun the rows they come from);
+// k_sl_rank block b runs the same waves' queues and adds its partial sums to block b's, so the
+// reductions keep a fixed order.
+// Fast accepts of the rank test (T* among the KNN nearest centroids); every centroid whose key is
+// below T*'s lies within R = |q - c_T*| of q.  (1) they lie within 2R of c_T*: fewer than KNN when
+// 2R is below the distance from c_T* to its KNN-th nearest other centroid (rho2) -- settles points
+// near the centroid; (2) they and c_T* lie within |q - v| + R of T*'s vertex v nearest to q: fewer
+// than KNN + 1 in all when that is below the distance from v to its (KNN + 1)-th nearest centroid
+// (rv2) -- settles points near vertices and edges, where back-traced points of slow flow gather.
+template <class LOC>
+__device__ __forceinline__ bool sl_fast(const LOC& L, const SlTri& r, double qx, double qy, double bestd, float rho2) {
+  if (4.0 * bestd * (1.0 + 1e-9) < (double)rho2 || (L.probe & 1)) return true;
+  const double d1 = (r.x1 - qx) * (r.x1 - qx) + (r.y1 - qy) * (r.y1 - qy);
+  const double d2 = (r.x2 - qx) * (r.x2 - qx) + (r.y2 - qy) * (r.y2 - qy);
+  const double d3 = (r.x3 - qx) * (r.x3 - qx) + (r.y3 - qy) * (r.y3 - qy);
+  const double dv = d1 <= d2 && d1 <= d3 ? d1 : (d2 <= d3 ? d2 : d3);
+  const int32_t v = d1 <= d2 && d1 <= d3 ? r.a : (d2 <= d3 ? r.b : r.d);
+  const double rr = sqrt(dv) + sqrt(bestd);
+  return rr * rr * (1.0 + 1e-9) < (double)L.rv2[v];
+}
+
+template <class LOC>
+__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, GridDev G, int64_t row0, int64_t n,
                                            const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                            const double* __restrict__ c, double* __restrict__ cout,
-                                           const double* __restrict__ wmix, int32_t* notfound, double* part) {
+                                           const double* __restrict__ wmix, int32_t* notfound, double* part,
+                                           int2* __restrict__ queue, int32_t* __restrict__ qcnt) {
   __shared__ double sh[4];
   double swc = 0.0, sw = 0.0, nnf = 0.0;
   int64_t r0, r1;
   block_rows(n, r0, r1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t qn = 0;
   for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
     const int64_t g = row0 + i;
-    const double xg = M.x[g], yg = M.y[g];
-    double xb = py_mod(xg - dt * ux[i] * 1.0, 1.0);
-    double yb = yg - dt * uy[i] * 1.0;
-    if (yb < 0.0) yb = 1e-12;
-    if (yb > 1.0) yb = 1.0 - 1e-12;
-    const int32_t found = sl_locate(L, G, xb, yb);
-    double cn;
-    if (found < 0) {
-      cn = c[g];
-      nnf += 1.0;
-    } else {
-      const SlTri r = sl_tri(L, found);
-      const int32_t a = r.a, b = r.b, k = r.d;
-      const double x1 = r.x1, y1 = r.y1, x2 = r.x2, y2 = r.y2, x3 = r.x3, y3 = r.y3;
-      const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
-      const double w1 = (pdx(x2, xb) * (y3 - yb) - pdx(x3, xb) * (y2 - yb)) / det;
-      const double w2 = (pdx(x3, xb) * (y1 - yb) - pdx(x1, xb) * (y3 - yb)) / det;
-      const double w3 = 1.0 - w1 - w2;
-      cn = w1 * c[a] + w2 * c[b] + w3 * c[k];
+    double xb, yb;
+    sl_point(M, g, ux[i], uy[i], dt, xb, yb);
+    SlTri r;
+    double bestd;
+    float rho2 = 0.0f;
+    const bool cand = sl_best(L, xb, yb, r, bestd, rho2);
+    const bool slow = cand && !sl_fast(L, r, xb, yb, bestd, rho2);
+    const uint64_t m = __ballot(slow);
+    if (slow) {
+      const int32_t p = qn + __popcll(m & ((1ull << lane) - 1ull));
+      queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)] = make_int2((int32_t)i, r.id);
     }
-    cout[g] = cn;
-    if (notfound) notfound[i] = found < 0 ? 1 : 0;
+    qn += __popcll(m);
     const double w = wmix ? wmix[i] : 0.0;
-    swc += w * cn;
     sw += w;
+    if (!slow) {
+      double cn;
+      if (!cand) {
+        cn = c[g];
+        nnf += 1.0;
+      } else {
+        cn = sl_value(r, xb, yb, c);
+      }
+      stnt(cout + g, cn);
+      if (notfound) notfound[i] = cand ? 0 : 1;
+      swc += w * cn;
+    }
   }
+  if (lane == 0) qcnt[BS / 64 * blockIdx.x + wv] = qn;
   const double a = block_sum(swc, sh), b = block_sum(sw, sh), d = block_sum(nnf, sh);
   if (threadIdx.x == 0) {
     part[blockIdx.x] = a;
     part[SLB + blockIdx.x] = b;
     part[2 * SLB + blockIdx.x] = d;
+  }
+}
+
+// second pass: the rank count for the queued points (same grid as k_sl)
+__global__ __launch_bounds__(BS) void k_sl_rank(MeshDev M, GridDev G, int64_t row0, int64_t n,
+                                                const double* __restrict__ ux, const double* __restrict__ uy, double dt,
+                                                const double* __restrict__ c, double* __restrict__ cout,
+                                                const double* __restrict__ wmix, int32_t* notfound, double* part,
+                                                const int2* __restrict__ queue, const int32_t* __restrict__ qcnt) {
+  __shared__ double sh[4];
+  double swc = 0.0, nnf = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t cnt = qcnt[BS / 64 * blockIdx.x + wv];
+  for (int32_t p = lane; p < cnt; p += 64) {
+    const int2 e = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)];
+    const int64_t i = e.x, g = row0 + i;
+    double xb, yb;
+    sl_point(M, g, ux[i], uy[i], dt, xb, yb);
+    const int32_t va = M.tri[3 * (int64_t)e.y], vb = M.tri[3 * (int64_t)e.y + 1], vc = M.tri[3 * (int64_t)e.y + 2];
+    const SlTri r{M.x[va], M.y[va], M.x[vb], M.y[vb], M.x[vc], M.y[vc], va, vb, vc, e.y};
+    // the key of k_sl's locate step, recomputed with the same operations
+    const double dx = (r.x1 + r.x2 + r.x3) / 3.0 - xb, dy = (r.y1 + r.y2 + r.y3) / 3.0 - yb;
+    const double bestd = dx * dx + dy * dy;
+    const bool ok = sl_rank_ok(G, xb, yb, bestd, e.y, 0.0f, 0);
+    double cn;
+    if (ok) {
+      cn = sl_value(r, xb, yb, c);
+    } else {
+      cn = c[g];
+      nnf += 1.0;
+    }
+    stnt(cout + g, cn);
+    if (notfound) notfound[i] = ok ? 0 : 1;
+    swc += (wmix ? wmix[i] : 0.0) * cn;
+  }
+  const double a = block_sum(swc, sh), d = block_sum(nnf, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] += a;
+    part[2 * SLB + blockIdx.x] += d;
   }
 }
 

@@ -114,5 +114,37 @@ PUCFEM_HD inline int32_t point(const FaceTab& f, int32_t n, int32_t i, int32_t j
   return f.base + rowbase(j - 1, n) + i - 1;
 }
 
+// any lattice point (i, j) of a face, corners included (va, vb, vc: the nodes at A, B, C)
+PUCFEM_HD inline int32_t vertex(const FaceTab& f, int32_t va, int32_t vb, int32_t vc, int32_t n, int32_t i, int32_t j) {
+  if (j == 0) return i == 0 ? va : (i == n ? vb : f.ab0 + f.abs * i);
+  if (i == 0) return j == n ? vc : f.ac0 + f.acs * j;
+  if (i + j == n) return f.bc0 + f.bcs * j;
+  return f.base + rowbase(j - 1, n) + i - 1;
+}
+
+// The small triangles of a face: cell (i, j, s) with s = 0 the "up" triangle (i, j), (i+1, j), (i, j+1)
+// (the face's own orientation; i + j <= n - 1) and s = 1 the "down" one (i+1, j), (i+1, j+1), (i, j+1)
+// (i + j <= n - 2), both listed counter-clockwise.  Red refinement keeps every child's orientation, so
+// a fine triangle's stored vertex order is one of the three rotations of its cell's list.
+PUCFEM_HD inline void cell_vertices(int32_t i, int32_t j, int32_t s, int32_t (&pi)[3], int32_t (&pj)[3]) {
+  if (s == 0) {
+    pi[0] = i, pj[0] = j, pi[1] = i + 1, pj[1] = j, pi[2] = i, pj[2] = j + 1;
+  } else {
+    pi[0] = i + 1, pj[0] = j, pi[1] = i + 1, pj[1] = j + 1, pi[2] = i, pj[2] = j + 1;
+  }
+}
+PUCFEM_HD inline int64_t cell_index(int32_t n, int32_t i, int32_t j, int32_t s) { return ((int64_t)j * n + i) * 2 + s; }
+
+// Per-face data of the lattice point location (semi-Lagrangian step): the frame (lattice coordinates
+// (u, v) = n M (q - A), M the inverse of [B - A, C - A]), the face table in GLOBAL internal ids, the
+// corner nodes and the caller id of the face's first fine triangle (children of t are 4t .. 4t+3, so
+// the fine triangles of face f are f 4^L .. (f + 1) 4^L - 1)
+struct SlFace {
+  double ax, ay, m00, m01, m10, m11;
+  FaceTab tab;
+  int32_t va, vb, vc, pad;
+  int64_t t0;
+};
+
 }  // namespace lat
 }  // namespace pucfem

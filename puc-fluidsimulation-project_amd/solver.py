@@ -209,7 +209,8 @@ class Context:
         visc = {0: "dense", 1: "block", 2: "multi-kernel"}
         pres = {0: "dense", 1: "block", 2: "jacobi-cg", 3: "mg-pcg"}
         return dict(viscous=visc[o[0]], pressure=pres[o[1]], reseeds=o[2], basis_p=o[3], basis_p2=o[4],
-                    visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7]))
+                    visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7] & 1),
+                    sl_locator="lattice" if o[7] & 2 else "records")
 
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))

@@ -137,6 +137,60 @@ def test_semilagrange_borderline_points(m, refine):
             assert np.abs(c - ref).max() < 1e-13, kind
 
 
+def sl_on(ctx, c, u, dt):
+    cin = np.ascontiguousarray(c, dtype=np.float64)
+    uu = np.ascontiguousarray(u, dtype=np.float64)
+    out = np.zeros_like(cin)
+    nf = np.zeros(len(cin), dtype=np.int32)
+    L.check(ctx.L.pucfem_sl_advect(ctx.h, L.dptr(cin), L.dptr(uu), float(dt), L.dptr(out), L.iptr(nf)), ctx.h)
+    return out, nf.astype(bool)
+
+
+@pytest.mark.parametrize("refine", [2, 3])
+def test_semilagrange_lattice_locator(refine, monkeypatch):
+    """The lattice locator (macro face + lattice cell arithmetic, production path on red-refined
+    hierarchies) returns the record locator's triangle for every point, bit for bit, including
+    points on vertices and edges where several triangles pass the weight test; and the oracle's
+    KDTree k=10 PointLocator on the same points (vertices / edges to 1e-13, as above)."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    X, T = mesh.coords, mesh.triangles
+    N = mesh.N
+    sim = stokes(mesh, tol=S.Tolerances.production())
+    assert sim.ctx.path_info()["sl_locator"] == "lattice"
+    monkeypatch.setenv("PUCFEM_SL_RECORDS", "1")
+    rec = stokes(mesh, tol=S.Tolerances.production())
+    assert rec.ctx.path_info()["sl_locator"] == "records"
+    rng = np.random.default_rng(11)
+    dt = 0.05
+    mid = 0.5 * (X[T[:, 0]] + X[T[:, 1]])
+    w = rng.random((N, 3))
+    w /= w.sum(1, keepdims=True)
+    kinds = {
+        "random": np.stack([rng.random(N), rng.random(N) * 1.2 - 0.1], 1),
+        "vertex": X[rng.integers(0, N, N)],
+        "edge": mid[rng.integers(0, len(T), N)],
+        "hole": 0.5 + 0.2 * (rng.random((N, 2)) - 0.5),
+        "inside": np.einsum("tk,tkd->td", w, X[T[rng.integers(0, len(T), N)]]),
+        "x_wrap": np.stack([rng.choice([0.0, 1.0 - 1e-17, 1e-300], N), rng.random(N)], 1),
+    }
+    c0 = np.sin(7 * X[:, 0]) * np.cos(5 * X[:, 1])
+    tree = KDTree(O.centroids(X, T))
+    for kind, q in kinds.items():
+        u = (X - q) / dt
+        c, nf = sl_on(sim.ctx, c0, u, dt)
+        c_rec, nf_rec = sl_on(rec.ctx, c0, u, dt)
+        assert np.array_equal(nf, nf_rec), kind
+        assert np.array_equal(c, c_rec), kind
+        ref, ref_nf = O.sl_advect(c0, u, dt, X, T, tree)
+        assert np.array_equal(nf, ref_nf), kind
+        if kind in ("random", "hole", "inside"):
+            assert np.array_equal(c, ref), kind
+        else:
+            assert np.abs(c - ref).max() < 1e-13, kind
+    sim.close()
+    rec.close()
+
+
 @pytest.mark.parametrize("m", ["mesh1", "fine"])
 def test_tracers_vs_reference(m, golden):
     g = golden(m)
