@@ -333,7 +333,7 @@ struct Ctx {
   LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
   bool lat_sl = false;
   double* part_sl = nullptr;  // k_sl partials, 3 x SLB
-  int2* sl_queue = nullptr;   // k_sl -> k_sl_rank: points whose rank needs the centroid count (mesh.N)
+  int32_t* sl_queue = nullptr; // k_sl -> k_sl_slow: rows off the lattice fast path (mesh.N)
   int32_t* sl_qcnt = nullptr; // per wave of k_sl: queued entries (SLB * BS / 64)
   bool has_cgrid = false, has_tgrid = false;
   double *c_full = nullptr, *c_new = nullptr, *ufx = nullptr, *ufy = nullptr;
@@ -498,15 +498,19 @@ struct Ctx {
   void sl_launch(int nb, i64 row0, i64 n, const double* vx, const double* vy, double dt, const double* cf, double* cn,
                  const double* w, int32_t* nf) {
     const MeshDev M{mx, my, mtri, mesh.T};
-    if (lat_sl)
-      klaunch(4, 8.0 * 6 * (double)n, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n,
-              vx, vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
-    else
-      klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx,
+    if (lat_sl) {
+      klaunch(4, 8.0 * 6 * (double)n, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
-    klaunch(8, 0.0, k_sl_rank, dim3(nb), dim3(BS), M, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt, cf, cn, w, nf,
-            part_sl, (const int2*)sl_queue, (const int32_t*)sl_qcnt);
+      klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
+              dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
+    } else {
+      klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
+              dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
+      klaunch(8, 0.0, k_sl_slow<LocDev>, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt,
+              cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
+    }
   }
+
 
 
   // ------------------------------------------------------------------ communication
@@ -1945,7 +1949,7 @@ void build(Ctx& c) {
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
   if (stokes) {
-    c.sl_queue = c.dalloc<int2>(m.N);
+    c.sl_queue = c.dalloc<int32_t>(m.N);
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
   }
   c.scal = c.dalloc<double>(32);
@@ -2018,12 +2022,23 @@ void build(Ctx& c) {
       }
       if (c.lat_sl) {
         Grid MG;
-        build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.5, MG, 1e-6);
+        build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, MG, 1e-6);
         GridDev mg{};
         dgrid(MG, mg, false);
-        c.llgrid = LatLocDev{mg.nx, mg.ny, mg.x0, mg.y0, mg.hx, mg.hy, mg.start, mg.item,
+        // home faces: the macro face of every face-interior row (the first face tried)
+        const LatticeLevel& LL = c.mg.back().latl;
+        std::vector<i32> home(N, -1);
+        for (i64 f = 0; f < c.macro.nf; ++f)
+          for (i64 k = 0; k < LL.F; ++k) home[LL.face_start[f] + k] = (i32)f;
+        c.llgrid = LatLocDev{mg.nx, mg.ny, mg.x0, mg.y0, 1.0 / mg.hx, 1.0 / mg.hy, mg.start, mg.item,
                              reinterpret_cast<const lat::SlFace*>(c.upload(sf)), c.upload(cells), dxy,
-                             c.upload(rho2), drv2, c.mg.back().latl.n, probe};
+                             c.upload(rho2), drv2, c.upload(home), nullptr, LL.n, probe};
+        // zero-velocity rows (walls): the answer for the row's own node, once
+        int32_t* dself = c.dalloc<int32_t>(N);
+        hipLaunchKernelGGL(k_sl_self<LatLocDev>, dim3(2048), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, m.T},
+                           c.llgrid, c.cgrid, (int64_t)N, dself);
+        KCHK();
+        c.llgrid.self = dself;
       } else {
         // inflated-bbox grid (~1 triangle per cell) + packed records
         Grid LG;

@@ -175,6 +175,17 @@ __device__ __forceinline__ double py_mod(double a, double b) {
   }
   return m;
 }
+// py_mod(a, 1.0) without fmod's loop: a - trunc(a) is fmod(a, 1) exactly (the fractional bits of a
+// are representable; NaN / inf propagate as fmod's do), then the same sign fix-up
+__device__ __forceinline__ double py_mod1(double a) {
+  double m = a - trunc(a);
+  if (m != 0.0) {
+    if (m < 0) m += 1.0;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
 
 }  // namespace dev
 }  // namespace pucfem

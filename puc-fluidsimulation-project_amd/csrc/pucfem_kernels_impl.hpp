@@ -1,6 +1,8 @@
 // Device kernels of libpucfem -- see pucfem_kernels.hpp for the layout / reduction conventions.
 // Included by pucfem_api.hip (single translation unit for the device code).
 #pragma once
+#include <type_traits>
+
 #include "pucfem_kernels.hpp"
 
 namespace pucfem {
@@ -895,7 +897,9 @@ struct LocDev {
   // per position: squared distance from the centroid to the 10th nearest other centroid (rounded down)
   const float* rho2;
   const float* rv2;  // per node: squared distance to its (KNN + 1)-th nearest centroid (rounded down)
-  int32_t probe;  // measurement knob (PUCFEM_SL_PROBE): 1 = accept T* without the rank count
+  // measurement knob (PUCFEM_SL_PROBE): bit 0 = accept T* without the rank count, bit 1 = not-found
+  // output 2 for the rows k_sl_slow finished (pucfem_sl_advect)
+  int32_t probe;
 };
 struct SlTri {
   double x1, y1, x2, y2, x3, y3;
@@ -944,10 +948,11 @@ __device__ __forceinline__ bool sl_test(const SlTri& r, double qx, double qy, do
   return true;
 }
 
-// Locate step (the rank test follows in k_sl / k_sl_rank): the passing triangle with the smallest
+// Locate step (the rank test follows in k_sl_slow): the passing triangle with the smallest
 // (d^2, id) key (false: none passes), its d^2 and its fast-accept radius.
 // Record locator: the records listed in q's cell of the inflated-bbox grid.
-__device__ __forceinline__ bool sl_best(const LocDev& L, double qx, double qy, SlTri& out, double& bestd, float& rho2) {
+__device__ __forceinline__ bool sl_best(const LocDev& L, int32_t, double qx, double qy, SlTri& out, double& bestd,
+                                        float& rho2) {
   const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
   const int64_t cell = (int64_t)cj * L.nx + ci;
   int32_t best = 0x7fffffff, bpos = -1;
@@ -983,7 +988,7 @@ __device__ __forceinline__ bool sl_best(const LocDev& L, double qx, double qy, S
 // are the record locator's, bit for bit.
 struct LatLocDev {
   int32_t nx, ny;
-  double x0, y0, hx, hy;
+  double x0, y0, ihx, ihy;       // macro grid: origin, inverse cell sizes
   const int32_t* start;          // macro grid cells -> face ids
   const int32_t* item;
   const lat::SlFace* face;
@@ -991,32 +996,70 @@ struct LatLocDev {
   const double2* xy;             // node coordinates (internal numbering)
   const float* rho2;             // per triangle id
   const float* rv2;              // per node, as LocDev::rv2
+  const int32_t* home;           // per row (internal id): its macro face (face-interior rows), else -1
+  // per row: the triangle the locator returns for the row's own node (a zero velocity: walls), -1 when
+  // none is accepted (k_sl_self, once at build); null until then
+  const int32_t* self;
   int32_t n, probe;
 };
 constexpr double SL_LDEL = 1e-7;
 
-// one lattice cell of face S as an SlTri (vertices in the mesh's stored order)
+// one lattice cell of face S as an SlTri (vertices in the mesh's stored order: the cell's list
+// rotated by the table's rotation; selects, not a dynamically indexed array, which would live in LDS)
 __device__ __forceinline__ SlTri sl_cell(const LatLocDev& L, const lat::SlFace& S, int32_t i, int32_t j, int32_t s) {
   const uint32_t ent = L.cell[lat::cell_index(L.n, i, j, s)];
   const int32_t rot = (int32_t)(ent & 3u);
-  int32_t pi[3], pj[3], vid[3];
+  int32_t pi[3], pj[3];
   lat::cell_vertices(i, j, s, pi, pj);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int32_t kk = (rot + k) % 3;
-    vid[k] = lat::vertex(S.tab, S.va, S.vb, S.vc, L.n, pi[kk], pj[kk]);
-  }
-  const double2 p = L.xy[vid[0]], q = L.xy[vid[1]], w = L.xy[vid[2]];
-  return SlTri{p.x, p.y, q.x, q.y, w.x, w.y, vid[0], vid[1], vid[2], (int32_t)(S.t0 + (int64_t)(ent >> 2))};
+  const int32_t c0 = lat::vertex(S.tab, S.va, S.vb, S.vc, L.n, pi[0], pj[0]);
+  const int32_t c1 = lat::vertex(S.tab, S.va, S.vb, S.vc, L.n, pi[1], pj[1]);
+  const int32_t c2 = lat::vertex(S.tab, S.va, S.vb, S.vc, L.n, pi[2], pj[2]);
+  const int32_t v0 = rot == 0 ? c0 : (rot == 1 ? c1 : c2);
+  const int32_t v1 = rot == 0 ? c1 : (rot == 1 ? c2 : c0);
+  const int32_t v2 = rot == 0 ? c2 : (rot == 1 ? c0 : c1);
+  const double2 p = L.xy[v0], q = L.xy[v1], w = L.xy[v2];
+  return SlTri{p.x, p.y, q.x, q.y, w.x, w.y, v0, v1, v2, (int32_t)(S.t0 + (int64_t)(ent >> 2))};
+}
+
+// q strictly inside one cell of face S (by SL_LDEL lattice units, hence inside the face and in no
+// other triangle's weight test): that cell; its key d is the reference's, exactly
+__device__ __forceinline__ bool sl_inner(const LatLocDev& L, const lat::SlFace& S, double qx, double qy, SlTri& out,
+                                         double& bestd, double& u, double& v) {
+  const int32_t n = L.n;
+  const double dx = qx - S.ax, dy = qy - S.ay;
+  u = (double)n * (S.m00 * dx + S.m01 * dy);
+  v = (double)n * (S.m10 * dx + S.m11 * dy);
+  const double fu = floor(u), fv = floor(v);
+  const double a = u - fu, b = v - fv;
+  const int32_t s = a + b > 1.0 ? 1 : 0;
+  const bool inner = s == 0 ? (a >= SL_LDEL && b >= SL_LDEL && a + b <= 1.0 - SL_LDEL)
+                            : (a <= 1.0 - SL_LDEL && b <= 1.0 - SL_LDEL && a + b >= 1.0 + SL_LDEL);
+  if (!(inner && fu >= 0.0 && fv >= 0.0 && fu + fv <= (double)(n - 1 - s))) return false;
+  out = sl_cell(L, S, (int32_t)fu, (int32_t)fv, s);
+  // the weights are >= SL_LDEL up to rounding: the weight test passes; only its det guard remains
+  const double det = (out.x2 - out.x1) * (out.y3 - out.y1) - (out.x3 - out.x1) * (out.y2 - out.y1);
+  if (!(fabs(det) >= 1e-14)) return false;
+  const double ex = (out.x1 + out.x2 + out.x3) / 3.0 - qx, ey = (out.y1 + out.y2 + out.y3) / 3.0 - qy;
+  bestd = ex * ex + ey * ey;
+  return true;
 }
 
 // Lattice locator.  Common case: q lies inside a macro face and inside one lattice cell by more than
 // SL_LDEL, so no other triangle can pass the weight test: that cell alone is tested.  Otherwise every
 // cell of every candidate face whose closure holds q up to SL_LDEL is tested, as the record locator
 // tests every record of its grid cell.
-__device__ __forceinline__ bool sl_best(const LatLocDev& L, double qx, double qy, SlTri& out, double& bestd,
-                                        float& rho2) {
-  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
+__device__ __forceinline__ bool sl_best(const LatLocDev& L, int32_t home, double qx, double qy, SlTri& out,
+                                        double& bestd, float& rho2) {
+  double u, v;
+  if (home >= 0 && sl_inner(L, L.face[home], qx, qy, out, bestd, u, v)) {
+    rho2 = L.rho2[out.id];
+    return true;
+  }
+  // cells of the macro grid by multiplication: a point within rounding of a cell line may land in
+  // either cell, and both list every face whose (inflated) bbox holds it
+  const double gx = floor((qx - L.x0) * L.ihx), gy = floor((qy - L.y0) * L.ihy);
+  const int32_t ci = !(gx >= 0.0) ? 0 : (gx >= (double)L.nx ? L.nx - 1 : (int32_t)gx);
+  const int32_t cj = !(gy >= 0.0) ? 0 : (gy >= (double)L.ny ? L.ny - 1 : (int32_t)gy);
   const int64_t gc = (int64_t)cj * L.nx + ci;
   const int32_t n = L.n;
   const double dn = (double)n;
@@ -1026,20 +1069,11 @@ __device__ __forceinline__ bool sl_best(const LatLocDev& L, double qx, double qy
   const int32_t e1 = L.start[gc + 1];
   for (int32_t e = L.start[gc]; e < e1 && !done; ++e) {
     const lat::SlFace& S = L.face[L.item[e]];
-    const double dx = qx - S.ax, dy = qy - S.ay;
-    const double u = dn * (S.m00 * dx + S.m01 * dy), v = dn * (S.m10 * dx + S.m11 * dy);
-    if (!(u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL)) continue;
-    const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
     {
-      const double a = u - i0, b = v - j0;
-      const int32_t s = a + b > 1.0 ? 1 : 0;
-      const bool inner = s == 0 ? (a >= SL_LDEL && b >= SL_LDEL && a + b <= 1.0 - SL_LDEL)
-                                : (a <= 1.0 - SL_LDEL && b <= 1.0 - SL_LDEL && a + b >= 1.0 + SL_LDEL);
-      if (inner && i0 + j0 <= n - 1 - s) {  // q strictly inside this cell (hence inside the face)
-        const SlTri r = sl_cell(L, S, i0, j0, s);
-        double d;
-        bool margin;
-        if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, bestd, best)) {
+      SlTri r;
+      double d;
+      if (sl_inner(L, S, qx, qy, r, d, u, v)) {
+        if (knn_less(d, r.id, bestd, best)) {
           bestd = d;
           best = r.id;
           out = r;
@@ -1047,6 +1081,8 @@ __device__ __forceinline__ bool sl_best(const LatLocDev& L, double qx, double qy
         break;
       }
     }
+    if (!(u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL)) continue;
+    const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
     for (int32_t j = max(j0 - 1, 0); j <= j0 + 1 && !done; ++j)
       for (int32_t i = max(i0 - 1, 0); i <= i0 + 1 && i + j <= n - 1 && !done; ++i) {
         const double a = u - i, b = v - j;
@@ -1083,7 +1119,7 @@ __device__ __forceinline__ double pdx(double a, double b) {  // StokesColor.py:3
 // back-traced point of row i (StokesColor.py:361-372): x mod 1, y clamped into (0, 1)
 __device__ __forceinline__ void sl_point(const MeshDev& M, int64_t g, double vx, double vy, double dt, double& xb,
                                          double& yb) {
-  xb = py_mod(M.x[g] - dt * vx * 1.0, 1.0);
+  xb = py_mod1(M.x[g] - dt * vx * 1.0);
   yb = M.y[g] - dt * vy * 1.0;
   if (yb < 0.0) yb = 1e-12;
   if (yb > 1.0) yb = 1.0 - 1e-12;
@@ -1098,16 +1134,87 @@ __device__ __forceinline__ double sl_value(const SlTri& r, double xb, double yb,
   return w1 * c[r.a] + w2 * c[r.b] + w3 * c[r.d];
 }
 
-// advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
-// nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
-// Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
-// Two passes.  k_sl locates every point and finishes those whose rank the fast accept settles (or
-// that no triangle holds); the rest, which need the centroid count, are queued and finished by
-// k_sl_rank, so the count's long loop runs on dense waves instead of stalling 63 finished lanes.
-// The queue is per wave and deterministic: wave w of block b writes its k-th entry into slot
-// k % 64 of the (k / 64)-th 64-row slice it processed (entries never outrun the rows they come from);
-// k_sl_rank block b runs the same waves' queues and adds its partial sums to block b's, so the
-// reductions keep a fixed order.
+// lattice fast path: q strictly inside a cell of its row's home face, every load of the point issued
+// together (coordinates, field values, radii), the rank settled by a fast accept (sl_fast's tests);
+// -> true with the interpolated value, false: the general locate of k_sl_slow decides.  Scalars
+// only (a struct here ends in scratch memory).
+__device__ __forceinline__ bool sl_lattice_fast(const LatLocDev& L, int64_t g, double qx, double qy,
+                                                const double* __restrict__ c, double& cn) {
+  // the face: the row's home face, else the faces of q's macro-grid cell (first one holding q
+  // strictly inside a cell)
+  const int32_t n = L.n;
+  const int32_t home = L.home[g];
+  int32_t f = -1;
+  double fu = 0.0, fv = 0.0;
+  int32_t s = 0;
+  auto inner = [&](int32_t cand) {
+    const lat::SlFace& S = L.face[cand];
+    const double dx = qx - S.ax, dy = qy - S.ay;
+    const double u = (double)n * (S.m00 * dx + S.m01 * dy), v = (double)n * (S.m10 * dx + S.m11 * dy);
+    fu = floor(u);
+    fv = floor(v);
+    const double a = u - fu, b = v - fv;
+    s = a + b > 1.0 ? 1 : 0;
+    const bool in = s == 0 ? (a >= SL_LDEL && b >= SL_LDEL && a + b <= 1.0 - SL_LDEL)
+                           : (a <= 1.0 - SL_LDEL && b <= 1.0 - SL_LDEL && a + b >= 1.0 + SL_LDEL);
+    return in && fu >= 0.0 && fv >= 0.0 && fu + fv <= (double)(n - 1 - s);
+  };
+  if (home >= 0 && inner(home)) {
+    f = home;
+  } else {
+    const double gx = floor((qx - L.x0) * L.ihx), gy = floor((qy - L.y0) * L.ihy);
+    const int32_t ci = !(gx >= 0.0) ? 0 : (gx >= (double)L.nx ? L.nx - 1 : (int32_t)gx);
+    const int32_t cj = !(gy >= 0.0) ? 0 : (gy >= (double)L.ny ? L.ny - 1 : (int32_t)gy);
+    const int64_t gc = (int64_t)cj * L.nx + ci;
+    const int32_t e1 = L.start[gc + 1];
+    for (int32_t e = L.start[gc]; e < e1; ++e) {
+      const int32_t cand = L.item[e];
+      if (cand != home && inner(cand)) {
+        f = cand;
+        break;
+      }
+    }
+    if (f < 0) return false;
+  }
+  const lat::SlFace& S = L.face[f];
+  const int32_t i = (int32_t)fu, j = (int32_t)fv;
+  const uint32_t ent = L.cell[lat::cell_index(n, i, j, s)];
+  const int32_t rot = (int32_t)(ent & 3u);
+  int32_t pi[3], pj[3];
+  lat::cell_vertices(i, j, s, pi, pj);
+  const int32_t c0 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[0], pj[0]);
+  const int32_t c1 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[1], pj[1]);
+  const int32_t c2 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[2], pj[2]);
+  const int32_t v0 = rot == 0 ? c0 : (rot == 1 ? c1 : c2);
+  const int32_t v1 = rot == 0 ? c1 : (rot == 1 ? c2 : c0);
+  const int32_t v2 = rot == 0 ? c2 : (rot == 1 ? c0 : c1);
+  const int32_t id = (int32_t)(S.t0 + (int64_t)(ent >> 2));
+  const double2 P1 = L.xy[v0], P2 = L.xy[v1], P3 = L.xy[v2];
+  const double f1 = c[v0], f2 = c[v1], f3 = c[v2];
+  const float rho2 = L.rho2[id], rv1 = L.rv2[v0], rv2 = L.rv2[v1], rv3 = L.rv2[v2];
+  const double x1 = P1.x, y1 = P1.y, x2 = P2.x, y2 = P2.y, x3 = P3.x, y3 = P3.y;
+  // the weights are >= SL_LDEL up to rounding: the weight test passes; only its det guard remains
+  const double det0 = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
+  if (!(fabs(det0) >= 1e-14)) return false;
+  const double ex = (x1 + x2 + x3) / 3.0 - qx, ey = (y1 + y2 + y3) / 3.0 - qy;
+  const double bestd = ex * ex + ey * ey;
+  if (!(4.0 * bestd * (1.0 + 1e-9) < (double)rho2 || (L.probe & 1))) {
+    const double d1 = (x1 - qx) * (x1 - qx) + (y1 - qy) * (y1 - qy);
+    const double d2 = (x2 - qx) * (x2 - qx) + (y2 - qy) * (y2 - qy);
+    const double d3 = (x3 - qx) * (x3 - qx) + (y3 - qy) * (y3 - qy);
+    const bool k1 = d1 <= d2 && d1 <= d3, k2 = !k1 && d2 <= d3;
+    const double rr = sqrt(k1 ? d1 : (k2 ? d2 : d3)) + sqrt(bestd);
+    if (!(rr * rr * (1.0 + 1e-9) < (double)(k1 ? rv1 : (k2 ? rv2 : rv3)))) return false;
+  }
+  // interpolation (StokesColor.py:374-386)
+  const double det = pdx(x2, x1) * (y3 - y1) - pdx(x3, x1) * (y2 - y1);
+  const double w1 = (pdx(x2, qx) * (y3 - qy) - pdx(x3, qx) * (y2 - qy)) / det;
+  const double w2 = (pdx(x3, qx) * (y1 - qy) - pdx(x1, qx) * (y3 - qy)) / det;
+  const double w3 = 1.0 - w1 - w2;
+  cn = w1 * f1 + w2 * f2 + w3 * f3;
+  return true;
+}
+
 // Fast accepts of the rank test (T* among the KNN nearest centroids); every centroid whose key is
 // below T*'s lies within R = |q - c_T*| of q.  (1) they lie within 2R of c_T*: fewer than KNN when
 // 2R is below the distance from c_T* to its KNN-th nearest other centroid (rho2) -- settles points
@@ -1120,51 +1227,89 @@ __device__ __forceinline__ bool sl_fast(const LOC& L, const SlTri& r, double qx,
   const double d1 = (r.x1 - qx) * (r.x1 - qx) + (r.y1 - qy) * (r.y1 - qy);
   const double d2 = (r.x2 - qx) * (r.x2 - qx) + (r.y2 - qy) * (r.y2 - qy);
   const double d3 = (r.x3 - qx) * (r.x3 - qx) + (r.y3 - qy) * (r.y3 - qy);
-  const double dv = d1 <= d2 && d1 <= d3 ? d1 : (d2 <= d3 ? d2 : d3);
-  const int32_t v = d1 <= d2 && d1 <= d3 ? r.a : (d2 <= d3 ? r.b : r.d);
-  const double rr = sqrt(dv) + sqrt(bestd);
-  return rr * rr * (1.0 + 1e-9) < (double)L.rv2[v];
+  const bool k1 = d1 <= d2 && d1 <= d3, k2 = !k1 && d2 <= d3;
+  const double rr = sqrt(k1 ? d1 : (k2 ? d2 : d3)) + sqrt(bestd);
+  return rr * rr * (1.0 + 1e-9) < (double)L.rv2[k1 ? r.a : (k2 ? r.b : r.d)];
 }
 
+// advect_semilagrange (StokesColor.py:347-389) + PointLocator.find (:314-345) for the owned
+// nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
+// Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
+// Two passes.  k_sl finishes the points of the lattice fast path (q strictly inside a cell of its
+// row's home face, rank settled by a fast accept: ~95 % of the rows) with a small register
+// footprint; the rest are queued and k_sl_slow runs the general locate and the centroid rank count
+// on dense waves.  The record locator has no fast path: k_sl queues every row.
+// The queue is per wave and deterministic: wave w of block b writes its k-th entry into slot
+// k % 64 of the (k / 64)-th 64-row slice it processed (entries never outrun the rows they come from);
+// k_sl_slow block b runs the same waves' queues and adds its partial sums to block b's, so the
+// reductions keep a fixed order.
 template <class LOC>
-__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, GridDev G, int64_t row0, int64_t n,
+__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, int64_t row0, int64_t n,
                                            const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                            const double* __restrict__ c, double* __restrict__ cout,
                                            const double* __restrict__ wmix, int32_t* notfound, double* part,
-                                           int2* __restrict__ queue, int32_t* __restrict__ qcnt) {
+                                           int32_t* __restrict__ queue, int32_t* __restrict__ qcnt) {
+  constexpr bool LAT = std::is_same<LOC, LatLocDev>::value;
   __shared__ double sh[4];
   double swc = 0.0, sw = 0.0, nnf = 0.0;
   int64_t r0, r1;
   block_rows(n, r0, r1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int32_t qn = 0;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+  // the row inputs of the next iteration are loaded one iteration ahead
+  int64_t i = r0 + threadIdx.x;
+  double nx_ = 0.0, ny_ = 0.0, nvx = 0.0, nvy = 0.0;
+  if (LAT && i < r1) {
+    nx_ = M.x[row0 + i];
+    ny_ = M.y[row0 + i];
+    nvx = ux[i];
+    nvy = uy[i];
+  }
+  for (; i < r1; i += BS) {
     const int64_t g = row0 + i;
-    double xb, yb;
-    sl_point(M, g, ux[i], uy[i], dt, xb, yb);
-    SlTri r;
-    double bestd;
-    float rho2 = 0.0f;
-    const bool cand = sl_best(L, xb, yb, r, bestd, rho2);
-    const bool slow = cand && !sl_fast(L, r, xb, yb, bestd, rho2);
-    const uint64_t m = __ballot(slow);
-    if (slow) {
+    bool done = false;
+    double cn = 0.0;
+    if constexpr (LAT) {
+      const double xg = nx_, yg = ny_, vx = nvx, vy = nvy;
+      if (i + BS < r1) {
+        nx_ = M.x[g + BS];
+        ny_ = M.y[g + BS];
+        nvx = ux[i + BS];
+        nvy = uy[i + BS];
+      }
+      double xb = py_mod1(xg - dt * vx * 1.0);
+      double yb = yg - dt * vy * 1.0;
+      if (yb < 0.0) yb = 1e-12;
+      if (yb > 1.0) yb = 1.0 - 1e-12;
+      if (vx == 0.0 && vy == 0.0 && L.self) {
+        // q is the row's own node (no-slip walls): on lattice lines, where several triangles pass the
+        // weight test; the answer for this q was settled once at build
+        const int32_t t = L.self[g];
+        if (t >= 0) {
+          const int32_t va = M.tri[3 * (int64_t)t], vb = M.tri[3 * (int64_t)t + 1], vc = M.tri[3 * (int64_t)t + 2];
+          const SlTri r{M.x[va], M.y[va], M.x[vb], M.y[vb], M.x[vc], M.y[vc], va, vb, vc, t};
+          cn = sl_value(r, xb, yb, c);
+        } else {
+          cn = c[g];
+          nnf += 1.0;
+        }
+        if (notfound) notfound[i] = t >= 0 ? 0 : 1;
+        done = true;
+      } else {
+        done = sl_lattice_fast(L, g, xb, yb, c, cn);
+        if (done && notfound) notfound[i] = 0;
+      }
+    }
+    const uint64_t m = __ballot(!done);
+    if (!done) {
       const int32_t p = qn + __popcll(m & ((1ull << lane) - 1ull));
-      queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)] = make_int2((int32_t)i, r.id);
+      queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)] = (int32_t)i;
     }
     qn += __popcll(m);
     const double w = wmix ? wmix[i] : 0.0;
     sw += w;
-    if (!slow) {
-      double cn;
-      if (!cand) {
-        cn = c[g];
-        nnf += 1.0;
-      } else {
-        cn = sl_value(r, xb, yb, c);
-      }
+    if (done) {
       stnt(cout + g, cn);
-      if (notfound) notfound[i] = cand ? 0 : 1;
       swc += w * cn;
     }
   }
@@ -1177,12 +1322,13 @@ __global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, GridDev G, int64_t 
   }
 }
 
-// second pass: the rank count for the queued points (same grid as k_sl)
-__global__ __launch_bounds__(BS) void k_sl_rank(MeshDev M, GridDev G, int64_t row0, int64_t n,
+// second pass: the queued points -- general locate, fast accepts, centroid rank count (same grid as k_sl)
+template <class LOC>
+__global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int64_t row0, int64_t n,
                                                 const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                                 const double* __restrict__ c, double* __restrict__ cout,
                                                 const double* __restrict__ wmix, int32_t* notfound, double* part,
-                                                const int2* __restrict__ queue, const int32_t* __restrict__ qcnt) {
+                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt) {
   __shared__ double sh[4];
   double swc = 0.0, nnf = 0.0;
   int64_t r0, r1;
@@ -1190,16 +1336,14 @@ __global__ __launch_bounds__(BS) void k_sl_rank(MeshDev M, GridDev G, int64_t ro
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t cnt = qcnt[BS / 64 * blockIdx.x + wv];
   for (int32_t p = lane; p < cnt; p += 64) {
-    const int2 e = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)];
-    const int64_t i = e.x, g = row0 + i;
+    const int64_t i = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)], g = row0 + i;
     double xb, yb;
     sl_point(M, g, ux[i], uy[i], dt, xb, yb);
-    const int32_t va = M.tri[3 * (int64_t)e.y], vb = M.tri[3 * (int64_t)e.y + 1], vc = M.tri[3 * (int64_t)e.y + 2];
-    const SlTri r{M.x[va], M.y[va], M.x[vb], M.y[vb], M.x[vc], M.y[vc], va, vb, vc, e.y};
-    // the key of k_sl's locate step, recomputed with the same operations
-    const double dx = (r.x1 + r.x2 + r.x3) / 3.0 - xb, dy = (r.y1 + r.y2 + r.y3) / 3.0 - yb;
-    const double bestd = dx * dx + dy * dy;
-    const bool ok = sl_rank_ok(G, xb, yb, bestd, e.y, 0.0f, 0);
+    SlTri r;
+    double bestd;
+    float rho2;
+    const bool cand = sl_best(L, -1, xb, yb, r, bestd, rho2);
+    const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok(G, xb, yb, bestd, r.id, 0.0f, 0));
     double cn;
     if (ok) {
       cn = sl_value(r, xb, yb, c);
@@ -1208,13 +1352,29 @@ __global__ __launch_bounds__(BS) void k_sl_rank(MeshDev M, GridDev G, int64_t ro
       nnf += 1.0;
     }
     stnt(cout + g, cn);
-    if (notfound) notfound[i] = ok ? 0 : 1;
+    if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;  // probe bit 1: mark the slow rows
     swc += (wmix ? wmix[i] : 0.0) * cn;
   }
   const double a = block_sum(swc, sh), d = block_sum(nnf, sh);
   if (threadIdx.x == 0) {
     part[blockIdx.x] += a;
     part[2 * SLB + blockIdx.x] += d;
+  }
+}
+
+// the locator's answer for every row's own node (q = its node after the x wrap: zero velocity), once
+// at build: the triangle id, or -1 when no triangle is accepted
+template <class LOC>
+__global__ __launch_bounds__(BS) void k_sl_self(MeshDev M, LOC L, GridDev G, int64_t n, int32_t* __restrict__ out) {
+  for (int64_t g = (int64_t)blockIdx.x * BS + threadIdx.x; g < n; g += (int64_t)gridDim.x * BS) {
+    double xb, yb;
+    sl_point(M, g, 0.0, 0.0, 0.0, xb, yb);
+    SlTri r;
+    double bestd;
+    float rho2;
+    const bool cand = sl_best(L, -1, xb, yb, r, bestd, rho2);
+    const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok(G, xb, yb, bestd, r.id, 0.0f, 0));
+    out[g] = ok ? r.id : -1;
   }
 }
 

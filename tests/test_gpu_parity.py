@@ -175,8 +175,12 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
     }
     c0 = np.sin(7 * X[:, 0]) * np.cos(5 * X[:, 1])
     tree = KDTree(O.centroids(X, T))
+    # zero velocity (no-slip walls): q is the row's own node, answered from the build-time table
+    kinds["zero"] = np.where(rng.random((N, 1)) < 0.5, X, kinds["random"])
     for kind, q in kinds.items():
         u = (X - q) / dt
+        if kind == "zero":
+            u[np.all(q == X, axis=1)] = 0.0
         c, nf = sl_on(sim.ctx, c0, u, dt)
         c_rec, nf_rec = sl_on(rec.ctx, c0, u, dt)
         assert np.array_equal(nf, nf_rec), kind
