@@ -92,6 +92,11 @@ typedef struct pucfem_params {
                           coarse mesh's triangles are matrix-free lattice stencils (per-face constants) and only
                           the nodes on coarse edges / vertices keep stored SELL rows; 1 = stored SELL operators
                           for every row */
+  int32_t dye_scheme;  /* STOKES_COLOR dye update: 0 = semi-Lagrangian (StokesColor.py:347-389); 1 = implicit
+                          FEM advection-diffusion (scripts/good_visualization.py:700-718: consistent mass +
+                          convection + diffusion, the periodic penalty restated as its exact merged limit,
+                          BiCGStab); single rank */
+  double dye_diffusivity; /* D of the implicit variant (good_visualization.py:404: 1e-3) */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -128,7 +133,8 @@ enum pucfem_op {
   PUCFEM_OP_GY = 4,
   PUCFEM_OP_DIV = 5,    /* calculate_divergence (StokesColor.py:130-165): x = u (N,2), y = div (N) */
   PUCFEM_OP_GRAD = 6,   /* calculate_gradiant  (StokesColor.py:224-263): x = p (N), y = (N,2) */
-  PUCFEM_OP_LIT = 7     /* literal heat operator I + DT*A (heatEq.py:305) or Poisson A (poisson.py:253-278) */
+  PUCFEM_OP_LIT = 7,    /* literal heat operator I + DT*A (heatEq.py:305) or Poisson A (poisson.py:253-278) */
+  PUCFEM_OP_MCONS = 8   /* consistent mass of the implicit dye variant (StokesColor.py:286-312; host CSR only) */
 };
 
 /* ---- library / context ---------------------------------------------------------- */
@@ -186,6 +192,16 @@ int pucfem_sl_advect(void* ctx, const double* c, const double* u, double dt, dou
                      int32_t* notfound);
 /* tracer step (StokesFood.py:482-499) on the tracers held in the context, with u given */
 int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps);
+/* makePerBCU / makeDirBCU (StokesColor.py:405-431) on a host velocity u (N,2), in place, through the
+   device's boundary kernels: which bit 0 = makePerBCU (slave <- master copies), bit 1 = makeDirBCU
+   (walls and squirmer surface); both: the periodic copies first, as the step applies them.
+   Single-rank Stokes contexts; the step's state is not touched (scratch buffers). */
+int pucfem_apply_bc(void* ctx, int32_t which, double* u);
+/* One implicit FEM dye step (scripts/good_visualization.py:700-718) on a context built with
+   dye_scheme = 1: c_out = A^-1 (M c) with A = M + dt (C_u + D K) + diag(dt M_lumped div u), periodic
+   pairs merged, then c[slave] = c[master]; c, c_out (N), u (N,2) in caller order; iters: BiCGStab
+   iterations (may be NULL).  The step's state is not touched. */
+int pucfem_dye_step(void* ctx, const double* c, const double* u, double* c_out, int32_t* iters);
 /* mixing_index (StokesColor.py:391-403) over marker==0 nodes: out = (I, mu, var) */
 int pucfem_mixing_index(void* ctx, const double* c, double* out3);
 

@@ -20,6 +20,7 @@ __all__ = [
     "visc_matrix", "PressureSolver", "centroids", "sl_advect", "mixing_index",
     "plane_coefficients", "locate_bary", "tracer_init", "tracer_step",
     "poisson_literal", "HeatLiteral", "StokesRef", "pressure_operator", "jacobi_pcg",
+    "mass_and_convection", "dye_implicit_step",
 ]
 
 TOL = 1e-6
@@ -554,6 +555,68 @@ class StokesRef:
         if tracers is not None:
             out["tracers"], out["status"] = tracer_step(tracers, status, un, dt, X, T)
         return out
+
+
+# ----------------------------------------------------------------------------- implicit dye variant
+def mass_and_convection(X, T, u):
+    """build_mass_and_convection (StokesColor.py:286-312 = good_visualization.py:348-374): the
+    consistent mass M_ij += area/12 (2 on the diagonal) and the convection matrix
+    C_ij += area/3 <u_c, grad_j> with u_c the triangle's vertex mean and grad_j scaled by 1/(2|det|)
+    (|det|, not the signed det), skipping |det| < 1e-14; accumulated in triangle order."""
+    x1, y1, x2, y2, x3, y3 = _xy(X, T)
+    det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2)
+    ok = np.abs(det) >= 1e-14
+    area = 0.5 * np.abs(det)
+    fac = np.where(np.eye(3, dtype=bool), 2.0, 1.0)
+    mv = (area / 12.0)[:, None, None] * fac[None]
+    uc = ((u[T[:, 0]] + u[T[:, 1]]) + u[T[:, 2]]) / 3.0
+    den = 2 * np.abs(det)
+    gx = np.stack([y2 - y3, y3 - y1, y1 - y2], 1) / den[:, None]
+    gy = np.stack([x3 - x2, x1 - x3, x2 - x1], 1) / den[:, None]
+    dot = uc[:, 0:1] * gx + uc[:, 1:2] * gy            # (T, 3): <u_c, grad_j>
+    cv = np.repeat(((area / 3)[:, None] * dot)[:, None, :], 3, 1)  # row i, column j
+    rows = np.repeat(T[:, :, None], 3, 2)[ok].ravel()
+    cols = np.repeat(T[:, None, :], 3, 1)[ok].ravel()
+    N = X.shape[0]
+    return _scatter_csr(N, rows, cols, mv[ok].ravel()), _scatter_csr(N, rows, cols, cv[ok].ravel())
+
+
+def dye_implicit_step(c, u, X, T, pairs, dt, D, K=None, merged=True):
+    """One step of the implicit FEM dye advection-diffusion (good_visualization.py:700-718):
+    A = M + dt (C_u + D K) + diag(G), G = dt M_lumped div(u) with G[slave] = G[master],
+    rhs = M c, c = A^-1 rhs, c[slave] = c[master].  The reference makes M and A periodic with a
+    1e10 penalty (apply_periodic_bc, :179-194, on M at :592 and on A at :711); merged=True solves
+    the penalty's limit exactly -- slave columns folded into the masters, the pair rows summed --
+    merged=False the literal penalised system (sparse LU)."""
+    N = X.shape[0]
+    M, C = mass_and_convection(X, T, u)
+    K = stiffness(X, T) if K is None else K
+    G = dt * (lumped_mass(X, T) * divergence(X, T, u))
+    pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    G[pairs[:, 1]] = G[pairs[:, 0]]
+    A = (M + dt * (C + D * K) + sp.diags(G)).tocsr()
+    if merged:
+        dof = np.arange(N)
+        dof[pairs[:, 1]] = pairs[:, 0]
+        P = sp.csr_matrix((np.ones(N), (np.arange(N), dof)), shape=(N, N))
+        Am = (P.T @ A @ P).tolil()
+        Am[pairs[:, 1], pairs[:, 1]] = 1.0
+        b = P.T @ (M @ c)
+        b[pairs[:, 1]] = c[pairs[:, 1]]
+        x = spla.spsolve(Am.tocsc(), b)
+    else:
+        pen = 1.0e10
+        Pn = sp.lil_matrix((N, N))
+        for m, s in pairs:
+            Pn[m, m] += pen
+            Pn[s, s] += pen
+            Pn[m, s] -= pen
+            Pn[s, m] -= pen
+        Mp = (M + Pn).tocsr()
+        x = spla.spsolve((Mp + dt * (C + D * K) + sp.diags(G) + Pn).tocsc(), Mp @ c)
+    x = np.asarray(x)
+    x[pairs[:, 1]] = x[pairs[:, 0]]
+    return x
 
 
 # ----------------------------------------------------------------------------- CPU baseline helpers

@@ -12,7 +12,8 @@ from ._lib import PucfemError, device_count, lib as _load_library  # noqa: F401
 from .mesh import (Mesh, boundary_sets, filter_wall_pairs, find_boundary_pairs, load_mesh, readEle,  # noqa: F401
                    readNode, readPoly, writeEle, writeNode, writePoly)
 from .ops import (advect_semilagrange, buildLumpedMassMatrix, buildStiffnessMatrix, calculate_divergence,  # noqa: F401
-                  calculate_gradiant, solve_pressure, solve_viscous)
+                  build_mass_and_convection_mass, calculate_gradiant, dye_implicit_step, makeDirBCU, makePerBCU,
+                  mixing_index, set_globals, solve_pressure, solve_viscous)
 from .solver import (Context, HeatSimulation, Result, SquirmerBC, StokesSimulation, Tolerances,  # noqa: F401
                      poisson_solve, solve, squirmer_values)
 from .tracers import tracer_init  # noqa: F401

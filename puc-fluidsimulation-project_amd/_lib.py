@@ -17,7 +17,7 @@ LIBNAME = "libpucfem.so"
 # enums (pucfem.h)
 STOKES_COLOR, STOKES_FOOD, HEAT, POISSON = 0, 1, 2, 3
 F_U, F_USTAR, F_P, F_P2, F_DIV_STAR, F_DIV_U, F_FINAL_DIV, F_C, F_SCALAR, F_TRACERS, F_STATUS = range(11)
-OP_K, OP_VISC, OP_PRES, OP_GX, OP_GY, OP_DIV, OP_GRAD, OP_LIT = range(8)
+OP_K, OP_VISC, OP_PRES, OP_GX, OP_GY, OP_DIV, OP_GRAD, OP_LIT, OP_MCONS = range(9)
 HOST_ONLY = -1
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOCONV", -4: "ESTATE", -5: "ENCCL", -6: "ENOMEM", -7: "ENODEV"}
 
@@ -38,7 +38,8 @@ class Params(ct.Structure):
         ("mg_degree", ct.c_int32), ("mg_ratio", ct.c_double), ("mg_post", ct.c_int32),
         ("mg_single", ct.c_int32), ("mg_rep_nodes", ct.c_int64), ("mg_f32_vals", ct.c_int32),
         ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("proj_k_visc", ct.c_int32), ("mg_kind", ct.c_int32),
-        ("solver_path", ct.c_int32), ("assembled", ct.c_int32),
+        ("solver_path", ct.c_int32), ("assembled", ct.c_int32), ("dye_scheme", ct.c_int32),
+        ("dye_diffusivity", ct.c_double),
     ]
 
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "pucfem_apply": ([_P, ct.c_int32, _D, _D], ct.c_int),
     "pucfem_solve": ([_P, ct.c_int32, _D, _D, ct.c_double, ct.c_int32, _I32], ct.c_int),
     "pucfem_sl_advect": ([_P, _D, _D, ct.c_double, _D, _I32], ct.c_int),
+    "pucfem_apply_bc": ([_P, ct.c_int32, _D], ct.c_int),
+    "pucfem_dye_step": ([_P, _D, _D, _D, _I32], ct.c_int),
     "pucfem_tracer_step": ([_P, _D, ct.c_double, ct.c_int32], ct.c_int),
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),

@@ -330,6 +330,14 @@ struct Ctx {
   int32_t* mtri = nullptr;
   GridDev cgrid{}, tgrid{};
   LocDev lgrid{};
+  // implicit FEM dye variant (prm.dye_scheme == 1, good_visualization.py:700-718)
+  bool dye_impl = false;
+  DevSell dDye{};              // the merged (Pp) pattern, every row stored
+  DyeDev dye{};
+  double *dDyeVal = nullptr, *dDyeM = nullptr, *dDyeW = nullptr, *dDyeDinv = nullptr, *dDyeB = nullptr;
+  int64_t* dDyeDiag = nullptr;  // SELL slot of each row's diagonal
+  int last_dye_it = 0;
+  DyeOp dyeop;  // host data of the implicit dye operator (built with the host operators)
   LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
   bool lat_sl = false;
   double* part_sl = nullptr;  // k_sl partials, 3 x SLB
@@ -1176,7 +1184,13 @@ struct Ctx {
     reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
-      sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
+      if (dye_impl) {
+        last_dye_it = dye_step(ux, uy, final_div, c_full, c_new);
+        hipLaunchKernelGGL(k_wsum, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, (const double*)c_new,
+                           (const double*)dwmix, part_sl);
+      } else {
+        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
+      }
       KCHK();
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
@@ -1197,6 +1211,36 @@ struct Ctx {
     its[0] = itv;
     its[1] = itp;
     its[2] = itp2;
+  }
+
+  // implicit dye step (good_visualization.py:700-718) from cin with velocity (vx, vy) and its lumped
+  // divergence dv into cout: assemble the merged operator, rhs = M c, BiCGStab from c, periodic copies
+  int dye_step(const double* vx, const double* vy, const double* dv, const double* cin, double* cout) {
+    const i64 n = lp.n_own;
+    hipLaunchKernelGGL(k_dye_w, dim3(grid_ew(mesh.T)), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, vx, vy, dDyeW);
+    hipLaunchKernelGGL(k_dye_assemble, dim3(grid_ew(dye.nslots)), dim3(BS), 0, st, dye, (const double*)dDyeW, dv,
+                       prm.dt, prm.dye_diffusivity, dDyeVal);
+    hipLaunchKernelGGL(k_dye_dinv, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const int64_t*)dDyeDiag,
+                       (const double*)dDyeVal, dDyeDinv);
+    KCHK();
+    with_c16(dDye, [&](auto c16) {
+      hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(dDye.nslices)), dim3(BS), 0, st, dDye.view(), nof(),
+                         (const double*)dDyeM, cin, dDyeB);
+    });
+    KCHK();
+    HIPCHK(hipMemcpyAsync(cout, cin, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    const int it = bicgstab(cout, dDyeB, std::max(prm.rtol_lin, 1e-13), prm.maxit_lin, &dDye, dDyeVal, dDyeDinv);
+    if (ncopy > 0) {  // c[slave] = c[master] (good_visualization.py:715-716)
+      if (bc_gather) {
+        hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcsrc,
+                           dbctmp, 1, cout, cout);
+        KCHK();
+      }
+      hipLaunchKernelGGL(k_bc_apply, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcdst, dcsrc,
+                         bc_gather ? (const double*)dbctmp : nullptr, 0, ddnode, ddval, 1, cout, cout);
+      KCHK();
+    }
+    return it;
   }
 
   void tracer_advance(double dt) {
@@ -1220,15 +1264,21 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ literal operators (heat / Poisson)
-  int bicgstab(double* x, const double* b, double tol, int maxit) {
+  // Jacobi-preconditioned BiCGStab on the literal operator (heat / Poisson) or, given A / av / dinv,
+  // on another fully stored SELL operator (the implicit dye system)
+  int bicgstab(double* x, const double* b, double tol, int maxit, const DevSell* A = nullptr,
+               const double* av = nullptr, const double* dinv_op = nullptr) {
     const i64 n = lp.n_own;
     const int nb = nb_rows(n), ge = grid_ew(n);
     double *r = litw[0], *rh = litw[1], *pp = litw[2], *v = litw[3], *s = litw[4], *t = litw[5], *ph = litw[6],
            *sh = litw[7];
+    const DevSell& AA = A ? *A : dLit;
+    const double* AV = A ? av : dLitv;
+    const double* dlit_dinv = A ? dinv_op : this->dlit_dinv;
     auto spmv = [&](const double* in, double* out) {
-      with_c16(dLit, [&](auto c16) {
-        hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(dLit.nslices)), dim3(BS), 0, st, dLit.view(), nof(),
-                           dLitv, in, out);
+      with_c16(AA, [&](auto c16) {
+        hipLaunchKernelGGL(k_spmv<decltype(c16)::value>, dim3(nb_for(AA.nslices)), dim3(BS), 0, st, AA.view(), nof(),
+                           AV, in, out);
       });
       KCHK();
     };
@@ -1506,6 +1556,9 @@ void build(Ctx& c) {
   HostMesh& m = c.mesh;
   // lattice operators: a multigrid hierarchy of >= 2 red refinements (face interiors exist)
   c.lattice = stokes && prm.precond == 1 && c.mg_levels >= 2 && prm.assembled == 0;
+  c.dye_impl = prm.scheme == PUCFEM_STOKES_COLOR && prm.dye_scheme == 1;
+  require(prm.dye_scheme == 0 || prm.dye_scheme == 1, "dye_scheme must be 0 (semi-Lagrangian) or 1 (implicit)");
+  require(!c.dye_impl || c.world == 1, "the implicit dye variant runs on one rank");
   if (c.lattice) {
     build_macro(c.coarse, prm.nstrips, c.mg_levels, c.macro);
     lattice_ordering(m, c.macro, c.mg_levels, c.ord, c.lat_fine);
@@ -1532,6 +1585,7 @@ void build(Ctx& c) {
     }
     c.n_free = N - (i64)c.op_pairs.size();
     build_pressure(c.P, c.as.K, c.dof, c.slave_of, c.Pp);
+    if (c.dye_impl) build_dye(m, c.ord, c.P, c.Pp, c.dof, c.dyeop);
   }
   c.use_mg = stokes && prm.precond == 1 && c.mg_levels > 0;
   if (c.use_mg) build_mg_host(c);
@@ -1684,6 +1738,38 @@ void build(Ctx& c) {
   c.dGx = c.upload(tmp);
   sell_values(c.P, lp, c.sP, c.as.Gy, tmp);
   c.dGy = c.upload(tmp);
+  if (c.dye_impl) {  // implicit dye operator on the merged pattern, every row stored
+    const DyeOp& D = c.dyeop;
+    Sell S;
+    build_sell(c.Pp, lp, S);
+    dsell(S, c.Pp, c.dDye);
+    const i64 nnzp = c.Pp.nnz();
+    std::vector<double> eid(nnzp);
+    for (i64 e = 0; e < nnzp; ++e) eid[e] = (double)(e + 1);
+    sell_values(c.Pp, lp, S, eid, tmp);
+    std::vector<i32> slot2e(S.padded);
+    for (i64 q = 0; q < S.padded; ++q) slot2e[q] = tmp[q] > 0.0 ? (i32)(tmp[q] - 1.0) : -1;
+    std::vector<double> mm(nnzp, 0.0);  // merged consistent mass, identity slave rows
+    for (i64 e = 0; e < nnzp; ++e) {
+      if (D.eptr[e] == D.eptr[e + 1]) mm[e] = 1.0;
+      for (i64 z = D.eptr[e]; z < D.eptr[e + 1]; ++z) mm[e] += D.mc[D.ek[z]];
+    }
+    sell_values(c.Pp, lp, S, mm, tmp);
+    c.dDyeM = c.upload(tmp);
+    std::vector<i64> dslot(N);
+    for (i64 r = 0; r < N; ++r) {
+      const i64 e = c.Pp.find(r, (i32)r);
+      require(e >= 0, "dye operator: a row without a diagonal");
+      dslot[r] = S.slice_off[r / 64] + (e - c.Pp.rowptr[r]) * 64 + r % 64;
+    }
+    c.dDyeDiag = c.upload(dslot);
+    c.dye = DyeDev{c.upload(slot2e), c.upload(D.eptr), c.upload(D.ek), c.upload(D.mc), c.upload(c.as.K),
+                   c.upload(D.cptr), c.upload(D.cw), c.upload(D.diag_row), c.upload(c.dof), c.upload(c.as.M), S.padded};
+    c.dDyeVal = c.dalloc<double>(S.padded);
+    c.dDyeW = c.dalloc<double>(3 * m.T);
+    c.dDyeDinv = c.dalloc<double>(c.nloc);
+    c.dDyeB = c.dalloc<double>(c.nloc);
+  }
   // Jacobi symmetric scaling S A S of A_visc
   auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
     sg.resize(N);
@@ -1957,7 +2043,7 @@ void build(Ctx& c) {
   c.redbuf = c.dalloc<double>(8 * 64);
   c.vals = c.dalloc<double>(16);
   c.bicg_sc = c.dalloc<double>(16);
-  if (literal) {
+  if (literal || c.dye_impl) {
     for (int q = 0; q < 9; ++q) c.litw[q] = c.dalloc<double>(c.nloc);
   }
   // full-mesh replica in internal numbering
@@ -2416,7 +2502,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       double* rec = c.dalloc<double>(8 * (i64)nsteps);
       int* dits = c.dalloc<int>(3 * (i64)nsteps);
       std::vector<int32_t> its(3 * (size_t)nsteps);
-      if (c.dense && !c.timer.on) {
+      if (c.dense && !c.timer.on && !c.dye_impl) {
         // direct-solve small-mesh path: every step is the same sequence of ~25 launches with no
         // host synchronisation -> capture it once, replay it per step
         if (!c.gexec) {
@@ -2747,6 +2833,72 @@ int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, d
   });
 }
 
+int pucfem_apply_bc(void* ctx, int32_t which, double* u) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.world == 1 && (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD),
+            "apply_bc needs a single-rank Stokes context");
+    require(which >= 1 && which <= 3, "apply_bc: which must be 1 (periodic), 2 (Dirichlet) or 3 (both)");
+    const i64 N = c.mesh.N;
+    std::vector<double> bx(N), by(N);
+    for (i64 g = 0; g < N; ++g) {
+      bx[g] = u[2 * c.ord.new2old[g]];
+      by[g] = u[2 * c.ord.new2old[g] + 1];
+    }
+    double *tx = c.cg_q[0], *ty = c.cg_q[1];  // scratch (the step's state stays untouched)
+    HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    const int ncopy = (which & 1) ? c.ncopy : 0, ndir = (which & 2) ? c.ndir : 0;
+    if (ncopy + ndir > 0) {
+      if (c.bc_gather && ncopy > 0) {
+        hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, c.st, ncopy,
+                           c.dcsrc, c.dbctmp, c.dir_ncomp, tx, ty);
+        KCHK();
+      }
+      const int nb = (int)std::min<i64>(1024, std::max<i64>(1, (ncopy + ndir + BS - 1) / BS));
+      hipLaunchKernelGGL(k_bc_apply, dim3(nb), dim3(BS), 0, c.st, ncopy, c.dcdst, c.dcsrc,
+                         c.bc_gather ? (const double*)c.dbctmp : nullptr, ndir, c.ddnode, c.ddval, c.dir_ncomp, tx, ty);
+      KCHK();
+    }
+    HIPCHK(hipMemcpyAsync(bx.data(), tx, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(by.data(), ty, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipStreamSynchronize(c.st));
+    for (i64 g = 0; g < N; ++g) {
+      u[2 * c.ord.new2old[g]] = bx[g];
+      u[2 * c.ord.new2old[g] + 1] = by[g];
+    }
+  });
+}
+
+int pucfem_dye_step(void* ctx, const double* cin, const double* u, double* cout, int32_t* iters) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(c.dye_impl, "dye_step needs a context built with dye_scheme = 1 (implicit)");
+    const i64 N = c.mesh.N;
+    std::vector<double> a(N), bx(N), by(N);
+    for (i64 g = 0; g < N; ++g) {
+      const i64 o = c.ord.new2old[g];
+      a[g] = cin[o];
+      bx[g] = u[2 * o];
+      by[g] = u[2 * o + 1];
+    }
+    double *tx = c.cg_q[0], *ty = c.cg_q[1], *cf = c.cg_pa[0], *cn = c.cg_pb[0], *dv = c.litw[8];
+    HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    c.div(tx, ty, dv, false);
+    const int it = c.dye_step(tx, ty, dv, cf, cn);
+    HIPCHK(hipMemcpyAsync(a.data(), cn, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipStreamSynchronize(c.st));
+    for (i64 g = 0; g < N; ++g) cout[c.ord.new2old[g]] = a[g];
+    if (iters) *iters = it;
+  });
+}
+
 int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
@@ -2957,6 +3109,11 @@ int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, in
     }
     switch (op) {
       case PUCFEM_OP_K: A = &c.P; v = &c.as.K; break;
+      case PUCFEM_OP_MCONS:
+        require(c.dye_impl, "the consistent mass exists on dye_scheme = 1 contexts");
+        A = &c.P;
+        v = &c.dyeop.mc;
+        break;
       case PUCFEM_OP_GX: A = &c.P; v = &c.as.Gx; break;
       case PUCFEM_OP_GY: A = &c.P; v = &c.as.Gy; break;
       case PUCFEM_OP_VISC: A = &c.P; v = &c.Kv; break;

@@ -1162,6 +1162,74 @@ void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double 
   }
 }
 
+void build_dye(const HostMesh& m, const Ordering& ord, const Csr& P, const Csr& Pp, const std::vector<i32>& dof,
+               DyeOp& D) {
+  const i64 T = m.T, nnz = P.nnz();
+  // P position of every (triangle, i, j) pair; -1 for skipped (degenerate) triangles
+  std::vector<i64> tpos(9 * (size_t)T, -1);
+  std::vector<double> area(T, 0.0);
+  std::vector<int> bad(1, 0);
+  std::mutex mx;
+  parallel_for(T, [&](i64 t0, i64 t1) {
+    for (i64 t = t0; t < t1; ++t) {
+      const i32 o0 = m.tri[3 * t], o1 = m.tri[3 * t + 1], o2 = m.tri[3 * t + 2];
+      const double x1 = m.x[o0], y1 = m.y[o0], x2 = m.x[o1], y2 = m.y[o1], x3 = m.x[o2], y3 = m.y[o2];
+      const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
+      if (!(std::fabs(det) >= 1e-14)) continue;
+      area[t] = 0.5 * std::fabs(det);
+      const i32 a[3] = {ord.old2new[o0], ord.old2new[o1], ord.old2new[o2]};
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          const i64 k = P.find(a[i], a[j]);
+          if (k < 0) {
+            std::lock_guard<std::mutex> lk(mx);
+            bad[0] = 1;
+          }
+          tpos[9 * t + 3 * i + j] = k;
+        }
+    }
+  });
+  if (bad[0]) throw std::runtime_error("dye operator: a triangle pair is missing from the stiffness pattern");
+  // per P entry, the contributing weights in triangle order (counting sort, stable in t)
+  D.cptr.assign(nnz + 1, 0);
+  for (i64 q = 0; q < 9 * T; ++q)
+    if (tpos[q] >= 0) ++D.cptr[tpos[q] + 1];
+  for (i64 k = 0; k < nnz; ++k) D.cptr[k + 1] += D.cptr[k];
+  D.cw.assign(D.cptr[nnz], 0);
+  D.mc.assign(nnz, 0.0);
+  {
+    std::vector<i64> fill(D.cptr.begin(), D.cptr.end() - 1);
+    for (i64 t = 0; t < T; ++t)
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          const i64 k = tpos[9 * t + 3 * i + j];
+          if (k < 0) continue;
+          D.cw[fill[k]++] = (i32)(3 * t + j);
+          D.mc[k] += (area[t] / 12.0) * (i != j ? 1.0 : 2.0);
+        }
+  }
+  D.diag_row.assign(nnz, -1);
+  for (i64 r = 0; r < P.nrows; ++r)
+    for (i64 k = P.rowptr[r]; k < P.rowptr[r + 1]; ++k)
+      if (P.col[k] == r) D.diag_row[k] = (i32)r;
+  // merged entries: P entry k (row r, column c) -> Pp entry of (dof[r], dof[c])
+  const i64 nnzp = Pp.nnz();
+  std::vector<i64> e_of(nnz);
+  parallel_for(P.nrows, [&](i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1; ++r)
+      for (i64 k = P.rowptr[r]; k < P.rowptr[r + 1]; ++k) e_of[k] = Pp.find(dof[r], dof[P.col[k]]);
+  });
+  D.eptr.assign(nnzp + 1, 0);
+  for (i64 k = 0; k < nnz; ++k) {
+    if (e_of[k] < 0) throw std::runtime_error("dye operator: a merged entry is missing from the pressure pattern");
+    ++D.eptr[e_of[k] + 1];
+  }
+  for (i64 e = 0; e < nnzp; ++e) D.eptr[e + 1] += D.eptr[e];
+  D.ek.assign(nnz, 0);
+  std::vector<i64> fill(D.eptr.begin(), D.eptr.end() - 1);
+  for (i64 k = 0; k < nnz; ++k) D.ek[fill[e_of[k]]++] = (i32)k;
+}
+
 void lattice_locator(const Macro& M, const LatticeLevel& LL, const HostMesh& m, const Ordering& ord,
                      std::vector<lat::SlFace>& faces, std::vector<uint32_t>& cells) {
   const int l = LL.l;

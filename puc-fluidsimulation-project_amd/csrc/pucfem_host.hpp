@@ -178,6 +178,24 @@ void lattice_tabs(const Macro& M, const LatticeLevel& LL, const std::vector<i32>
                   const LocalPlan& lp, const std::vector<i32>* dof, std::vector<lat::FaceTab>& out);
 // Coefficient records (lat::NCOEF doubles per face of `faces`) at level l
 void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double dtnu, std::vector<double>& out);
+// Implicit FEM dye advection-diffusion (scripts/good_visualization.py:700-718): the per-entry data of
+// A = M + dt (C_u + D K) + diag(G) on the stiffness pattern P and of its periodic-merged form on Pp.
+// mc: the consistent mass of every P entry (build_mass_and_convection, StokesColor.py:286-312,
+// accumulated in triangle order); cptr / cw: per P entry the convection weights that sum into it,
+// w index 3 t + j (triangle t, its vertex j = the column), ascending t; diag_row: the row of a
+// diagonal P entry, else -1; eptr / ek: per Pp entry the P entries folded into it (the pair rows
+// summed, slave columns onto the master's).  Triangles with |det| < 1e-14 contribute nothing.
+struct DyeOp {
+  std::vector<double> mc;
+  std::vector<i64> cptr;
+  std::vector<i32> cw;
+  std::vector<i32> diag_row;
+  std::vector<i64> eptr;
+  std::vector<i32> ek;
+};
+void build_dye(const HostMesh& m, const Ordering& ord, const Csr& P, const Csr& Pp, const std::vector<i32>& dof,
+               DyeOp& D);
+
 // Point location on the finest level of a lattice hierarchy (the semi-Lagrangian step): one SlFace per
 // macro face (frame, face table in global internal ids of `ord`, corners, first fine triangle) and the
 // cell table, per cell (i, j, s) of a face (lat::cell_index) the fine triangle's offset in its face

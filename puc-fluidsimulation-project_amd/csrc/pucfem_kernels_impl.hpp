@@ -1378,6 +1378,97 @@ __global__ __launch_bounds__(BS) void k_sl_self(MeshDev M, LOC L, GridDev G, int
   }
 }
 
+// ----------------------------------------------------------------------------- implicit dye variant
+// scripts/good_visualization.py:700-718 (build_mass_and_convection, StokesColor.py:286-312).
+// Per triangle t the convection weights w[3 t + j] = area/3 <u_c, grad_j>: u_c the vertex mean of u,
+// grad_j = (y_{j+1} - y_{j+2}, x_{j+2} - x_{j+1}) / (2 |det|); C[i][j] is their sum over the triangles
+// holding i and j, independent of i.  Degenerate triangles (|det| < 1e-14) contribute nothing.
+__global__ __launch_bounds__(BS) void k_dye_w(MeshDev M, const double* __restrict__ ux, const double* __restrict__ uy,
+                                              double* __restrict__ w) {
+  for (int64_t t = (int64_t)blockIdx.x * BS + threadIdx.x; t < M.T; t += (int64_t)gridDim.x * BS) {
+    const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
+    const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[d], y3 = M.y[d];
+    const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+    if (fabs(det) >= 1e-14) {
+      const double area = 0.5 * fabs(det), den = 2 * fabs(det);
+      const double ucx = ((ux[a] + ux[b]) + ux[d]) / 3.0, ucy = ((uy[a] + uy[b]) + uy[d]) / 3.0;
+      w0 = (area / 3) * (ucx * ((y2 - y3) / den) + ucy * ((x3 - x2) / den));
+      w1 = (area / 3) * (ucx * ((y3 - y1) / den) + ucy * ((x1 - x3) / den));
+      w2 = (area / 3) * (ucx * ((y1 - y2) / den) + ucy * ((x2 - x1) / den));
+    }
+    w[3 * t] = w0;
+    w[3 * t + 1] = w1;
+    w[3 * t + 2] = w2;
+  }
+}
+
+// The merged operator's SELL values: slot -> Pp entry e (-1: padding, value 0); e's P entries k each
+// give (M_k + dt (C_k + D K_k)) (+ G of the row's master on a diagonal, G = dt M_lumped div u); the
+// slave rows of Pp (no P entries) are identity rows.
+struct DyeDev {
+  const int32_t* slot2e;
+  const int64_t* eptr;
+  const int32_t* ek;
+  const double* mc;
+  const double* kv;
+  const int64_t* cptr;
+  const int32_t* cw;
+  const int32_t* diag_row;
+  const int32_t* dof;
+  const double* ml;
+  int64_t nslots;
+};
+__global__ __launch_bounds__(BS) void k_dye_assemble(DyeDev D, const double* __restrict__ w,
+                                                     const double* __restrict__ div, double dt, double diff,
+                                                     double* __restrict__ val) {
+  for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < D.nslots; q += (int64_t)gridDim.x * BS) {
+    const int32_t e = D.slot2e[q];
+    double v = 0.0;
+    if (e >= 0) {
+      const int64_t k0 = D.eptr[e], k1 = D.eptr[e + 1];
+      if (k0 == k1) v = 1.0;
+      for (int64_t z = k0; z < k1; ++z) {
+        const int32_t k = D.ek[z];
+        double ck = 0.0;
+        for (int64_t y = D.cptr[k]; y < D.cptr[k + 1]; ++y) ck += w[D.cw[y]];
+        double a = D.mc[k] + dt * (ck + diff * D.kv[k]);
+        const int32_t r = D.diag_row[k];
+        if (r >= 0) {
+          const int32_t m = D.dof[r];
+          a = a + dt * (D.ml[m] * div[m]);
+        }
+        v += a;
+      }
+    }
+    val[q] = v;
+  }
+}
+__global__ void k_dye_dinv(int64_t n, const int64_t* __restrict__ diag_slot, const double* __restrict__ val,
+                           double* __restrict__ dinv) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS)
+    dinv[r] = 1.0 / val[diag_slot[r]];
+}
+// mixing partials of a dye field (the k_sl partial layout): [0] sum w c, [1] sum w, [2] 0
+__global__ __launch_bounds__(BS) void k_wsum(int64_t row0, int64_t n, const double* __restrict__ c,
+                                             const double* __restrict__ wmix, double* part) {
+  __shared__ double sh[4];
+  double swc = 0.0, sw = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    const double w = wmix[i];
+    swc += w * c[row0 + i];
+    sw += w;
+  }
+  const double a = block_sum(swc, sh), b = block_sum(sw, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = a;
+    part[SLB + blockIdx.x] = b;
+    part[2 * SLB + blockIdx.x] = 0.0;
+  }
+}
+
 // mixing_index second pass (StokesColor.py:399-401): partial sum w (c - mu)^2, mu from pass 1.
 __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const double* __restrict__ c,
                                              const double* __restrict__ wmix, const double* part1, int nb1,

@@ -52,6 +52,63 @@ def _stokes_context(mesh: Mesh, dt, nu, bc: SquirmerBC, device=0):
     return ctx
 
 
+# The reference's functions read module globals (nodes_coords, triangles, pairs, B1, B2, ...,
+# StokesColor.py:359,369,405-431); set_globals() plays that role for the shims that keep the
+# reference's short signatures (advect_semilagrange(c, u, DT), makeDirBCU(u), makePerBCU(u)).
+_globals: dict = {}
+
+
+def set_globals(mesh: Mesh, bc: SquirmerBC | None = None):
+    """Bind the mesh (and squirmer parameters) the reference-signature shims act on."""
+    _globals.clear()
+    _globals.update(mesh=mesh, bc=bc or SquirmerBC())
+
+
+def _mesh_or_global(mesh):
+    if mesh is None:
+        mesh = _globals.get("mesh")
+    if mesh is None:
+        raise ValueError("no mesh: pass mesh= or call set_globals(mesh) first (the reference's module globals)")
+    return mesh
+
+
+def makeDirBCU(u, mesh: Mesh | None = None, bc: SquirmerBC | None = None):
+    """StokesColor.py:405-427 in place on u (N,2): walls to 0, squirmer surface to the tangential
+    squirmer velocity, through the device's boundary kernel."""
+    mesh = _mesh_or_global(mesh)
+    _apply_bc(u, mesh, bc or _globals.get("bc") or SquirmerBC(), 2)
+
+
+def makePerBCU(u, mesh: Mesh | None = None, bc: SquirmerBC | None = None):
+    """StokesColor.py:429-431 in place on u (N,2): u[slave] = u[master] for the filtered pairs."""
+    mesh = _mesh_or_global(mesh)
+    _apply_bc(u, mesh, bc or _globals.get("bc") or SquirmerBC(), 1)
+
+
+def _apply_bc(u, mesh, bc, which):
+    if not (isinstance(u, np.ndarray) and u.dtype == np.float64 and u.flags.c_contiguous and u.shape == (mesh.N, 2)):
+        raise TypeError("u must be a C-contiguous float64 array of shape (N, 2) (modified in place)")
+    ctx = _stokes_context(mesh, 0.05, bc.nu, bc)
+    _lib.check(ctx.L.pucfem_apply_bc(ctx.h, which, _lib.dptr(u)), ctx.h)
+
+
+def mixing_index(c, mass, mask=None, mesh: Mesh | None = None):
+    """StokesColor.py:391-403: (I, mu, var) of c weighted by `mass` over `mask`, on the device.
+    The device reduction's weights are the mesh's lumped mass over its marker==0 nodes (the only
+    weights the reference passes, StokesColor.py:497/:580); other weights are refused."""
+    mesh = _mesh_or_global(mesh)
+    M = buildLumpedMassMatrix(mesh.coords, mesh.triangles)
+    want = np.where(mesh.markers == 0)[0]
+    mask = np.arange(mesh.N) if mask is None else np.asarray(mask)
+    if not (np.array_equal(np.asarray(mass), M) and np.array_equal(np.sort(mask), want)):
+        raise ValueError("mixing_index: mass must be buildLumpedMassMatrix(mesh) and mask the marker==0 nodes")
+    ctx = _stokes_context(mesh, 0.05, 0.1, _globals.get("bc") or SquirmerBC())
+    out = np.zeros(3)
+    _lib.check(ctx.L.pucfem_mixing_index(ctx.h, _lib.dptr(np.ascontiguousarray(c, dtype=np.float64)),
+                                         _lib.dptr(out)), ctx.h)
+    return float(out[0]), float(out[1]), float(out[2])
+
+
 def calculate_divergence(nodes, triangles, u_star):
     """StokesColor.py:130-165 on the GPU: (N,) lumped nodal divergence."""
     ctx = context_for(nodes, triangles)
@@ -65,11 +122,13 @@ def calculate_gradiant(nodes, triangles, p_scalar):
     return g[:, 0].copy(), g[:, 1].copy()
 
 
-def advect_semilagrange(c, u, DT, nodes, triangles):
+def advect_semilagrange(c, u, DT, nodes=None, triangles=None):
     """StokesColor.py:347-389 on the GPU, in place on c like the reference (c[:] = c_new).
+    advect_semilagrange(c, u, DT) as in the reference acts on the set_globals() mesh.
     Returns the not-found mask (nodes that kept c[n])."""
-    import ctypes as ct
-
+    if nodes is None or triangles is None:
+        m = _mesh_or_global(None)
+        nodes, triangles = m.coords, m.triangles
     ctx = context_for(nodes, triangles)
     cin = np.ascontiguousarray(c, dtype=np.float64)
     uu = np.ascontiguousarray(u, dtype=np.float64).reshape(-1, 2)
@@ -124,6 +183,43 @@ def solve_pressure(mesh: Mesh, b_p, dt=0.05, nu=0.1, bc: SquirmerBC | None = Non
     ctx = _stokes_context(mesh, dt, nu, bc or SquirmerBC(nu=nu))
     x, it = ctx.solve(_lib.OP_PRES, np.asarray(b_p, dtype=np.float64), rtol=rtol)
     return x
+
+
+def _dye_context(mesh: Mesh, dt, D, device=0):
+    k = ("dye", mesh.N, mesh.T, hash(mesh.coords.tobytes()), hash(mesh.triangles.tobytes()), dt, D)
+    ctx = _cache.get(k)
+    if ctx is None:
+        bc = SquirmerBC()
+        ctx = Context(device)
+        ctx.upload(mesh)
+        pairs, nodes, vals = stokes_setup(mesh, bc)
+        ctx.set_pairs(0, pairs)
+        ctx.set_pairs(1, pairs)
+        ctx.set_dirichlet(nodes, vals)
+        ctx.build("color", dt, bc.nu, Tolerances(dye="implicit", dye_diffusivity=D))
+        _cache[k] = ctx
+    return ctx
+
+
+def dye_implicit_step(c, u, mesh: Mesh, dt=0.05, D=1e-3):
+    """One implicit FEM dye advection-diffusion step (scripts/good_visualization.py:700-718) on the
+    GPU: A = M + dt (C_u + D K) + diag(dt M_lumped div u), c <- A^-1 M c with the periodic pairs
+    merged exactly (the reference's 1e10 penalty in its limit), then c[slave] = c[master].
+    Returns (c_new, BiCGStab iterations)."""
+    ctx = _dye_context(mesh, dt, D)
+    cin = np.ascontiguousarray(c, dtype=np.float64)
+    uu = np.ascontiguousarray(u, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros_like(cin)
+    it = np.zeros(1, dtype=np.int32)
+    _lib.check(ctx.L.pucfem_dye_step(ctx.h, _lib.dptr(cin), _lib.dptr(uu), _lib.dptr(out), _lib.iptr(it)), ctx.h)
+    return out, int(it[0])
+
+
+def build_mass_and_convection_mass(mesh: Mesh):
+    """The M of build_mass_and_convection (StokesColor.py:286-312): the consistent mass, host-assembled
+    (scipy CSR, caller numbering); C_u is assembled on the device inside every implicit dye step."""
+    ctx = _dye_context(mesh, 0.05, 1e-3)
+    return ctx.host_csr(_lib.OP_MCONS)
 
 
 def clear_cache():

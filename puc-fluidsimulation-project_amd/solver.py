@@ -73,6 +73,10 @@ class Tolerances:
     # "auto": on multigrid hierarchies (>= 2 levels) the rows of the nodes inside the coarse triangles are
     # matrix-free lattice stencils; "assembled": stored SELL rows everywhere
     operators: str = "auto"
+    # StokesColor dye update: "semilagrange" (StokesColor.py:347-389) or "implicit" (the FEM advection-
+    # diffusion variant of scripts/good_visualization.py:700-718, diffusivity dye_diffusivity; one rank)
+    dye: str = "semilagrange"
+    dye_diffusivity: float = 1e-3
 
     @classmethod
     def production(cls, **kw):
@@ -161,7 +165,8 @@ class Context:
                         mg_f32_vals=2 if tol.mg_f16_vals == "coarse" else int(not tol.mg_f16_vals),
                         idx32=int(not tol.index16), proj_k=tol.proj_k, proj_k_visc=tol.proj_k_visc,
                         mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path],
-                        assembled={"auto": 0, "assembled": 1}[tol.operators])
+                        assembled={"auto": 0, "assembled": 1}[tol.operators],
+                        dye_scheme={"semilagrange": 0, "implicit": 1}[tol.dye], dye_diffusivity=tol.dye_diffusivity)
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 

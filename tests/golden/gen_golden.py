@@ -19,6 +19,7 @@ Two harnesses:
 
 Run:  python tests/golden/gen_golden.py            (per-kernel + short runs, ~1 min)
       python tests/golden/gen_golden.py --long     (adds 6000-step mesh.1 traces, ~15 min)
+      python tests/golden/gen_golden.py --dye      (implicit dye variant, good_visualization.py)
 """
 from __future__ import annotations
 
@@ -330,15 +331,60 @@ def export_meshes():
                             segments=seg, segment_markers=segm)
 
 
+def gen_dye(name, steps=3, dt=0.05, D=1e-3):
+    """The implicit FEM dye advection-diffusion variant: good_visualization.py's
+    own functions (build_mass_and_convection :348, apply_periodic_bc :179, calculate_divergence
+    :100, buildLumpedMassMatrix :248, buildStiffnessMatrix :64) and its step (:700-718, M made
+    periodic once at :591-592) on a fixed velocity field, from a dye field that is periodic in x."""
+    node, ele, _ = (os.path.join(REF, p) for p in MESHES[name])
+    V = _extract("scripts/good_visualization.py")
+    X, mk = V["readNode"](node)
+    T = V["readEle"](ele)
+    N = X.shape[0]
+    tol, H = 1e-6, 1.0
+    pairs = [(m, s) for m, s in V["find_boundary_pairs"](X, L=1.0)
+             if not (abs(X[m, 1] - 0.0) < tol or abs(X[m, 1] - H) < tol)]
+    K, _ = V["buildStiffnessMatrix"](X, T, g_source=0.0)
+    Ml = V["buildLumpedMassMatrix"](X, T)
+    r = X - 0.5
+    u = np.stack([-r[:, 1], r[:, 0]], 1) * 1.5 + np.array([0.4, 0.1])
+    c = np.exp(-((X[:, 0] - 0.5) ** 2 + (X[:, 1] - 0.7) ** 2) / 0.02) + 0.3 * np.cos(3.0 * X[:, 1])
+    out = dict(dye_u=u, dye_c0=c.copy(), dye_pairs=np.array(pairs, dtype=np.int64).reshape(-1, 2),
+               dye_dt=np.array(dt), dye_D=np.array(D))
+    M, C = V["build_mass_and_convection"](X, T, u)
+    out["dye_M_ij"], out["dye_M_v"] = _coo(M)
+    out["dye_C_ij"], out["dye_C_v"] = _coo(C)
+    V["apply_periodic_bc"](M, pairs)
+    div = V["calculate_divergence"](X, T, u)
+    out["dye_div"] = div
+    for k in range(steps):
+        G = dt * (Ml * div)
+        for m, s in pairs:
+            G[s] = G[m]
+        A = M + dt * (C + D * K) + np.diag(G)
+        V["apply_periodic_bc"](A, pairs)
+        c = np.linalg.solve(A, M @ c)
+        for m, s in pairs:
+            c[s] = c[m]
+        out[f"dye_c{k + 1}"] = c.copy()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--long", action="store_true")
+    ap.add_argument("--dye", action="store_true", help="only the implicit dye variant fixtures (golden_dye_*.npz)")
     ap.add_argument("--only", default=None)
     a = ap.parse_args()
     _install_stubs()
     export_meshes()
     if a.long:
         np.savez_compressed(os.path.join(OUT, "long_mesh1.npz"), **gen_long())
+        return
+    if a.dye:
+        for name in ("mesh1", "fine"):
+            np.savez_compressed(os.path.join(OUT, f"golden_dye_{name}.npz"), **gen_dye(name))
+            print("dye", name)
         return
     for name in MESHES:
         if a.only and name != a.only:

@@ -1,0 +1,100 @@
+"""The implicit FEM dye advection-diffusion variant (scripts/good_visualization.py
+:700-718) on the CPU: the oracle pinned against the reference's own outputs (golden_dye_*.npz,
+tests/golden/gen_golden.py --dye), the well-posed restatement of its periodic penalty, and the host
+assembly of the consistent mass.
+
+The reference makes M and A periodic with a 1e10 penalty (apply_periodic_bc, :179-194).  That system
+is ill-conditioned: two exact-in-principle LU solves of it (numpy dense, scipy sparse) differ by
+~1e-2, and its solution converges to the exact merged limit as the penalty shrinks (1e2: 2e-8 away,
+1e4: 4e-9, 1e10: 3e-3).  The library solves the limit (the pair rows summed, slave columns folded):
+contract (ii) vs the oracle's merged solve at 1e-10, contract (iii) vs the literal reference at its
+noise floor (2e-2), as for the pressure.
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import oracle as O
+from conftest import GOLDEN, load_pkg
+
+pf = load_pkg()
+from importlib import import_module  # noqa: E402
+
+L = import_module("puc-fluidsimulation-project_amd._lib")
+S = import_module("puc-fluidsimulation-project_amd.solver")
+
+
+def gold(name):
+    return np.load(os.path.join(GOLDEN, f"golden_dye_{name}.npz"))
+
+
+def coo(ij, v, n):
+    return sp.csr_matrix((v, (ij[0], ij[1])), shape=(n, n))
+
+
+@pytest.mark.parametrize("name", ["mesh1", "fine"])
+def test_oracle_mass_and_convection_vs_reference(name):
+    g = gold(name)
+    m = pf.load_mesh(name)
+    M, C = O.mass_and_convection(m.coords, m.triangles, g["dye_u"])
+    Mr, Cr = coo(g["dye_M_ij"], g["dye_M_v"], m.N), coo(g["dye_C_ij"], g["dye_C_v"], m.N)
+    assert abs(M - Mr).max() == 0.0
+    assert abs(C - Cr).max() <= 1e-15 * abs(Cr).max()
+    np.testing.assert_array_equal(O.divergence(m.coords, m.triangles, g["dye_u"]), g["dye_div"])
+
+
+@pytest.mark.parametrize("name", ["mesh1", "fine"])
+def test_oracle_steps_vs_reference_noise_floor(name):
+    g = gold(name)
+    m = pf.load_mesh(name)
+    c = g["dye_c0"]
+    for k in range(3):
+        c = O.dye_implicit_step(c, g["dye_u"], m.coords, m.triangles, g["dye_pairs"], float(g["dye_dt"]),
+                                float(g["dye_D"]))
+        assert np.abs(c - g[f"dye_c{k + 1}"]).max() < 2e-2, k
+        p = g["dye_pairs"]
+        np.testing.assert_array_equal(c[p[:, 1]], c[p[:, 0]])
+
+
+def test_penalty_converges_to_the_merged_limit():
+    """The literal penalised system at small penalties (where LU is accurate) approaches the merged
+    solve; the reference's 1e10 only adds rounding noise."""
+    g = gold("fine")
+    m = pf.load_mesh("fine")
+    X, T, u, c, pairs = m.coords, m.triangles, g["dye_u"], g["dye_c0"], g["dye_pairs"]
+    ref = O.dye_implicit_step(c, u, X, T, pairs, 0.05, 1e-3)
+    M, Cm = O.mass_and_convection(X, T, u)
+    K = O.stiffness(X, T)
+    G = 0.05 * (O.lumped_mass(X, T) * O.divergence(X, T, u))
+    G[pairs[:, 1]] = G[pairs[:, 0]]
+    for pen, tol in ((1e2, 1e-7), (1e4, 1e-7)):
+        Pn = sp.lil_matrix((m.N, m.N))
+        for a, b in pairs:
+            Pn[a, a] += pen
+            Pn[b, b] += pen
+            Pn[a, b] -= pen
+            Pn[b, a] -= pen
+        Mp = (M + Pn).tocsr()
+        A = (Mp + 0.05 * (Cm + 1e-3 * K) + sp.diags(G) + Pn).toarray()
+        x = np.linalg.solve(A, Mp @ c)
+        x[pairs[:, 1]] = x[pairs[:, 0]]
+        assert np.abs(x - ref).max() < tol, pen
+
+
+def test_host_consistent_mass_bit_exact():
+    """The library's host assembly of M (triangle order, |det| >= 1e-14) = the oracle = the reference."""
+    g = gold("fine")
+    mesh = pf.load_mesh("fine")
+    ctx = S.Context(L.HOST_ONLY)
+    ctx.upload(mesh)
+    pairs, nodes, vals = S.stokes_setup(mesh, S.SquirmerBC())
+    ctx.set_pairs(0, pairs)
+    ctx.set_pairs(1, pairs)
+    ctx.set_dirichlet(nodes, vals)
+    ctx.build("color", 0.05, 0.1, S.Tolerances(dye="implicit"))
+    Mh = ctx.host_csr(L.OP_MCONS)
+    Mr = coo(g["dye_M_ij"], g["dye_M_v"], mesh.N)
+    assert abs(Mh - Mr).max() == 0.0
+    ctx.close()
