@@ -596,13 +596,18 @@ def dye_implicit_step(c, u, X, T, pairs, dt, D, K=None, merged=True):
     G[pairs[:, 1]] = G[pairs[:, 0]]
     A = (M + dt * (C + D * K) + sp.diags(G)).tocsr()
     if merged:
+        # the limit: the summed pair rows (penalties cancel) and 2 pen (x_m - x_s) = pen (c_m - c_s) + O(1),
+        # i.e. x_s = x_m - delta_s with delta_s = (c_m - c_s) / 2 (zero once c is periodic); with
+        # x = P y - delta:  P^T A P y = P^T (M c + A delta), and the final copy leaves c = P y
         dof = np.arange(N)
         dof[pairs[:, 1]] = pairs[:, 0]
         P = sp.csr_matrix((np.ones(N), (np.arange(N), dof)), shape=(N, N))
         Am = (P.T @ A @ P).tolil()
         Am[pairs[:, 1], pairs[:, 1]] = 1.0
-        b = P.T @ (M @ c)
-        b[pairs[:, 1]] = c[pairs[:, 1]]
+        delta = np.zeros(N)
+        delta[pairs[:, 1]] = (c[pairs[:, 0]] - c[pairs[:, 1]]) / 2
+        b = P.T @ (M @ c + A @ delta)
+        b[pairs[:, 1]] = c[pairs[:, 0]]
         x = spla.spsolve(Am.tocsc(), b)
     else:
         pen = 1.0e10

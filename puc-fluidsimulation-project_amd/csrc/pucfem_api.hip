@@ -336,6 +336,9 @@ struct Ctx {
   DyeDev dye{};
   double *dDyeVal = nullptr, *dDyeM = nullptr, *dDyeW = nullptr, *dDyeDinv = nullptr, *dDyeB = nullptr;
   int64_t* dDyeDiag = nullptr;  // SELL slot of each row's diagonal
+  int32_t *dDyeSrow = nullptr, *dDyeSk = nullptr, *dDyeSc = nullptr;
+  int64_t* dDyeSptr = nullptr;
+  int32_t dye_nsrow = 0;
   int last_dye_it = 0;
   DyeOp dyeop;  // host data of the implicit dye operator (built with the host operators)
   LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
@@ -1228,6 +1231,12 @@ struct Ctx {
                          (const double*)dDyeM, cin, dDyeB);
     });
     KCHK();
+    if (dye_nsrow > 0) {
+      hipLaunchKernelGGL(k_dye_rhs_fix, dim3(std::min(256, (dye_nsrow + BS - 1) / BS)), dim3(BS), 0, st, dye_nsrow,
+                         (const int32_t*)dDyeSrow, (const int64_t*)dDyeSptr, (const int32_t*)dDyeSk,
+                         (const int32_t*)dDyeSc, dye, (const double*)dDyeW, dv, prm.dt, prm.dye_diffusivity, cin, dDyeB);
+      KCHK();
+    }
     HIPCHK(hipMemcpyAsync(cout, cin, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     const int it = bicgstab(cout, dDyeB, std::max(prm.rtol_lin, 1e-13), prm.maxit_lin, &dDye, dDyeVal, dDyeDinv);
     if (ncopy > 0) {  // c[slave] = c[master] (good_visualization.py:715-716)
@@ -1765,6 +1774,13 @@ void build(Ctx& c) {
     c.dDyeDiag = c.upload(dslot);
     c.dye = DyeDev{c.upload(slot2e), c.upload(D.eptr), c.upload(D.ek), c.upload(D.mc), c.upload(c.as.K),
                    c.upload(D.cptr), c.upload(D.cw), c.upload(D.diag_row), c.upload(c.dof), c.upload(c.as.M), S.padded};
+    c.dye_nsrow = (int32_t)D.srow.size();
+    if (c.dye_nsrow > 0) {
+      c.dDyeSrow = c.upload(D.srow);
+      c.dDyeSptr = c.upload(D.sptr);
+      c.dDyeSk = c.upload(D.sk);
+      c.dDyeSc = c.upload(D.sc);
+    }
     c.dDyeVal = c.dalloc<double>(S.padded);
     c.dDyeW = c.dalloc<double>(3 * m.T);
     c.dDyeDinv = c.dalloc<double>(c.nloc);

@@ -1228,6 +1228,39 @@ void build_dye(const HostMesh& m, const Ordering& ord, const Csr& P, const Csr& 
   D.ek.assign(nnz, 0);
   std::vector<i64> fill(D.eptr.begin(), D.eptr.end() - 1);
   for (i64 k = 0; k < nnz; ++k) D.ek[fill[e_of[k]]++] = (i32)k;
+  // entries in slave columns, grouped by merged row (rows in ascending order, entries by k)
+  std::vector<std::vector<std::pair<i32, i32>>> byrow;
+  std::vector<i32> rowid;
+  std::vector<i32> slot(P.nrows, -1);
+  for (i64 r = 0; r < P.nrows; ++r)
+    for (i64 k = P.rowptr[r]; k < P.rowptr[r + 1]; ++k) {
+      const i32 cc = P.col[k];
+      if (dof[cc] == cc) continue;
+      const i32 R = dof[r];
+      if (slot[R] < 0) {
+        slot[R] = (i32)rowid.size();
+        rowid.push_back(R);
+        byrow.emplace_back();
+      }
+      byrow[slot[R]].push_back({(i32)k, cc});
+    }
+  std::vector<i32> order(rowid.size());
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](i32 a, i32 b) { return rowid[a] < rowid[b]; });
+  D.srow.clear();
+  D.sptr.assign(1, 0);
+  D.sk.clear();
+  D.sc.clear();
+  for (i32 o : order) {
+    auto& v = byrow[o];
+    std::sort(v.begin(), v.end());
+    D.srow.push_back(rowid[o]);
+    for (auto& e : v) {
+      D.sk.push_back(e.first);
+      D.sc.push_back(e.second);
+    }
+    D.sptr.push_back((i64)D.sk.size());
+  }
 }
 
 void lattice_locator(const Macro& M, const LatticeLevel& LL, const HostMesh& m, const Ordering& ord,

@@ -185,6 +185,8 @@ void lattice_coefs(const Macro& M, const std::vector<i32>& faces, int l, double 
 // w index 3 t + j (triangle t, its vertex j = the column), ascending t; diag_row: the row of a
 // diagonal P entry, else -1; eptr / ek: per Pp entry the P entries folded into it (the pair rows
 // summed, slave columns onto the master's).  Triangles with |det| < 1e-14 contribute nothing.
+// srow / sptr / sk / sc: the merged rows that hold P entries in a slave's column, with those entries
+// and their slave columns (the right-hand side term of a dye field that is not periodic at the pairs).
 struct DyeOp {
   std::vector<double> mc;
   std::vector<i64> cptr;
@@ -192,6 +194,9 @@ struct DyeOp {
   std::vector<i32> diag_row;
   std::vector<i64> eptr;
   std::vector<i32> ek;
+  std::vector<i32> srow;
+  std::vector<i64> sptr;
+  std::vector<i32> sk, sc;
 };
 void build_dye(const HostMesh& m, const Ordering& ord, const Csr& P, const Csr& Pp, const std::vector<i32>& dof,
                DyeOp& D);

@@ -1444,6 +1444,31 @@ __global__ __launch_bounds__(BS) void k_dye_assemble(DyeDev D, const double* __r
     val[q] = v;
   }
 }
+// rhs of a dye field that is not periodic at the pairs: the penalty's limit keeps
+// x_s = x_m - delta_s, delta_s = (c_m - c_s) / 2, which adds (A_k - 2 M_k) delta_s to the merged row
+// of every P entry k in a slave's column (rhs = P^T (M c + A delta) with M c taken on merged columns)
+__global__ void k_dye_rhs_fix(int32_t nrows, const int32_t* __restrict__ srow, const int64_t* __restrict__ sptr,
+                              const int32_t* __restrict__ sk, const int32_t* __restrict__ sc, DyeDev D,
+                              const double* __restrict__ w, const double* __restrict__ div, double dt, double diff,
+                              const double* __restrict__ c, double* __restrict__ rhs) {
+  for (int32_t q = blockIdx.x * BS + threadIdx.x; q < nrows; q += gridDim.x * BS) {
+    double add = 0.0;
+    for (int64_t z = sptr[q]; z < sptr[q + 1]; ++z) {
+      const int32_t k = sk[z], s = sc[z];
+      const double delta = (c[D.dof[s]] - c[s]) / 2;
+      double ck = 0.0;
+      for (int64_t y = D.cptr[k]; y < D.cptr[k + 1]; ++y) ck += w[D.cw[y]];
+      double a = D.mc[k] + dt * (ck + diff * D.kv[k]);
+      const int32_t r = D.diag_row[k];
+      if (r >= 0) {
+        const int32_t m = D.dof[r];
+        a = a + dt * (D.ml[m] * div[m]);
+      }
+      add += (a - 2.0 * D.mc[k]) * delta;
+    }
+    rhs[srow[q]] += add;
+  }
+}
 __global__ void k_dye_dinv(int64_t n, const int64_t* __restrict__ diag_slot, const double* __restrict__ val,
                            double* __restrict__ dinv) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS)

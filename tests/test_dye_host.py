@@ -7,8 +7,9 @@ The reference makes M and A periodic with a 1e10 penalty (apply_periodic_bc, :17
 is ill-conditioned: two exact-in-principle LU solves of it (numpy dense, scipy sparse) differ by
 ~1e-2, and its solution converges to the exact merged limit as the penalty shrinks (1e2: 2e-8 away,
 1e4: 4e-9, 1e10: 3e-3).  The library solves the limit (the pair rows summed, slave columns folded):
-contract (ii) vs the oracle's merged solve at 1e-10, contract (iii) vs the literal reference at its
-noise floor (2e-2), as for the pressure.
+contract (ii) vs the oracle's merged solve, contract (iii) vs the literal reference at its
+noise floor (2e-2), as for the pressure.  The GPU solve (BiCGStab to a relative
+residual of 1e-13) lands within 1e-8 (relative) of the oracle's sparse LU of the same merged system.
 """
 import os
 
@@ -58,18 +59,22 @@ def test_oracle_steps_vs_reference_noise_floor(name):
         np.testing.assert_array_equal(c[p[:, 1]], c[p[:, 0]])
 
 
-def test_penalty_converges_to_the_merged_limit():
+@pytest.mark.parametrize("periodic", [True, False])
+def test_penalty_converges_to_the_merged_limit(periodic):
     """The literal penalised system at small penalties (where LU is accurate) approaches the merged
-    solve; the reference's 1e10 only adds rounding noise."""
+    solve; the reference's 1e10 only adds rounding noise.  A dye field that is not periodic at the
+    pairs (StokesColor's initial 1[x < 0.5]) enters the limit through x_s = x_m - (c_m - c_s) / 2."""
     g = gold("fine")
     m = pf.load_mesh("fine")
     X, T, u, c, pairs = m.coords, m.triangles, g["dye_u"], g["dye_c0"], g["dye_pairs"]
+    if not periodic:
+        c = c + (X[:, 0] < 0.5)
     ref = O.dye_implicit_step(c, u, X, T, pairs, 0.05, 1e-3)
     M, Cm = O.mass_and_convection(X, T, u)
     K = O.stiffness(X, T)
     G = 0.05 * (O.lumped_mass(X, T) * O.divergence(X, T, u))
     G[pairs[:, 1]] = G[pairs[:, 0]]
-    for pen, tol in ((1e2, 1e-7), (1e4, 1e-7)):
+    for pen, tol in ((1e4, 1e-7), (1e6, 1e-6)):
         Pn = sp.lil_matrix((m.N, m.N))
         for a, b in pairs:
             Pn[a, a] += pen

@@ -1,7 +1,7 @@
 """The implicit FEM dye variant on the GPU (scripts/good_visualization.py:700-718):
 device assembly of A = M + dt (C_u + D K) + diag(dt M_lumped div u) on the merged pattern, BiCGStab,
 periodic copies.  Contract (ii): the oracle's merged solve (tests/test_dye_host.py explains why the
-penalty's limit) at 1e-10; contract (iii): the reference's literal outputs at their noise floor 2e-2.
+penalty's limit) at 1e-8 relative (BiCGStab to a 1e-13 relative residual); contract (iii): the reference's literal outputs at their noise floor 2e-2.
 """
 import os
 
@@ -30,20 +30,23 @@ def gold(name):
     return np.load(os.path.join(GOLDEN, f"golden_dye_{name}.npz"))
 
 
+@pytest.mark.parametrize("periodic", [True, False])
 @pytest.mark.parametrize("name", ["mesh1", "fine"])
-def test_dye_steps_vs_oracle_and_reference(name):
+def test_dye_steps_vs_oracle_and_reference(name, periodic):
+    """periodic=False: a first dye field that differs at the pair nodes (the limit's x_s = x_m - delta)."""
     g = gold(name)
     mesh = pf.load_mesh(name)
     u = g["dye_u"]
-    c = g["dye_c0"]
+    c = g["dye_c0"] if periodic else g["dye_c0"] + (mesh.coords[:, 0] < 0.5)
     co = c.copy()
     for k in range(3):
         c, it = pf.dye_implicit_step(c, u, mesh, float(g["dye_dt"]), float(g["dye_D"]))
         co = O.dye_implicit_step(co, u, mesh.coords, mesh.triangles, g["dye_pairs"], float(g["dye_dt"]),
                                  float(g["dye_D"]))
         assert 0 < it < 200
-        assert np.abs(c - co).max() < 1e-10 * np.abs(co).max(), (k, np.abs(c - co).max())
-        assert np.abs(c - g[f"dye_c{k + 1}"]).max() < 2e-2
+        assert np.abs(c - co).max() < 1e-8 * np.abs(co).max(), (k, np.abs(c - co).max())
+        if periodic:
+            assert np.abs(c - g[f"dye_c{k + 1}"]).max() < 2e-2
         p = g["dye_pairs"]
         np.testing.assert_array_equal(c[p[:, 1]], c[p[:, 0]])
 
@@ -63,7 +66,7 @@ def test_dye_step_on_a_lattice_hierarchy():
     L.check(sim.ctx.L.pucfem_dye_step(sim.ctx.h, L.dptr(np.ascontiguousarray(c)), L.dptr(np.ascontiguousarray(u)),
                                       L.dptr(cg), L.iptr(it)), sim.ctx.h)
     co = O.dye_implicit_step(c, u, X, mesh.triangles, pairs, 0.05, 1e-3)
-    assert np.abs(cg - co).max() < 1e-10 * np.abs(co).max()
+    assert np.abs(cg - co).max() < 1e-8 * np.abs(co).max()
     sim.close()
 
 
@@ -85,7 +88,7 @@ def test_stokes_color_with_implicit_dye():
         np.testing.assert_array_equal(u, ref.u)
         co = O.dye_implicit_step(c, u, mesh.coords, mesh.triangles, sim.pairs, 0.05, 1e-3)
         c = sim.c
-        assert np.abs(c - co).max() < 1e-9, (k, np.abs(c - co).max())
+        assert np.abs(c - co).max() < 1e-8, (k, np.abs(c - co).max())
         w = M[mask]
         mu = (w @ c[mask]) / w.sum()
         assert abs(st.mix_mu - mu) < 1e-12
