@@ -16,6 +16,7 @@ from .ops import (advect_semilagrange, buildLumpedMassMatrix, buildStiffnessMatr
                   mixing_index, set_globals, solve_pressure, solve_viscous)
 from .solver import (Context, HeatSimulation, Result, SquirmerBC, StokesSimulation, Tolerances,  # noqa: F401
                      poisson_solve, solve, squirmer_values)
+from .frames import FrameRecorder, load_npz, render, save_npz, write_vtk  # noqa: F401
 from .tracers import tracer_init  # noqa: F401
 
 __version__ = "0.1.0"

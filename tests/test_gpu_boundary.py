@@ -93,3 +93,17 @@ def test_mixing_index_and_short_semilagrange_signature(golden):
     np.testing.assert_allclose([I, mu, var], g["mixing_sl_small"], rtol=1e-12, atol=0)
     with pytest.raises(ValueError):
         pf.mixing_index(c, 2 * M, mask=np.where(mesh.markers == 0)[0])
+
+
+def test_frame_recorder_on_a_run(tmp_path):
+    """Frame export around a real StokesColor run (good_visualization2.py:724): frames after steps
+    0, 50, 100; the last one is the simulation's final state; a VTK of it carries the same fields."""
+    mesh = pf.load_mesh("mesh1")
+    sim = pf.StokesSimulation(mesh)
+    rec = pf.FrameRecorder(mesh, interval=50, dtype=np.float64)
+    st = rec.run(sim, 101)
+    assert len(st) == 101 and rec.steps == [0, 50, 100]
+    np.testing.assert_array_equal(rec.dye[-1], sim.c)
+    np.testing.assert_array_equal(rec.vel[-1], sim.u)
+    pf.write_vtk(str(tmp_path / "last.vtk"), mesh.coords, mesh.triangles, {"dye": sim.c, "velocity": sim.u})
+    sim.close()
