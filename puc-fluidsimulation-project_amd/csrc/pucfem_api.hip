@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -1361,44 +1362,76 @@ int guard(void* ctx, F&& f) {
   }
 }
 
-void require(bool ok, const std::string& msg) {
+// const char* overload first: a check inside a hot loop must not build a std::string per call
+inline void require(bool ok, const char* msg) {
+  if (!ok) throw Error(PUCFEM_EINVAL, msg);
+}
+inline void require(bool ok, const std::string& msg) {
   if (!ok) throw Error(PUCFEM_EINVAL, msg);
 }
 
 // ------------------------------------------------------------------ multigrid hierarchy (host)
 double lmax_estimate(const Csr& A) {
-  // min(Gershgorin bound, 1.1 x 30-step power iteration) of D^-1 A
+  // min(Gershgorin bound, 1.1 x 30-step power iteration) of D^-1 A; rows in fixed chunks (threads),
+  // the norms summed per chunk and then in chunk order: the same value on every machine
   const i64 n = A.nrows;
   std::vector<double> dinv(n), x(n), y(n);
-  double gersh = 0.0;
-  for (i64 r = 0; r < n; ++r) {
-    double d = 1.0, s = 0.0;
-    for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
-      if (A.col[k] == r) d = A.val[k];
-      s += std::fabs(A.val[k]);
+  std::vector<double> cg(PAR_CHUNKS, 0.0), cx(PAR_CHUNKS), cy(PAR_CHUNKS);
+  parallel_chunks(n, [&](int ch, i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1; ++r) {
+      double d = 1.0, s = 0.0;
+      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+        if (A.col[k] == r) d = A.val[k];
+        s += std::fabs(A.val[k]);
+      }
+      dinv[r] = 1.0 / d;
+      cg[ch] = std::max(cg[ch], s / d);
     }
-    dinv[r] = 1.0 / d;
-    gersh = std::max(gersh, s / d);
-  }
+  });
+  double gersh = 0.0;
+  for (double g : cg) gersh = std::max(gersh, g);
   for (i64 i = 0; i < n; ++i) x[i] = 1.0 + 0.5 * std::sin((double)i);
   double lam = 0.0;
   for (int it = 0; it < 30; ++it) {
+    parallel_chunks(n, [&](int ch, i64 r0, i64 r1) {
+      double nx = 0.0, ny = 0.0;
+      for (i64 r = r0; r < r1; ++r) {
+        double a = 0.0;
+        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) a += A.val[k] * x[A.col[k]];
+        y[r] = dinv[r] * a;
+        nx += x[r] * x[r];
+        ny += y[r] * y[r];
+      }
+      cx[ch] = nx;
+      cy[ch] = ny;
+    });
     double nx = 0.0, ny = 0.0;
-    for (i64 r = 0; r < n; ++r) {
-      double a = 0.0;
-      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) a += A.val[k] * x[A.col[k]];
-      y[r] = dinv[r] * a;
-      nx += x[r] * x[r];
-      ny += y[r] * y[r];
+    for (int ch = 0; ch < PAR_CHUNKS; ++ch) {
+      nx += cx[ch];
+      ny += cy[ch];
     }
     lam = std::sqrt(ny / nx);
     const double inv = 1.0 / std::sqrt(ny);
-    for (i64 r = 0; r < n; ++r) x[r] = y[r] * inv;
+    parallel_for(n, [&](i64 r0, i64 r1) {
+      for (i64 r = r0; r < r1; ++r) x[r] = y[r] * inv;
+    });
   }
   return std::min(gersh, 1.1 * lam);
 }
 
-void build_mg_host(Ctx& c) {
+// wall time per setup phase on stderr (PUCFEM_SETUP_TIMING=1)
+struct SetupClock {
+  bool on = std::getenv("PUCFEM_SETUP_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[setup] %-34s %8.3f s\n", what, std::chrono::duration<double>(n - t).count());
+    t = n;
+  }
+};
+
+void build_mg_host(Ctx& c, SetupClock& clk) {
   const int Lv = c.mg_levels;
   c.mg.clear();
   c.mg.resize(Lv + 1);
@@ -1414,13 +1447,16 @@ void build_mg_host(Ctx& c) {
               "the uploaded mesh is not the red refinement of the hierarchy's coarse mesh");
     }
   }
+  clk.mark("  mg: refinements");
   for (int l = 0; l < Lv; ++l) {
     MgLevel& L = c.mg[l];
     if (c.lattice) lattice_ordering(L.mesh, c.macro, l, L.ord, L.latl);
     else make_ordering_cuts(L.mesh, c.ord.cuts, L.ord);
-    build_pattern(L.mesh, L.ord, L.P);
+    Incidence inc;
+    build_incidence(L.mesh, L.ord, inc);
+    build_pattern(L.mesh, L.ord, L.P, &inc);
     Assembly A;
-    assemble_stokes(L.mesh, L.ord, L.P, A);
+    assemble_stokes(L.mesh, L.ord, L.P, A, &inc);
     L.pairs = level_pairs(L.mesh, 1.0, 1e-6, 1.0);
     const i64 n = L.mesh.N;
     L.dof.resize(n);
@@ -1437,6 +1473,7 @@ void build_mg_host(Ctx& c) {
     build_pressure(L.P, A.K, L.dof, L.slave_of, L.Pp);
     L.P = Csr();  // only the merged operator is needed on coarse levels
   }
+  clk.mark("  mg: coarse level operators");
   MgLevel& F = c.mg[Lv];
   F.ord = c.ord;
   if (c.lattice) F.latl = std::move(c.lat_fine);
@@ -1448,7 +1485,9 @@ void build_mg_host(Ctx& c) {
     build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
     transpose(L.Pr, C.mesh.N, L.R);
   }
+  clk.mark("  mg: transfers");
   for (int l = 0; l <= Lv; ++l) c.mg[l].lmax = lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
+  clk.mark("  mg: lmax estimates");
 }
 
 // ------------------------------------------------------------------ operator build
@@ -1553,7 +1592,9 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
   }
 }
 
+
 void build(Ctx& c) {
+  SetupClock clk;
   require(c.has_mesh, "mesh not uploaded");
   const pucfem_params& prm = c.prm;
   c.scheme = prm.scheme;
@@ -1574,8 +1615,13 @@ void build(Ctx& c) {
   } else {
     make_ordering(m, prm.nstrips, c.ord);
   }
-  build_pattern(m, c.ord, c.P);
-  assemble_stokes(m, c.ord, c.P, c.as);
+  clk.mark("ordering");
+  Incidence inc;
+  build_incidence(m, c.ord, inc);
+  build_pattern(m, c.ord, c.P, &inc);
+  clk.mark("pattern");
+  assemble_stokes(m, c.ord, c.P, c.as, &inc);
+  inc = Incidence();
   const i64 N = m.N;
 
   // periodic pressure merge maps (internal numbering)
@@ -1597,11 +1643,13 @@ void build(Ctx& c) {
     if (c.dye_impl) build_dye(m, c.ord, c.P, c.Pp, c.dof, c.dyeop);
   }
   c.use_mg = stokes && prm.precond == 1 && c.mg_levels > 0;
-  if (c.use_mg) build_mg_host(c);
+  clk.mark("assembly + pressure merge");
+  if (c.use_mg) build_mg_host(c, clk);
   if (literal) {
     assemble_literal(m, c.ord, c.g_tri, c.op_pairs, c.dir_nodes, c.dir_vals,
                      prm.scheme == PUCFEM_HEAT ? prm.dt : -1.0, c.Lit, c.litb);
   }
+  clk.mark("multigrid hierarchy (host)");
   // A_visc on P (StokesColor.py:471-475)
   std::vector<uint8_t> isdir(N, 0);
   for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
@@ -1614,6 +1662,7 @@ void build(Ctx& c) {
       else if (isdir[j]) c.Kv[k] = 0.0;
       else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
     }
+  clk.mark("A_visc");
   // partition + local plan
   if (stokes) partition_rows(c.P, c.ord, c.world, c.row_start);
   else c.row_start = {0, N};
@@ -1700,6 +1749,7 @@ void build(Ctx& c) {
       }
     }
   }
+  clk.mark("partition, plans, level tables");
   if (c.lattice) {
     const LatticeLevel& LL = c.mg.back().latl;
     std::vector<i32> rows;
@@ -1721,6 +1771,7 @@ void build(Ctx& c) {
       dump_sell(path, c.sPp, v);
     }
   }
+  clk.mark("SELL images");
   if (c.host_only) return;
 
   // ---------------------------------------------------------------- device upload
@@ -1786,6 +1837,7 @@ void build(Ctx& c) {
     c.dDyeDinv = c.dalloc<double>(c.nloc);
     c.dDyeB = c.dalloc<double>(c.nloc);
   }
+  clk.mark("device: K, G, dye operator");
   // Jacobi symmetric scaling S A S of A_visc
   auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
     sg.resize(N);
@@ -1904,6 +1956,7 @@ void build(Ctx& c) {
   }
   c.block_cg = c.prm.solver_path != 1;
   c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1 && c.prm.solver_path != 1;
+  clk.mark("device: A_visc, pressure, multigrid");
   // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
   // small meshes need no better start)
   // (a basis needs room for the re-seeded span and one new direction: at least 3)
@@ -1960,6 +2013,7 @@ void build(Ctx& c) {
     for (i64 g = 0; g < N; ++g) dinv[g] = 1.0 / diag_of(c.Lit, c.Lit.val, g);
     c.dlit_dinv = c.upload(dinv);
   }
+  clk.mark("device: projections, dense");
   // per-row data
   {
     std::vector<double> as1(no), mp(no), wm(no);
@@ -2062,6 +2116,7 @@ void build(Ctx& c) {
   if (literal || c.dye_impl) {
     for (int q = 0; q < 9; ++q) c.litw[q] = c.dalloc<double>(c.nloc);
   }
+  clk.mark("device: per-row data, BCs, halo, workspace");
   // full-mesh replica in internal numbering
   {
     std::vector<double> X(N), Y(N);
@@ -2088,20 +2143,26 @@ void build(Ctx& c) {
     };
     if (stokes) {  // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
       std::vector<double> cx(m.T), cy(m.T);
-      for (i64 t = 0; t < m.T; ++t) {
-        const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
-        cx[t] = (m.x[a] + m.x[b] + m.x[d]) / 3;
-        cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
-      }
+      parallel_for(m.T, [&](i64 t0, i64 t1) {
+        for (i64 t = t0; t < t1; ++t) {
+          const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
+          cx[t] = (m.x[a] + m.x[b] + m.x[d]) / 3;
+          cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
+        }
+      });
       Grid G;
       build_centroid_grid(cx, cy, 2.0, G);
       dgrid(G, c.cgrid, true);
       c.has_cgrid = true;
-      Grid TG;
-      build_tri_grid(X, Y, tri, 4.0, TG);
-      dgrid(TG, c.tgrid, false);
-      c.has_tgrid = true;
+      if (prm.scheme == PUCFEM_STOKES_FOOD) {  // tracer location (StokesFood only)
+        Grid TG;
+        build_tri_grid(X, Y, tri, 4.0, TG);
+        dgrid(TG, c.tgrid, false);
+        c.has_tgrid = true;
+      }
+      clk.mark("SL: centroid / triangle grids");
       const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
+      clk.mark("SL: centroid 10-NN radii");
       const float* drv2 = c.upload(knn_radius2(G, X, Y, KNN + 1, false));
       std::vector<double> xy(2 * (size_t)N);
       for (i64 i = 0; i < N; ++i) {
@@ -2109,6 +2170,7 @@ void build(Ctx& c) {
         xy[2 * i + 1] = Y[i];
       }
       const double2* dxy = reinterpret_cast<const double2*>(c.upload(xy));
+      clk.mark("SL: vertex 11-NN radii");
       const int probe = std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0;
       // semi-Lagrangian point location: on a lattice hierarchy the lattice locator (no per-triangle
       // records); PUCFEM_SL_RECORDS=1 forces the record locator (measurement / cross-check knob)
@@ -2122,6 +2184,7 @@ void build(Ctx& c) {
           c.lat_sl = false;  // a hierarchy not numbered face by face: the record locator below
         }
       }
+      clk.mark("SL: lattice locator tables");
       if (c.lat_sl) {
         Grid MG;
         build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, MG, 1e-6);
@@ -2189,6 +2252,7 @@ void build(Ctx& c) {
     HIPCHK(hipMemcpyAsync(c.c_full, c0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
   }
   HIPCHK(hipStreamSynchronize(c.st));
+  clk.mark("SL: locator / self table, initial state");
 }
 
 }  // namespace
@@ -2290,7 +2354,9 @@ int pucfem_mesh_upload(void* ctx, int64_t N, const double* xy, const int32_t* mk
     }
     m.mk.assign(mk, mk + N);
     m.tri.assign(tris, tris + 3 * T);
-    for (i64 k = 0; k < 3 * T; ++k) require(m.tri[k] >= 0 && m.tri[k] < N, "triangle index out of range");
+    bool ok = true;
+    for (i64 k = 0; k < 3 * T; ++k) ok &= m.tri[k] >= 0 && m.tri[k] < N;
+    require(ok, "triangle index out of range");
     m.fp32 = coord_fp32 != 0;
     c.has_mesh = true;
     c.built = false;
@@ -2921,6 +2987,7 @@ int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
     c.need_dev();
     c.need_built();
     require(c.world == 1, "tracer_step unit op is single-rank");
+    require(c.has_tgrid, "tracer_step needs a STOKES_FOOD context (the tracer grid)");
     const i64 N = c.mesh.N;
     std::vector<double> bx(N), by(N);
     for (i64 g = 0; g < N; ++g) {
@@ -3057,7 +3124,31 @@ int pucfem_refine(int64_t N, const double* xy, const int32_t* mk, int64_t T, con
                   int64_t* N_out, int64_t* T_out, double* xy_out, int32_t* mk_out, int32_t* tris_out) {
   return guard(nullptr, [&] {
     require(levels >= 0 && levels <= 12, "levels in [0, 12]");
-    // sizes: N' = N + E, T' = 4T per level (E from Euler: E = (3T + Eb)/2), computed exactly by refining
+    if (!xy_out) {  // sizes only: N' = N + E, T' = 4T, E = (3T + Eb) / 2 with Eb doubling per level
+      std::vector<std::pair<i32, i32>> es(3 * (size_t)T);
+      for (i64 t = 0; t < T; ++t)
+        for (int e = 0; e < 3; ++e) {
+          const i32 a = tris[3 * t + e], b = tris[3 * t + (e + 1) % 3];
+          es[3 * t + e] = {std::min(a, b), std::max(a, b)};
+        }
+      std::sort(es.begin(), es.end());
+      i64 Eb = 0;
+      for (size_t i = 0; i < es.size();) {
+        size_t j = i;
+        while (j < es.size() && es[j] == es[i]) ++j;
+        if (j - i == 1) ++Eb;
+        i = j;
+      }
+      i64 n = N, t = T;
+      for (int l = 0; l < levels; ++l) {
+        n += (3 * t + Eb) / 2;
+        t *= 4;
+        Eb *= 2;
+      }
+      *N_out = n;
+      *T_out = t;
+      return;
+    }
     HostMesh a;
     a.N = N;
     a.T = T;

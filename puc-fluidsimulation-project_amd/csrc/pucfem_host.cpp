@@ -3,6 +3,7 @@
 #include "pucfem_host.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <numeric>
@@ -32,24 +33,37 @@ void red_refine(const HostMesh& in, HostMesh& out, std::vector<i32>* edge_a, std
         bval[fill[std::min(a, b)]++] = std::max(a, b);
       }
   }
-  // unique edges per bucket, with their multiplicity
+  // unique edges per bucket, with their multiplicity (buckets are independent: sort and count in
+  // parallel, then a prefix sum gives every bucket its edge ids)
   std::vector<i64> eptr(N + 1, 0);
-  std::vector<i32> eb;
-  std::vector<uint8_t> emult;
-  eb.reserve(bval.size() / 2 + N);
-  for (i64 a = 0; a < N; ++a) {
-    auto s = bval.begin() + bptr[a], e = bval.begin() + bptr[a + 1];
-    std::sort(s, e);
-    for (auto it = s; it != e;) {
-      auto j = it;
-      while (j != e && *j == *it) ++j;
-      eb.push_back(*it);
-      emult.push_back((uint8_t)std::min<i64>(255, j - it));
-      it = j;
+  parallel_for(N, [&](i64 a0, i64 a1) {
+    for (i64 a = a0; a < a1; ++a) {
+      auto s = bval.begin() + bptr[a], e = bval.begin() + bptr[a + 1];
+      std::sort(s, e);  // duplicates stay: their count is the edge's multiplicity
+      i64 d = 0;
+      for (auto it = s; it != e; ++it)
+        if (it == s || *it != *(it - 1)) ++d;
+      eptr[a + 1] = d;
     }
-    eptr[a + 1] = (i64)eb.size();
-  }
-  const i64 E = (i64)eb.size();
+  });
+  for (i64 a = 0; a < N; ++a) eptr[a + 1] += eptr[a];
+  const i64 E = eptr[N];
+  std::vector<i32> eb(E);
+  std::vector<uint8_t> emult(E);
+  parallel_for(N, [&](i64 a0, i64 a1) {
+    for (i64 a = a0; a < a1; ++a) {
+      auto s = bval.begin() + bptr[a], e = bval.begin() + bptr[a + 1];
+      i64 k = eptr[a];
+      for (auto it = s; it != e;) {
+        auto j = it;
+        while (j != e && *j == *it) ++j;
+        eb[k] = *it;
+        emult[k] = (uint8_t)std::min<i64>(255, j - it);
+        ++k;
+        it = j;
+      }
+    }
+  });
   auto edge_id = [&](i32 a, i32 b) -> i64 {
     if (a > b) std::swap(a, b);
     auto s = eb.begin() + eptr[a], e = eb.begin() + eptr[a + 1];
@@ -65,33 +79,39 @@ void red_refine(const HostMesh& in, HostMesh& out, std::vector<i32>* edge_a, std
   std::copy(in.x.begin(), in.x.end(), out.x.begin());
   std::copy(in.y.begin(), in.y.end(), out.y.begin());
   std::copy(in.mk.begin(), in.mk.end(), out.mk.begin());
-  for (i64 a = 0; a < N; ++a)
-    for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
-      i32 b = eb[k];
-      i64 n = N + k;
-      out.x[n] = (in.x[a] + in.x[b]) * 0.5;
-      out.y[n] = (in.y[a] + in.y[b]) * 0.5;
-      if (emult[k] == 1)  // boundary edge: midpoint stays on the boundary segment
-        out.mk[n] = (in.mk[a] == 2 && in.mk[b] == 2) ? 2 : 1;
-      else
-        out.mk[n] = 0;
-    }
+  parallel_for(N, [&](i64 a0, i64 a1) {
+    for (i64 a = a0; a < a1; ++a)
+      for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
+        i32 b = eb[k];
+        i64 n = N + k;
+        out.x[n] = (in.x[a] + in.x[b]) * 0.5;
+        out.y[n] = (in.y[a] + in.y[b]) * 0.5;
+        if (emult[k] == 1)  // boundary edge: midpoint stays on the boundary segment
+          out.mk[n] = (in.mk[a] == 2 && in.mk[b] == 2) ? 2 : 1;
+        else
+          out.mk[n] = 0;
+      }
+  });
   if (edge_a && edge_b) {
     edge_a->resize(E);
     edge_b->resize(E);
-    for (i64 a = 0; a < N; ++a)
-      for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
-        (*edge_a)[k] = (i32)a;
-        (*edge_b)[k] = eb[k];
-      }
+    parallel_for(N, [&](i64 a0, i64 a1) {
+      for (i64 a = a0; a < a1; ++a)
+        for (i64 k = eptr[a]; k < eptr[a + 1]; ++k) {
+          (*edge_a)[k] = (i32)a;
+          (*edge_b)[k] = eb[k];
+        }
+    });
   }
   out.tri.resize(3 * out.T);
-  for (i64 t = 0; t < T; ++t) {
-    i32 a = in.tri[3 * t], b = in.tri[3 * t + 1], c = in.tri[3 * t + 2];
-    i32 ab = (i32)(N + edge_id(a, b)), bc = (i32)(N + edge_id(b, c)), ca = (i32)(N + edge_id(c, a));
-    const i32 ch[12] = {a, ab, ca, ab, b, bc, ca, bc, c, ab, bc, ca};
-    std::copy(ch, ch + 12, out.tri.begin() + 12 * t);
-  }
+  parallel_for(T, [&](i64 t0, i64 t1) {
+    for (i64 t = t0; t < t1; ++t) {
+      i32 a = in.tri[3 * t], b = in.tri[3 * t + 1], c = in.tri[3 * t + 2];
+      i32 ab = (i32)(N + edge_id(a, b)), bc = (i32)(N + edge_id(b, c)), ca = (i32)(N + edge_id(c, a));
+      const i32 ch[12] = {a, ab, ca, ab, b, bc, ca, bc, c, ab, bc, ca};
+      std::copy(ch, ch + 12, out.tri.begin() + 12 * t);
+    }
+  });
 }
 
 // ----------------------------------------------------------------------------- ordering
@@ -140,69 +160,130 @@ void make_ordering_cuts(const HostMesh& m, const std::vector<double>& cuts, Orde
 }
 
 // ----------------------------------------------------------------------------- pattern
-void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P) {
+// node -> incident triangles (internal node ids), triangles in ascending order per node
+void build_incidence(const HostMesh& m, const Ordering& ord, Incidence& I) {
+  std::vector<i64>& ptr = I.ptr;
+  std::vector<i32>& tri = I.tri;
   const i64 N = m.N, T = m.T;
-  std::vector<i64> cnt(N + 1, 0);
-  for (i64 t = 0; t < T; ++t)
-    for (int i = 0; i < 3; ++i) cnt[ord.old2new[m.tri[3 * t + i]] + 1] += 3;
-  for (i64 i = 0; i < N; ++i) cnt[i + 1] += cnt[i];
-  std::vector<i32> tmp(cnt[N]);
-  std::vector<i64> fill(cnt.begin(), cnt.end() - 1);
-  for (i64 t = 0; t < T; ++t)
-    for (int i = 0; i < 3; ++i) {
-      i32 r = ord.old2new[m.tri[3 * t + i]];
-      for (int j = 0; j < 3; ++j) tmp[fill[r]++] = ord.old2new[m.tri[3 * t + j]];
+  ptr.assign(N + 1, 0);
+  for (i64 q = 0; q < 3 * T; ++q) ++ptr[ord.old2new[m.tri[q]] + 1];
+  for (i64 i = 0; i < N; ++i) ptr[i + 1] += ptr[i];
+  tri.resize(ptr[N]);
+  // fill with atomic cursors (any order), then sort every node's list: ascending triangle ids
+  std::vector<std::atomic<i64>> cur(N);
+  parallel_for(N, [&](i64 a, i64 b) {
+    for (i64 i = a; i < b; ++i) cur[i].store(ptr[i], std::memory_order_relaxed);
+  });
+  parallel_for(T, [&](i64 t0, i64 t1) {
+    for (i64 t = t0; t < t1; ++t)
+      for (int i = 0; i < 3; ++i) tri[cur[ord.old2new[m.tri[3 * t + i]]].fetch_add(1, std::memory_order_relaxed)] = (i32)t;
+  });
+  parallel_for(N, [&](i64 a, i64 b) {
+    for (i64 i = a; i < b; ++i) std::sort(tri.begin() + ptr[i], tri.begin() + ptr[i + 1]);
+  });
+}
+
+void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P, const Incidence* inc) {
+  const i64 N = m.N;
+  Incidence own;
+  if (!inc) {
+    build_incidence(m, ord, own);
+    inc = &own;
+  }
+  const std::vector<i64>& iptr = inc->ptr;
+  const std::vector<i32>& itri = inc->tri;
+  // rows are independent: each chunk gathers, sorts and dedups its rows, then the chunks are
+  // concatenated in row order
+  std::vector<std::vector<i32>> ccol(PAR_CHUNKS);
+  std::vector<std::vector<i64>> clen(PAR_CHUNKS);
+  parallel_chunks(N, [&](int ch, i64 r0, i64 r1) {
+    std::vector<i32>& out = ccol[ch];
+    std::vector<i64>& len = clen[ch];
+    std::vector<i32> tmp;
+    for (i64 r = r0; r < r1; ++r) {
+      tmp.clear();
+      for (i64 e = iptr[r]; e < iptr[r + 1]; ++e) {
+        const i64 t = itri[e];
+        for (int j = 0; j < 3; ++j) tmp.push_back(ord.old2new[m.tri[3 * t + j]]);
+      }
+      std::sort(tmp.begin(), tmp.end());
+      tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+      if (tmp.empty()) tmp.push_back((i32)r);  // isolated node: keep a diagonal entry
+      out.insert(out.end(), tmp.begin(), tmp.end());
+      len.push_back((i64)tmp.size());
     }
+  });
   P.nrows = N;
   P.rowptr.assign(N + 1, 0);
-  P.col.clear();
-  P.col.reserve(cnt[N] / 2 + N);
-  for (i64 r = 0; r < N; ++r) {
-    auto s = tmp.begin() + cnt[r], e = tmp.begin() + cnt[r + 1];
-    std::sort(s, e);
-    e = std::unique(s, e);
-    if (s == e) P.col.push_back((i32)r);  // isolated node: keep a diagonal entry
-    P.col.insert(P.col.end(), s, e);
-    P.rowptr[r + 1] = (i64)P.col.size();
-  }
+  i64 r = 0;
+  for (int ch = 0; ch < PAR_CHUNKS; ++ch)
+    for (i64 l : clen[ch]) {
+      P.rowptr[r + 1] = P.rowptr[r] + l;
+      ++r;
+    }
+  P.col.resize(P.rowptr[N]);
+  std::vector<i64> cstart(PAR_CHUNKS + 1, 0);
+  for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)ccol[ch].size();
+  parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
+    for (i64 ch = c0; ch < c1; ++ch) std::copy(ccol[ch].begin(), ccol[ch].end(), P.col.begin() + cstart[ch]);
+  });
 }
 
 // ----------------------------------------------------------------------------- assembly
-void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A) {
-  const i64 N = m.N, T = m.T, nnz = P.nnz();
+// Row-parallel: every row gathers the contributions of its incident triangles in ascending triangle
+// order, which is the order the reference's scatter loop (StokesColor.py:98-128, :224-284) adds them
+// to each entry -- the values are the sequential scatter's, bit for bit.
+void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A, const Incidence* inc) {
+  const i64 N = m.N, nnz = P.nnz();
   A.K.assign(nnz, 0.0);
   A.Gx.assign(nnz, 0.0);
   A.Gy.assign(nnz, 0.0);
   A.M.assign(N, 0.0);
   A.asum.assign(N, 0.0);
-  for (i64 t = 0; t < T; ++t) {
-    const i32 o[3] = {m.tri[3 * t], m.tri[3 * t + 1], m.tri[3 * t + 2]};
-    const i32 n[3] = {ord.old2new[o[0]], ord.old2new[o[1]], ord.old2new[o[2]]};
-    const double x1 = m.x[o[0]], y1 = m.y[o[0]], x2 = m.x[o[1]], y2 = m.y[o[1]], x3 = m.x[o[2]],
-                 y3 = m.y[o[2]];
-    // StokesColor.py:277-283 (buildLumpedMassMatrix): no degenerate skip
-    const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
-    const double area = 0.5 * std::fabs(det);
-    for (int i = 0; i < 3; ++i) A.M[n[i]] += area / 3.0;
-    if (std::fabs(det) < 1e-14) continue;  // StokesColor.py:113, :146, :239
-    const double yd[3] = {y2 - y3, y3 - y1, y1 - y2};
-    const double xd[3] = {x3 - x2, x1 - x3, x2 - x1};
-    const double den = 2 * std::fabs(det);
-    i64 pos[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) pos[i][j] = P.find(n[i], n[j]);
-    for (int i = 0; i < 3; ++i)  // StokesColor.py:120-126
-      for (int j = 0; j < 3; ++j) A.K[pos[i][j]] += (yd[i] * yd[j] + xd[i] * xd[j]) / den;
-    const double inv2A = 1.0 / det;  // StokesColor.py:149 / :241
-    const double a3 = area / 3.0;
-    for (int i = 0; i < 3; ++i) {
-      A.asum[n[i]] += a3;
-      for (int k = 0; k < 3; ++k) {
-        A.Gx[pos[i][k]] += (yd[k] * inv2A) * a3;
-        A.Gy[pos[i][k]] += (xd[k] * inv2A) * a3;
+  Incidence own;
+  if (!inc) {
+    build_incidence(m, ord, own);
+    inc = &own;
+  }
+  const std::vector<i64>& iptr = inc->ptr;
+  const std::vector<i32>& itri = inc->tri;
+  parallel_for(N, [&](i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1; ++r) {
+      const i64 b = P.rowptr[r], e = P.rowptr[r + 1];
+      auto pos = [&](i32 col) {
+        const auto it = std::lower_bound(P.col.begin() + b, P.col.begin() + e, col);
+        return (i64)(it - P.col.begin());
+      };
+      for (i64 q = iptr[r]; q < iptr[r + 1]; ++q) {
+        const i64 t = itri[q];
+        const i32 o[3] = {m.tri[3 * t], m.tri[3 * t + 1], m.tri[3 * t + 2]};
+        const i32 n[3] = {ord.old2new[o[0]], ord.old2new[o[1]], ord.old2new[o[2]]};
+        const double x1 = m.x[o[0]], y1 = m.y[o[0]], x2 = m.x[o[1]], y2 = m.y[o[1]], x3 = m.x[o[2]],
+                     y3 = m.y[o[2]];
+        // StokesColor.py:277-283 (buildLumpedMassMatrix): no degenerate skip
+        const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);
+        const double area = 0.5 * std::fabs(det);
+        for (int i = 0; i < 3; ++i)
+          if (n[i] == r) A.M[r] += area / 3.0;
+        if (std::fabs(det) < 1e-14) continue;  // StokesColor.py:113, :146, :239
+        const double yd[3] = {y2 - y3, y3 - y1, y1 - y2};
+        const double xd[3] = {x3 - x2, x1 - x3, x2 - x1};
+        const double den = 2 * std::fabs(det);
+        const double inv2A = 1.0 / det;  // StokesColor.py:149 / :241
+        const double a3 = area / 3.0;
+        for (int i = 0; i < 3; ++i) {
+          if (n[i] != r) continue;
+          A.asum[r] += a3;
+          for (int j = 0; j < 3; ++j) {
+            const i64 k = pos(n[j]);
+            A.K[k] += (yd[i] * yd[j] + xd[i] * xd[j]) / den;  // StokesColor.py:120-126
+            A.Gx[k] += (yd[j] * inv2A) * a3;
+            A.Gy[k] += (xd[j] * inv2A) * a3;
+          }
+        }
       }
     }
-  }
+  });
 }
 
 namespace {
@@ -303,37 +384,54 @@ void assemble_literal(const HostMesh& m, const Ordering& ord, const std::vector<
 void build_pressure(const Csr& P, const std::vector<double>& K, const std::vector<i32>& dof,
                     const std::vector<i32>& slave_of, Csr& Pp) {
   const i64 N = P.nrows;
+  // rows are independent (chunks of rows merged in parallel, then concatenated in row order)
+  std::vector<std::vector<std::pair<i32, double>>> cent(PAR_CHUNKS);
+  std::vector<std::vector<i64>> clen(PAR_CHUNKS);
+  parallel_chunks(N, [&](int ch, i64 r0, i64 r1) {
+    std::vector<std::pair<i32, double>> tmp;
+    for (i64 r = r0; r < r1; ++r) {
+      tmp.clear();
+      if (dof[r] != r) {  // slave: identity row, decoupled
+        tmp.push_back({(i32)r, 1.0});
+      } else {
+        auto add_row = [&](i64 src) {
+          for (i64 k = P.rowptr[src]; k < P.rowptr[src + 1]; ++k) tmp.push_back({dof[P.col[k]], K[k]});
+        };
+        add_row(r);
+        if (slave_of[r] >= 0) add_row(slave_of[r]);
+        // combine duplicates in insertion order (stable by column)
+        std::stable_sort(tmp.begin(), tmp.end(),
+                         [](const std::pair<i32, double>& a, const std::pair<i32, double>& b) { return a.first < b.first; });
+        size_t w = 0;
+        for (size_t k = 0; k < tmp.size(); ++k) {
+          if (w > 0 && tmp[w - 1].first == tmp[k].first) tmp[w - 1].second += tmp[k].second;
+          else tmp[w++] = tmp[k];
+        }
+        tmp.resize(w);
+      }
+      cent[ch].insert(cent[ch].end(), tmp.begin(), tmp.end());
+      clen[ch].push_back((i64)tmp.size());
+    }
+  });
   Pp.nrows = N;
   Pp.rowptr.assign(N + 1, 0);
-  Pp.col.clear();
-  Pp.val.clear();
-  std::vector<std::pair<i32, double>> tmp;
-  for (i64 r = 0; r < N; ++r) {
-    tmp.clear();
-    if (dof[r] != r) {  // slave: identity row, decoupled
-      tmp.push_back({(i32)r, 1.0});
-    } else {
-      auto add_row = [&](i64 src) {
-        for (i64 k = P.rowptr[src]; k < P.rowptr[src + 1]; ++k) tmp.push_back({dof[P.col[k]], K[k]});
-      };
-      add_row(r);
-      if (slave_of[r] >= 0) add_row(slave_of[r]);
-      // combine duplicates in insertion order (stable by column)
-      std::stable_sort(tmp.begin(), tmp.end(),
-                       [](const std::pair<i32, double>& a, const std::pair<i32, double>& b) { return a.first < b.first; });
-      size_t w = 0;
-      for (size_t k = 0; k < tmp.size(); ++k) {
-        if (w > 0 && tmp[w - 1].first == tmp[k].first) tmp[w - 1].second += tmp[k].second;
-        else tmp[w++] = tmp[k];
+  i64 r = 0;
+  for (int ch = 0; ch < PAR_CHUNKS; ++ch)
+    for (i64 l : clen[ch]) {
+      Pp.rowptr[r + 1] = Pp.rowptr[r] + l;
+      ++r;
+    }
+  Pp.col.resize(Pp.rowptr[N]);
+  Pp.val.resize(Pp.rowptr[N]);
+  std::vector<i64> cstart(PAR_CHUNKS + 1, 0);
+  for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)cent[ch].size();
+  parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
+    for (i64 ch = c0; ch < c1; ++ch)
+      for (size_t q = 0; q < cent[ch].size(); ++q) {
+        Pp.col[cstart[ch] + q] = cent[ch][q].first;
+        Pp.val[cstart[ch] + q] = cent[ch][q].second;
       }
-      tmp.resize(w);
-    }
-    for (auto& e : tmp) {
-      Pp.col.push_back(e.first);
-      Pp.val.push_back(e.second);
-    }
-    Pp.rowptr[r + 1] = (i64)Pp.col.size();
-  }
+  });
 }
 
 // ----------------------------------------------------------------------------- partition
@@ -504,10 +602,10 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
   const i64 nc = (i64)G.nx * G.ny;
   std::vector<i32> cell(T);
   G.cell_start.assign(nc + 1, 0);
-  for (i64 t = 0; t < T; ++t) {
-    cell[t] = cell_of(cy[t], G.y0, G.hy, G.ny) * G.nx + cell_of(cx[t], G.x0, G.hx, G.nx);
-    G.cell_start[cell[t] + 1]++;
-  }
+  parallel_for(T, [&](i64 t0, i64 t1) {
+    for (i64 t = t0; t < t1; ++t) cell[t] = cell_of(cy[t], G.y0, G.hy, G.ny) * G.nx + cell_of(cx[t], G.x0, G.hx, G.nx);
+  });
+  for (i64 t = 0; t < T; ++t) G.cell_start[cell[t] + 1]++;
   for (i64 c = 0; c < nc; ++c) G.cell_start[c + 1] += G.cell_start[c];
   G.item.assign(T, 0);
   G.px.assign(T, 0);
@@ -880,19 +978,6 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
     }
 }
 
-namespace {
-template <class F>
-void parallel_for(i64 n, F&& f) {
-  const int nt = (int)std::max<i64>(1, std::min<i64>({64, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
-  if (nt == 1) {
-    f((i64)0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int w = 0; w < nt; ++w) th.emplace_back([&, w] { f(n * w / nt, n * (w + 1) / nt); });
-  for (auto& h : th) h.join();
-}
-}  // namespace
 
 void build_macro(const HostMesh& c, int strips, int lw, Macro& M) {
   M.nv = c.N;

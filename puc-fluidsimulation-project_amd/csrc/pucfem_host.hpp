@@ -4,6 +4,8 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "pucfem_lattice.hpp"
@@ -12,6 +14,37 @@ namespace pucfem {
 
 using i32 = int32_t;
 using i64 = int64_t;
+
+// ----------------------------------------------------------------------------- host threading
+// f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to 64)
+template <class F>
+void parallel_for(i64 n, F&& f) {
+  const int nt = (int)std::max<i64>(1, std::min<i64>({64, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
+  if (nt == 1) {
+    f((i64)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int w = 0; w < nt; ++w) th.emplace_back([&, w] { f(n * w / nt, n * (w + 1) / nt); });
+  for (auto& h : th) h.join();
+}
+// f(chunk, r0, r1) over PAR_CHUNKS fixed chunks of [0, n) (independent of the machine's thread
+// count: per-chunk partial sums combined in chunk order are reproducible everywhere)
+constexpr int PAR_CHUNKS = 64;
+template <class F>
+void parallel_chunks(i64 n, F&& f) {
+  const int nt = (int)std::max<i64>(1, std::min<i64>({PAR_CHUNKS, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
+  auto run = [&](int w) {
+    for (int ch = w; ch < PAR_CHUNKS; ch += nt) f(ch, n * ch / PAR_CHUNKS, n * (ch + 1) / PAR_CHUNKS);
+  };
+  if (nt == 1) {
+    run(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int w = 0; w < nt; ++w) th.emplace_back(run, w);
+  for (auto& h : th) h.join();
+}
 
 struct HostMesh {
   i64 N = 0, T = 0;
@@ -56,7 +89,13 @@ void make_ordering_cuts(const HostMesh& m, const std::vector<double>& cuts, Orde
 int auto_strips(i64 N);
 
 // Node-adjacency pattern (incl. diagonal) in internal numbering, sorted columns.
-void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P);
+// node -> incident triangles (internal ids; ascending triangle ids per node)
+struct Incidence {
+  std::vector<i64> ptr;
+  std::vector<i32> tri;
+};
+void build_incidence(const HostMesh& m, const Ordering& ord, Incidence& I);
+void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P, const Incidence* I = nullptr);
 
 struct Assembly {
   std::vector<double> K;     // on P (StokesColor.py:98-128), reference triangle order
@@ -64,7 +103,7 @@ struct Assembly {
   std::vector<double> M;     // lumped mass (StokesColor.py:266-284), internal numbering
   std::vector<double> asum;  // area_sum of calculate_divergence (|det| >= 1e-14 only)
 };
-void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A);
+void assemble_stokes(const HostMesh& m, const Ordering& ord, const Csr& P, Assembly& A, const Incidence* I = nullptr);
 
 // poisson.py:100-146 in fp32 arithmetic (bit-exact), fp64 accumulation, then the literal
 // periodic row-merge (poisson.py:187-213) and Dirichlet rows (poisson.py:258-278).

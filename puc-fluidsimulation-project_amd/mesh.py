@@ -111,8 +111,10 @@ def find_boundary_pairs(nodes_coords, L=1.0, tol=TOL):
     if len(left) == 0 or len(right) == 0:
         return np.zeros((0, 2), dtype=np.int64)
     tree = KDTree(X[right, 1].reshape(-1, 1))
-    j = [int(tree.query([X[i, 1]])[1]) for i in left]
-    return np.stack([left, right[j]], 1).astype(np.int64)
+    # one batched query: each point is searched exactly as a single query would be (same tree, same
+    # tie rule), so the pairs are the reference's one-query-per-node loop's
+    _, j = tree.query(X[left, 1].reshape(-1, 1))
+    return np.stack([left, right[np.asarray(j, dtype=np.int64)]], 1).astype(np.int64)
 
 
 def filter_wall_pairs(nodes_coords, pairs, tol=TOL, H=1.0):
@@ -129,8 +131,11 @@ def boundary_sets(nodes_coords, markers, tol=TOL, H=1.0):
     X = np.asarray(nodes_coords)
     wall = np.where(np.isclose(X[:, 1], 0.0, atol=tol) | np.isclose(X[:, 1], H, atol=tol))[0]
     inner = np.where(markers == INNER_BOUNDARY_MARKER)[0]
-    dirichlet = np.union1d(wall, inner)
-    interior = np.setdiff1d(np.arange(X.shape[0]), dirichlet)
+    mask = np.zeros(X.shape[0], dtype=bool)
+    mask[wall] = True
+    mask[inner] = True
+    dirichlet = np.flatnonzero(mask)  # = np.union1d(wall, inner), sorted
+    interior = np.flatnonzero(~mask)
     return wall, inner, dirichlet, interior
 
 
