@@ -341,6 +341,8 @@ struct Ctx {
   int64_t* dDyeSptr = nullptr;
   int32_t dye_nsrow = 0;
   int last_dye_it = 0;
+  bool lmax_dev = false;            // the finest level's lmax: power iteration on the device
+  std::vector<double> lmax_dinv;    // its D^-1 (host, Gershgorin pass)
   DyeOp dyeop;  // host data of the implicit dye operator (built with the host operators)
   LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
   bool lat_sl = false;
@@ -1217,6 +1219,40 @@ struct Ctx {
     its[2] = itp2;
   }
 
+  // the finest multigrid level's lmax (lmax_estimate's power iteration, on the device operator):
+  // min(Gershgorin bound gersh, 1.1 x 30 steps of x <- D^-1 A x / |D^-1 A x|)
+  double lmax_device(double gersh) {
+    const i64 n = lp.n_own;
+    double* x = dalloc<double>(nloc);
+    double* y = dalloc<double>(nloc);
+    std::vector<double> x0(n);
+    for (i64 i = 0; i < n; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)i);
+    const double* dinv = upload(lmax_dinv);
+    HIPCHK(hipMemcpyAsync(x, x0.data(), sizeof(double) * n, hipMemcpyHostToDevice, st));
+    const int nb = nb_rows(n), ge = grid_ew(n);
+    double lam = 0.0;
+    for (int it = 0; it < 30; ++it) {
+      spmv_on(st, dPp, fP.full(), dKp_raw, x, y);
+      hipLaunchKernelGGL(k_vmul, dim3(ge), dim3(BS), 0, st, n, (const double*)y, dinv, y);
+      hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, (const double*)x, (const double*)x, (const double*)y,
+                         (const double*)y, part_a);
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, redbuf);
+      KCHK();
+      HIPCHK(hipMemcpyAsync(h_pinned, redbuf, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const double nx = h_pinned[0], ny = h_pinned[1];
+      lam = std::sqrt(ny / nx);
+      hipLaunchKernelGGL(k_axpbypcz, dim3(ge), dim3(BS), 0, st, n, (const double*)nullptr, (const double*)y,
+                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr, (const double*)nullptr,
+                         1.0 / std::sqrt(ny), 0.0, 0.0, x);
+      KCHK();
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    lmax_dinv.clear();
+    lmax_dinv.shrink_to_fit();
+    return std::min(gersh, 1.1 * lam);
+  }
+
   // implicit dye step (good_visualization.py:700-718) from cin with velocity (vx, vy) and its lumped
   // divergence dv into cout: assemble the merged operator, rhs = M c, BiCGStab from c, periodic copies
   int dye_step(const double* vx, const double* vy, const double* dv, const double* cin, double* cout) {
@@ -1371,11 +1407,13 @@ inline void require(bool ok, const std::string& msg) {
 }
 
 // ------------------------------------------------------------------ multigrid hierarchy (host)
-double lmax_estimate(const Csr& A) {
-  // min(Gershgorin bound, 1.1 x 30-step power iteration) of D^-1 A; rows in fixed chunks (threads),
-  // the norms summed per chunk and then in chunk order: the same value on every machine
+// min(Gershgorin bound, 1.1 x 30-step power iteration) of D^-1 A; rows in fixed chunks (threads),
+// the norms summed per chunk and then in chunk order: the same value on every machine.  power = false:
+// the Gershgorin bound only, with D^-1 in *dinv_out (the finest level's power iteration then runs on
+// the device, Ctx::lmax_device)
+double lmax_estimate(const Csr& A, bool power = true, std::vector<double>* dinv_out = nullptr) {
   const i64 n = A.nrows;
-  std::vector<double> dinv(n), x(n), y(n);
+  std::vector<double> dinv(n), x(power ? n : 0), y(power ? n : 0);
   std::vector<double> cg(PAR_CHUNKS, 0.0), cx(PAR_CHUNKS), cy(PAR_CHUNKS);
   parallel_chunks(n, [&](int ch, i64 r0, i64 r1) {
     for (i64 r = r0; r < r1; ++r) {
@@ -1390,6 +1428,10 @@ double lmax_estimate(const Csr& A) {
   });
   double gersh = 0.0;
   for (double g : cg) gersh = std::max(gersh, g);
+  if (!power) {
+    if (dinv_out) dinv_out->swap(dinv);
+    return gersh;
+  }
   for (i64 i = 0; i < n; ++i) x[i] = 1.0 + 0.5 * std::sin((double)i);
   double lam = 0.0;
   for (int it = 0; it < 30; ++it) {
@@ -1486,7 +1528,11 @@ void build_mg_host(Ctx& c, SetupClock& clk) {
     transpose(L.Pr, C.mesh.N, L.R);
   }
   clk.mark("  mg: transfers");
-  for (int l = 0; l <= Lv; ++l) c.mg[l].lmax = lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
+  // the finest level's power iteration runs on the device at the end of build() (single rank)
+  c.lmax_dev = c.world == 1 && !c.host_only;
+  for (int l = 0; l <= Lv; ++l)
+    c.mg[l].lmax = l == Lv && c.lmax_dev ? lmax_estimate(c.Pp, false, &c.lmax_dinv)
+                                         : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
   clk.mark("  mg: lmax estimates");
 }
 
@@ -1841,10 +1887,14 @@ void build(Ctx& c) {
   // Jacobi symmetric scaling S A S of A_visc
   auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
     sg.resize(N);
-    for (i64 g = 0; g < N; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
+    parallel_for(N, [&](i64 g0, i64 g1) {
+      for (i64 g = g0; g < g1; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
+    });
     std::vector<double> out(val.size());
-    for (i64 r = 0; r < N; ++r)
-      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) out[k] = sg[r] * val[k] * sg[A.col[k]];
+    parallel_for(N, [&](i64 r0, i64 r1) {
+      for (i64 r = r0; r < r1; ++r)
+        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) out[k] = sg[r] * val[k] * sg[A.col[k]];
+    });
     return out;
   };
   auto local_vec = [&](const std::vector<double>& g) {  // owned + ghost entries of a global vector
@@ -2253,6 +2303,11 @@ void build(Ctx& c) {
   }
   HIPCHK(hipStreamSynchronize(c.st));
   clk.mark("SL: locator / self table, initial state");
+  if (c.use_mg && c.lmax_dev) {
+    MgLevel& F = c.mg[c.mg_levels];
+    F.lmax = c.lmax_device(F.lmax);
+    clk.mark("finest lmax (device power iteration)");
+  }
 }
 
 }  // namespace

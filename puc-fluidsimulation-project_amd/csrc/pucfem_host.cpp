@@ -566,13 +566,15 @@ void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::ve
                  std::vector<double>& out) {
   if (!S.rows.empty()) return sell_values_rows(A, lp.r0, S, val, out);
   out.assign(S.padded, 0.0);
-  for (i64 s = 0; s < S.nslices; ++s)
-    for (i64 l = 0; l < 64; ++l) {
-      i64 r = s * 64 + l;
-      if (r >= S.nrows) continue;
-      i64 b = A.rowptr[lp.r0 + r], len = A.rowptr[lp.r0 + r + 1] - b;
-      for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
-    }
+  parallel_for(S.nslices, [&](i64 s0, i64 s1) {
+    for (i64 s = s0; s < s1; ++s)
+      for (i64 l = 0; l < 64; ++l) {
+        i64 r = s * 64 + l;
+        if (r >= S.nrows) continue;
+        i64 b = A.rowptr[lp.r0 + r], len = A.rowptr[lp.r0 + r + 1] - b;
+        for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
+      }
+  });
 }
 
 // ----------------------------------------------------------------------------- grids
@@ -916,13 +918,15 @@ void build_sell_x(const Csr& A, i64 r0, i64 n, const LocalPlan& cols, Sell& S, b
 void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out) {
   if (!S.rows.empty()) return sell_values_rows(A, r0, S, val, out);
   out.assign(S.padded, 0.0);
-  for (i64 s = 0; s < S.nslices; ++s)
-    for (i64 l = 0; l < 64; ++l) {
-      const i64 r = s * 64 + l;
-      if (r >= S.nrows) continue;
-      const i64 b = A.rowptr[r0 + r], len = A.rowptr[r0 + r + 1] - b;
-      for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
-    }
+  parallel_for(S.nslices, [&](i64 s0, i64 s1) {
+    for (i64 s = s0; s < s1; ++s)
+      for (i64 l = 0; l < 64; ++l) {
+        const i64 r = s * 64 + l;
+        if (r >= S.nrows) continue;
+        const i64 b = A.rowptr[r0 + r], len = A.rowptr[r0 + r + 1] - b;
+        for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
+      }
+  });
 }
 
 }  // namespace pucfem

@@ -1653,6 +1653,9 @@ __global__ __launch_bounds__(BS) void k_dot2(int64_t n, const double* a, const d
   }
 }
 // generic: z = a*x + b*y + c*w with coefficients read from device scalars (sign flags on the host)
+__global__ void k_vmul(int64_t n, const double* a, const double* b, double* out) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = a[i] * b[i];
+}
 __global__ void k_axpbypcz(int64_t n, const double* ca, const double* x, const double* cb, const double* y,
                            const double* cc, const double* w, double sa, double sb, double sc, double* z) {
   const double a = sa * (ca ? *ca : 1.0), b = sb * (cb ? *cb : 1.0), c = sc * (cc ? *cc : 1.0);
