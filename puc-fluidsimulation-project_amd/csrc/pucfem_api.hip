@@ -342,6 +342,15 @@ struct Ctx {
   int32_t dye_nsrow = 0;
   int last_dye_it = 0;
   bool lmax_dev = false;            // the finest level's lmax: power iteration on the device
+  // multi-rank dye replica: a wide halo instead of an all-gather (dye_halo)
+  std::vector<double> strip_ylo, strip_yhi;  // per strip (internal order): the y extent of its nodes
+  std::vector<i64> rank_s0, rank_s1;         // per rank: its strips [s0, s1)
+  std::vector<double> rank_ylo, rank_yhi;    // per rank: the y extent of its nodes
+  double tri_hy = 0.0;                       // largest y extent of a triangle
+  double* part_u = nullptr;                  // max |u_y| partials
+  double* trv = nullptr;                     // multi-rank tracer velocities (3 x ntr, all-reduced)
+  int32_t* dghost_global = nullptr;          // lp.ghost_global on the device
+  i64 dye_halo_values = 0;                   // values received by the last dye_halo (diagnostics)
   std::vector<double> lmax_dinv;    // its D^-1 (host, Gershgorin pass)
   DyeOp dyeop;  // host data of the implicit dye operator (built with the host operators)
   LatLocDev llgrid{};  // lattice locator (lat_sl): replaces lgrid's records on lattice hierarchies
@@ -569,6 +578,52 @@ struct Ctx {
   void mg_halo(MgLevel& L, T* a) {
     if (&L == &mg.back()) halo_lp(lp, dsend, bufs<T>(L).sendbuf, nsend, a);
     else halo_lp(L.lp, L.dsend, bufs<T>(L).sendbuf, L.nsend, a);
+  }
+  // Before the semi-Lagrangian step on W > 1 ranks: refresh the dye replica where this step's
+  // back-traced points can reach -- the strips within dt max|u_y| + (largest triangle height) of each
+  // rank's own y extent -- with point-to-point copies of contiguous internal-id ranges (every rank's
+  // own segment is current: its SL wrote it).  Replaces the all-gather of the whole field (SURVEY.md
+  // §8e: the departure distance bounds the gather).
+  void dye_halo(const double* vy, double dt) {
+    if (world == 1) return;
+    const i64 n = lp.n_own;
+    const int nb = nb_rows(n);
+    hipLaunchKernelGGL(k_absmax, dim3(nb), dim3(BS), 0, st, n, vy, part_u);
+    KCHK();
+    Red r = reduce_global(part_u, nb, 1, true, 40);
+    HIPCHK(hipMemcpyAsync(h_pinned, r.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const double reach = std::fabs(dt) * h_pinned[0] + tri_hy + 1e-9;
+    const i64 S = (i64)strip_ylo.size();
+    auto need = [&](int j, i64& a, i64& b) {  // internal-id range rank j reads
+      i64 sa = 0, sb = S;
+      while (sa < S && strip_yhi[sa] < rank_ylo[j] - reach) ++sa;
+      while (sb > sa && strip_ylo[sb - 1] > rank_yhi[j] + reach) --sb;
+      a = ord.strip_ptr[sa];
+      b = ord.strip_ptr[sb];
+    };
+    const i64 o0 = row_start[rank], o1 = row_start[rank + 1];
+    dye_halo_values = 0;
+    comm->group_start();
+    for (int j = 0; j < world; ++j) {
+      if (j == rank) continue;
+      i64 a, b;
+      need(j, a, b);
+      a = std::max(a, o0);
+      b = std::min(b, o1);
+      if (b > a) comm->send(c_full + a, (size_t)(b - a), j, st);
+    }
+    i64 a0, b0;
+    need(rank, a0, b0);
+    for (int j = 0; j < world; ++j) {
+      if (j == rank) continue;
+      const i64 a = std::max(a0, row_start[j]), b = std::min(b0, row_start[j + 1]);
+      if (b > a) {
+        comm->recv(c_full + a, (size_t)(b - a), j, st);
+        dye_halo_values += b - a;
+      }
+    }
+    comm->group_end(st);
   }
   // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
   void allgather_full(double* full) {
@@ -1195,15 +1250,17 @@ struct Ctx {
         hipLaunchKernelGGL(k_wsum, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, (const double*)c_new,
                            (const double*)dwmix, part_sl);
       } else {
+        dye_halo(uy, prm.dt);
         sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
       }
       KCHK();
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+      } else if (world > 1) {  // the replica keeps its (halo) values; only the owned segment is new
+        HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
       } else {
         std::swap(c_full, c_new);
       }
-      allgather_full(c_full);
       reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
       const int nbm = nb_rows(lp.n_own);
       hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
@@ -1296,13 +1353,27 @@ struct Ctx {
     }
     if (!has_tgrid) throw Error(PUCFEM_ESTATE, "tracer grid not built (scheme is not STOKES_FOOD)");
     double *fx = ux, *fy = uy;
-    if (world > 1) {  // full replica of u (internal numbering is rank-contiguous)
+    if (world > 1) {
+      // no replica of u: each rank interpolates the tracers in its own triangles from its owned and
+      // ghost values (placed at their global ids), then one all-reduce of 3 x ntr values hands every
+      // rank all the velocities (StokesFood's 488 tracers: ~12 KB per step instead of the whole u)
       HIPCHK(hipMemcpyAsync(ufx + lp.r0, ux, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
       HIPCHK(hipMemcpyAsync(ufy + lp.r0, uy, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-      allgather_full(ufx);
-      allgather_full(ufy);
-      fx = ufx;
-      fy = ufy;
+      if (lp.n_ghost > 0) {
+        hipLaunchKernelGGL(k_scatter_ghosts, dim3(grid_ew(lp.n_ghost)), dim3(BS), 0, st, lp.n_ghost,
+                           (const int32_t*)dghost_global, (const double*)(ux + lp.n_own), ufx);
+        hipLaunchKernelGGL(k_scatter_ghosts, dim3(grid_ew(lp.n_ghost)), dim3(BS), 0, st, lp.n_ghost,
+                           (const int32_t*)dghost_global, (const double*)(uy + lp.n_own), ufy);
+      }
+      hipLaunchKernelGGL(k_tracer_vel, dim3((ntr + BS - 1) / BS), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T},
+                         tgrid, (const double*)ufx, (const double*)ufy, ntr, (const double*)trx, (const double*)try_,
+                         (int64_t)lp.r0, (int64_t)lp.r1, trv);
+      KCHK();
+      comm->allreduce(trv, 3 * (size_t)ntr, false, st);
+      hipLaunchKernelGGL(k_tracer_move, dim3(1), dim3(BS), 0, st, ntr, trx, try_, trs, (const double*)trv, dt,
+                         prm.center_x, prm.center_y, prm.capture_radius, vals + 6);
+      KCHK();
+      return;
     }
     hipLaunchKernelGGL(k_tracer, dim3(1), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T}, tgrid, fx, fy, ntr, trx,
                        try_, trs, dt, prm.center_x, prm.center_y, prm.capture_radius, vals + 6);
@@ -1795,6 +1866,31 @@ void build(Ctx& c) {
       }
     }
   }
+  if (stokes && c.world > 1) {  // wide-halo tables of the dye replica (Ctx::dye_halo)
+    const i64 S = (i64)c.ord.strip_ptr.size() - 1;
+    c.strip_ylo.assign(S, INFINITY);
+    c.strip_yhi.assign(S, -INFINITY);
+    for (i64 s = 0; s < S; ++s)
+      for (i64 g = c.ord.strip_ptr[s]; g < c.ord.strip_ptr[s + 1]; ++g) {
+        const double y = m.y[c.ord.new2old[g]];
+        c.strip_ylo[s] = std::min(c.strip_ylo[s], y);
+        c.strip_yhi[s] = std::max(c.strip_yhi[s], y);
+      }
+    c.rank_ylo.assign(c.world, INFINITY);
+    c.rank_yhi.assign(c.world, -INFINITY);
+    for (int r = 0; r < c.world; ++r)
+      for (i64 g = c.row_start[r]; g < c.row_start[r + 1]; ++g) {
+        const double y = m.y[c.ord.new2old[g]];
+        c.rank_ylo[r] = std::min(c.rank_ylo[r], y);
+        c.rank_yhi[r] = std::max(c.rank_yhi[r], y);
+      }
+    double hy = 0.0;
+    for (i64 t = 0; t < m.T; ++t) {
+      const double a = m.y[m.tri[3 * t]], b = m.y[m.tri[3 * t + 1]], d = m.y[m.tri[3 * t + 2]];
+      hy = std::max(hy, std::max({a, b, d}) - std::min({a, b, d}));
+    }
+    c.tri_hy = hy;
+  }
   clk.mark("partition, plans, level tables");
   if (c.lattice) {
     const LatticeLevel& LL = c.mg.back().latl;
@@ -2154,6 +2250,7 @@ void build(Ctx& c) {
   }
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
+  c.part_u = c.dalloc<double>(MAXB);
   if (stokes) {
     c.sl_queue = c.dalloc<int32_t>(m.N);
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
@@ -2291,6 +2388,7 @@ void build(Ctx& c) {
     if (c.world > 1) {
       c.ufx = c.dalloc<double>(N);
       c.ufy = c.dalloc<double>(N);
+      if (c.lp.n_ghost > 0) c.dghost_global = c.upload(c.lp.ghost_global);
     }
   }
   // initial state: u = 0 then makeDirBCU (StokesColor.py:482-483); c = 1[x < 0.5] (:493-495)
@@ -2542,6 +2640,7 @@ int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count)
           c.trx = c.dalloc<double>(n);
           c.try_ = c.dalloc<double>(n);
           c.trs = c.dalloc<double>(n);
+          if (c.world > 1) c.trv = c.dalloc<double>(3 * n);
         }
         std::vector<double> x(n), y(n);
         for (i64 k = 0; k < n; ++k) {
@@ -2599,6 +2698,7 @@ int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count) {
       case PUCFEM_F_SCALAR: get1(c.scalar); break;
       case PUCFEM_F_C: {
         require(count == N, "c is (N,)");
+        c.allgather_full(c.c_full);  // multi-rank: collective (every rank reads c), the full field
         std::vector<double> x(N);
         HIPCHK(hipMemcpyAsync(x.data(), c.c_full, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipStreamSynchronize(c.st));

@@ -117,8 +117,8 @@ struct LocalComm : Comm {
   std::shared_ptr<LocalShared> S;
   int rank, world;
   std::vector<LocalShared::Op> pending;
-  static constexpr size_t MAXRED = 128;  // >= 2 * PROJ_MAX + 4 (the projection's multi-dot)
-  double* tmp = nullptr;  // reduction output, up to MAXRED values
+  size_t cap = 128;       // >= 2 * PROJ_MAX + 4 (the projection's multi-dot); grows on demand (tracers)
+  double* tmp = nullptr;  // reduction output, up to cap values
   double** dptrs = nullptr;
 
   LocalComm(const std::string& key, int w, int r) : rank(r), world(w) {
@@ -134,7 +134,7 @@ struct LocalComm : Comm {
     if (S->world != w) throw std::runtime_error("LocalComm world mismatch");
     if (hipEventCreateWithFlags(&S->ready[r], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S->done[r], hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&tmp, MAXRED * sizeof(double)) != hipSuccess || hipMalloc(&dptrs, 64 * sizeof(double*)) != hipSuccess)
+        hipMalloc(&tmp, cap * sizeof(double)) != hipSuccess || hipMalloc(&dptrs, 64 * sizeof(double*)) != hipSuccess)
       throw std::runtime_error("LocalComm: HIP allocation failed");
     S->barrier();  // every rank has created its events
   }
@@ -146,8 +146,13 @@ struct LocalComm : Comm {
     if (e != hipSuccess) throw std::runtime_error(std::string("LocalComm HIP: ") + hipGetErrorString(e));
   }
   void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) override {
-    if (n > MAXRED) throw std::runtime_error("LocalComm allreduce supports <= 128 values");
     if (world > 64) throw std::runtime_error("LocalComm supports <= 64 ranks");
+    if (n > cap) {  // this rank's output buffer only: no other rank touches it
+      chk(hipStreamSynchronize(st));
+      chk(hipFree(tmp));
+      cap = n;
+      chk(hipMalloc(&tmp, cap * sizeof(double)));
+    }
     chk(hipEventRecord(S->ready[rank], st));
     S->red[rank] = buf;
     S->barrier();

@@ -1516,6 +1516,62 @@ __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const doub
 // ----------------------------------------------------------------------------- tracers
 // StokesFood.py:482-499: LinearTriInterpolator (matplotlib plane coefficients, NaN outside the
 // mesh), forward Euler, x mod 1, sticky capture.  One thread per tracer; full-mesh u replica.
+// LinearTriInterpolator at one point (StokesFood.py:482-487, matplotlib TrapezoidMapTriFinder +
+// plane coefficients): the first triangle of the point's grid cell whose three orientation tests pass
+// (-1: outside the mesh); the interpolated velocity when u is given
+__device__ __forceinline__ int32_t tracer_locate(const MeshDev& M, const GridDev& G, double px, double py) {
+  if (!(isfinite(px) && isfinite(py))) return -1;
+  const int32_t ci = gcell(px, G.x0, G.hx, G.nx), cj = gcell(py, G.y0, G.hy, G.ny);
+  const bool inside = px >= G.x0 && px <= G.x0 + G.nx * G.hx && py >= G.y0 && py <= G.y0 + G.ny * G.hy;
+  if (!inside) return -1;
+  const int64_t c = (int64_t)cj * G.nx + ci;
+  for (int32_t e = G.start[c]; e < G.start[c + 1]; ++e) {
+    const int32_t t = G.item[e];
+    const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
+    const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[d], y3 = M.y[d];
+    const double o1 = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
+    const double o2 = (x3 - x2) * (py - y2) - (y3 - y2) * (px - x2);
+    const double o3 = (x1 - x3) * (py - y3) - (y1 - y3) * (px - x3);
+    if (o1 >= 0.0 && o2 >= 0.0 && o3 >= 0.0) return t;
+  }
+  return -1;
+}
+__device__ __forceinline__ void tracer_interp(const MeshDev& M, int32_t t, const double* __restrict__ ux,
+                                              const double* __restrict__ uy, double px, double py, double& vx,
+                                              double& vy) {
+  const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
+  const double x0 = M.x[a], y0 = M.y[a];
+  const double s1x = M.x[b] - x0, s1y = M.y[b] - y0, s2x = M.x[d] - x0, s2y = M.y[d] - y0;
+  const double nz = s1x * s2y - s1y * s2x;
+  double zv[2];
+  const double* uu[2] = {ux, uy};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // Triangulation::calculate_plane_coefficients
+    const double z0 = uu[q][a];
+    const double s1z = uu[q][b] - z0, s2z = uu[q][d] - z0;
+    const double nx = s1y * s2z - s1z * s2y;
+    const double ny = s1z * s2x - s1x * s2z;
+    const double pa = -nx / nz, pb = -ny / nz;
+    const double pc = (nx * x0 + ny * y0 + nz * z0) / nz;
+    zv[q] = pa * px + pb * py + pc;
+  }
+  vx = zv[0];
+  vy = zv[1];
+}
+// forward Euler, x mod 1, sticky capture (StokesFood.py:488-499)
+__device__ __forceinline__ double tracer_move(double* tx, double* ty, double* status, int32_t k, double vx, double vy,
+                                              double dt, double cx, double cy, double capture) {
+  const double px = tx[k], py = ty[k];
+  double nx_ = px + vx * dt, ny_ = py + vy * dt;
+  nx_ = py_mod(nx_, 1.0);
+  tx[k] = nx_;
+  ty[k] = ny_;
+  const double ddx = nx_ - cx, ddy = ny_ - cy;
+  const double dist = sqrt(ddx * ddx + ddy * ddy);
+  if (dist <= capture) status[k] = 1.0;
+  return status[k];
+}
+
 __global__ void k_tracer(MeshDev M, GridDev G, const double* __restrict__ ux, const double* __restrict__ uy,
                          int32_t ntr, double* tx, double* ty, double* status, double dt, double cx, double cy,
                          double capture, double* eaten_out) {
@@ -1524,54 +1580,50 @@ __global__ void k_tracer(MeshDev M, GridDev G, const double* __restrict__ ux, co
   for (int32_t k = threadIdx.x; k < ntr; k += blockDim.x) {
     const double px = tx[k], py = ty[k];
     double vx = NAN, vy = NAN;
-    if (isfinite(px) && isfinite(py)) {
-      const int32_t ci = gcell(px, G.x0, G.hx, G.nx), cj = gcell(py, G.y0, G.hy, G.ny);
-      const bool inside = px >= G.x0 && px <= G.x0 + G.nx * G.hx && py >= G.y0 && py <= G.y0 + G.ny * G.hy;
-      const int64_t c = (int64_t)cj * G.nx + ci;
-      int32_t found = -1;
-      if (inside) {
-        for (int32_t e = G.start[c]; e < G.start[c + 1] && found < 0; ++e) {
-          const int32_t t = G.item[e];
-          const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
-          const double x1 = M.x[a], y1 = M.y[a], x2 = M.x[b], y2 = M.y[b], x3 = M.x[d], y3 = M.y[d];
-          const double o1 = (x2 - x1) * (py - y1) - (y2 - y1) * (px - x1);
-          const double o2 = (x3 - x2) * (py - y2) - (y3 - y2) * (px - x2);
-          const double o3 = (x1 - x3) * (py - y3) - (y1 - y3) * (px - x3);
-          if (o1 >= 0.0 && o2 >= 0.0 && o3 >= 0.0) found = t;
-        }
-      }
-      if (found >= 0) {
-        const int32_t a = M.tri[3 * found], b = M.tri[3 * found + 1], d = M.tri[3 * found + 2];
-        const double x0 = M.x[a], y0 = M.y[a];
-        const double s1x = M.x[b] - x0, s1y = M.y[b] - y0, s2x = M.x[d] - x0, s2y = M.y[d] - y0;
-        const double nz = s1x * s2y - s1y * s2x;
-        double zv[2];
-        const double* uu[2] = {ux, uy};
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {  // Triangulation::calculate_plane_coefficients
-          const double z0 = uu[q][a];
-          const double s1z = uu[q][b] - z0, s2z = uu[q][d] - z0;
-          const double nx = s1y * s2z - s1z * s2y;
-          const double ny = s1z * s2x - s1x * s2z;
-          const double pa = -nx / nz, pb = -ny / nz;
-          const double pc = (nx * x0 + ny * y0 + nz * z0) / nz;
-          zv[q] = pa * px + pb * py + pc;
-        }
-        vx = zv[0];
-        vy = zv[1];
-      }
-    }
-    double nx_ = px + vx * dt, ny_ = py + vy * dt;
-    nx_ = py_mod(nx_, 1.0);
-    tx[k] = nx_;
-    ty[k] = ny_;
-    const double ddx = nx_ - cx, ddy = ny_ - cy;
-    const double dist = sqrt(ddx * ddx + ddy * ddy);
-    if (dist <= capture) status[k] = 1.0;
-    eaten += status[k];
+    const int32_t found = tracer_locate(M, G, px, py);
+    if (found >= 0) tracer_interp(M, found, ux, uy, px, py, vx, vy);
+    eaten += tracer_move(tx, ty, status, k, vx, vy, dt, cx, cy, capture);
   }
   const double t = block_sum(eaten, sh);
   if (threadIdx.x == 0) *eaten_out = t;
+}
+
+// multi-rank tracer step, part 1: every rank interpolates the tracers whose triangle it owns (its
+// first vertex is one of the rank's rows: the other two are then owned or ghosts, filled into the
+// global-index arrays fx / fy); tv[3k..3k+2] = (vx, vy, 1) there, zeros elsewhere -- summed over ranks
+__global__ void k_tracer_vel(MeshDev M, GridDev G, const double* __restrict__ fx, const double* __restrict__ fy,
+                             int32_t ntr, const double* tx, const double* ty, int64_t own0, int64_t own1, double* tv) {
+  for (int32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < ntr; k += gridDim.x * blockDim.x) {
+    const double px = tx[k], py = ty[k];
+    double vx = 0.0, vy = 0.0, f = 0.0;
+    const int32_t t = tracer_locate(M, G, px, py);
+    if (t >= 0 && M.tri[3 * t] >= own0 && M.tri[3 * t] < own1) {
+      tracer_interp(M, t, fx, fy, px, py, vx, vy);
+      f = 1.0;
+    }
+    tv[3 * k] = vx;
+    tv[3 * k + 1] = vy;
+    tv[3 * k + 2] = f;
+  }
+}
+// part 2 (after the all-reduce, identical on every rank): the move with the owner's velocity (NaN
+// where no rank holds the tracer: outside the mesh)
+__global__ void k_tracer_move(int32_t ntr, double* tx, double* ty, double* status, const double* tv, double dt,
+                              double cx, double cy, double capture, double* eaten_out) {
+  __shared__ double sh[4];
+  double eaten = 0.0;
+  for (int32_t k = threadIdx.x; k < ntr; k += blockDim.x) {
+    const bool found = tv[3 * k + 2] > 0.5;
+    eaten += tracer_move(tx, ty, status, k, found ? tv[3 * k] : NAN, found ? tv[3 * k + 1] : NAN, dt, cx, cy, capture);
+  }
+  const double t = block_sum(eaten, sh);
+  if (threadIdx.x == 0) *eaten_out = t;
+}
+// ghost values of a local vector into their global positions of a full-size array
+__global__ void k_scatter_ghosts(int64_t ng, const int32_t* __restrict__ ghost_global, const double* __restrict__ v,
+                                 double* __restrict__ full) {
+  for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < ng; k += (int64_t)gridDim.x * BS)
+    full[ghost_global[k]] = v[k];
 }
 
 // ----------------------------------------------------------------------------- misc
@@ -1653,6 +1705,16 @@ __global__ __launch_bounds__(BS) void k_dot2(int64_t n, const double* a, const d
   }
 }
 // generic: z = a*x + b*y + c*w with coefficients read from device scalars (sign flags on the host)
+// partial max |v| (block max over the block's rows)
+__global__ __launch_bounds__(BS) void k_absmax(int64_t n, const double* __restrict__ v, double* part) {
+  __shared__ double sh[4];
+  double m = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) m = fmax(m, fabs(v[i]));
+  const double t = block_max(m, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
 __global__ void k_vmul(int64_t n, const double* a, const double* b, double* out) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = a[i] * b[i];
 }
