@@ -240,6 +240,10 @@ int pucfem_info(void* ctx, int64_t* out12);
    interiors (pucfem_params.assembled = 0 with a hierarchy; clear: every row is a stored SELL row),
    bit 1: the semi-Lagrangian point location uses the lattice locator (else per-triangle records) */
 int pucfem_path_info(void* ctx, int64_t* out8);
+/* multi-rank data flow of the last step: out[0] dye values this rank received in the wide halo before
+   the semi-Lagrangian step, out[1] the values a full all-gather of the dye would have received
+   (N - n_own), out[2] values all-reduced for the StokesFood tracers (3 x tracers), out[3] reserved */
+int pucfem_comm_info(void* ctx, int64_t* out4);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

@@ -347,7 +347,9 @@ struct Ctx {
   std::vector<i64> rank_s0, rank_s1;         // per rank: its strips [s0, s1)
   std::vector<double> rank_ylo, rank_yhi;    // per rank: the y extent of its nodes
   double tri_hy = 0.0;                       // largest y extent of a triangle
-  double* part_u = nullptr;                  // max |u_y| partials
+  double* part_u = nullptr;                  // back-traced y range partials (1 - min, max)
+  double *yr_own = nullptr, *yr_all = nullptr;  // this rank's (1 - min, max); every rank's (2 W)
+  std::vector<double> h_yr;
   double* trv = nullptr;                     // multi-rank tracer velocities (3 x ntr, all-reduced)
   int32_t* dghost_global = nullptr;          // lp.ghost_global on the device
   i64 dye_halo_values = 0;                   // values received by the last dye_halo (diagnostics)
@@ -588,17 +590,23 @@ struct Ctx {
     if (world == 1) return;
     const i64 n = lp.n_own;
     const int nb = nb_rows(n);
-    hipLaunchKernelGGL(k_absmax, dim3(nb), dim3(BS), 0, st, n, vy, part_u);
+    // every rank's range of back-traced y (StokesColor.py:361-372), all-gathered as a max-reduction
+    // of a 2 W vector holding (1 - min, max) in each rank's slot
+    hipLaunchKernelGGL(k_yrange, dim3(nb), dim3(BS), 0, st, n, my + lp.r0, vy, dt, part_u);
     KCHK();
-    Red r = reduce_global(part_u, nb, 1, true, 40);
-    HIPCHK(hipMemcpyAsync(h_pinned, r.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_u, nb, MAXB, 2, 1, yr_own);
+    hipLaunchKernelGGL(k_place2, dim3(1), dim3(64), 0, st, world, rank, (const double*)yr_own, yr_all);
+    KCHK();
+    comm->allreduce(yr_all, 2 * (size_t)world, true, st);
+    HIPCHK(hipMemcpyAsync(h_yr.data(), yr_all, sizeof(double) * 2 * world, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const double reach = std::fabs(dt) * h_pinned[0] + tri_hy + 1e-9;
     const i64 S = (i64)strip_ylo.size();
-    auto need = [&](int j, i64& a, i64& b) {  // internal-id range rank j reads
+    auto need = [&](int j, i64& a, i64& b) {  // internal-id range rank j reads: the strips that meet
+      // its back-traced y range widened by a triangle height (the located triangle's vertices)
+      const double lo = (1.0 - h_yr[2 * j]) - tri_hy - 1e-9, hi = h_yr[2 * j + 1] + tri_hy + 1e-9;
       i64 sa = 0, sb = S;
-      while (sa < S && strip_yhi[sa] < rank_ylo[j] - reach) ++sa;
-      while (sb > sa && strip_ylo[sb - 1] > rank_yhi[j] + reach) --sb;
+      while (sa < S && strip_yhi[sa] < lo) ++sa;
+      while (sb > sa && strip_ylo[sb - 1] > hi) --sb;
       a = ord.strip_ptr[sa];
       b = ord.strip_ptr[sb];
     };
@@ -2250,7 +2258,10 @@ void build(Ctx& c) {
   }
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
-  c.part_u = c.dalloc<double>(MAXB);
+  c.part_u = c.dalloc<double>(2 * MAXB);
+  c.yr_own = c.dalloc<double>(2);
+  c.yr_all = c.dalloc<double>(2 * c.world);
+  c.h_yr.assign(2 * c.world, 0.0);
   if (stokes) {
     c.sl_queue = c.dalloc<int32_t>(m.N);
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
@@ -3271,6 +3282,17 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0);
+  });
+}
+
+int pucfem_comm_info(void* ctx, int64_t* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    o[0] = c.world > 1 ? c.dye_halo_values : 0;
+    o[1] = c.world > 1 ? c.mesh.N - c.lp.n_own : 0;
+    o[2] = c.world > 1 ? 3 * (int64_t)c.ntr : 0;
+    o[3] = 0;
   });
 }
 

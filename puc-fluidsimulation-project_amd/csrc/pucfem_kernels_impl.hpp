@@ -1705,6 +1705,32 @@ __global__ __launch_bounds__(BS) void k_dot2(int64_t n, const double* a, const d
   }
 }
 // generic: z = a*x + b*y + c*w with coefficients read from device scalars (sign flags on the host)
+// partial (1 - min, max) of the back-traced y of the rows (StokesColor.py:362-366: y - dt u_y, clamped
+// into [1e-12, 1 - 1e-12]; both in [0, 1], as k_reduce's maxima start at 0); part[b] = 1 - min,
+// part[MAXB + b] = max
+__global__ __launch_bounds__(BS) void k_yrange(int64_t n, const double* __restrict__ y, const double* __restrict__ vy,
+                                               double dt, double* part) {
+  __shared__ double sh[4];
+  double lo = 0.0, hi = 0.0;  // lo holds 1 - min
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    double yb = y[i] - dt * vy[i] * 1.0;
+    if (yb < 0.0) yb = 1e-12;
+    if (yb > 1.0) yb = 1.0 - 1e-12;
+    lo = fmax(lo, 1.0 - yb);
+    hi = fmax(hi, yb);
+  }
+  const double a = block_max(lo, sh), b = block_max(hi, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = a;
+    part[MAXB + blockIdx.x] = b;
+  }
+}
+// out[2 W] = -inf except this rank's slot (the all-gather of one pair as a max all-reduce)
+__global__ void k_place2(int world, int rank, const double* v, double* out) {
+  for (int i = threadIdx.x; i < 2 * world; i += blockDim.x) out[i] = i / 2 == rank ? v[i % 2] : -INFINITY;
+}
 // partial max |v| (block max over the block's rows)
 __global__ __launch_bounds__(BS) void k_absmax(int64_t n, const double* __restrict__ v, double* part) {
   __shared__ double sh[4];

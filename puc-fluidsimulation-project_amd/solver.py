@@ -217,6 +217,12 @@ class Context:
                     visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7] & 1),
                     sl_locator="lattice" if o[7] & 2 else "records")
 
+    def comm_info(self):
+        """Multi-rank data flow of the last step (pucfem_comm_info)."""
+        o = (ct.c_int64 * 4)()
+        self._c(self.L.pucfem_comm_info(self.h, o))
+        return dict(dye_halo_values=o[0], allgather_values=o[1], tracer_allreduce_values=o[2])
+
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))
 

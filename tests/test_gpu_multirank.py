@@ -29,7 +29,8 @@ def run_ranks(mesh, world, scheme, tol, steps, bc, dt):
         try:
             sim = pf.StokesSimulation(mesh, bc, dt, scheme, device=0, tol=tol, dist=(r, world, uid))
             st = sim.step(steps)
-            res = {"u": sim.u, "info": sim.ctx.info(), "stats": st, "lattice": sim.ctx.path_info()["lattice"]}
+            res = {"u": sim.u, "info": sim.ctx.info(), "stats": st, "lattice": sim.ctx.path_info()["lattice"],
+                   "comm": sim.ctx.comm_info()}
             if scheme == "color":
                 res["c"] = sim.c
             else:
@@ -68,6 +69,10 @@ def test_color_partitioned_matches_single_rank(world, precond, single, rep):
     assert all(o["lattice"] == lattice for o in out)
     if not lattice:
         assert all(o["info"]["index16_P"] and o["info"]["index16_Pp"] for o in out)
+    # the dye replica: a wide halo around each rank's back-traced range, a fraction of an all-gather
+    for o in out:
+        cm = o["comm"]
+        assert 0 < cm["dye_halo_values"] < cm["allgather_values"], cm
     u = sum(o["u"] for o in out)  # every rank fills its owned rows
     ref = pf.StokesSimulation(mesh, bc, 0.05, "color", tol=tol)
     st = ref.step(3)
