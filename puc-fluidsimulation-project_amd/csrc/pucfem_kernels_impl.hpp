@@ -40,6 +40,40 @@ __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t 
   }
 }
 
+// The same work items as face_rows, handed to fn in groups of K rows of one thread (rows t0 + r BS):
+// fn(F, lf, t[K], i[K], j[K], ok[K]) loads every row of the group before computing any, so the
+// group's memory round trips overlap.  Rows past the face end are clamped to its last row (valid
+// addresses; ok = false: not stored).
+template <int K, class Fn>
+__device__ __forceinline__ void face_rows_k(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
+  static_assert(FACE_RPT % K == 0, "group size divides the rows per thread");
+  const int32_t items = fc.nf * fc.cpf;
+  if (nbf == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows)
+    const int32_t x = b & 7, q = items >> 3, rem = items & 7;
+    b = x * q + (x < rem ? x : rem) + (b >> 3);
+    nbf = items + 1;
+  }
+  for (int32_t it = b; it < items; it += nbf) {
+    const int32_t lf = it / fc.cpf;
+    const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT) + (int32_t)threadIdx.x;
+    const lat::FaceTab F = fc.tab[lf];
+#pragma unroll
+    for (int32_t g = 0; g < FACE_RPT; g += K) {
+      if (t0 + g * BS >= fc.F) break;
+      int32_t t[K], i[K], j[K];
+      bool ok[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int32_t tt = t0 + (g + r) * BS;
+        ok[r] = tt < fc.F;
+        t[r] = ok[r] ? tt : fc.F - 1;
+        lat::coords(t[r], fc.n, fc.rinv, i[r], j[r]);
+      }
+      fn(F, lf, t, i, j, ok);
+    }
+  }
+}
+
 // entries of an interior row of a stiffness-type face operator: a[0] the row's own, a[1 + k] its
 // neighbour k (lat::neighbours order).  op 0: K (every level's operator, the merged pressure
 // operator with the merged table); op 1: the Jacobi-scaled A_visc, S A S with s_f inside the face
@@ -307,27 +341,50 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
-      double a[7];
-      face_kcoefs(fc, lf, nb, in, a);
-      const int64_t row = F.base + t;
+    // groups of K rows per thread, every load of the group first (face_rows_k)
+    constexpr int K = NR == 1 ? 2 : 1;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
 #pragma unroll
-      for (int c = 0; c < NR; ++c) {
-        const double* r = v.r[c];
-        const double* po = v.po[c];
-        double g[6];
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      double a[K][7];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) g[k] = r[nb[k]] + beta[c] * po[nb[k]];
-        const double p = r[row] + beta[c] * po[row];
-        double q = a[0] * p;
+      for (int r = 0; r < K; ++r) face_kcoefs(fc, lf, nb[r], in[r], a[r]);
+      double rv[K][NR][7], pv[K][NR][7];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) q += a[1 + k] * g[k];
-        stnt(v.pn[c] + row, p);
-        stnt(v.q[c] + row, q);
-        pq[c] += p * q;
+      for (int r = 0; r < K; ++r) {
+        const int64_t row = F.base + t[r];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          rv[r][c][6] = v.r[c][row];
+          pv[r][c][6] = v.po[c][row];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            rv[r][c][k] = v.r[c][nb[r][k]];
+            pv[r][c][k] = v.po[c][nb[r][k]];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        const int64_t row = F.base + t[r];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          double g[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) g[k] = rv[r][c][k] + beta[c] * pv[r][c][k];
+          const double p = rv[r][c][6] + beta[c] * pv[r][c][6];
+          double q = a[r][0] * p;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) q += a[r][1 + k] * g[k];
+          stnt(v.pn[c] + row, p);
+          stnt(v.q[c] + row, q);
+          pq[c] += p * q;
+        }
       }
     });
   } else {
@@ -1862,6 +1919,101 @@ __device__ __forceinline__ T sell_row_dot(const SellDev& A, const VT* __restrict
 // for the final step that writes the preconditioned residual z).
 // LV: a level tag with no effect on the code (1: the finest level, 2: pucfem_bench_kernel), so that
 // profilers report the finest level's launches apart from the coarser levels' ones.
+// One Chebyshev step specialised on the mode and on whether <rdot, x_out> is accumulated: the row body
+// is one basic block, so every load of a row -- the gathered x (or b and dinv), the row's b, d and
+// rdot -- issues before the first use.  (With a runtime mode the row streams b / d sat behind the
+// gathers' branch: two dependent round trips per row.)  Face rows run in groups of 4 per thread with
+// all loads of the group first.
+template <int MODE, bool RD, typename T, typename TB, typename TO, typename VT, bool C16>
+__device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, const VT* __restrict__ val,
+                                          const T* __restrict__ dinv, const TB* __restrict__ b,
+                                          const T* __restrict__ xin, TO* __restrict__ xout, T* __restrict__ d,
+                                          T tc1, T tc2, T tc20, const double* __restrict__ rdot, double& acc_rz) {
+  // the step's row update from A x (ax), the row's 1 / diag, b and (mode 1) x_in and d
+  auto finish = [&](int64_t row, T ax, T di, T brow, T xrow, T drow, double rrow) {
+    T dn, xo;
+    if constexpr (MODE == 0) {
+      dn = tc2 * di * brow;
+      xo = dn;
+    } else {
+      const T x1 = MODE == 2 ? tc20 * di * brow : xrow;
+      const T d1 = MODE == 2 ? x1 : drow;
+      dn = tc1 * d1 + tc2 * di * (brow - ax);
+      xo = x1 + dn;
+    }
+    stnt(d + row, dn);
+    stnt(xout + row, (TO)xo);
+    if constexpr (RD) acc_rz += rrow * (double)xo;
+  };
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    constexpr int K = 4;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
+#pragma unroll
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      T a[7];
+      face_kcoefs(fc, lf, nb[0], in[0], a);
+      const T di = std::is_same<T, float>::value ? (T)fc.coef32[lf * lat::NCOEF + lat::C_DINV]
+                                                 : (T)fc.coef[lf * lat::NCOEF + lat::C_DINV];
+      T g[K][7], brow[K], xrow[K], drow[K];
+      double rrow[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int64_t row = F.base + t[r];
+        brow[r] = (T)b[row];
+        xrow[r] = drow[r] = (T)0;
+        rrow[r] = 0.0;
+        if constexpr (MODE == 1) {
+          xrow[r] = xin[row];
+          drow[r] = d[row];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) g[r][k] = xin[nb[r][k]];
+        } else if constexpr (MODE == 2) {
+          // x1 = c20 Dinv b at the gathered columns (skeleton columns: their own dinv)
+#pragma unroll
+          for (int k = 0; k < 6; ++k) g[r][k] = tc20 * (in[r][k] ? di : dinv[nb[r][k]]) * (T)b[nb[r][k]];
+        }
+        if constexpr (RD) rrow[r] = rdot[row];
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        const int64_t row = F.base + t[r];
+        T ax = 0;
+        if constexpr (MODE == 1) {
+          ax = a[0] * xrow[r];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) ax += a[1 + k] * g[r][k];
+        } else if constexpr (MODE == 2) {
+          ax = a[0] * (tc20 * di * brow[r]);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) ax += a[1 + k] * g[r][k];
+        }
+        finish(row, ax, di, brow[r], xrow[r], drow[r], rrow[r]);
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t row = sell_row(A, s, lane);
+      const int64_t rr = row >= 0 ? row : 0;
+      const T brow = (T)b[rr], di = dinv[rr];
+      const T xrow = MODE == 1 ? xin[rr] : (T)0, drow = MODE == 1 ? d[rr] : (T)0;
+      const double rrow = RD ? rdot[rr] : 0.0;
+      T ax = 0;
+      if constexpr (MODE == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
+      else if constexpr (MODE == 2)
+        ax = sell_row_dot_g<C16, T>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
+      if (row >= 0) finish(row, ax, di, brow, xrow, drow, rrow);
+    }
+  }
+}
+
 template <typename T, typename TB, typename TO, typename VT, bool C16, int LV = 0>
 __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __restrict__ val,
                                              const T* __restrict__ dinv, const TB* __restrict__ b,
@@ -1872,57 +2024,19 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
   if (ctl && ctl[0]) return;
   const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
   double acc_rz = 0.0;
-  // the step's row update from A x (ax), the row's 1 / diag and the fused first step's x1
-  auto finish = [&](int64_t row, T ax, T di) {
-    T dn, xo;
-    if (mode == 0) {
-      dn = tc2 * di * (T)b[row];
-      xo = dn;
-    } else {
-      const T x1 = mode == 2 ? tc20 * di * (T)b[row] : xin[row];
-      const T d1 = mode == 2 ? x1 : d[row];
-      dn = tc1 * d1 + tc2 * di * ((T)b[row] - ax);
-      xo = x1 + dn;
-    }
-    stnt(d + row, dn);
-    stnt(xout + row, (TO)xo);
-    if (rdot) acc_rz += rdot[row] * (double)xo;
-  };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
-      T a[7];
-      face_kcoefs(fc, lf, nb, in, a);
-      const T di = std::is_same<T, float>::value ? (T)fc.coef32[lf * lat::NCOEF + lat::C_DINV]
-                                                 : (T)fc.coef[lf * lat::NCOEF + lat::C_DINV];
-      const int64_t row = F.base + t;
-      T ax = 0;
-      if (mode == 1) {
-        ax = a[0] * xin[row];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) ax += a[1 + k] * xin[nb[k]];
-      } else if (mode == 2) {  // x1 = c20 Dinv b at the gathered columns (skeleton columns: their own dinv)
-        ax = a[0] * (tc20 * di * (T)b[row]);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) ax += a[1 + k] * (tc20 * (in[k] ? di : dinv[nb[k]]) * (T)b[nb[k]]);
-      }
-      finish(row, ax, di);
-    });
+#define PUCFEM_CHEB(M, R) \
+  cheb_body<M, R, T, TB, TO, VT, C16>(A, fc, val, dinv, b, xin, xout, d, tc1, tc2, tc20, rdot, acc_rz)
+  if (mode == 1) {
+    if (rdot) PUCFEM_CHEB(1, true);
+    else PUCFEM_CHEB(1, false);
+  } else if (mode == 2) {
+    if (rdot) PUCFEM_CHEB(2, true);
+    else PUCFEM_CHEB(2, false);
   } else {
-    int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    for (int64_t s = s0 + wv; s < s1; s += 4) {
-      const int64_t row = sell_row(A, s, lane);
-      T ax = 0;
-      if (mode == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
-      else if (mode == 2)
-        ax = sell_row_dot_g<C16, T>(A, val, [=](int32_t j) { return tc20 * dinv[j] * (T)b[j]; }, s, lane);
-      if (row >= 0) finish(row, ax, dinv[row]);
-    }
+    if (rdot) PUCFEM_CHEB(0, true);
+    else PUCFEM_CHEB(0, false);
   }
+#undef PUCFEM_CHEB
   if (rdot) {
     const double t = block_sum(acc_rz, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = t;
@@ -1936,17 +2050,33 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
                                               T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
-      T a[7];
-      face_kcoefs(fc, lf, nb, in, a);
-      const int64_t row = F.base + t;
-      T ax = a[0] * x[row];
+    constexpr int K = 4;  // groups of K rows per thread, every load first (face_rows_k)
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) ax += a[1 + k] * x[nb[k]];
-      stnt(res + row, (T)b[row] - ax);
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      T a[7];
+      face_kcoefs(fc, lf, nb[0], in[0], a);
+      T xv[K][7], bv[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int64_t row = F.base + t[r];
+        xv[r][6] = x[row];
+        bv[r] = (T)b[row];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) xv[r][k] = x[nb[r][k]];
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        T ax = a[0] * xv[r][6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ax += a[1 + k] * xv[r][k];
+        stnt(res + F.base + t[r], bv[r] - ax);
+      }
     });
     return;
   }
