@@ -225,35 +225,35 @@ template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* val, const double* x, double* y);
 // k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size
 template <int M>
-void mdot2_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* b, const double* av,
+void mdot2_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* b, const double* av,
                   const double* v, const int32_t* master_of, double* part) {
   hipLaunchKernelGGL(k_mdot2<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, b, av, v, master_of, part);
 }
-using Mdot2Fn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
+using Mdot2Fn = void (*)(hipStream_t, int, int64_t, const ProjT*, int64_t, const double*, const double*,
                          const double*, const int32_t*, double*);
 template <int... M>
 constexpr std::array<Mdot2Fn, sizeof...(M)> mdot2_table(std::integer_sequence<int, M...>) {
   return {&mdot2_launch<M>...};
 }
-void mdot2_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* b, const double* av,
+void mdot2_on(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, int m, const double* b, const double* av,
               const double* v, const int32_t* master_of, double* part) {
   static constexpr auto tab = mdot2_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
   if (m < 0 || m > PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
   tab[m](s, nb, n, X, ld, b, av, v, master_of, part);
 }
 template <int M>
-void pcomb_launch(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, const double* K, const double* v,
-                  const int32_t* master_of, double* xm, double* y, double* x0) {
+void pcomb_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* K, const double* v,
+                  const int32_t* master_of, ProjT* xm, double* y, double* x0) {
   hipLaunchKernelGGL(k_pcomb<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, K, v, master_of, xm, y, x0);
 }
-using PcombFn = void (*)(hipStream_t, int, int64_t, const double*, int64_t, const double*, const double*,
-                         const int32_t*, double*, double*, double*);
+using PcombFn = void (*)(hipStream_t, int, int64_t, const ProjT*, int64_t, const double*, const double*,
+                         const int32_t*, ProjT*, double*, double*);
 template <int... M>
 constexpr std::array<PcombFn, sizeof...(M)> pcomb_table(std::integer_sequence<int, M...>) {
   return {&pcomb_launch<M>...};
 }
-void pcomb_on(hipStream_t s, int nb, int64_t n, const double* X, int64_t ld, int m, const double* K, const double* v,
-              const int32_t* master_of, double* xm, double* y, double* x0) {
+void pcomb_on(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, int m, const double* K, const double* v,
+              const int32_t* master_of, ProjT* xm, double* y, double* x0) {
   static constexpr auto tab = pcomb_table(std::make_integer_sequence<int, PROJ_MAX>{});
   if (m < 0 || m >= PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
   tab[m](s, nb, n, X, ld, K, v, master_of, xm, y, x0);
@@ -404,7 +404,7 @@ struct Ctx {
   // up to proj_k solution directions, the projected guess x0 and the new direction
   // (which = 3, 4: the viscous solve's x and y components, proj_k_visc directions each)
   int proj_k = 0, proj_k_visc = 0;
-  double* projX[5] = {};
+  ProjT* projX[5] = {};
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
   // Deferred update (project_guess): after a solve only v = y - x0 and A v are formed; the next
@@ -415,7 +415,7 @@ struct Ctx {
   // default 8): seeds kept.
   static constexpr int NCOEF = 2 * PROJ_MAX + 4;
   double* h_coef = nullptr;
-  double* projXalt[5] = {};
+  ProjT* projXalt[5] = {};
   struct ProjHist {
     std::vector<std::vector<double>> sols;  // coordinates of the last solutions
     std::vector<double> gamma;              // coordinates of the last guess x0
@@ -1194,7 +1194,7 @@ struct Ctx {
     for (int i = 0; i < kq; ++i)
       for (int j = 0; j < m; ++j) qm.q[i][j] = Q[i][j];
     const i64 n = lp.n_own;
-    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const double*)projX[which], nloc, m, qm, kq,
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], nloc, m, qm, kq,
                        projXalt[which]);
     KCHK();
     std::swap(projX[which], projXalt[which]);
@@ -2121,9 +2121,9 @@ void build(Ctx& c) {
   for (int w = 1; w <= 4; ++w) {
     const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
     if (k > 0) {
-      c.projX[w] = c.dalloc<double>((i64)k * c.nloc);
+      c.projX[w] = c.dalloc<ProjT>((i64)k * c.nloc);
       c.proj_x0[w] = c.dalloc<double>(c.nloc);
-      c.projXalt[w] = c.dalloc<double>((i64)k * c.nloc);  // re-seeding target
+      c.projXalt[w] = c.dalloc<ProjT>((i64)k * c.nloc);  // re-seeding target
     }
   }
   if (stokes && !c.dense && !block_visc && c.proj_k_visc == 0 && c.visc_extrap > 0)

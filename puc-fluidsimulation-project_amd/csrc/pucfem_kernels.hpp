@@ -112,12 +112,16 @@ __device__ __forceinline__ double block_max(double v, double* sh) {
   return fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
 }
 // Sum of `nb` partials at stride 1 starting at p (fixed order -> identical in every block).
+// nb == 1 (a k_reduce scalar slot, the usual case): the value itself, no block barrier, so the
+// consumers' scalar loads issue together
 __device__ __forceinline__ double reduce_partials(const double* p, int nb, double* sh) {
+  if (nb == 1) return p[0];
   double a = 0.0;
   for (int i = threadIdx.x; i < nb; i += BS) a += p[i];
   return block_sum(a, sh);
 }
 __device__ __forceinline__ double reduce_partials_max(const double* p, int nb, double* sh) {
+  if (nb == 1) return fmax(0.0, p[0]);
   double a = 0.0;
   for (int i = threadIdx.x; i < nb; i += BS) a = fmax(a, p[i]);
   return block_max(a, sh);
@@ -132,8 +136,8 @@ struct Wn {
   static constexpr int value = N;
 };
 // f(Wn<w>{}) for the common SELL slice widths -- straight-line code in which every index / value
-// load of the slice issues before the dependent gathers -- and f(Wn<0>{}) (a runtime-width loop)
-// otherwise.  w must be wave-uniform.
+// load of the slice issues before the dependent gathers (widths 6-14: merged periodic-master
+// rows are wider than the 7-entry stencil rows) -- and f(Wn<0>{}) (a runtime-width loop) otherwise.  w must be wave-uniform.
 template <class F>
 __device__ __forceinline__ void by_width(int w, F&& f) {
   switch (w) {
@@ -142,6 +146,10 @@ __device__ __forceinline__ void by_width(int w, F&& f) {
     case 8: f(Wn<8>{}); break;
     case 9: f(Wn<9>{}); break;
     case 10: f(Wn<10>{}); break;
+    case 11: f(Wn<11>{}); break;
+    case 12: f(Wn<12>{}); break;
+    case 13: f(Wn<13>{}); break;
+    case 14: f(Wn<14>{}); break;
     default: f(Wn<0>{}); break;
   }
 }

@@ -442,26 +442,31 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
 // A-orthonormal basis X of their recent solution directions; the initial guess is the A-orthogonal
 // projection of the new solution onto span X, x0 = sum_i <X_i, b> X_i.  X: m vectors at stride ld.
 constexpr int PROJ_MAX = 32;
+// Storage of the basis vectors: fp32.  The guess only has to start the CG close to the solution (its
+// relative residual is 1e-6 .. 1e-5 against the solve's rtol 1e-8), and rounding the A-orthonormal
+// directions to fp32 perturbs their A-inner products by ~1e-7, below that; the dots and the
+// combinations are formed in fp64.  Halves the two passes over the basis (2 m vector reads per solve).
+using ProjT = float;
 
 // basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X
 constexpr int PROJ_KEEP_MAX = 8;
 struct QMat {
   double q[PROJ_KEEP_MAX][PROJ_MAX];
 };
-__global__ __launch_bounds__(BS) void k_reseed(int64_t n, const double* __restrict__ X, int64_t ld, int m, QMat Q,
-                                               int kq, double* __restrict__ out) {
+__global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restrict__ X, int64_t ld, int m, QMat Q,
+                                               int kq, ProjT* __restrict__ out) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
     double acc[PROJ_KEEP_MAX];
 #pragma unroll
     for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] = 0.0;
     for (int j = 0; j < m; ++j) {
-      const double x = X[j * ld + r];
+      const double x = (double)X[j * ld + r];
 #pragma unroll
       for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] += Q.q[i][j] * x;
     }
 #pragma unroll
     for (int i = 0; i < PROJ_KEEP_MAX; ++i)
-      if (i < kq) out[i * ld + r] = acc[i];
+      if (i < kq) out[i * ld + r] = (ProjT)acc[i];
   }
 }
 
@@ -472,7 +477,7 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const double* __restri
 // the M loads of a row are unconditional (all in flight together); grid-stride rows keep the
 // resident waves on one compact window of every vector.
 template <int M>
-__global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const double* __restrict__ X, int64_t ld,
+__global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
                                               const double* __restrict__ v, const int32_t* __restrict__ master_of,
                                               double* part) {
@@ -486,7 +491,7 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const double* __restric
     const double br = b[r], ar = av[r], vr = v[r];
     double x[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    for (int i = 0; i < M; ++i) x[i] = (double)X[i * ld + r];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       acc[i] += x[i] * br;
@@ -546,9 +551,9 @@ __global__ void k_pcoef(const double* __restrict__ D, int m, QMat Q, int kq, dou
 // pass 2: the new direction X_M = s (v - mu 1_free - sum_i c_i X_i) and the guess
 // x0 = sum_i a_i X_i + alpha X_M (written to y and x0), one pass over the M basis vectors
 template <int M>
-__global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const double* __restrict__ X, int64_t ld,
+__global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ K, const double* __restrict__ v,
-                                              const int32_t* __restrict__ master_of, double* __restrict__ xm_out,
+                                              const int32_t* __restrict__ master_of, ProjT* __restrict__ xm_out,
                                               double* __restrict__ y, double* __restrict__ x0) {
   double ka[M > 0 ? M : 1], kc[M > 0 ? M : 1];
 #pragma unroll
@@ -560,7 +565,7 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const double* __restric
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
     double x[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    for (int i = 0; i < M; ++i) x[i] = (double)X[i * ld + r];
     double sa = 0.0, sc = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -569,7 +574,7 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const double* __restric
     }
     const double xm = s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
     const double g = sa + alpha * xm;
-    stnt(xm_out + r, xm);
+    stnt(xm_out + r, (ProjT)xm);
     stnt(y + r, g);
     stnt(x0 + r, g);
   }
