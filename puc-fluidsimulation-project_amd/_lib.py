@@ -100,6 +100,13 @@ _lib = None
 
 
 def lib_path():
+    # PUCFEM_LIB_VARIANT=v loads libpucfem.v.so from the same directory (A/B builds of the measurement
+    # tools; the default is the library __graft_entry__.build() makes)
+    v = os.environ.get("PUCFEM_LIB_VARIANT")
+    if v:
+        if os.path.basename(v) != v:
+            raise PucfemError(-1, "PUCFEM_LIB_VARIANT is a bare variant name")
+        return os.path.join(HERE, f"libpucfem.{v}.so")
     return os.path.join(HERE, LIBNAME)
 
 

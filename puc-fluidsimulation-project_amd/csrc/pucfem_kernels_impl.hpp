@@ -300,6 +300,12 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
   }
 }
 
+#ifndef PUCFEM_DIR_K1
+#define PUCFEM_DIR_K1 2
+#endif
+#ifndef PUCFEM_DIR_K2
+#define PUCFEM_DIR_K2 1
+#endif
 template <int NR, int WMAX, bool NT, bool C16>
 __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
@@ -342,7 +348,7 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // groups of K rows per thread, every load of the group first (face_rows_k)
-    constexpr int K = NR == 1 ? 2 : 1;
+    constexpr int K = NR == 1 ? PUCFEM_DIR_K1 : PUCFEM_DIR_K2;
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
