@@ -97,6 +97,10 @@ typedef struct pucfem_params {
                           convection + diffusion, the periodic penalty restated as its exact merged limit,
                           BiCGStab); single rank */
   double dye_diffusivity; /* D of the implicit variant (good_visualization.py:404: 1e-3) */
+  int32_t assembly;    /* 0 = auto: on a context bound to a device, the node-triangle incidence, the stiffness
+                          pattern and the K / Gx / Gy / lumped-mass values of every level (buildStiffnessMatrix,
+                          buildLumpedMassMatrix and the divergence / gradient coefficients, StokesColor.py:98-128,
+                          130-284) are assembled on the device, bit-identical to the host assembly; 1 = host C++ */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */
@@ -134,7 +138,9 @@ enum pucfem_op {
   PUCFEM_OP_DIV = 5,    /* calculate_divergence (StokesColor.py:130-165): x = u (N,2), y = div (N) */
   PUCFEM_OP_GRAD = 6,   /* calculate_gradiant  (StokesColor.py:224-263): x = p (N), y = (N,2) */
   PUCFEM_OP_LIT = 7,    /* literal heat operator I + DT*A (heatEq.py:305) or Poisson A (poisson.py:253-278) */
-  PUCFEM_OP_MCONS = 8   /* consistent mass of the implicit dye variant (StokesColor.py:286-312; host CSR only) */
+  PUCFEM_OP_MCONS = 8,  /* consistent mass of the implicit dye variant (StokesColor.py:286-312; host CSR only) */
+  PUCFEM_OP_MLUMP = 9,  /* lumped mass M (StokesColor.py:266-284) as a diagonal (host CSR only) */
+  PUCFEM_OP_ASUM = 10   /* area_sum of calculate_divergence (StokesColor.py:151-163) as a diagonal (host CSR only) */
 };
 
 /* ---- library / context ---------------------------------------------------------- */

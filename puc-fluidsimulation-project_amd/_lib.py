@@ -17,7 +17,7 @@ LIBNAME = "libpucfem.so"
 # enums (pucfem.h)
 STOKES_COLOR, STOKES_FOOD, HEAT, POISSON = 0, 1, 2, 3
 F_U, F_USTAR, F_P, F_P2, F_DIV_STAR, F_DIV_U, F_FINAL_DIV, F_C, F_SCALAR, F_TRACERS, F_STATUS = range(11)
-OP_K, OP_VISC, OP_PRES, OP_GX, OP_GY, OP_DIV, OP_GRAD, OP_LIT, OP_MCONS = range(9)
+OP_K, OP_VISC, OP_PRES, OP_GX, OP_GY, OP_DIV, OP_GRAD, OP_LIT, OP_MCONS, OP_MLUMP, OP_ASUM = range(11)
 HOST_ONLY = -1
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOCONV", -4: "ESTATE", -5: "ENCCL", -6: "ENOMEM", -7: "ENODEV"}
 
@@ -39,7 +39,7 @@ class Params(ct.Structure):
         ("mg_single", ct.c_int32), ("mg_rep_nodes", ct.c_int64), ("mg_f32_vals", ct.c_int32),
         ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("proj_k_visc", ct.c_int32), ("mg_kind", ct.c_int32),
         ("solver_path", ct.c_int32), ("assembled", ct.c_int32), ("dye_scheme", ct.c_int32),
-        ("dye_diffusivity", ct.c_double),
+        ("dye_diffusivity", ct.c_double), ("assembly", ct.c_int32),
     ]
 
 

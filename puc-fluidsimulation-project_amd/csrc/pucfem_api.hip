@@ -488,6 +488,8 @@ struct Ctx {
       D.wrap = (int32_t)nloc;
     }
   }
+  // operator assembly on the device (prm.assembly 0 on a context bound to a device)
+  bool dev_asm() const { return !host_only && prm.assembly == 0; }
   void need_dev() const {
     if (host_only) throw Error(PUCFEM_ENODEV, "compute call on a host-only context");
   }
@@ -1552,6 +1554,8 @@ struct SetupClock {
   }
 };
 
+void assemble_device(Ctx& c, const HostMesh& m, const Ordering& ord, Csr& P, Assembly& A);
+
 void build_mg_host(Ctx& c, SetupClock& clk) {
   const int Lv = c.mg_levels;
   c.mg.clear();
@@ -1573,11 +1577,15 @@ void build_mg_host(Ctx& c, SetupClock& clk) {
     MgLevel& L = c.mg[l];
     if (c.lattice) lattice_ordering(L.mesh, c.macro, l, L.ord, L.latl);
     else make_ordering_cuts(L.mesh, c.ord.cuts, L.ord);
-    Incidence inc;
-    build_incidence(L.mesh, L.ord, inc);
-    build_pattern(L.mesh, L.ord, L.P, &inc);
     Assembly A;
-    assemble_stokes(L.mesh, L.ord, L.P, A, &inc);
+    if (c.dev_asm()) {
+      assemble_device(c, L.mesh, L.ord, L.P, A);
+    } else {
+      Incidence inc;
+      build_incidence(L.mesh, L.ord, inc);
+      build_pattern(L.mesh, L.ord, L.P, &inc);
+      assemble_stokes(L.mesh, L.ord, L.P, A, &inc);
+    }
     L.pairs = level_pairs(L.mesh, 1.0, 1e-6, 1.0);
     const i64 n = L.mesh.N;
     L.dof.resize(n);
@@ -1656,6 +1664,88 @@ T* upload_as(Ctx& c, const std::vector<double>& v) {
     std::vector<T> w(v.begin(), v.end());
     return c.upload(w);
   }
+}
+
+// ------------------------------------------------------------------ device assembly
+// Scratch device buffer of one setup phase (freed on scope exit, not kept with the context).
+template <class T>
+struct DevTmp {
+  T* p = nullptr;
+  explicit DevTmp(i64 n, hipStream_t st) {
+    HIPCHK(hipMalloc(&p, sizeof(T) * (size_t)std::max<i64>(1, n)));
+    HIPCHK(hipMemsetAsync(p, 0, sizeof(T) * (size_t)std::max<i64>(1, n), st));
+  }
+  DevTmp(const std::vector<T>& v, hipStream_t st) : DevTmp((i64)v.size(), st) {
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
+  }
+  ~DevTmp() { (void)hipFree(p); }
+  DevTmp(const DevTmp&) = delete;
+  DevTmp& operator=(const DevTmp&) = delete;
+  void get(std::vector<T>& v, i64 n, hipStream_t st) const {
+    v.resize((size_t)n);
+    if (n > 0) HIPCHK(hipMemcpyAsync(v.data(), p, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost, st));
+  }
+};
+
+// The stiffness pattern P and the K / Gx / Gy / lumped-mass / area-sum values of a mesh assembled on the
+// device (pucfem_kernels_impl.hpp k_inc_* / k_pat_* / k_asm): the same arrays pucfem_host.cpp's
+// build_incidence + build_pattern + assemble_stokes produce, bit for bit (tests/test_gpu_assembly.py).
+// Only the two prefix sums (row counts -> offsets) run on the host.
+void assemble_device(Ctx& c, const HostMesh& m, const Ordering& ord, Csr& P, Assembly& A) {
+  hipStream_t st = c.st;
+  const i64 N = m.N, T = m.T;
+  const int nb = (int)std::min<i64>(16384, std::max<i64>(1, (3 * T + BS - 1) / BS));
+  const int nbr = (int)std::min<i64>(16384, std::max<i64>(1, (N + BS - 1) / BS));
+  DevTmp<i32> dtri(m.tri, st), dold2new(ord.old2new, st);
+  DevTmp<double> dx(m.x, st), dy(m.y, st);
+  // incidence
+  DevTmp<i32> cnt(N, st);
+  hipLaunchKernelGGL(k_inc_count, dim3(nb), dim3(BS), 0, st, 3 * T, (const i32*)dtri.p, (const i32*)dold2new.p, cnt.p);
+  KCHK();
+  std::vector<i32> hc;
+  cnt.get(hc, N, st);
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<i64> ptr(N + 1, 0);
+  for (i64 i = 0; i < N; ++i) ptr[i + 1] = ptr[i] + hc[i];
+  DevTmp<i64> dptr(ptr, st);
+  DevTmp<i32> cur(N, st), itri(ptr[N], st), err(1, st);
+  hipLaunchKernelGGL(k_inc_fill, dim3(nb), dim3(BS), 0, st, 3 * T, (const i32*)dtri.p, (const i32*)dold2new.p,
+                     (const i64*)dptr.p, cur.p, itri.p);
+  KCHK();
+  hipLaunchKernelGGL(k_inc_sort, dim3(nbr), dim3(BS), 0, st, N, (const i64*)dptr.p, itri.p, err.p);
+  KCHK();
+  // pattern
+  hipLaunchKernelGGL(k_pat_count, dim3(nbr), dim3(BS), 0, st, N, (const i64*)dptr.p, (const i32*)itri.p,
+                     (const i32*)dtri.p, (const i32*)dold2new.p, cnt.p);
+  KCHK();
+  int herr = 0;
+  HIPCHK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  cnt.get(hc, N, st);
+  HIPCHK(hipStreamSynchronize(st));
+  require(herr == 0, "device assembly: a node has more than 32 incident triangles (use assembly = 1)");
+  P.nrows = N;
+  P.rowptr.assign(N + 1, 0);
+  for (i64 i = 0; i < N; ++i) P.rowptr[i + 1] = P.rowptr[i] + hc[i];
+  const i64 nnz = P.rowptr[N];
+  DevTmp<i64> drow(P.rowptr, st);
+  DevTmp<i32> dcol(nnz, st);
+  hipLaunchKernelGGL(k_pat_fill, dim3(nbr), dim3(BS), 0, st, N, (const i64*)dptr.p, (const i32*)itri.p,
+                     (const i32*)dtri.p, (const i32*)dold2new.p, (const i64*)drow.p, dcol.p);
+  KCHK();
+  // values
+  DevTmp<double> K(nnz, st), Gx(nnz, st), Gy(nnz, st), M(N, st), as(N, st);
+  hipLaunchKernelGGL(k_asm, dim3(nbr), dim3(BS), 0, st, N, (const i64*)dptr.p, (const i32*)itri.p, (const i32*)dtri.p,
+                     (const i32*)dold2new.p, (const double*)dx.p, (const double*)dy.p, (const i64*)drow.p,
+                     (const i32*)dcol.p, K.p, Gx.p, Gy.p, M.p, as.p);
+  KCHK();
+  dcol.get(P.col, nnz, st);
+  P.val.clear();
+  K.get(A.K, nnz, st);
+  Gx.get(A.Gx, nnz, st);
+  Gy.get(A.Gy, nnz, st);
+  M.get(A.M, N, st);
+  as.get(A.asum, N, st);
+  HIPCHK(hipStreamSynchronize(st));
 }
 
 // device values and work vectors of every multigrid level in the V-cycle's type T.
@@ -1741,12 +1831,16 @@ void build(Ctx& c) {
     make_ordering(m, prm.nstrips, c.ord);
   }
   clk.mark("ordering");
-  Incidence inc;
-  build_incidence(m, c.ord, inc);
-  build_pattern(m, c.ord, c.P, &inc);
-  clk.mark("pattern");
-  assemble_stokes(m, c.ord, c.P, c.as, &inc);
-  inc = Incidence();
+  if (c.dev_asm()) {
+    assemble_device(c, m, c.ord, c.P, c.as);
+    clk.mark("pattern + assembly (device)");
+  } else {
+    Incidence inc;
+    build_incidence(m, c.ord, inc);
+    build_pattern(m, c.ord, c.P, &inc);
+    clk.mark("pattern");
+    assemble_stokes(m, c.ord, c.P, c.as, &inc);
+  }
   const i64 N = m.N;
 
   // periodic pressure merge maps (internal numbering)
@@ -3388,6 +3482,23 @@ int pucfem_host_get_csr(void* ctx, int32_t op, int64_t* n_rows, int64_t* nnz, in
           ++k;
         }
         rowptr[o + 1] = k;
+      }
+      return;
+    }
+    if (op == PUCFEM_OP_MLUMP || op == PUCFEM_OP_ASUM) {  // diagonals, owned rows in caller numbering
+      const std::vector<double>& d = op == PUCFEM_OP_MLUMP ? c.as.M : c.as.asum;
+      require(!d.empty(), "operator not built for this scheme");
+      std::vector<i64> rows;
+      for (i64 g = c.lp.r0; g < c.lp.r1; ++g) rows.push_back(c.ord.new2old[g]);
+      std::sort(rows.begin(), rows.end());
+      *n_rows = (i64)rows.size();
+      *nnz = (i64)rows.size();
+      if (!col) return;
+      rowptr[0] = 0;
+      for (size_t r = 0; r < rows.size(); ++r) {
+        col[r] = rows[r];
+        val[r] = d[c.ord.old2new[rows[r]]];
+        rowptr[r + 1] = (i64)r + 1;
       }
       return;
     }

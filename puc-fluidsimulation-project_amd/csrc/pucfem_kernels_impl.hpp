@@ -1694,6 +1694,123 @@ __global__ void k_scatter_ghosts(int64_t ng, const int32_t* __restrict__ ghost_g
     full[ghost_global[k]] = v[k];
 }
 
+// ----------------------------------------------------------------------------- device assembly
+// buildStiffnessMatrix / buildLumpedMassMatrix / the lumped divergence and gradient coefficients
+// (StokesColor.py:98-128, 130-284) on the device, row-parallel.  Every row gathers
+// its incident triangles in ascending triangle order -- the order in which the reference's scatter
+// loops add to each entry -- with pucfem_host.cpp assemble_stokes's arithmetic (no contraction), so
+// the values are the host assembly's (and the sequential scatter's) bit for bit.
+constexpr int ASM_MAXDEG = 32;  // incident triangles per node (red refinement keeps the coarse degrees)
+
+// node -> number of incident triangles (internal node ids)
+__global__ void k_inc_count(int64_t n3, const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new,
+                            int32_t* cnt) {
+  for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < n3; q += (int64_t)gridDim.x * BS)
+    atomicAdd(cnt + old2new[tri[q]], 1);
+}
+// node -> incident triangles (any order; k_inc_sort orders them)
+__global__ void k_inc_fill(int64_t n3, const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new,
+                           const int64_t* __restrict__ ptr, int32_t* cur, int32_t* __restrict__ itri) {
+  for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < n3; q += (int64_t)gridDim.x * BS) {
+    const int32_t v = old2new[tri[q]];
+    itri[ptr[v] + atomicAdd(cur + v, 1)] = (int32_t)(q / 3);
+  }
+}
+// ascending triangle ids per node (insertion sort of the node's short list); err[0] = 1 when a node has
+// more than ASM_MAXDEG triangles
+__global__ void k_inc_sort(int64_t n, const int64_t* __restrict__ ptr, int32_t* __restrict__ itri, int* err) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    const int64_t b = ptr[r], e = ptr[r + 1];
+    if (e - b > ASM_MAXDEG) err[0] = 1;
+    for (int64_t k = b + 1; k < e; ++k) {
+      const int32_t t = itri[k];
+      int64_t m = k;
+      while (m > b && itri[m - 1] > t) {
+        itri[m] = itri[m - 1];
+        --m;
+      }
+      itri[m] = t;
+    }
+  }
+}
+// the sorted distinct vertices (internal ids) of row r's incident triangles; an isolated node keeps
+// a diagonal entry (build_pattern)
+__device__ __forceinline__ int asm_row_cols(int64_t r, const int64_t* __restrict__ ptr, const int32_t* __restrict__ itri,
+                                            const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new,
+                                            int32_t (&c)[3 * ASM_MAXDEG]) {
+  int len = 0;
+  const int64_t b = ptr[r], e = min(ptr[r + 1], b + ASM_MAXDEG);
+  for (int64_t q = b; q < e; ++q) {
+    const int64_t t = itri[q];
+    for (int j = 0; j < 3; ++j) {
+      const int32_t v = old2new[tri[3 * t + j]];
+      int m = len;
+      while (m > 0 && c[m - 1] > v) --m;
+      if (m > 0 && c[m - 1] == v) continue;
+      for (int k = len; k > m; --k) c[k] = c[k - 1];
+      c[m] = v;
+      ++len;
+    }
+  }
+  if (len == 0) c[len++] = (int32_t)r;
+  return len;
+}
+__global__ void k_pat_count(int64_t n, const int64_t* __restrict__ ptr, const int32_t* __restrict__ itri,
+                            const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new, int32_t* __restrict__ cnt) {
+  int32_t c[3 * ASM_MAXDEG];
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS)
+    cnt[r] = asm_row_cols(r, ptr, itri, tri, old2new, c);
+}
+__global__ void k_pat_fill(int64_t n, const int64_t* __restrict__ ptr, const int32_t* __restrict__ itri,
+                           const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new,
+                           const int64_t* __restrict__ rowptr, int32_t* __restrict__ col) {
+  int32_t c[3 * ASM_MAXDEG];
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    const int len = asm_row_cols(r, ptr, itri, tri, old2new, c);
+    for (int k = 0; k < len; ++k) col[rowptr[r] + k] = c[k];
+  }
+}
+// values of row r on the pattern (K, Gx, Gy, lumped mass M, area_sum), assemble_stokes's loop
+__global__ void k_asm(int64_t n, const int64_t* __restrict__ ptr, const int32_t* __restrict__ itri,
+                      const int32_t* __restrict__ tri, const int32_t* __restrict__ old2new, const double* __restrict__ x,
+                      const double* __restrict__ y, const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                      double* __restrict__ K, double* __restrict__ Gx, double* __restrict__ Gy, double* __restrict__ M,
+                      double* __restrict__ asum) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    const int64_t b = rowptr[r], e = rowptr[r + 1];
+    double m = 0.0, as = 0.0;
+    for (int64_t q = ptr[r]; q < ptr[r + 1]; ++q) {
+      const int64_t t = itri[q];
+      const int32_t o[3] = {tri[3 * t], tri[3 * t + 1], tri[3 * t + 2]};
+      const int32_t nn[3] = {old2new[o[0]], old2new[o[1]], old2new[o[2]]};
+      const double x1 = x[o[0]], y1 = y[o[0]], x2 = x[o[1]], y2 = y[o[1]], x3 = x[o[2]], y3 = y[o[2]];
+      const double det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2);  // StokesColor.py:277-283
+      const double area = 0.5 * fabs(det);
+      for (int i = 0; i < 3; ++i)
+        if (nn[i] == r) m += area / 3.0;
+      if (fabs(det) < 1e-14) continue;  // StokesColor.py:113, :146, :239
+      const double yd[3] = {y2 - y3, y3 - y1, y1 - y2};
+      const double xd[3] = {x3 - x2, x1 - x3, x2 - x1};
+      const double den = 2 * fabs(det);
+      const double inv2A = 1.0 / det;  // StokesColor.py:149 / :241
+      const double a3 = area / 3.0;
+      for (int i = 0; i < 3; ++i) {
+        if (nn[i] != r) continue;
+        as += a3;
+        for (int j = 0; j < 3; ++j) {
+          int64_t k = b;
+          while (k < e && col[k] != nn[j]) ++k;
+          K[k] += (yd[i] * yd[j] + xd[i] * xd[j]) / den;  // StokesColor.py:120-126
+          Gx[k] += (yd[j] * inv2A) * a3;
+          Gy[k] += (xd[j] * inv2A) * a3;
+        }
+      }
+    }
+    M[r] = m;
+    asum[r] = as;
+  }
+}
+
 // ----------------------------------------------------------------------------- misc
 // 1-block reduction of nv partial arrays (sum or max) into out[0..nv): the consumers of a producer
 // kernel's partials read one scalar.  RB threads, each with RU independent loads in flight (the

@@ -77,6 +77,8 @@ class Tolerances:
     # diffusion variant of scripts/good_visualization.py:700-718, diffusivity dye_diffusivity; one rank)
     dye: str = "semilagrange"
     dye_diffusivity: float = 1e-3
+    # operator assembly: "auto" = on the device when the context has one (bit-identical to the host's), "host"
+    assembly: str = "auto"
 
     @classmethod
     def production(cls, **kw):
@@ -166,7 +168,8 @@ class Context:
                         idx32=int(not tol.index16), proj_k=tol.proj_k, proj_k_visc=tol.proj_k_visc,
                         mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path],
                         assembled={"auto": 0, "assembled": 1}[tol.operators],
-                        dye_scheme={"semilagrange": 0, "implicit": 1}[tol.dye], dye_diffusivity=tol.dye_diffusivity)
+                        dye_scheme={"semilagrange": 0, "implicit": 1}[tol.dye], dye_diffusivity=tol.dye_diffusivity,
+                        assembly={"auto": 0, "device": 0, "host": 1}[tol.assembly])
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 
