@@ -93,8 +93,11 @@ class Tolerances:
 
 
 # pressure CG tolerance of the measured configuration (bench.py); tests/test_gpu_production.py checks
-# that it keeps every step within 1e-6 of the oracle's exact solves
-PRODUCTION_RTOL_PRES = 1e-8
+# that it keeps every step within 1e-6 of the oracle's exact solves.  tools/rtol_probe.py (48 steps
+# on mesh_fine x3, worst deviation from the oracle along the trajectory, r2q):
+#   rtol_pres 1e-8: |u| 6.1e-10, |c| 1.1e-8;  1e-7: |u| 6.5e-9, |c| 6.6e-8;  1e-6: |u| 3.0e-8, |c| 5.4e-7
+# 1e-7 keeps a 15x margin to the 1e-6 bar and saves ~20 % of the pressure iterations.
+PRODUCTION_RTOL_PRES = 1e-7
 
 
 class Context:
