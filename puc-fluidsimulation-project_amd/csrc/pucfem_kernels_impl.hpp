@@ -182,7 +182,6 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
       const double r = b - acc[c];
       stnt(v.r[c] + row, r);
       if (r32) stnt(r32 + row, (float)r);
-      stnt(v.po[c] + row, 0.0);
       rr[c] += r * r;
       bb[c] += b * b;
     }
@@ -226,12 +225,6 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
       if (row >= 0) finish(row, acc);
     }
   }
-  // zero the ghost part of p_old (ghost r arrives by halo exchange)
-  for (int64_t g = A.n_own + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.n_own + n_ghost;
-       g += (int64_t)gridDim.x * BS) {
-#pragma unroll
-    for (int c = 0; c < NR; ++c) v.po[c][g] = 0.0;
-  }
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
     const double t = block_sum(rr[c], sh);
@@ -248,7 +241,8 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
 // does not evict the gathered vectors from L2 / MALL.
 template <int NR, int WMAX, bool NT, bool C16>
 __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __restrict__ val, const CgVecs<NR>& v,
-                                          const double (&beta)[NR], int64_t s, int lane, double (&pq)[NR]) {
+                                          const double (&beta)[NR], bool first, int64_t s, int lane,
+                                          double (&pq)[NR]) {
   const int64_t off = A.off[s];
   const int w = A.w[s];
   const int64_t row = sell_row(A, s, lane);
@@ -262,7 +256,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
       const double a = NT ? ldnt(val + e) : val[e];
       const int32_t j = sell_col<C16, NT>(A, e, base);
 #pragma unroll
-      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * v.po[c][j]);
+      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * (first ? 0.0 : v.po[c][j]));
     }
   };
   if constexpr (WMAX > 0) {
@@ -280,7 +274,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 #pragma unroll
         for (int k = 0; k < WN; ++k) {
 #pragma unroll
-          for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * v.po[c][cj[k]]);
+          for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * (first ? 0.0 : v.po[c][cj[k]]));
         }
       } else {
         generic();
@@ -292,7 +286,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
   if (row >= 0) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
-      const double p = v.r[c][row] + beta[c] * v.po[c][row];
+      const double p = v.r[c][row] + beta[c] * (first ? 0.0 : v.po[c][row]);
       stnt(v.pn[c] + row, p);
       stnt(v.q[c] + row, acc[c]);
       pq[c] += p * acc[c];
@@ -346,6 +340,9 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
   double pq[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) pq[c] = 0.0;
+  // the first iteration's direction is r itself: p_old is neither read nor needed (k_cg_init does not
+  // clear it; a uniform branch skips its loads)
+  const bool first = it == 0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // groups of K rows per thread, every load of the group first (face_rows_k)
     constexpr int K = NR == 1 ? PUCFEM_DIR_K1 : PUCFEM_DIR_K2;
@@ -366,11 +363,11 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
 #pragma unroll
         for (int c = 0; c < NR; ++c) {
           rv[r][c][6] = v.r[c][row];
-          pv[r][c][6] = v.po[c][row];
+          pv[r][c][6] = first ? 0.0 : v.po[c][row];
 #pragma unroll
           for (int k = 0; k < 6; ++k) {
             rv[r][c][k] = v.r[c][nb[r][k]];
-            pv[r][c][k] = v.po[c][nb[r][k]];
+            pv[r][c][k] = first ? 0.0 : v.po[c][nb[r][k]];
           }
         }
       }
@@ -397,12 +394,12 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
     int64_t s0, s1;
     block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
-    for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, s, lane, pq);
+    for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, first, s, lane, pq);
   }
   for (int64_t g = A.n_own + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.n_own + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
-    for (int c = 0; c < NR; ++c) v.pn[c][g] = v.r[c][g] + beta[c] * v.po[c][g];
+    for (int c = 0; c < NR; ++c) v.pn[c][g] = v.r[c][g] + beta[c] * (first ? 0.0 : v.po[c][g]);
   }
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
