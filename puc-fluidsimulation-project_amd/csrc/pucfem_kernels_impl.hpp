@@ -2215,34 +2215,55 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
   }
 }
 
-// y = T x (restriction) or y += T x (prolongation, add = 1).  Face part: prolongation rows are the
-// fine level's interior nodes (linear interpolation from the coarse lattice, fc.tab2 = the coarse
-// level's merged table); restriction rows the coarse level's interior nodes (the transpose: the
-// fine node on top with weight 1 and its six midpoint neighbours with 1/2, all fine interior nodes).
-template <typename T>
-__global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T* __restrict__ val,
-                                                 const T* __restrict__ x, T* __restrict__ y, int add, const int* ctl) {
-  if (ctl && ctl[0]) return;
+// Specialised on the direction (prolongation adds), so a row body is one basic block with every load of a
+// 4-row group first.  Prolongation: v = (x[pa] + x[pb]) / 2 with pa = pb at the coarse lattice points
+// (exact: (a + a) / 2 = a), so the four parity cases of (i, j) are one branch-free body instead of four
+// divergent ones.
+template <bool ADD, typename T>
+__device__ __forceinline__ void transfer_body(const SellDev& M, const FaceDev& fc, const T* __restrict__ val,
+                                              const T* __restrict__ x, T* __restrict__ y) {
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     const int32_t n2 = fc.n2;
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+    constexpr int K = 4;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
       const lat::FaceTab G = fc.tab2[lf];
-      const int64_t row = F.base + t;
-      if (add) {
-        const int32_t i0 = i >> 1, i1 = (i + 1) >> 1, j0 = j >> 1, j1 = (j + 1) >> 1;
-        T v;
-        if (!(i & 1) && !(j & 1)) v = x[lat::point(G, n2, i0, j0)];
-        else if (!(j & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i1, j0)]);
-        else if (!(i & 1)) v = (T)0.5 * (x[lat::point(G, n2, i0, j0)] + x[lat::point(G, n2, i0, j1)]);
-        else v = (T)0.5 * (x[lat::point(G, n2, i0, j1)] + x[lat::point(G, n2, i1, j0)]);
-        stnt(y + row, y[row] + v);
+      if constexpr (ADD) {
+        T xa[K], xb[K], yr[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          const int32_t i0 = i[r] >> 1, i1 = (i[r] + 1) >> 1, j0 = j[r] >> 1, j1 = (j[r] + 1) >> 1;
+          const bool ie = !(i[r] & 1), je = !(j[r] & 1);
+          // even/even: the coarse point; even j: along i; even i: along j; odd/odd: the diagonal
+          const int32_t pa = lat::point(G, n2, i0, (ie || je) ? j0 : j1);
+          const int32_t pb = lat::point(G, n2, ie ? i0 : i1, je ? j0 : (ie ? j1 : j0));
+          xa[r] = x[pa];
+          xb[r] = x[pb];
+          yr[r] = y[F.base + t[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < K; ++r)
+          if (ok[r]) stnt(y + F.base + t[r], yr[r] + (T)0.5 * (xa[r] + xb[r]));
       } else {
-        const int32_t I = 2 * i, J = 2 * j;
-        const T c = x[lat::point(G, n2, I, J)];
-        const T h = x[lat::point(G, n2, I - 1, J)] + x[lat::point(G, n2, I + 1, J)] + x[lat::point(G, n2, I, J - 1)] +
-                    x[lat::point(G, n2, I, J + 1)] + x[lat::point(G, n2, I + 1, J - 1)] +
-                    x[lat::point(G, n2, I - 1, J + 1)];
-        stnt(y + row, c + (T)0.5 * h);
+        T v[K][7];
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          const int32_t I = 2 * i[r], J = 2 * j[r];
+          v[r][0] = x[lat::point(G, n2, I, J)];
+          v[r][1] = x[lat::point(G, n2, I - 1, J)];
+          v[r][2] = x[lat::point(G, n2, I + 1, J)];
+          v[r][3] = x[lat::point(G, n2, I, J - 1)];
+          v[r][4] = x[lat::point(G, n2, I, J + 1)];
+          v[r][5] = x[lat::point(G, n2, I + 1, J - 1)];
+          v[r][6] = x[lat::point(G, n2, I - 1, J + 1)];
+        }
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          if (!ok[r]) continue;
+          const T h = v[r][1] + v[r][2] + v[r][3] + v[r][4] + v[r][5] + v[r][6];
+          stnt(y + F.base + t[r], v[r][0] + (T)0.5 * h);
+        }
       }
     });
     return;
@@ -2254,13 +2275,26 @@ __global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T*
     const int64_t off = M.off[s];
     const int w = M.w[s];
     const int64_t row = sell_row(M, s, lane);
+    const T yr = ADD && row >= 0 ? y[row] : (T)0;
     T acc = 0;
     for (int k = 0; k < w; ++k) {
       const int64_t e = off + (int64_t)k * 64 + lane;
       acc += val[e] * x[M.col[e]];
     }
-    if (row >= 0) stnt(y + row, add ? y[row] + acc : acc);
+    if (row >= 0) stnt(y + row, ADD ? yr + acc : acc);
   }
+}
+
+// y = T x (restriction) or y += T x (prolongation, add = 1).  Face part: prolongation rows are the
+// fine level's interior nodes (linear interpolation from the coarse lattice, fc.tab2 = the coarse
+// level's merged table); restriction rows the coarse level's interior nodes (the transpose: the
+// fine node on top with weight 1 and its six midpoint neighbours with 1/2, all fine interior nodes).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T* __restrict__ val,
+                                                 const T* __restrict__ x, T* __restrict__ y, int add, const int* ctl) {
+  if (ctl && ctl[0]) return;
+  if (add) transfer_body<true>(M, fc, val, x, y);
+  else transfer_body<false>(M, fc, val, x, y);
 }
 
 // coarse solve: y = Ainv x (dense, n x n row-major fp64, replicated); one wave per row
