@@ -674,6 +674,8 @@ struct Ctx {
       if (h_ctl[0] != 1) throw Error(PUCFEM_ENOCONV, "CG did not converge within maxit=" + std::to_string(maxit));
       return h_ctl[1];
     }
+    // multi-kernel Jacobi-scaled CG with the direction updated in place (k_cgr_*): an iteration is
+    // the SpMV with its three dots, the update (y, r, p) with the exact <r, r>, and the control test
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
     CgVecs<NR> v;
@@ -681,50 +683,54 @@ struct Ctx {
       v.y[c] = y[c];
       v.b[c] = b[c];
       v.r[c] = cg_r[c];
-      v.po[c] = cg_pa[c];
+      v.po[c] = cg_pa[c];  // the direction p
       v.pn[c] = cg_pb[c];
       v.q[c] = cg_q[c];
     }
+    auto halo_p = [&]() {
+      if (NR == 2) halo(cg_pa[0], cg_pa[1]);
+      else halo(cg_pa[0]);
+    };
     if (NR == 2) halo(y[0], y[1]);
     else halo(y[0]);
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
     with_c16(A, [&](auto c16) {
       hipLaunchKernelGGL((k_cg_init<NR, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), fc, val, v,
-                         lp.n_ghost, part_a, part_b);
+                         lp.n_ghost, part_a, part_b, (float*)nullptr, 1);
     });
     KCHK();
     Red rr = reduce_global(part_a, nb, NR, false, 0);
     Red bb = reduce_global(part_b, nb, NR, false, 1);
-    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
-    if (NR == 2) halo(cg_r[0], cg_r[1]);
-    else halo(cg_r[0]);
     const double tol2 = tol * tol;
+    hipLaunchKernelGGL(k_cgr_ctl, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, maxit, NR);
+    KCHK();
+    halo_p();
+    // algorithmic bytes: dir gathers p once per row and reads r, writes q; upd reads y, p, r, q and
+    // writes y, r, p
     const double bytes_dir =
-        (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 32.0 * NR * (double)A.own();
-    const double bytes_upd = 48.0 * NR * (double)A.own();
+        (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 24.0 * NR * (double)A.own();
+    const double bytes_upd = 56.0 * NR * (double)A.own();
     int it = 0;
-    // host convergence checks: the first after as many iterations as the last solve took (k_conv
-    // after each update lets the check see convergence without a further direction launch)
+    // host convergence checks: the first after as many iterations as the last solve took (the control
+    // test after each update lets the check see convergence without a further launch)
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
     for (;;) {
       for (int k = 0; k < chunk; ++k, ++it) {
         // HIP-event timing samples every 8th iteration (bounded event count for long solves)
         const bool samp = (it & 7) == 0;
         with_c16(A, [&](auto c16) {
-          klaunch(samp ? 1 : -1, bytes_dir, k_cg_dir<NR, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(),
-                  fc, val, v, lp.n_ghost, rr.p, rr.nb, rr.stride, bb.p, bb.nb, bb.stride, scal, ctl, it, maxit, tol2,
-                  part_c, (const double*)nullptr, 0, 0);
+          klaunch(samp ? 1 : -1, bytes_dir, k_cgr_dir<NR, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(), fc,
+                  val, v, (const int*)ctl, part_c);
         });
         KCHK();
-        Red pq = reduce_global(part_c, nb, NR, false, 2);
-        klaunch(samp ? 2 : -1, bytes_upd, k_cg_upd<NR>, dim3(nb_rows(A.own())), dim3(BS), v, A.own(), pq.p, pq.nb,
-                pq.stride, (const double*)scal, (const int*)ctl, part_a, (float*)nullptr);
+        Red dots = reduce_global(part_c, nb, 3 * NR, false, 2);
+        klaunch(samp ? 2 : -1, bytes_upd, k_cgr_upd<NR>, dim3(nb_rows(A.own())), dim3(BS), v, A.own(),
+                (const double*)dots.p, (const double*)rr.p, (const int*)ctl, part_a);
         KCHK();
         rr = reduce_global(part_a, nb_rows(A.own()), NR, false, 0);
-        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, NR);
+        hipLaunchKernelGGL(k_cgr_ctl, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, maxit, NR);
         KCHK();
-        if (NR == 2) halo(cg_r[0], cg_r[1]);
-        else halo(cg_r[0]);
-        for (int c = 0; c < NR; ++c) std::swap(v.po[c], v.pn[c]);
+        halo_p();
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -2350,7 +2356,8 @@ void build(Ctx& c) {
     c.cg_pb[q] = c.dalloc<double>(c.nloc);
     c.cg_q[q] = c.dalloc<double>(c.nloc);
   }
-  for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(4 * MAXB);
+  // 6 MAXB: the recurrence CG direction kernel writes 3 dots per right-hand side
+  for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(6 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
   c.part_u = c.dalloc<double>(2 * MAXB);
   c.yr_own = c.dalloc<double>(2);

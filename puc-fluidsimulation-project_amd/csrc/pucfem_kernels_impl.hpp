@@ -110,6 +110,12 @@ __device__ __forceinline__ void face_grad(const double* c, const int32_t (&nb)[6
   gx = c[lat::C_G1X] * d1 + c[lat::C_G2X] * d2 + c[lat::C_G3X] * d3;
   gy = c[lat::C_G1Y] * d1 + c[lat::C_G2Y] * d2 + c[lat::C_G3Y] * d3;
 }
+// the same from the six neighbour values v[k] = x[nb[k]] (loaded beforehand)
+__device__ __forceinline__ void face_grad_v(const double* c, const double (&v)[6], double& gx, double& gy) {
+  const double d1 = v[1] - v[0], d2 = v[2] - v[3], d3 = v[4] - v[5];
+  gx = c[lat::C_G1X] * d1 + c[lat::C_G2X] * d2 + c[lat::C_G3X] * d3;
+  gy = c[lat::C_G1Y] * d1 + c[lat::C_G2Y] * d2 + c[lat::C_G3Y] * d3;
+}
 
 // ----------------------------------------------------------------------------- SpMV
 // y = A x over owned rows (generic; unit `pucfem_apply`, residuals).
@@ -167,10 +173,11 @@ struct CgVecs {
 
 // r32 (optional): fp32 copy of r for the mixed-precision V-cycle, whose right-hand side is only
 // ever used in fp32 (bit-identical to converting inside the cycle, at half the bytes per read)
+// write_p: also p = r into v.po (the first direction of k_cgr_dir / k_cgr_upd)
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                 int64_t n_ghost, double* part_rr, double* part_bb,
-                                                float* __restrict__ r32 = nullptr) {
+                                                float* __restrict__ r32 = nullptr, int write_p = 0) {
   __shared__ double sh[4];
   double rr[NR], bb[NR];
 #pragma unroll
@@ -182,6 +189,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
       const double r = b - acc[c];
       stnt(v.r[c] + row, r);
       if (r32) stnt(r32 + row, (float)r);
+      if (write_p) stnt(v.po[c] + row, r);
       rr[c] += r * r;
       bb[c] += b * b;
     }
@@ -587,6 +595,183 @@ __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) stnt(out + r, a[r] - b[r]);
 }
 
+// ----------------------------------------------------------------------------- CG, direction updated in place
+// Jacobi-scaled CG (no preconditioner: the viscous solve, the Jacobi pressure path) with the direction
+// formed in the update kernel instead of at the direction kernel's gathered columns: the SpMV then
+// gathers one vector per right-hand side (p) instead of two (r and p_old).  beta needs <r_new, r_new>
+// before r_new exists; it comes from the recurrence <r - a q, r - a q> = rr - 2 a <r, q> + a^2 <q, q>
+// with the direction kernel's dots (relative error ~ eps * rr / rr_new, ~1e-12 here); the convergence
+// test keeps the exact <r_new, r_new> of the update's partials, and so does the next alpha.
+//   dir: q = A^ p; partials <p, q>, <r, q>, <q, q>          (stride MAXB, [c], [NR + c], [2 NR + c])
+//   upd: a = rr / <p, q>; y += a p; r -= a q; p = r + b p; partial <r, r>
+template <int NR, bool C16>
+__global__ __launch_bounds__(BS) void k_cgr_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
+                                                const int* ctl, double* part) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  double pq[NR], rq[NR], qq[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) pq[c] = rq[c] = qq[c] = 0.0;
+  auto finish = [&](int c, double p, double r, double q, int64_t row) {
+    stnt(v.q[c] + row, q);
+    pq[c] += p * q;
+    rq[c] += r * q;
+    qq[c] += q * q;
+  };
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    constexpr int K = NR == 1 ? 4 : 2;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
+#pragma unroll
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      double a[K][7];
+#pragma unroll
+      for (int r = 0; r < K; ++r) face_kcoefs(fc, lf, nb[r], in[r], a[r]);
+      double pv[K][NR][7], rv[K][NR];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int64_t row = F.base + t[r];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          pv[r][c][6] = v.po[c][row];
+          rv[r][c] = v.r[c][row];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) pv[r][c][k] = v.po[c][nb[r][k]];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          double q = a[r][0] * pv[r][c][6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) q += a[r][1 + k] * pv[r][c][k];
+          finish(c, pv[r][c][6], rv[r][c], q, F.base + t[r]);
+        }
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t row = sell_row(A, s, lane);
+      const int64_t rr = row >= 0 ? row : 0;
+      double acc[NR], pr[NR], rr_[NR];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        pr[c] = v.po[c][rr];
+        rr_[c] = v.r[c][rr];
+      }
+      if constexpr (NR == 1) {
+        acc[0] = sell_row_dot_g<C16, double>(A, val, [&](int32_t j) { return v.po[0][j]; }, s, lane);
+      } else {
+        const int64_t off = A.off[s];
+        const int w = A.w[s];
+        const int32_t base = (int32_t)(s * 64);
+#pragma unroll
+        for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+        by_width(w, [&](auto wc) {
+          constexpr int WN = decltype(wc)::value;
+          if constexpr (WN > 0) {
+            int32_t cj[WN];
+            double av[WN];
+#pragma unroll
+            for (int k = 0; k < WN; ++k) {
+              const int64_t e = off + (int64_t)k * 64 + lane;
+              cj[k] = sell_col<C16>(A, e, base);
+              av[k] = ldnt(val + e);
+            }
+#pragma unroll
+            for (int k = 0; k < WN; ++k) {
+#pragma unroll
+              for (int c = 0; c < NR; ++c) acc[c] += av[k] * v.po[c][cj[k]];
+            }
+          } else {
+            for (int k = 0; k < w; ++k) {
+              const int64_t e = off + (int64_t)k * 64 + lane;
+              const double av = ldnt(val + e);
+              const int32_t j = sell_col<C16>(A, e, base);
+#pragma unroll
+              for (int c = 0; c < NR; ++c) acc[c] += av * v.po[c][j];
+            }
+          }
+        });
+      }
+      if (row >= 0) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c) finish(c, pr[c], rr_[c], acc[c], row);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t1 = block_sum(pq[c], sh);
+    const double t2 = block_sum(rq[c], sh);
+    const double t3 = block_sum(qq[c], sh);
+    if (threadIdx.x == 0) {
+      part[(int64_t)c * MAXB + blockIdx.x] = t1;
+      part[(int64_t)(NR + c) * MAXB + blockIdx.x] = t2;
+      part[(int64_t)(2 * NR + c) * MAXB + blockIdx.x] = t3;
+    }
+  }
+}
+
+// dots: the reduced [<p, q> (NR), <r, q> (NR), <q, q> (NR)]; rr: the reduced exact <r, r> (NR)
+template <int NR>
+__global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, const double* __restrict__ dots,
+                                                const double* __restrict__ rr, const int* ctl, double* part_rr) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  double alpha[NR], beta[NR], acc[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double r0 = rr[c], pq = dots[c], rq = dots[NR + c], qq = dots[2 * NR + c];
+    alpha[c] = r0 / pq;
+    const double r1 = r0 - 2.0 * alpha[c] * rq + alpha[c] * alpha[c] * qq;
+    beta[c] = r0 > 0.0 ? fmax(r1, 0.0) / r0 : 0.0;
+    acc[c] = 0.0;
+  }
+  int64_t r0, r1;
+  block_rows(nrows, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      const double p = v.po[c][i], q = v.q[c][i];
+      stnt(v.y[c] + i, v.y[c][i] + alpha[c] * p);
+      const double r = v.r[c][i] - alpha[c] * q;
+      stnt(v.r[c] + i, r);
+      stnt(v.po[c] + i, r + beta[c] * p);
+      acc[c] += r * r;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t = block_sum(acc[c], sh);
+    if (threadIdx.x == 0) part_rr[(int64_t)c * MAXB + blockIdx.x] = t;
+  }
+}
+
+// the recurrence CG's control after an update: converged (1), maxit (2), not finite (3); it = the
+// iterations done
+__global__ void k_cgr_ctl(const double* rr, const double* bb, double tol2, int* ctl, int it, int maxit, int nr) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[0] == 0) {
+    bool conv = true, bad = false;
+    for (int c = 0; c < nr; ++c) {
+      conv = conv && rr[c] <= tol2 * bb[c];
+      bad = bad || !isfinite(rr[c]);
+    }
+    if (conv || bad || it >= maxit) {
+      ctl[0] = conv ? 1 : (bad ? 3 : 2);
+      ctl[1] = it;
+    }
+  }
+}
+
 // CG convergence test right after the residual update: ctl = (1, it) when <r_c, r_c> <= tol2 <b_c, b_c>
 // for every right-hand side c < nr, so the host's check after an iteration sees it (and a V-cycle
 // or direction kernel launched after it returns at once).  k_cg_dir would find the same at
@@ -672,23 +857,40 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
   double mx = 0.0, sb = 0.0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
+    // groups of 2 rows per thread, the 24 gathered values of a group loaded first
+    constexpr int K = 2;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
       const double* c = fc.coef + lf * lat::NCOEF;
-      double ax, ay, bx, by;
-      face_grad(c, nb, ux, ax, ay);
-      face_grad(c, nb, uy, bx, by);
-      const int64_t row = F.base + t;
+      double vx[K][6], vy[K][6];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        int32_t nb[6];
+        bool in[6];
+        lat::neighbours(F, fc.n, t[r], i[r], j[r], nb, in);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          vx[r][k] = ux[nb[k]];
+          vy[r][k] = uy[nb[k]];
+        }
+      }
       const double as = c[lat::C_AS1];
-      const double d = (ax + by) / as;
-      stnt(div + row, d);
-      mx = fmax(mx, fabs(d));
-      if (braw) {
-        const double b = as * (negidt * d);
-        stnt(braw + row, b);
-        sb += b;
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        double ax, ay, bx, by;
+        face_grad_v(c, vx[r], ax, ay);
+        face_grad_v(c, vy[r], bx, by);
+        const int64_t row = F.base + t[r];
+        const double d = (ax + by) / as;
+        stnt(div + row, d);
+        mx = fmax(mx, fabs(d));
+        if (braw) {
+          const double b = as * (negidt * d);
+          stnt(braw + row, b);
+          sb += b;
+        }
       }
     });
   } else {
@@ -763,34 +965,44 @@ __global__ void k_pres_rhs(int64_t n, const double* __restrict__ braw, const int
   }
 }
 
-// projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
-// projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
-template <bool C16>
-__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const double* __restrict__ gx,
-                                                  const double* __restrict__ gy, const double* __restrict__ p,
-                                                  const double* __restrict__ as1, double dt, int mode,
-                                                  const uint8_t* __restrict__ dirflag, const double* usx,
-                                                  const double* usy, double* ux, double* uy) {
-  auto finish = [&](int64_t row, double gpx, double gpy, bool dirichlet) {
-    if (mode == 0) {
-      stnt(ux + row, usx[row] - dt * gpx);
-      stnt(uy + row, usy[row] - dt * gpy);
-    } else if (!dirichlet) {
-      stnt(ux + row, ux[row] - dt * gpx);
-      stnt(uy + row, uy[row] - dt * gpy);
-    }
-  };
+// Specialised on the mode, so each row body is one basic block: the row's u* (mode 0) or u (mode 1) loads
+// issue with the gathers (4-row groups on the face interiors).
+template <int MODE, bool C16>
+__device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& fc, const double* __restrict__ gx,
+                                               const double* __restrict__ gy, const double* __restrict__ p,
+                                               const double* __restrict__ as1, double dt,
+                                               const uint8_t* __restrict__ dirflag, const double* usx,
+                                               const double* usy, double* ux, double* uy) {
+  const double* bx = MODE == 0 ? usx : ux;
+  const double* by = MODE == 0 ? usy : uy;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows are never Dirichlet nodes
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
+    constexpr int K = 4;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
       const double* c = fc.coef + lf * lat::NCOEF;
-      double ax, ay;
-      face_grad(c, nb, p, ax, ay);
+      double v[K][6], ox[K], oy[K];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        int32_t nb[6];
+        bool in[6];
+        lat::neighbours(F, fc.n, t[r], i[r], j[r], nb, in);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v[r][k] = p[nb[k]];
+        ox[r] = bx[F.base + t[r]];
+        oy[r] = by[F.base + t[r]];
+      }
       const double d = c[lat::C_AS1];
-      finish(F.base + t, ax / d, ay / d, false);
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        double ax, ay;
+        face_grad_v(c, v[r], ax, ay);
+        const int64_t row = F.base + t[r];
+        stnt(ux + row, ox[r] - dt * (ax / d));
+        stnt(uy + row, oy[r] - dt * (ay / d));
+      }
     });
     return;
   }
@@ -802,6 +1014,9 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const d
     const int w = A.w[s];
     const int64_t row = sell_row(A, s, lane);
     const int32_t base = (int32_t)(s * 64);
+    const int64_t rr = row >= 0 ? row : 0;
+    const double ox = bx[rr], oy = by[rr], d = as1[rr];
+    const bool dirichlet = MODE == 1 && dirflag[rr] != 0;
     double ax = 0.0, ay = 0.0;
     by_width(w, [&](auto wc) {
       constexpr int WN = decltype(wc)::value;
@@ -830,11 +1045,23 @@ __global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const d
         }
       }
     });
-    if (row >= 0) {
-      const double d = as1[row];
-      finish(row, ax / d, ay / d, dirflag[row] != 0);
+    if (row >= 0 && !dirichlet) {
+      stnt(ux + row, ox - dt * (ax / d));
+      stnt(uy + row, oy - dt * (ay / d));
     }
   }
+}
+
+// projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
+// projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
+template <bool C16>
+__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const double* __restrict__ gx,
+                                                  const double* __restrict__ gy, const double* __restrict__ p,
+                                                  const double* __restrict__ as1, double dt, int mode,
+                                                  const uint8_t* __restrict__ dirflag, const double* usx,
+                                                  const double* usy, double* ux, double* uy) {
+  if (mode == 0) grad_proj_body<0, C16>(A, fc, gx, gy, p, as1, dt, dirflag, usx, usy, ux, uy);
+  else grad_proj_body<1, C16>(A, fc, gx, gy, p, as1, dt, dirflag, usx, usy, ux, uy);
 }
 
 // gradient only (calculate_gradiant, StokesColor.py:224-263) for the unit op
