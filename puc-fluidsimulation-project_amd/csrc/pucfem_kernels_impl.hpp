@@ -195,21 +195,40 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
     }
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
-      int32_t nb[6];
-      bool in[6];
-      lat::neighbours(F, fc.n, t, i, j, nb, in);
-      double a[7];
-      face_kcoefs(fc, lf, nb, in, a);
-      const int64_t row = F.base + t;
-      double acc[NR];
+    // groups of K rows per thread, every gathered value of a group loaded first (face_rows_k)
+    constexpr int K = NR == 1 ? 4 : 2;
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
 #pragma unroll
-      for (int c = 0; c < NR; ++c) {
-        acc[c] = a[0] * v.y[c][row];
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      double a[K][7];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) acc[c] += a[1 + k] * v.y[c][nb[k]];
+      for (int r = 0; r < K; ++r) face_kcoefs(fc, lf, nb[r], in[r], a[r]);
+      double yv[K][NR][7];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          yv[r][c][6] = v.y[c][F.base + t[r]];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) yv[r][c][k] = v.y[c][nb[r][k]];
+        }
       }
-      finish(row, acc);
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+        double acc[NR];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          acc[c] = a[r][0] * yv[r][c][6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) acc[c] += a[r][1 + k] * yv[r][c][k];
+        }
+        finish(F.base + t[r], acc);
+      }
     });
   } else {
     int64_t s0, s1;
