@@ -22,7 +22,12 @@ constexpr int BS = 256;     // threads per block
 constexpr int MAXB = 8192;  // max blocks of a partial-producing launch (= partial stride)
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
 constexpr int SLB = 4096;   // max blocks (= partial stride) of the semi-Lagrangian kernel
-constexpr int FACE_RPT = 4; // face-interior rows per thread of a lattice work item (BS * FACE_RPT rows of one face)
+#ifndef PUCFEM_FACE_RPT
+#define PUCFEM_FACE_RPT 4
+#endif
+constexpr int FACE_RPT = PUCFEM_FACE_RPT; // face-interior rows per thread of a lattice work item (BS * FACE_RPT rows of one face)
+// row-group size of a face kernel (face_rows_k): the kernel's choice, at most the rows per thread
+constexpr int face_k(int k) { return k < FACE_RPT ? k : FACE_RPT; }
 
 struct SellDev {
   const int64_t* off;  // nslices+1

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // groups of K rows per thread, every gathered value of a group loaded first (face_rows_k)
-    constexpr int K = NR == 1 ? 4 : 2;
+    constexpr int K = face_k(NR == 1 ? 4 : 2);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
   const bool first = it == 0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // groups of K rows per thread, every load of the group first (face_rows_k)
-    constexpr int K = NR == 1 ? PUCFEM_DIR_K1 : PUCFEM_DIR_K2;
+    constexpr int K = face_k(NR == 1 ? PUCFEM_DIR_K1 : PUCFEM_DIR_K2);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(BS) void k_cgr_dir(SellDev A, FaceDev fc, const dou
     qq[c] += q * q;
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    constexpr int K = NR == 1 ? 4 : 2;
+    constexpr int K = face_k(NR == 1 ? 4 : 2);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
     // groups of 2 rows per thread, the 24 gathered values of a group loaded first
-    constexpr int K = 2;
+    constexpr int K = face_k(2);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -996,7 +996,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
   const double* by = MODE == 0 ? usy : uy;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows are never Dirichlet nodes
-    constexpr int K = 4;
+    constexpr int K = face_k(4);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -2317,7 +2317,7 @@ __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, c
     if constexpr (RD) acc_rz += rrow * (double)xo;
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    constexpr int K = 4;
+    constexpr int K = face_k(4);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -2421,7 +2421,7 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
                                               T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    constexpr int K = 4;  // groups of K rows per thread, every load first (face_rows_k)
+    constexpr int K = face_k(4);  // groups of K rows per thread, every load first (face_rows_k)
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -2470,7 +2470,7 @@ __device__ __forceinline__ void transfer_body(const SellDev& M, const FaceDev& f
                                               const T* __restrict__ x, T* __restrict__ y) {
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     const int32_t n2 = fc.n2;
-    constexpr int K = 4;
+    constexpr int K = face_k(4);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
