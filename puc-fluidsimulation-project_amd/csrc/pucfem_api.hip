@@ -388,6 +388,10 @@ struct Ctx {
   Macro macro;
   LatticeLevel lat_fine;  // the finest level's layout until build_mg_host moves it into mg.back()
   HFace fK, fVisc, fP;  // finest level: K / Gx / Gy (plain table), scaled A_visc (plain), pressure (merged)
+  // Gershgorin radius of the Jacobi-scaled A_visc, max_i sum_{j != i} |a_ij| / sqrt(a_ii a_jj): its spectrum
+  // lies in [1 - visc_R, 1 + visc_R] (the Chebyshev viscous solve's interval)
+  double visc_R = 1.0;
+  int visc_solver = 0;  // 0 = Chebyshev iteration when visc_R < 0.25 (multi-kernel path), 1 = CG
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
   static FaceDev nof() { return FaceDev{}; }
 
@@ -745,6 +749,78 @@ struct Ctx {
     return h_ctl[1];
   }
 
+  // Chebyshev iteration for the Jacobi-scaled viscous system (k_vcheb): y (warm start, overwritten only
+  // through the double buffer) and b as for cg<NR>; the converged iterate is returned in out[] (y itself
+  // or the alternate buffer cg_pb).  Same stopping rule as the CG: <r, r> <= tol^2 <b, b>.
+  template <int NR>
+  int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
+            double tol, int maxit, int which, double* out[NR]) {
+    const FaceDev fc = hf.part();
+    const int nb = grid_part(fc, A);
+    double* xa[NR];
+    double* xb[NR];
+    for (int c = 0; c < NR; ++c) {
+      xa[c] = y[c];
+      xb[c] = cg_pb[c];
+    }
+    auto halo_x = [&](double* const* x) {
+      if (NR == 2) halo(x[0], x[1]);
+      else halo(x[0]);
+    };
+    halo_x(xa);
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    const double delta = visc_R, sigma = 1.0 / visc_R, tol2 = tol * tol;
+    double rho_old = 1.0 / sigma;
+    Red bb{};
+    // algorithmic bytes: x gathered once, b, d read (not at the first step), d and x_out written
+    const double bytes = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
+                         40.0 * NR * (double)A.own();
+    int it = 0;
+    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] + 1 : 4));
+    for (;;) {
+      for (int k = 0; k < chunk; ++k, ++it) {
+        double c1 = 0.0, c2 = 1.0;  // the first step: d = r / theta, theta = 1
+        if (it > 0) {
+          const double rho = 1.0 / (2.0 * sigma - rho_old);
+          c1 = rho * rho_old;
+          c2 = 2.0 * rho / delta;
+          rho_old = rho;
+        }
+        ChebVecs<NR> v;
+        for (int c = 0; c < NR; ++c) {
+          v.xin[c] = xa[c];
+          v.xout[c] = xb[c];
+          v.b[c] = b[c];
+          v.d[c] = cg_pa[c];
+        }
+        const bool samp = (it & 7) == 0;
+        with_c16(A, [&](auto c16) {
+          klaunch(samp ? 1 : -1, bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(), fc, val, v,
+                  c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a, it == 0 ? part_b : (double*)nullptr);
+        });
+        KCHK();
+        Red rr = reduce_global(part_a, nb, NR, false, 0);
+        if (it == 0) bb = reduce_global(part_b, nb, NR, false, 1);
+        // x_it (this step's input) passed when its residual is small enough
+        hipLaunchKernelGGL(k_cgr_ctl, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it, maxit, NR);
+        KCHK();
+        halo_x(xb);
+        for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
+      }
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (timer.on) timer.flush();
+      if (h_ctl[0]) break;
+      chunk = std::max(1, std::min(64, it / 8));
+    }
+    last_it[which] = h_ctl[1];
+    if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "Chebyshev residual is not finite (step " + std::to_string(h_ctl[1]) + ")");
+    if (h_ctl[0] != 1)
+      throw Error(PUCFEM_ENOCONV, "Chebyshev iteration did not converge within maxit=" + std::to_string(maxit));
+    for (int c = 0; c < NR; ++c) out[c] = (h_ctl[1] & 1) ? cg_pb[c] : y[c];
+    return h_ctl[1];
+  }
+
   // ------------------------------------------------------------------ multigrid V-cycle / PCG
   // Polynomial smoothing (deg steps) for D^-1 A: Chebyshev on [lmax / mg_ratio, lmax] (mg_kind 1), or
   // the fourth-kind Chebyshev recurrence on [0, lmax] (mg_kind 4, Lottes 2022: d_0 = 4/(3 lmax) D^-1 r,
@@ -1039,14 +1115,18 @@ struct Ctx {
       project_guess(3, bvx, yvx);
       project_guess(4, bvy, yvy);
     }
-    iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    double* yo[2] = {yvx, yvy};  // the converged iterate (the Chebyshev double buffer may hold it)
+    const bool cheb = visc_solver == 0 && visc_R < 0.25 && !(world == 1 && block_cg && !fVisc.items &&
+                                                             dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
+    if (cheb) iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo);
+    else iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
     if (proj) {
-      project_update(3, yvx);
-      project_update(4, yvy);
+      project_update(3, yo[0]);
+      project_update(4, yo[1]);
     }
     if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
       const int last = 2 * (visc_extrap - 1);
-      hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yvx, yvy, ux, uy, usx, usy,
+      hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yo[0], yo[1], ux, uy, usx, usy,
                          dvinc[last], dvinc[last + 1]);
       for (int k = last; k >= 2; k -= 2) {
         std::swap(dvinc[k], dvinc[k - 2]);
@@ -1054,7 +1134,7 @@ struct Ctx {
       }
       have_vinc = std::min(have_vinc + 1, visc_extrap);
     } else {
-      hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
+      hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yo[0], yo[1], usx, usy,
                          (const int32_t*)nullptr);
     }
     KCHK();
@@ -1887,6 +1967,19 @@ void build(Ctx& c) {
       else if (isdir[j]) c.Kv[k] = 0.0;
       else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
     }
+  if (stokes) {  // Gershgorin radius of the Jacobi-scaled A_visc (Ctx::visc_R)
+    std::vector<double> dg(N);
+    for (i64 r = 0; r < N; ++r) dg[r] = diag_of(c.P, c.Kv, r);
+    double R = 0.0;
+    for (i64 r = 0; r < N; ++r) {
+      double sr = 0.0;
+      for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k)
+        if (c.P.col[k] != r) sr += std::fabs(c.Kv[k]) / std::sqrt(dg[r] * dg[c.P.col[k]]);
+      R = std::max(R, sr);
+    }
+    c.visc_R = R;
+    if (const char* e = std::getenv("PUCFEM_VISC_SOLVER")) c.visc_solver = std::atoi(e);  // 1: CG (measurement)
+  }
   clk.mark("A_visc");
   // partition + local plan
   if (stokes) partition_rows(c.P, c.ord, c.world, c.row_start);
@@ -3382,7 +3475,8 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[4] = c.proj_m[2];
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
-    o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0);
+    o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
+           (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0);
   });
 }
 

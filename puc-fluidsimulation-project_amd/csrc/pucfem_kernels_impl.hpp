@@ -775,6 +775,136 @@ __global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, con
   }
 }
 
+// ----------------------------------------------------------------------------- Chebyshev iteration (viscous)
+// The Jacobi-scaled A_visc (unit diagonal) has its spectrum inside the Gershgorin interval [1 - R, 1 + R]
+// with R = max_i sum_{j != i} |A^_ij| (~0.02: A_visc = I + DT nu K, condition ~1.04), so the Chebyshev
+// iteration on that interval converges at a guaranteed rate (T_k(1 / R) ~ (2 / R)^k / 2: ~100x per step)
+// with no inner products.  One kernel per step:
+//   r = b - A^ x_in;  d = c1 d + c2 r;  x_out = x_in + d;  partial <r, r> (and <b, b> at the first step)
+// The residual test of x_in follows the kernel (k_cgr_ctl); the iterate that passed is x_in, kept intact
+// by the double buffer.  first: c1 = 0 (d is not read).
+template <int NR>
+struct ChebVecs {
+  const double* xin[NR];
+  double* xout[NR];
+  const double* b[NR];
+  double* d[NR];
+};
+template <int NR, bool C16>
+__global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
+                                              double c1, double c2, int first, const int* ctl, double* part_rr,
+                                              double* part_bb) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  double rr[NR], bb[NR];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
+  auto finish = [&](int c, int64_t row, double ax, double x0, double br, double dr) {
+    const double r = br - ax;
+    const double dn = first ? c2 * r : c1 * dr + c2 * r;
+    stnt(v.d[c] + row, dn);
+    stnt(v.xout[c] + row, x0 + dn);
+    rr[c] += r * r;
+    bb[c] += br * br;
+  };
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    constexpr int K = face_k(NR == 1 ? 4 : 2);
+    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
+#pragma unroll
+      for (int r = 0; r < K; ++r) lat::neighbours(F, fc.n, t[r], i[r], j[r], nb[r], in[r]);
+      double a[K][7];
+#pragma unroll
+      for (int r = 0; r < K; ++r) face_kcoefs(fc, lf, nb[r], in[r], a[r]);
+      double xv[K][NR][7], bv[K][NR], dv[K][NR];
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int64_t row = F.base + t[r];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          xv[r][c][6] = v.xin[c][row];
+          bv[r][c] = v.b[c][row];
+          dv[r][c] = first ? 0.0 : v.d[c][row];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) xv[r][c][k] = v.xin[c][nb[r][k]];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        if (!ok[r]) continue;
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+          double ax = a[r][0] * xv[r][c][6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) ax += a[r][1 + k] * xv[r][c][k];
+          finish(c, F.base + t[r], ax, xv[r][c][6], bv[r][c], dv[r][c]);
+        }
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t row = sell_row(A, s, lane);
+      const int64_t rw = row >= 0 ? row : 0;
+      double acc[NR], x0[NR], br[NR], dr[NR];
+#pragma unroll
+      for (int c = 0; c < NR; ++c) {
+        x0[c] = v.xin[c][rw];
+        br[c] = v.b[c][rw];
+        dr[c] = first ? 0.0 : v.d[c][rw];
+        acc[c] = 0.0;
+      }
+      const int64_t off = A.off[s];
+      const int w = A.w[s];
+      const int32_t base = (int32_t)(s * 64);
+      by_width(w, [&](auto wc) {
+        constexpr int WN = decltype(wc)::value;
+        if constexpr (WN > 0) {
+          int32_t cj[WN];
+          double av[WN];
+#pragma unroll
+          for (int k = 0; k < WN; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            cj[k] = sell_col<C16>(A, e, base);
+            av[k] = ldnt(val + e);
+          }
+#pragma unroll
+          for (int k = 0; k < WN; ++k) {
+#pragma unroll
+            for (int c = 0; c < NR; ++c) acc[c] += av[k] * v.xin[c][cj[k]];
+          }
+        } else {
+          for (int k = 0; k < w; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            const double av = ldnt(val + e);
+            const int32_t j = sell_col<C16>(A, e, base);
+#pragma unroll
+            for (int c = 0; c < NR; ++c) acc[c] += av * v.xin[c][j];
+          }
+        }
+      });
+      if (row >= 0) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c) finish(c, row, acc[c], x0[c], br[c], dr[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    const double t1 = block_sum(rr[c], sh);
+    if (threadIdx.x == 0) part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
+    if (part_bb) {
+      const double t2 = block_sum(bb[c], sh);
+      if (threadIdx.x == 0) part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
+    }
+  }
+}
+
 // the recurrence CG's control after an update: converged (1), maxit (2), not finite (3); it = the
 // iterations done
 __global__ void k_cgr_ctl(const double* rr, const double* bb, double tol2, int* ctl, int it, int maxit, int nr) {

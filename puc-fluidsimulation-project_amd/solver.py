@@ -221,7 +221,8 @@ class Context:
         pres = {0: "dense", 1: "block", 2: "jacobi-cg", 3: "mg-pcg"}
         return dict(viscous=visc[o[0]], pressure=pres[o[1]], reseeds=o[2], basis_p=o[3], basis_p2=o[4],
                     visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7] & 1),
-                    sl_locator="lattice" if o[7] & 2 else "records")
+                    sl_locator="lattice" if o[7] & 2 else "records",
+                    viscous_iteration="chebyshev" if o[7] & 4 else "cg")
 
     def comm_info(self):
         """Multi-rank data flow of the last step (pucfem_comm_info)."""
