@@ -151,3 +151,27 @@ def test_custom_tracers_shape():
     sim.step(2)
     assert sim.tracers.shape == (3, 2)
     sim.close()
+
+
+def test_chebyshev_viscous_matches_cg(monkeypatch):
+    """The production viscous solve is the Chebyshev iteration on the Gershgorin interval of the
+    Jacobi-scaled A_visc; the CG (PUCFEM_VISC_SOLVER=1) stops at the same residual test,
+    so the two runs agree within contract (ii)'s 1e-6 over a run of steps (L2, production settings)."""
+    mesh = pf.load_mesh("fine", refine=2)
+    tol = S.Tolerances.production()
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    assert sim.ctx.path_info()["viscous_iteration"] == "chebyshev"
+    monkeypatch.setenv("PUCFEM_VISC_SOLVER", "1")
+    ref = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
+    monkeypatch.delenv("PUCFEM_VISC_SOLVER")
+    assert ref.ctx.path_info()["viscous_iteration"] == "cg"
+    its = 0
+    for k in range(12):
+        a, _ = sim.step(1)[0], ref.step(1)[0]
+        its += a.it_visc
+        # contract (ii)'s bar: the two differ only through the solves' stopping points
+        assert np.abs(sim.u - ref.u).max() < 1e-6, k
+        assert np.abs(sim.c - ref.c).max() < 1e-6, k
+    assert its > 0
+    sim.close()
+    ref.close()
