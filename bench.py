@@ -43,9 +43,9 @@ def parse():
     ap.add_argument("--mg-vals", default="f32", choices=["f16", "f32", "coarse-f16"],
                     help="fp32 V-cycle operator storage: fp16 on every level, fp32, or fp16 below the finest level")
     ap.add_argument("--index32", action="store_true", help="int32 SELL columns instead of int16 deltas")
-    ap.add_argument("--mg-pre", type=int, default=2, help="Chebyshev pre-smoothing degree")
-    ap.add_argument("--mg-post", type=int, default=2, help="Chebyshev post-smoothing degree")
-    ap.add_argument("--mg-ratio", type=float, default=10.0, help="Chebyshev interval [lmax / ratio, lmax]")
+    ap.add_argument("--mg-pre", type=int, default=3, help="Chebyshev pre-smoothing degree")
+    ap.add_argument("--mg-post", type=int, default=3, help="Chebyshev post-smoothing degree")
+    ap.add_argument("--mg-ratio", type=float, default=15.0, help="Chebyshev interval [lmax / ratio, lmax]")
     ap.add_argument("--mg-kind", type=int, default=1, choices=[1, 4], help="Chebyshev smoother of the first / fourth kind")
     ap.add_argument("--proj-k", type=int, default=24,
                     help="pressure initial guess: A-projection onto the last K solutions (0: warm start only)")

@@ -85,8 +85,10 @@ class Tolerances:
         """The settings bench.py measures (and the production-path parity tests check): multigrid-
         preconditioned pressure CG with the fp32 V-cycle, the 24-direction projected pressure guess,
         int16 column deltas, the extrapolated viscous start, pressure rtol PRODUCTION_RTOL_PRES."""
+        # V(3,3) Chebyshev smoothing on [lmax / 15, lmax]: measured at L7 against V(2,2) / ratio 10 and the
+        # neighbouring choices (DESIGN.md §5; driver command 90.7 -> 97.6 steps/s)
         base = dict(rtol_visc=1e-12, rtol_pres=PRODUCTION_RTOL_PRES, precond="mg", mg_single=True,
-                    mg_f16_vals=False, index16=True, mg_degree=2, mg_post=2, mg_ratio=10.0, mg_kind=1,
+                    mg_f16_vals=False, index16=True, mg_degree=3, mg_post=3, mg_ratio=15.0, mg_kind=1,
                     proj_k=24, proj_k_visc=0)
         base.update(kw)
         return cls(**base)
