@@ -390,7 +390,7 @@ struct Ctx {
   HFace fK, fVisc, fP;  // finest level: K / Gx / Gy (plain table), scaled A_visc (plain), pressure (merged)
   // Gershgorin radius of the Jacobi-scaled A_visc, max_i sum_{j != i} |a_ij| / sqrt(a_ii a_jj): its spectrum
   // lies in [1 - visc_R, 1 + visc_R] (the Chebyshev viscous solve's interval)
-  double visc_R = 1.0;
+  double visc_R = 1.0, visc_lo = 0.0;
   int visc_solver = 0;  // 0 = Chebyshev iteration when visc_R < 0.25 (multi-kernel path), 1 = CG
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
   static FaceDev nof() { return FaceDev{}; }
@@ -435,7 +435,7 @@ struct Ctx {
   // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that;
   // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. 3, default 3 (L7, 40 steps: viscous
   // iterations per step 5 / 4 / 3 / 2-3 for orders 0-3, 17.47 / 16.82 / 16.12 / 15.75 ms per step)
-  double* dvinc[6] = {};
+  float* dvinc[6] = {};
   int have_vinc = 0;
   int visc_extrap = std::getenv("PUCFEM_VISC_EXTRAP") ? std::max(0, std::min(3, std::atoi(std::getenv("PUCFEM_VISC_EXTRAP")))) : 3;
   // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
@@ -769,7 +769,9 @@ struct Ctx {
     };
     halo_x(xa);
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
-    const double delta = visc_R, sigma = 1.0 / visc_R, tol2 = tol * tol;
+    // the interval [visc_lo, 1 + visc_R]: theta its centre, delta its half-width
+    const double hi = 1.0 + visc_R, lo = visc_lo;
+    const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo), sigma = theta / delta, tol2 = tol * tol;
     double rho_old = 1.0 / sigma;
     Red bb{};
     // algorithmic bytes: x gathered once, b, d read (not at the first step), d and x_out written
@@ -779,7 +781,7 @@ struct Ctx {
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] + 1 : 4));
     for (;;) {
       for (int k = 0; k < chunk; ++k, ++it) {
-        double c1 = 0.0, c2 = 1.0;  // the first step: d = r / theta, theta = 1
+        double c1 = 0.0, c2 = 1.0 / theta;  // the first step: d = r / theta
         if (it > 0) {
           const double rho = 1.0 / (2.0 * sigma - rho_old);
           c1 = rho * rho_old;
@@ -1967,17 +1969,29 @@ void build(Ctx& c) {
       else if (isdir[j]) c.Kv[k] = 0.0;
       else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
     }
-  if (stokes) {  // Gershgorin radius of the Jacobi-scaled A_visc (Ctx::visc_R)
+  if (stokes) {  // spectral interval of the Jacobi-scaled A_visc (Ctx::visc_R, Ctx::visc_lo)
     std::vector<double> dg(N);
-    for (i64 r = 0; r < N; ++r) dg[r] = diag_of(c.P, c.Kv, r);
-    double R = 0.0;
-    for (i64 r = 0; r < N; ++r) {
-      double sr = 0.0;
-      for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k)
-        if (c.P.col[k] != r) sr += std::fabs(c.Kv[k]) / std::sqrt(dg[r] * dg[c.P.col[k]]);
-      R = std::max(R, sr);
-    }
-    c.visc_R = R;
+    parallel_for(N, [&](i64 r0, i64 r1) {
+      for (i64 r = r0; r < r1; ++r) dg[r] = diag_of(c.P, c.Kv, r);
+    });
+    std::vector<double> cr(PAR_CHUNKS, 0.0), cd(PAR_CHUNKS, 0.0);
+    parallel_chunks(N, [&](int ch, i64 r0, i64 r1) {
+      double R = 0.0, dmax = 0.0;
+      for (i64 r = r0; r < r1; ++r) {
+        double sr = 0.0;
+        for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k)
+          if (c.P.col[k] != r) sr += std::fabs(c.Kv[k]) / std::sqrt(dg[r] * dg[c.P.col[k]]);
+        R = std::max(R, sr);
+        dmax = std::max(dmax, dg[r]);
+      }
+      cr[ch] = R;
+      cd[ch] = dmax;
+    });
+    c.visc_R = *std::max_element(cr.begin(), cr.end());
+    // A_visc = I + DT nu K on the free rows (K PSD), identity on the Dirichlet rows: its eigenvalues are
+    // >= 1, so the scaled x^T S A S x >= |S x|^2 >= |x|^2 / max_i a_ii (a rigorous lower end, tighter
+    // than Gershgorin's 1 - R)
+    c.visc_lo = std::max(1.0 - c.visc_R, 1.0 / *std::max_element(cd.begin(), cd.end()));
     if (const char* e = std::getenv("PUCFEM_VISC_SOLVER")) c.visc_solver = std::atoi(e);  // 1: CG (measurement)
   }
   clk.mark("A_visc");
@@ -2320,7 +2334,7 @@ void build(Ctx& c) {
     }
   }
   if (stokes && !c.dense && !block_visc && c.proj_k_visc == 0 && c.visc_extrap > 0)
-    for (int k = 0; k < 2 * c.visc_extrap; ++k) c.dvinc[k] = c.dalloc<double>(c.nloc);
+    for (int k = 0; k < 2 * c.visc_extrap; ++k) c.dvinc[k] = c.dalloc<float>(c.nloc);
   if (c.proj_k > 0 || c.proj_k_visc > 0) {
     for (int w = 1; w <= 4; ++w)
       if (c.projX[w]) {

@@ -952,8 +952,11 @@ __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const 
 // warm start u^n + a polynomial extrapolation of the viscous increment u* - u from the last steps
 // (it changes smoothly from step to step): d = (d_1x, d_1y, d_2x, ...) the last `order` increments,
 // newest first; u^n + d_1 (order 1), + 2 d_1 - d_2 (2), + 3 d_1 - 3 d_2 + d_3 (3)
+// The increments are stored in fp32: they only shape the warm start, which the solve corrects to its
+// rtol (1e-12 relative residual); an fp32-rounded increment moves the start by ~1e-7 of the increment,
+// far below the extrapolation's own error.  Halves the increments' share of k_visc_prep / k_visc_fin.
 struct VincDev {
-  const double* d[6];
+  const float* d[6];
   int order;
 };
 __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
@@ -964,15 +967,18 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
     stnt(bx + i, s[i] * a);
     stnt(by + i, s[i] * b);
     double ga = a, gb = b;
+    double e[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e[k] = k < 2 * D.order ? (double)D.d[k][i] : 0.0;
     if (D.order == 1) {
-      ga += D.d[0][i];
-      gb += D.d[1][i];
+      ga += e[0];
+      gb += e[1];
     } else if (D.order == 2) {
-      ga += 2.0 * D.d[0][i] - D.d[2][i];
-      gb += 2.0 * D.d[1][i] - D.d[3][i];
+      ga += 2.0 * e[0] - e[2];
+      gb += 2.0 * e[1] - e[3];
     } else if (D.order == 3) {
-      ga += 3.0 * (D.d[0][i] - D.d[2][i]) + D.d[4][i];
-      gb += 3.0 * (D.d[1][i] - D.d[3][i]) + D.d[5][i];
+      ga += 3.0 * (e[0] - e[2]) + e[4];
+      gb += 3.0 * (e[1] - e[3]) + e[5];
     }
     stnt(yx + i, sq[i] * ga);
     stnt(yy + i, sq[i] * gb);
@@ -981,14 +987,14 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
 // u* = S y (both components) and the increment u* - u for the next step's warm start
 __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double* __restrict__ yx,
                            const double* __restrict__ yy, const double* __restrict__ ux, const double* __restrict__ uy,
-                           double* __restrict__ usx, double* __restrict__ usy, double* __restrict__ dx,
-                           double* __restrict__ dy) {
+                           double* __restrict__ usx, double* __restrict__ usy, float* __restrict__ dx,
+                           float* __restrict__ dy) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = s[i] * yx[i], b = s[i] * yy[i];
     stnt(usx + i, a);
     stnt(usy + i, b);
-    stnt(dx + i, a - ux[i]);
-    stnt(dy + i, b - uy[i]);
+    stnt(dx + i, (float)(a - ux[i]));
+    stnt(dy + i, (float)(b - uy[i]));
   }
 }
 

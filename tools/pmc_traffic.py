@@ -8,8 +8,9 @@ MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's me
 counters, FETCH_SIZE under-reports wide streaming reads by exactly 2x on gfx950, and other access
 widths must be calibrated on a known byte count in one's own access pattern.  The guide's
 corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_visc_fin, a pure 8-B/lane
-elementwise kernel whose algorithmic traffic is exactly 40 B/row read (s, yx, yy, ux, uy) and 32 B/row
-written (u*x, u*y and the two increments), nrows from the bench line.  (k_visc_prep, the check of
+elementwise kernel whose algorithmic traffic is exactly 40 B/row read (s, yx, yy, ux, uy) and 24 B/row
+written (u*x, u*y in fp64, the two increments in fp32; 32 B/row before the increments went to fp32),
+nrows from the bench line.  (k_visc_prep, the check of
 round 1, reads 32-80 B/row depending on the extrapolation order of the step, so it no longer is one.)  Raw counter values are kept next
 to the corrected bytes.  Caveat: the L2 is write-back, so up to ~32 MiB of one kernel's dirty lines
 are evicted (and counted) during the next kernel.
@@ -73,8 +74,8 @@ def main():
             pass
     # gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a
     # streaming read, WRITE_SIZE counts streaming stores exactly; both in KiB.  Checked on k_visc_fin,
-    # a pure 8-B/lane elementwise kernel with exactly 40 B/row read (s, yx, yy, ux, uy) and 32 B/row
-    # written (usx, usy, dx, dy): the corrected values must equal the algorithmic bytes.
+    # a pure elementwise kernel with exactly 40 B/row read (s, yx, yy, ux, uy) and 24 B/row written
+    # (usx, usy fp64; dx, dy fp32): the corrected values must equal the algorithmic bytes.
     res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
     fr, fw = 2.0 * 1024.0, 1.0 * 1024.0
     check = None
@@ -83,7 +84,7 @@ def main():
         f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
         w_avg = sum(write[cal[0]]) / len(write[cal[0]])
         check = {"kernel": "k_visc_fin", "nrows": nrows, "algorithmic_read": 40.0 * nrows,
-                 "corrected_read": f_avg * fr, "algorithmic_write": 32.0 * nrows, "corrected_write": w_avg * fw}
+                 "corrected_read": f_avg * fr, "algorithmic_write": 24.0 * nrows, "corrected_write": w_avg * fw}
     res["calibration"] = {"read_bytes_per_unit": fr, "write_bytes_per_unit": fw,
                           "note": "FETCH_SIZE x2 KiB, WRITE_SIZE x1 KiB (guide's gfx950 corrections)",
                           "check": check}
