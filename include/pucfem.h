@@ -250,6 +250,10 @@ int pucfem_path_info(void* ctx, int64_t* out8);
    the semi-Lagrangian step, out[1] the values a full all-gather of the dye would have received
    (N - n_own), out[2] values all-reduced for the StokesFood tracers (3 x tracers), out[3] reserved */
 int pucfem_comm_info(void* ctx, int64_t* out4);
+/* The viscous Chebyshev iteration's interval for the Jacobi-scaled A_visc (StokesColor.py:471-475):
+   out2 = [lo, hi], lo = max(1 - R, 1 / max_i a_ii), hi = 1 + R, R the Gershgorin radius.  Every
+   eigenvalue lies inside (tests/test_host_assembly.py checks it against scipy's eigensolver). */
+int pucfem_visc_interval(void* ctx, double* out2);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

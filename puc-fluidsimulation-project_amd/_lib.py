@@ -81,6 +81,7 @@ SIGNATURES = {
     "pucfem_apply_bc": ([_P, ct.c_int32, _D], ct.c_int),
     "pucfem_dye_step": ([_P, _D, _D, _D, _I32], ct.c_int),
     "pucfem_comm_info": ([_P, ct.POINTER(ct.c_int64)], ct.c_int),
+    "pucfem_visc_interval": ([_P, ct.POINTER(ct.c_double)], ct.c_int),
     "pucfem_tracer_step": ([_P, _D, ct.c_double, ct.c_int32], ct.c_int),
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),

@@ -3494,6 +3494,16 @@ int pucfem_path_info(void* ctx, int64_t* o) {
   });
 }
 
+int pucfem_visc_interval(void* ctx, double* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    require(c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD, "a Stokes context");
+    o[0] = c.visc_lo;
+    o[1] = 1.0 + c.visc_R;
+  });
+}
+
 int pucfem_comm_info(void* ctx, int64_t* o) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);

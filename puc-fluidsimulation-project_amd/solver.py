@@ -226,6 +226,12 @@ class Context:
                     sl_locator="lattice" if o[7] & 2 else "records",
                     viscous_iteration="chebyshev" if o[7] & 4 else "cg")
 
+    def visc_interval(self):
+        """[lo, hi] of the viscous Chebyshev iteration (pucfem_visc_interval)."""
+        o = (ct.c_double * 2)()
+        self._c(self.L.pucfem_visc_interval(self.h, o))
+        return float(o[0]), float(o[1])
+
     def comm_info(self):
         """Multi-rank data flow of the last step (pucfem_comm_info)."""
         o = (ct.c_int64 * 4)()

@@ -138,3 +138,23 @@ def test_refined_mesh_operators_match_oracle():
     assert abs(K - Kref).max() == 0.0
     # constants are in the kernel of K (pure Neumann)
     assert np.abs(K @ np.ones(mesh.N)).max() < 1e-12
+
+
+@pytest.mark.parametrize("refine", [0, 2])
+def test_viscous_chebyshev_interval_contains_the_spectrum(refine):
+    """The viscous solve's Chebyshev interval [max(1 - R, 1/max a_ii), 1 + R] holds every
+    eigenvalue of the Jacobi-scaled A_visc (StokesColor.py:471-475): the iteration's convergence rate is
+    guaranteed only then."""
+    import scipy.sparse.linalg as sla
+
+    mesh = pf.load_mesh("fine", refine=refine) if refine else pf.load_mesh("fine")
+    tol = S.Tolerances.production(operators="assembled") if refine else S.Tolerances()
+    sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", device=L.HOST_ONLY, tol=tol)
+    lo, hi = sim.ctx.visc_interval()
+    A = sim.ctx.host_csr(L.OP_VISC).tocsr()
+    s = 1.0 / np.sqrt(A.diagonal())
+    Ah = sp.diags(s) @ A @ sp.diags(s)
+    lmin = sla.eigsh(Ah, k=1, which="SA", return_eigenvectors=False, tol=1e-10)[0]
+    lmax = sla.eigsh(Ah, k=1, which="LA", return_eigenvectors=False, tol=1e-10)[0]
+    assert 0.0 < lo <= lmin and lmax <= hi and hi - lo < 0.25, (lo, lmin, lmax, hi)
+    sim.close()
