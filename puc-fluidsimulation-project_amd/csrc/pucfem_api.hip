@@ -911,6 +911,10 @@ struct Ctx {
   }
   // z = M^-1 r on level l (b = r_l); the finest level passes rdot = r for the <r, z> partials and
   // writes z (fp64) directly from its last smoothing step
+  // smoothing degrees below the finest level (measurement knobs PUCFEM_MG_PRE_COARSE /
+  // PUCFEM_MG_POST_COARSE; 0: the finest level's)
+  int mg_pre_coarse = std::getenv("PUCFEM_MG_PRE_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_PRE_COARSE")) : 0;
+  int mg_post_coarse = std::getenv("PUCFEM_MG_POST_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_POST_COARSE")) : 0;
   template <typename T, typename TB>
   T* vcycle(int l, const TB* b, const double* rdot, double* part) {
     MgLevel& L = mg[l];
@@ -932,11 +936,12 @@ struct Ctx {
         throw Error(PUCFEM_ESTATE, "multigrid hierarchy has a single level");
       }
     }
+    const int pre = finest || mg_pre_coarse <= 0 ? prm.mg_degree : mg_pre_coarse;
     if constexpr (std::is_same<T, TB>::value) {
       // coarse levels: the fused first smoothing step reads b at ghost columns
-      if (prm.mg_degree >= 2) mg_halo(L, const_cast<T*>(b));
+      if (pre >= 2) mg_halo(L, const_cast<T*>(b));
     }
-    T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, prm.mg_degree);
+    T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, pre);
     mg_halo(L, x);
     // residual: matrix entries, x gathered once, b read, res written
     const double bytes_res = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
@@ -982,8 +987,9 @@ struct Ctx {
             x, 1, (const int*)ctl);
     KCHK();
     T* other = (x == xa) ? xb : xa;
+    const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
     return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest ? z : nullptr, rdot, part,
-                            prm.mg_post > 0 ? prm.mg_post : prm.mg_degree);
+                            finest || mg_post_coarse <= 0 ? post : mg_post_coarse);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
