@@ -138,7 +138,8 @@ def main():
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
     names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl",
              "k_resid (MG residual, finest level)", "k_transfer (restriction from finest)",
-             "k_transfer (prolongation to finest)", "k_sl_slow (general locate + rank count)"]
+             "k_transfer (prolongation to finest)", "k_sl_slow (general locate + rank count)",
+             "k_vcheb (viscous Chebyshev step)"]
     ktab = {}
     for k, nm in enumerate(names):
         ms, n, b = sim.ctx.timing_get(k)

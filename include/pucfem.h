@@ -219,7 +219,7 @@ int pucfem_timing_enable(void* ctx, int32_t on);
    (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl),
    5 = multigrid residual on the finest level (k_resid), 6 = restriction from the finest level,
    7 = prolongation to the finest level (k_transfer), 8 = the semi-Lagrangian second pass (k_sl_slow: general locate
-   and rank count of the rows off the lattice fast path) */
+   and rank count of the rows off the lattice fast path), 9 = the viscous Chebyshev step (k_vcheb) */
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);

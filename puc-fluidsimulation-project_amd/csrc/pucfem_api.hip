@@ -117,7 +117,7 @@ struct Timer {
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
-  static constexpr int NCLS = 9;
+  static constexpr int NCLS = 10;
   double ms[NCLS] = {};
   double bytes[NCLS] = {};
   int64_t n[NCLS] = {};
@@ -403,7 +403,10 @@ struct Ctx {
   double* dKp_raw = nullptr;        // unscaled finest pressure operator on sPp
   double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
   bool mg_single = false;                        // fp32 V-cycle
-  double* z = nullptr;              // preconditioned residual (finest)
+  double* z = nullptr;              // preconditioned residual (finest; the fp64 V-cycle's)
+  // the fp32 V-cycle's z: its last smoothing step computes in fp32, so z is fp32-exact -- stored as such,
+  // the direction kernel gathers 4 B per point instead of 8 and p = z + beta p_old is the same
+  float* z32 = nullptr;
   // successive right-hand sides: per pressure solve (which = 1: p, 2: p2) an A-orthonormal basis of
   // up to proj_k solution directions, the projected guess x0 and the new direction
   // (which = 3, 4: the viscous solve's x and y components, proj_k_visc directions each)
@@ -779,8 +782,13 @@ struct Ctx {
                          40.0 * NR * (double)A.own();
     int it = 0;
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] + 1 : 4));
-    for (;;) {
+    // (step, first timing sample): the steps after the converged one return at once, their samples
+    // are dropped
+    std::vector<std::pair<int, size_t>> marks;
+    for (bool firstc = true;; firstc = false) {
+      if (!firstc) marks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
+        marks.push_back({it, timer.pend.size()});
         double c1 = 0.0, c2 = 1.0 / theta;  // the first step: d = r / theta
         if (it > 0) {
           const double rho = 1.0 / (2.0 * sigma - rho_old);
@@ -795,10 +803,11 @@ struct Ctx {
           v.b[c] = b[c];
           v.d[c] = cg_pa[c];
         }
-        const bool samp = (it & 7) == 0;
+        // timing class 9; the first step reads no d (8 B/row per right-hand side less)
         with_c16(A, [&](auto c16) {
-          klaunch(samp ? 1 : -1, bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb), dim3(BS), A.view(), fc, val, v,
-                  c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a, it == 0 ? part_b : (double*)nullptr);
+          klaunch(9, it == 0 ? bytes - 8.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
+                  dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a,
+                  it == 0 ? part_b : (double*)nullptr);
         });
         KCHK();
         Red rr = reduce_global(part_a, nb, NR, false, 0);
@@ -811,7 +820,15 @@ struct Ctx {
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      if (timer.on) timer.flush();
+      if (timer.on) {
+        if (h_ctl[0])
+          for (auto& mk : marks)
+            if (mk.first > h_ctl[1]) {
+              timer.drop_from(mk.second);
+              break;
+            }
+        timer.flush();
+      }
       if (h_ctl[0]) break;
       chunk = std::max(1, std::min(64, it / 8));
     }
@@ -844,8 +861,9 @@ struct Ctx {
   }
 
   template <typename T, typename TB>
+  // toz: the last step writes the preconditioned residual (z32 in the fp32 cycle, z in the fp64 one)
   T* mg_smooth(MgLevel& L, const DevSell& A, const HFace& hf, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb,
-               double* zout, const double* rdot, double* part, int deg) {
+               bool tozr, const double* rdot, double* part, int deg) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
@@ -877,7 +895,7 @@ struct Ctx {
       const bool last = k == deg - 1;
       const bool timed = finest && mode != 0;
       const double* rd = last ? rdot : nullptr;
-      const bool toz = last && zout;
+      const bool toz = last && tozr;
       const FaceDev fc = rd ? hf.part() : hf.full();
       const int nb = rd ? grid_part(fc, A) : grid_full(fc, A);
       const T* xi = mode == 1 ? cur : nullptr;
@@ -886,16 +904,19 @@ struct Ctx {
       // read no matrix and no dinv (per-face constants)
       const double rd_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + (rd ? 8.0 : 0.0);
       const double rd_face = (mode == 1 ? 2.0 * sizeof(T) : 0.0) + sizeof(TB) + (rd ? 8.0 : 0.0);
-      const double wr_row = sizeof(T) + (toz ? 8.0 : sizeof(T));
+      const double wr_row = 2.0 * sizeof(T);
       const double bytes = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz +
                            (double)A.nrows * (rd_row + wr_row + A.row_bytes()) + (double)hf.rows * (rd_face + wr_row);
       B.with_vals([&](auto* val) {
         using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
         with_c16(A, [&](auto c16) {
           constexpr bool C = decltype(c16)::value;
+          T* zo = nullptr;
+          if constexpr (std::is_same<T, float>::value) zo = z32;
+          else zo = z;
           if (toz)
-            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, double, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
-                    (const T*)B.dinv, b, xi, zout, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
+                    (const T*)B.dinv, b, xi, zo, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
           else if (finest)
             klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
                     (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
@@ -941,7 +962,7 @@ struct Ctx {
       // coarse levels: the fused first smoothing step reads b at ghost columns
       if (pre >= 2) mg_halo(L, const_cast<T*>(b));
     }
-    T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, nullptr, nullptr, nullptr, pre);
+    T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, false, nullptr, nullptr, pre);
     mg_halo(L, x);
     // residual: matrix entries, x gathered once, b read, res written
     const double bytes_res = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
@@ -988,7 +1009,7 @@ struct Ctx {
     KCHK();
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
-    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest ? z : nullptr, rdot, part,
+    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part,
                             finest || mg_post_coarse <= 0 ? post : mg_post_coarse);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
@@ -1011,6 +1032,7 @@ struct Ctx {
     v.y[0] = y;
     v.b[0] = b;
     v.r[0] = z;  // the gathered "r" of k_cg_dir is the preconditioned residual
+    v.zf[0] = z32;  // (in fp32 from the fp32 V-cycle)
     v.po[0] = cg_pa[0];
     v.pn[0] = cg_pb[0];
     v.q[0] = cg_q[0];
@@ -1034,8 +1056,9 @@ struct Ctx {
     std::vector<std::pair<int, size_t>> marks;
     hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
     KCHK();
-    const double bytes_dir =
-        (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows + 32.0 * (double)n;
+    // direction: z (4 B in the fp32 cycle) and p_old gathered once, p and q written
+    const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
+                             (mg_single ? 28.0 : 32.0) * (double)n;
     const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)n;  // + the fp32 r copy
     int it = 0;
     // an iteration = V-cycle, direction, update, convergence test (k_conv): the host checks right
@@ -1049,11 +1072,17 @@ struct Ctx {
         marks.push_back({it, timer.pend.size()});  // this iteration's V-cycle works iff not converged at it
         precondition();
         Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-        halo(z);
+        if (mg_single) mg_halo(mg.back(), z32);
+        else halo(z);
         with_c16(dPp, [&](auto c16) {
-          klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(), fc,
-                  (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl, it,
-                  maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+          if (mg_single)
+            klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
+                    (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl,
+                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+          else
+            klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(), fc,
+                    (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl,
+                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
         });
         KCHK();
         Red pq = reduce_global(part_c, nb, 1, false, 2);
@@ -2250,6 +2279,7 @@ void build(Ctx& c) {
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
     c.dKp_raw = c.upload(tmp);
     c.z = c.dalloc<double>(c.nloc);
+    c.z32 = c.dalloc<float>(c.nloc);
 
     c.r32 = c.dalloc<float>(c.nloc);
     c.mg_single = c.prm.mg_single != 0;

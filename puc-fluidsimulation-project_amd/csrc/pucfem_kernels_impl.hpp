@@ -169,7 +169,14 @@ struct CgVecs {
   double* pn[NR];
   double* q[NR];
   const double* b[NR];
+  const float* zf[NR];  // k_cg_dir<..., ZF = true>: the gathered residual in fp32 (the fp32 V-cycle's z)
 };
+// the residual k_cg_dir gathers: r (fp64) or, ZF, the fp32-exact preconditioned residual
+template <bool ZF, int NR>
+__device__ __forceinline__ double cg_rg(const CgVecs<NR>& v, int c, int64_t j) {
+  if constexpr (ZF) return (double)v.zf[c][j];
+  else return v.r[c][j];
+}
 
 // r32 (optional): fp32 copy of r for the mixed-precision V-cycle, whose right-hand side is only
 // ever used in fp32 (bit-identical to converting inside the cycle, at half the bytes per read)
@@ -266,7 +273,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
 // One SELL slice of q = A^ (r + beta p_old): WMAX > 0 unrolls the entry loop (all index/value
 // loads issued before the dependent gathers); NT streams the matrix with non-temporal loads so it
 // does not evict the gathered vectors from L2 / MALL.
-template <int NR, int WMAX, bool NT, bool C16>
+template <int NR, int WMAX, bool NT, bool C16, bool ZF = false>
 __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __restrict__ val, const CgVecs<NR>& v,
                                           const double (&beta)[NR], bool first, int64_t s, int lane,
                                           double (&pq)[NR]) {
@@ -283,7 +290,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
       const double a = NT ? ldnt(val + e) : val[e];
       const int32_t j = sell_col<C16, NT>(A, e, base);
 #pragma unroll
-      for (int c = 0; c < NR; ++c) acc[c] += a * (v.r[c][j] + beta[c] * (first ? 0.0 : v.po[c][j]));
+      for (int c = 0; c < NR; ++c) acc[c] += a * (cg_rg<ZF>(v, c, j) + beta[c] * (first ? 0.0 : v.po[c][j]));
     }
   };
   if constexpr (WMAX > 0) {
@@ -301,7 +308,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 #pragma unroll
         for (int k = 0; k < WN; ++k) {
 #pragma unroll
-          for (int c = 0; c < NR; ++c) acc[c] += a[k] * (v.r[c][cj[k]] + beta[c] * (first ? 0.0 : v.po[c][cj[k]]));
+          for (int c = 0; c < NR; ++c) acc[c] += a[k] * (cg_rg<ZF>(v, c, cj[k]) + beta[c] * (first ? 0.0 : v.po[c][cj[k]]));
         }
       } else {
         generic();
@@ -313,7 +320,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
   if (row >= 0) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
-      const double p = v.r[c][row] + beta[c] * (first ? 0.0 : v.po[c][row]);
+      const double p = cg_rg<ZF>(v, c, row) + beta[c] * (first ? 0.0 : v.po[c][row]);
       stnt(v.pn[c] + row, p);
       stnt(v.q[c] + row, acc[c]);
       pq[c] += p * acc[c];
@@ -327,7 +334,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 #ifndef PUCFEM_DIR_K2
 #define PUCFEM_DIR_K2 1
 #endif
-template <int NR, int WMAX, bool NT, bool C16>
+template <int NR, int WMAX, bool NT, bool C16, bool ZF = false>
 __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
@@ -389,11 +396,11 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
         const int64_t row = F.base + t[r];
 #pragma unroll
         for (int c = 0; c < NR; ++c) {
-          rv[r][c][6] = v.r[c][row];
+          rv[r][c][6] = cg_rg<ZF>(v, c, row);
           pv[r][c][6] = first ? 0.0 : v.po[c][row];
 #pragma unroll
           for (int k = 0; k < 6; ++k) {
-            rv[r][c][k] = v.r[c][nb[r][k]];
+            rv[r][c][k] = cg_rg<ZF>(v, c, nb[r][k]);
             pv[r][c][k] = first ? 0.0 : v.po[c][nb[r][k]];
           }
         }
@@ -421,12 +428,12 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
     int64_t s0, s1;
     block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
-    for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16>(A, val, v, beta, first, s, lane, pq);
+    for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16, ZF>(A, val, v, beta, first, s, lane, pq);
   }
   for (int64_t g = A.n_own + (int64_t)blockIdx.x * BS + threadIdx.x; g < A.n_own + n_ghost;
        g += (int64_t)gridDim.x * BS) {
 #pragma unroll
-    for (int c = 0; c < NR; ++c) v.pn[c][g] = v.r[c][g] + beta[c] * (first ? 0.0 : v.po[c][g]);
+    for (int c = 0; c < NR; ++c) v.pn[c][g] = cg_rg<ZF>(v, c, g) + beta[c] * (first ? 0.0 : v.po[c][g]);
   }
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
