@@ -777,9 +777,9 @@ struct Ctx {
     const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo), sigma = theta / delta, tol2 = tol * tol;
     double rho_old = 1.0 / sigma;
     Red bb{};
-    // algorithmic bytes: x gathered once, b, d read (not at the first step), d and x_out written
+    // algorithmic bytes: x gathered once, b, d (fp32; not at the first step) read, d and x_out written
     const double bytes = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
-                         40.0 * NR * (double)A.own();
+                         32.0 * NR * (double)A.own();
     int it = 0;
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] + 1 : 4));
     // (step, first timing sample): the steps after the converged one return at once, their samples
@@ -801,11 +801,11 @@ struct Ctx {
           v.xin[c] = xa[c];
           v.xout[c] = xb[c];
           v.b[c] = b[c];
-          v.d[c] = cg_pa[c];
+          v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
         }
         // timing class 9; the first step reads no d (8 B/row per right-hand side less)
         with_c16(A, [&](auto c16) {
-          klaunch(9, it == 0 ? bytes - 8.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
+          klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
                   dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a,
                   it == 0 ? part_b : (double*)nullptr);
         });

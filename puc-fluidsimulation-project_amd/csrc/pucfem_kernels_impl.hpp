@@ -790,12 +790,15 @@ __global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, con
 //   r = b - A^ x_in;  d = c1 d + c2 r;  x_out = x_in + d;  partial <r, r> (and <b, b> at the first step)
 // The residual test of x_in follows the kernel (k_cgr_ctl); the iterate that passed is x_in, kept intact
 // by the double buffer.  first: c1 = 0 (d is not read).
+// d, the Chebyshev increment, is stored in fp32: x_out = x_in + d takes the fp64 value, and the next
+// step's d = c1 d + c2 r only damps the stored one (c1 < 1; the residual test runs on the fp64 x), so the
+// rounding perturbs the polynomial by ~1e-7 of a shrinking correction -- 16 of the 80 B/row saved
 template <int NR>
 struct ChebVecs {
   const double* xin[NR];
   double* xout[NR];
   const double* b[NR];
-  double* d[NR];
+  float* d[NR];
 };
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
@@ -809,7 +812,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
   auto finish = [&](int c, int64_t row, double ax, double x0, double br, double dr) {
     const double r = br - ax;
     const double dn = first ? c2 * r : c1 * dr + c2 * r;
-    stnt(v.d[c] + row, dn);
+    stnt(v.d[c] + row, (float)dn);
     stnt(v.xout[c] + row, x0 + dn);
     rr[c] += r * r;
     bb[c] += br * br;
@@ -834,7 +837,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
         for (int c = 0; c < NR; ++c) {
           xv[r][c][6] = v.xin[c][row];
           bv[r][c] = v.b[c][row];
-          dv[r][c] = first ? 0.0 : v.d[c][row];
+          dv[r][c] = first ? 0.0 : (double)v.d[c][row];
 #pragma unroll
           for (int k = 0; k < 6; ++k) xv[r][c][k] = v.xin[c][nb[r][k]];
         }
@@ -863,7 +866,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
       for (int c = 0; c < NR; ++c) {
         x0[c] = v.xin[c][rw];
         br[c] = v.b[c][rw];
-        dr[c] = first ? 0.0 : v.d[c][rw];
+        dr[c] = first ? 0.0 : (double)v.d[c][rw];
         acc[c] = 0.0;
       }
       const int64_t off = A.off[s];
