@@ -775,69 +775,75 @@ struct Ctx {
     // the interval [visc_lo, 1 + visc_R]: theta its centre, delta its half-width
     const double hi = 1.0 + visc_R, lo = visc_lo;
     const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo), sigma = theta / delta, tol2 = tol * tol;
-    double rho_old = 1.0 / sigma;
-    Red bb{};
     // algorithmic bytes: x gathered once, b, d (fp32; not at the first step) read, d and x_out written
     const double bytes = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                          32.0 * NR * (double)A.own();
-    int it = 0;
-    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] + 1 : 4));
-    // (step, first timing sample): the steps after the converged one return at once, their samples
-    // are dropped
-    std::vector<std::pair<int, size_t>> marks;
-    for (bool firstc = true;; firstc = false) {
-      if (!firstc) marks.clear();
-      for (int k = 0; k < chunk; ++k, ++it) {
-        marks.push_back({it, timer.pend.size()});
-        double c1 = 0.0, c2 = 1.0 / theta;  // the first step: d = r / theta
-        if (it > 0) {
-          const double rho = 1.0 / (2.0 * sigma - rho_old);
-          c1 = rho * rho_old;
-          c2 = 2.0 * rho / delta;
-          rho_old = rho;
-        }
-        ChebVecs<NR> v;
-        for (int c = 0; c < NR; ++c) {
-          v.xin[c] = xa[c];
-          v.xout[c] = xb[c];
-          v.b[c] = b[c];
-          v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
-        }
-        // timing class 9; the first step reads no d (8 B/row per right-hand side less)
-        with_c16(A, [&](auto c16) {
-          klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
-                  dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a,
-                  it == 0 ? part_b : (double*)nullptr);
-        });
-        KCHK();
-        Red rr = reduce_global(part_a, nb, NR, false, 0);
-        if (it == 0) bb = reduce_global(part_b, nb, NR, false, 1);
-        // x_it (this step's input) passed when its residual is small enough
-        hipLaunchKernelGGL(k_cgr_ctl, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it, maxit, NR);
-        KCHK();
-        halo_x(xb);
-        for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
+    // One step: x_out = x_in + d, d = c1 d + c2 (b - A^ x_in); the first step also yields |r_0| and |b|.
+    auto step = [&](int it, double c1, double c2) {
+      ChebVecs<NR> v;
+      for (int c = 0; c < NR; ++c) {
+        v.xin[c] = xa[c];
+        v.xout[c] = xb[c];
+        v.b[c] = b[c];
+        v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
       }
-      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (timer.on) {
-        if (h_ctl[0])
-          for (auto& mk : marks)
-            if (mk.first > h_ctl[1]) {
-              timer.drop_from(mk.second);
-              break;
-            }
-        timer.flush();
+      // timing class 9; the first step reads no d (4 B/row per right-hand side less)
+      with_c16(A, [&](auto c16) {
+        klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
+                dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a,
+                it == 0 ? part_b : (double*)nullptr);
+      });
+      KCHK();
+      halo_x(xb);
+      for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
+    };
+    // Step 0 gives r_0 = b - A^ x_0.  The residual polynomial of the Chebyshev iteration on an interval
+    // holding the spectrum is bounded by 1 / T_k(sigma) there, so |r_k| <= |r_0| / T_k(sigma): the step
+    // count K that meets the CG's test |r_K| <= rtol |b| is known after step 0, and steps 1 .. K-1 run with
+    // no residual checks, no reductions and no host round trip.  (The bound is rigorous for the interval
+    // [visc_lo, 1 + visc_R], which tests/test_host_assembly.py checks against the spectrum; the
+    // adaptive test it replaces needed one extra step per solve to see the passing residual.)
+    step(0, 0.0, 1.0 / theta);
+    Red rr = reduce_global(part_a, nb, NR, false, 0);
+    Red bb = reduce_global(part_b, nb, NR, false, 1);
+    HIPCHK(hipMemcpyAsync(h_pinned, rr.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_pinned + 8, bb.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (timer.on) timer.flush();
+    int K = 1;  // x_1 exists now; x_0 (y) is the answer when r_0 already passes
+    bool pass0 = true;
+    for (int c = 0; c < NR; ++c) {
+      const double r0 = h_pinned[c], bn = h_pinned[8 + c];
+      if (!std::isfinite(r0) || !std::isfinite(bn)) throw Error(PUCFEM_ENOCONV, "Chebyshev residual is not finite");
+      if (r0 <= tol2 * bn) continue;
+      pass0 = false;
+      // smallest k with T_k(sigma) >= |r_0| / (rtol |b|)
+      const double need = std::sqrt(r0 / (tol2 * bn));
+      double tm = 1.0, tk = sigma;
+      int k = 1;
+      while (tk < need && k < maxit) {
+        const double tn = 2.0 * sigma * tk - tm;
+        tm = tk;
+        tk = tn;
+        ++k;
       }
-      if (h_ctl[0]) break;
-      chunk = std::max(1, std::min(64, it / 8));
+      if (tk < need) throw Error(PUCFEM_ENOCONV, "Chebyshev iteration would not converge within maxit=" + std::to_string(maxit));
+      K = std::max(K, k);
     }
-    last_it[which] = h_ctl[1];
-    if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "Chebyshev residual is not finite (step " + std::to_string(h_ctl[1]) + ")");
-    if (h_ctl[0] != 1)
-      throw Error(PUCFEM_ENOCONV, "Chebyshev iteration did not converge within maxit=" + std::to_string(maxit));
-    for (int c = 0; c < NR; ++c) out[c] = (h_ctl[1] & 1) ? cg_pb[c] : y[c];
-    return h_ctl[1];
+    if (pass0) {
+      for (int c = 0; c < NR; ++c) out[c] = y[c];
+      last_it[which] = 0;
+      return 0;
+    }
+    double rho_old = 1.0 / sigma;
+    for (int it = 1; it < K; ++it) {
+      const double rho = 1.0 / (2.0 * sigma - rho_old);
+      step(it, rho * rho_old, 2.0 * rho / delta);
+      rho_old = rho;
+    }
+    for (int c = 0; c < NR; ++c) out[c] = xa[c];  // x_K
+    last_it[which] = K;
+    return K;
   }
 
   // ------------------------------------------------------------------ multigrid V-cycle / PCG
