@@ -790,8 +790,8 @@ struct Ctx {
       // timing class 9; the first step reads no d (4 B/row per right-hand side less)
       with_c16(A, [&](auto c16) {
         klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
-                dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, part_a,
-                it == 0 ? part_b : (double*)nullptr);
+                dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl,
+                it == 0 ? part_a : (double*)nullptr, it == 0 ? part_b : (double*)nullptr);
       });
       KCHK();
       halo_x(xb);
@@ -808,8 +808,22 @@ struct Ctx {
     Red bb = reduce_global(part_b, nb, NR, false, 1);
     HIPCHK(hipMemcpyAsync(h_pinned, rr.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(h_pinned + 8, bb.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (timer.on) timer.flush();
+    hipEvent_t have_r0 = timer.get();
+    HIPCHK(hipEventRecord(have_r0, st));
+    // while the host waits for |r_0|, the GPU already runs the steps the last solve certainly needed
+    // (one fewer than its count): the round trip hides behind them
+    double rho_old = 1.0 / sigma;
+    int done = 1;
+    auto advance = [&](int upto) {
+      for (; done < upto; ++done) {
+        const double rho = 1.0 / (2.0 * sigma - rho_old);
+        step(done, rho * rho_old, 2.0 * rho / delta);
+        rho_old = rho;
+      }
+    };
+    advance(std::max(1, last_it[which] - 1));
+    HIPCHK(hipEventSynchronize(have_r0));
+    timer.pool.push_back(have_r0);
     int K = 1;  // x_1 exists now; x_0 (y) is the answer when r_0 already passes
     bool pass0 = true;
     for (int c = 0; c < NR; ++c) {
@@ -830,20 +844,15 @@ struct Ctx {
       if (tk < need) throw Error(PUCFEM_ENOCONV, "Chebyshev iteration would not converge within maxit=" + std::to_string(maxit));
       K = std::max(K, k);
     }
-    if (pass0) {
+    if (pass0 && done == 1) {
       for (int c = 0; c < NR; ++c) out[c] = y[c];
       last_it[which] = 0;
       return 0;
     }
-    double rho_old = 1.0 / sigma;
-    for (int it = 1; it < K; ++it) {
-      const double rho = 1.0 / (2.0 * sigma - rho_old);
-      step(it, rho * rho_old, 2.0 * rho / delta);
-      rho_old = rho;
-    }
-    for (int c = 0; c < NR; ++c) out[c] = xa[c];  // x_K
+    advance(K);  // (steps beyond K, already launched, only reduce the residual further)
+    for (int c = 0; c < NR; ++c) out[c] = xa[c];  // x_done, done >= K
     last_it[which] = K;
-    return K;
+    return done;
   }
 
   // ------------------------------------------------------------------ multigrid V-cycle / PCG

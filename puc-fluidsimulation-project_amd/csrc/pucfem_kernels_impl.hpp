@@ -904,6 +904,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
       }
     }
   }
+  if (!part_rr) return;  // steps after the first: no residual norms needed (the step count is known)
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
     const double t1 = block_sum(rr[c], sh);
