@@ -466,6 +466,10 @@ struct Ctx {
       if (h_coef) (void)hipHostFree(h_coef);
       if (h_pinned) (void)hipHostFree(h_pinned);
       comm.reset();
+      if (st_sl) (void)hipStreamSynchronize(st_sl);
+      if (ev_u) (void)hipEventDestroy(ev_u);
+      if (ev_sl) (void)hipEventDestroy(ev_sl);
+      if (st_sl) (void)hipStreamDestroy(st_sl);
       if (st) (void)hipStreamDestroy(st);
     }
   }
@@ -1375,6 +1379,24 @@ struct Ctx {
     KCHK();
   }
 
+  // side stream of the overlapped dye advection (stokes_step)
+  hipStream_t st_sl = nullptr;
+  hipEvent_t ev_u = nullptr, ev_sl = nullptr;
+  bool sl_overlap = true, sl_pending = false;
+  int sl_prio = 0;
+  double* part_mx = nullptr;  // k_mix2 partials (part_b belongs to the solvers of the main stream)
+  struct StreamSwap {  // run the enclosed launches on the other stream (restored on unwind)
+    hipStream_t &a, &b;
+    StreamSwap(hipStream_t& x, hipStream_t& y) : a(x), b(y) { std::swap(a, b); }
+    ~StreamSwap() { std::swap(a, b); }
+  };
+  // order the main stream after the pending dye advection
+  void sl_join() {
+    if (!sl_pending) return;
+    HIPCHK(hipStreamWaitEvent(st, ev_sl, 0));
+    sl_pending = false;
+  }
+
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
@@ -1382,6 +1404,7 @@ struct Ctx {
     div(usx, usy, div_star, true);
     reduce_into(part_d, div_grid(), 1, true, 0);  // max |div u*|
     const int itp = pressure(yp, p, 1);
+    sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
     grad_proj(p, 0);
     bc(ux, uy);
     halo(ux, uy);
@@ -1391,7 +1414,44 @@ struct Ctx {
     halo(ux, uy);
     div(ux, uy, final_div, false);
     reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
-    if (scheme == PUCFEM_STOKES_COLOR) {
+    // single-rank explicit dye: the advection of this step (reads the final u and c, writes c_new and
+    // its own partials) runs on a side stream, overlapped with the next step's viscous solve and first
+    // pressure solve; the main stream waits for it before its next write to u (sl_join above)
+    const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && world == 1;
+    if (ovl) {
+      if (!st_sl) {
+        if (sl_prio != 0) {  // measurement knob: 1 = the side stream at the lowest priority, -1 = highest
+          int lo = 0, hi = 0;
+          HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+          HIPCHK(hipStreamCreateWithPriority(&st_sl, hipStreamNonBlocking, sl_prio > 0 ? lo : hi));
+        } else {
+          HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
+        }
+        HIPCHK(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_sl, hipEventDisableTiming));
+      }
+      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);
+      KCHK();
+      HIPCHK(hipEventRecord(ev_u, st));
+      HIPCHK(hipStreamWaitEvent(st_sl, ev_u, 0));
+      {
+        StreamSwap sw(st, st_sl);
+        const int nb = nb_sl(lp.n_own);
+        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
+        KCHK();
+        std::swap(c_full, c_new);
+        reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+        const int nbm = nb_rows(lp.n_own);
+        hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
+                           part_mx);
+        KCHK();
+        reduce_into(part_mx, nbm, 1, false, 5);
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 2);
+        KCHK();
+      }
+      HIPCHK(hipEventRecord(ev_sl, st_sl));
+      sl_pending = true;
+    } else if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       if (dye_impl) {
         last_dye_it = dye_step(ux, uy, final_div, c_full, c_new);
@@ -1411,14 +1471,16 @@ struct Ctx {
       }
       reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
       const int nbm = nb_rows(lp.n_own);
-      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_b);
+      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx);
       KCHK();
-      reduce_into(part_b, nbm, 1, false, 5);
+      reduce_into(part_mx, nbm, 1, false, 5);
     } else {
       tracer_advance(prm.dt);
     }
-    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec);
-    KCHK();
+    if (!ovl) {
+      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 3);
+      KCHK();
+    }
     its[0] = itv;
     its[1] = itp;
     its[2] = itp2;
@@ -2517,6 +2579,9 @@ void build(Ctx& c) {
   // 6 MAXB: the recurrence CG direction kernel writes 3 dots per right-hand side
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(6 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
+  c.part_mx = c.dalloc<double>(MAXB);
+  if (const char* e = std::getenv("PUCFEM_SL_OVERLAP")) c.sl_overlap = std::atoi(e) != 0;  // 0: one stream
+  if (const char* e = std::getenv("PUCFEM_SL_PRIO")) c.sl_prio = std::atoi(e);
   c.part_u = c.dalloc<double>(2 * MAXB);
   c.yr_own = c.dalloc<double>(2);
   c.yr_all = c.dalloc<double>(2 * c.world);
@@ -3041,8 +3106,11 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
+          c.sl_join();
         } catch (...) {
           c.dits = nullptr;
+          if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
+          c.sl_pending = false;
           throw;
         }
         c.dits = nullptr;
@@ -3454,7 +3522,7 @@ int pucfem_mixing_index(void* ctx, const double* cin, double* out3) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
     HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
     double* rec = c.vals + 8;
-    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec, 3);
     KCHK();
     double h[8];
     HIPCHK(hipMemcpyAsync(h, rec, sizeof(double) * 7, hipMemcpyDeviceToHost, c.st));

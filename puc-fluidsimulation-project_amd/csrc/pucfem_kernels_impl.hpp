@@ -2248,17 +2248,23 @@ __global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const T* __re
 // per-step diagnostics -> stats record.
 // vals: [0] max|div*| [1] max|final div| [2] sum w c [3] sum w [4] not-found [5] sum w (c-mu)^2 [6] eaten
 // out : [0] max|div*| [1] max|final div| [2] I [3] mu [4] var [5] eaten [6] not-found
-__global__ void k_stats(const double* vals, double* out) {
+// parts & 1: the divergence records out[0..1]; parts & 2: the dye records out[2..6] (written by
+// the semi-Lagrangian stream when it overlaps the next step)
+__global__ void k_stats(const double* vals, double* out, int parts) {
   if (threadIdx.x == 0) {
-    const double W = vals[3];
-    const double mu = vals[2] / W, var = vals[5] / W;
-    out[0] = vals[0];
-    out[1] = vals[1];
-    out[2] = var / (mu * (1 - mu) + 1e-16);  // StokesColor.py:402
-    out[3] = mu;
-    out[4] = var;
-    out[5] = vals[6];
-    out[6] = vals[4];
+    if (parts & 1) {
+      out[0] = vals[0];
+      out[1] = vals[1];
+    }
+    if (parts & 2) {
+      const double W = vals[3];
+      const double mu = vals[2] / W, var = vals[5] / W;
+      out[2] = var / (mu * (1 - mu) + 1e-16);  // StokesColor.py:402
+      out[3] = mu;
+      out[4] = var;
+      out[5] = vals[6];
+      out[6] = vals[4];
+    }
   }
 }
 
