@@ -1060,14 +1060,15 @@ struct Ctx {
     halo(y);
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
     float* r32o = mg_single ? r32 : nullptr;
+    // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: k_cg_init
+    // keeps r0 in pav (its "first direction" output; pcg_mg's directions live elsewhere)
+    const bool keep_r0 = proj_k > 0 && (which == 1 || which == 2);
+    if (keep_r0) vi.po[0] = pav[which];
     with_c16(dPp, [&](auto c16) {
       hipLaunchKernelGGL((k_cg_init<1, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(), fc, dKp_raw, vi,
-                         lp.n_ghost, part_a, part_b, r32o);
+                         lp.n_ghost, part_a, part_b, r32o, keep_r0 ? 1 : 0);
     });
     KCHK();
-    // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: keep r0
-    if (proj_k > 0 && (which == 1 || which == 2))
-      HIPCHK(hipMemcpyAsync(pav[which], cg_r[0], sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     Red rr = reduce_global(part_a, nb, 1, false, 0);
     Red bb = reduce_global(part_b, nb, 1, false, 1);
     const double tol2 = tol * tol;
@@ -1356,13 +1357,14 @@ struct Ctx {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     double *v = pv[which], *av = pav[which];
-    hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
-    KCHK();
-    if (r_final) {
+    if (r_final) {  // v = y - x0 and A v = r0 - r_final in one pass
       const bool whole = proj_m[which] == 0;
-      hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, whole ? b : av, r_final, av);
+      hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], v,
+                         whole ? b : (const double*)av, r_final, av);
       KCHK();
     } else {
+      hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);
+      KCHK();
       halo(v);
       spmv_on(st, *op.A, op.fc, op.val, v, av);
     }

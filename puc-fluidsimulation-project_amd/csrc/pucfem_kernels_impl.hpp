@@ -621,6 +621,16 @@ __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) stnt(out + r, a[r] - b[r]);
 }
 
+// out = a - b and out2 = a2 - b2 (out2 may alias a2: each row reads before it writes)
+__global__ void k_diff2(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out,
+                        const double* a2, const double* __restrict__ b2, double* out2) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    const double x = a[r], y = b[r], x2 = a2[r], y2 = b2[r];
+    stnt(out + r, x - y);
+    stnt(out2 + r, x2 - y2);
+  }
+}
+
 // ----------------------------------------------------------------------------- CG, direction updated in place
 // Jacobi-scaled CG (no preconditioner: the viscous solve, the Jacobi pressure path) with the direction
 // formed in the update kernel instead of at the direction kernel's gathered columns: the SpMV then

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel time inside the bench's timed window from a rocprofv3 kernel trace.
 
-The window is the kernels between the end of warm-up step W (the W-th k_stats launch) and the end of
-the last timed step (k_stats launch W+K).  Prints total / calls / average per kernel (name shortened,
+The window is the kernels between the end of warm-up step W (the W-th k_stats launch; with the
+overlapped dye advection, the W-th on the k_sl stream) and the end of the last timed step (k_stats
+launch W+K).  Prints total / calls / average per kernel (name shortened,
 grid size kept so multigrid levels stay apart), the window's span, busy time and idle gaps.
 
   python tools/trace_window.py kernel_trace.csv --warmup 5 --steps 20
@@ -28,7 +29,14 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    stats_idx = [i for i, r in enumerate(rows) if "k_stats" in r["Kernel_Name"]]
+    # a step ends with its last k_stats: with the dye advection on a side stream (one k_stats per
+    # stream per step) that is the side stream's, the stream k_sl runs on
+    col = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
+    sl = [r[col] for r in rows if "k_sl<" in r["Kernel_Name"]]
+    nst = [r[col] for r in rows if "k_stats" in r["Kernel_Name"]]
+    two = sl and len(nst) > 0 and len(set(nst)) > 1
+    stats_idx = [i for i, r in enumerate(rows)
+                 if "k_stats" in r["Kernel_Name"] and (not two or r[col] == sl[0])]
     i0 = stats_idx[a.warmup - 1] + 1
     i1 = stats_idx[a.warmup + a.steps - 1] + 1
     win = rows[i0:i1]
