@@ -1201,13 +1201,13 @@ struct Ctx {
   }
   // grid of k_div (its partials: max |div|, sum braw)
   int div_grid() const { return grid_part(fK.part(), dP); }
-  void div(const double* ax, const double* ay, double* out, bool rhs) {
+  void div(const double* ax, const double* ay, double* out, bool rhs, double* part = nullptr) {
     const FaceDev fc = fK.part();
     with_c16(dP, [&](auto c16) {
       klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
               k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
-              rhs ? braw : (double*)nullptr, part_d);
+              rhs ? braw : (double*)nullptr, part ? part : part_d);
     });
     KCHK();
   }
@@ -1387,6 +1387,7 @@ struct Ctx {
   bool sl_overlap = true, sl_pending = false;
   int sl_prio = 0;
   double* part_mx = nullptr;  // k_mix2 partials (part_b belongs to the solvers of the main stream)
+  double* part_fd = nullptr;  // final-divergence partials (part_d: the main stream's)
   struct StreamSwap {  // run the enclosed launches on the other stream (restored on unwind)
     hipStream_t &a, &b;
     StreamSwap(hipStream_t& x, hipStream_t& y) : a(x), b(y) { std::swap(a, b); }
@@ -1414,12 +1415,15 @@ struct Ctx {
     const int itp2 = pressure(yp2, p2, 2);
     grad_proj(p2, 1);
     halo(ux, uy);
-    div(ux, uy, final_div, false);
-    reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
-    // single-rank explicit dye: the advection of this step (reads the final u and c, writes c_new and
-    // its own partials) runs on a side stream, overlapped with the next step's viscous solve and first
-    // pressure solve; the main stream waits for it before its next write to u (sl_join above)
+    // single-rank explicit dye: the final-divergence record and the advection of this step (they read
+    // the final u and c, write final_div, c_new and their own partials) run on a side stream,
+    // overlapped with the next step's viscous solve and first pressure solve; the main stream waits
+    // for them before its next write to u (sl_join above)
     const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && world == 1;
+    if (!ovl) {
+      div(ux, uy, final_div, false);
+      reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
+    }
     if (ovl) {
       if (!st_sl) {
         if (sl_prio != 0) {  // measurement knob: 1 = the side stream at the lowest priority, -1 = highest
@@ -1432,12 +1436,14 @@ struct Ctx {
         HIPCHK(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_sl, hipEventDisableTiming));
       }
-      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);
+      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);  // max |div u*|
       KCHK();
       HIPCHK(hipEventRecord(ev_u, st));
       HIPCHK(hipStreamWaitEvent(st_sl, ev_u, 0));
       {
         StreamSwap sw(st, st_sl);
+        div(ux, uy, final_div, false, part_fd);
+        reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
         const int nb = nb_sl(lp.n_own);
         sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
         KCHK();
@@ -1448,7 +1454,7 @@ struct Ctx {
                            part_mx);
         KCHK();
         reduce_into(part_mx, nbm, 1, false, 5);
-        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 2);
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
         KCHK();
       }
       HIPCHK(hipEventRecord(ev_sl, st_sl));
@@ -1480,7 +1486,7 @@ struct Ctx {
       tracer_advance(prm.dt);
     }
     if (!ovl) {
-      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 3);
+      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 7);
       KCHK();
     }
     its[0] = itv;
@@ -2582,6 +2588,7 @@ void build(Ctx& c) {
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(6 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
   c.part_mx = c.dalloc<double>(MAXB);
+  c.part_fd = c.dalloc<double>(2 * MAXB);
   if (const char* e = std::getenv("PUCFEM_SL_OVERLAP")) c.sl_overlap = std::atoi(e) != 0;  // 0: one stream
   if (const char* e = std::getenv("PUCFEM_SL_PRIO")) c.sl_prio = std::atoi(e);
   c.part_u = c.dalloc<double>(2 * MAXB);
@@ -3524,7 +3531,7 @@ int pucfem_mixing_index(void* ctx, const double* cin, double* out3) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
     HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
     double* rec = c.vals + 8;
-    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec, 3);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec, 7);
     KCHK();
     double h[8];
     HIPCHK(hipMemcpyAsync(h, rec, sizeof(double) * 7, hipMemcpyDeviceToHost, c.st));

@@ -2258,15 +2258,13 @@ __global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const T* __re
 // per-step diagnostics -> stats record.
 // vals: [0] max|div*| [1] max|final div| [2] sum w c [3] sum w [4] not-found [5] sum w (c-mu)^2 [6] eaten
 // out : [0] max|div*| [1] max|final div| [2] I [3] mu [4] var [5] eaten [6] not-found
-// parts & 1: the divergence records out[0..1]; parts & 2: the dye records out[2..6] (written by
-// the semi-Lagrangian stream when it overlaps the next step)
+// parts & 1: max |div u*| out[0]; & 2: max |final div| out[1]; & 4: the dye records out[2..6]
+// (2 and 4 are written by the side stream when the dye advection overlaps the next step)
 __global__ void k_stats(const double* vals, double* out, int parts) {
   if (threadIdx.x == 0) {
-    if (parts & 1) {
-      out[0] = vals[0];
-      out[1] = vals[1];
-    }
-    if (parts & 2) {
+    if (parts & 1) out[0] = vals[0];
+    if (parts & 2) out[1] = vals[1];
+    if (parts & 4) {
       const double W = vals[3];
       const double mu = vals[2] / W, var = vals[5] / W;
       out[2] = var / (mu * (1 - mu) + 1e-16);  // StokesColor.py:402
