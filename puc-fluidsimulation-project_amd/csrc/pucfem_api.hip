@@ -435,12 +435,15 @@ struct Ctx {
   bool proj_pend[5] = {false, false, false, false, false};  // v / A v wait for the next guess
   double *pv[5] = {}, *pav[5] = {};
   // viscous warm start u^n + a polynomial extrapolation of the increments u* - u of the last steps:
-  // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that;
-  // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. 3, default 3 (L7, 40 steps: viscous
-  // iterations per step 5 / 4 / 3 / 2-3 for orders 0-3, 17.47 / 16.82 / 16.12 / 15.75 ms per step)
-  float* dvinc[6] = {};
+  // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that, ...;
+  // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. VINC_MAX, default 5 (round 2, L7 driver
+  // command with the Chebyshev solve: 77 / 71 / 67 viscous steps per 20 steps for orders 3 / 4 / 5,
+  // 106.1 / 107.0 / 107.2 steps/s, r5e; L7, 40 steps,
+  // round 1: viscous iterations per step 5 / 4 / 3 / 2-3 for orders 0-3, 17.47 / 16.82 / 16.12 /
+  // 15.75 ms per step)
+  float* dvinc[2 * VINC_MAX] = {};
   int have_vinc = 0;
-  int visc_extrap = std::getenv("PUCFEM_VISC_EXTRAP") ? std::max(0, std::min(3, std::atoi(std::getenv("PUCFEM_VISC_EXTRAP")))) : 3;
+  int visc_extrap = std::getenv("PUCFEM_VISC_EXTRAP") ? std::max(0, std::min(VINC_MAX, std::atoi(std::getenv("PUCFEM_VISC_EXTRAP")))) : 5;
   // the operator a basis is A-orthonormal for: the pressure solves' unscaled merged operator (null
   // space: constants on the free dofs, cleared from new directions) or the Jacobi-scaled A_visc
   struct ProjOp {
@@ -1162,7 +1165,7 @@ struct Ctx {
     const bool ext = dvinc[0] != nullptr && !proj_k_visc;
     VincDev vd{};
     vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
-    for (int k = 0; k < 6; ++k) vd.d[k] = dvinc[k];
+    for (int k = 0; k < 2 * VINC_MAX; ++k) vd.d[k] = dvinc[k];
     hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
     KCHK();
     double* y[2] = {yvx, yvy};

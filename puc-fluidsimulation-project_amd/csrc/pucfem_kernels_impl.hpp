@@ -972,12 +972,14 @@ __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const 
 // viscous preparation: b^ = S u (rhs), y0 = S^-1 u (warm start x0 = u^n), StokesColor.py:540-545
 // warm start u^n + a polynomial extrapolation of the viscous increment u* - u from the last steps
 // (it changes smoothly from step to step): d = (d_1x, d_1y, d_2x, ...) the last `order` increments,
-// newest first; u^n + d_1 (order 1), + 2 d_1 - d_2 (2), + 3 d_1 - 3 d_2 + d_3 (3)
+// newest first; u^n + d_1 (order 1), + 2 d_1 - d_2 (2), + 3 d_1 - 3 d_2 + d_3 (3), and the binomial
+// rows 4 d_1 - 6 d_2 + 4 d_3 - d_4 (4), 5 d_1 - 10 d_2 + 10 d_3 - 5 d_4 + d_5 (5)
 // The increments are stored in fp32: they only shape the warm start, which the solve corrects to its
 // rtol (1e-12 relative residual); an fp32-rounded increment moves the start by ~1e-7 of the increment,
 // far below the extrapolation's own error.  Halves the increments' share of k_visc_prep / k_visc_fin.
+constexpr int VINC_MAX = 5;  // highest extrapolation order
 struct VincDev {
-  const float* d[6];
+  const float* d[2 * VINC_MAX];
   int order;
 };
 __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
@@ -988,9 +990,9 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
     stnt(bx + i, s[i] * a);
     stnt(by + i, s[i] * b);
     double ga = a, gb = b;
-    double e[6];
+    double e[2 * VINC_MAX];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) e[k] = k < 2 * D.order ? (double)D.d[k][i] : 0.0;
+    for (int k = 0; k < 2 * VINC_MAX; ++k) e[k] = k < 2 * D.order ? (double)D.d[k][i] : 0.0;
     if (D.order == 1) {
       ga += e[0];
       gb += e[1];
@@ -1000,6 +1002,12 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
     } else if (D.order == 3) {
       ga += 3.0 * (e[0] - e[2]) + e[4];
       gb += 3.0 * (e[1] - e[3]) + e[5];
+    } else if (D.order == 4) {
+      ga += 4.0 * (e[0] + e[4]) - 6.0 * e[2] - e[6];
+      gb += 4.0 * (e[1] + e[5]) - 6.0 * e[3] - e[7];
+    } else if (D.order == 5) {
+      ga += 5.0 * (e[0] - e[6]) + 10.0 * (e[4] - e[2]) + e[8];
+      gb += 5.0 * (e[1] - e[7]) + 10.0 * (e[5] - e[3]) + e[9];
     }
     stnt(yx + i, sq[i] * ga);
     stnt(yy + i, sq[i] * gb);

@@ -321,18 +321,22 @@ def test_mg_pressure_solve_matches_oracle(golden, single):
     sim.close()
 
 
-def test_viscous_extrapolated_start_same_steps(monkeypatch):
-    """The viscous CG starts from u^n plus a third-order extrapolation of the last viscous increments
-    instead of u^n: only the start changes, so 16 steps equal the plain warm-started run to the CG
-    tolerance (rtol 1e-12), with fewer viscous iterations once three increments exist."""
+@pytest.mark.parametrize("order", ["3", "4", "5"])
+def test_viscous_extrapolated_start_same_steps(monkeypatch, order):
+    """The viscous solve starts from u^n plus an extrapolation of the last viscous increments (order 5
+    by default) instead of u^n: only the start changes, so 16 steps equal the plain warm-started run to
+    the solve's tolerance (rtol 1e-12), with fewer viscous iterations once the increments exist."""
     mesh = pf.load_mesh("fine", refine=2)
+    monkeypatch.setenv("PUCFEM_VISC_EXTRAP", order)  # read when a context is created
     a = stokes(mesh)
-    monkeypatch.setenv("PUCFEM_VISC_EXTRAP", "0")  # read when a context is created
+    assert a.ctx.path_info()["visc_extrap_order"] == 0  # no increments yet
+    monkeypatch.setenv("PUCFEM_VISC_EXTRAP", "0")
     b = stokes(mesh)
     sa, sb = a.step(16), b.step(16)
     assert np.abs(a.u - b.u).max() < 1e-9
     assert np.abs(a.c - b.c).max() < 1e-9
     assert sum(x.it_visc for x in sa[4:]) < sum(x.it_visc for x in sb[4:])
+    assert a.ctx.path_info()["visc_extrap_order"] == int(order)
     a.close()
     b.close()
 

@@ -65,7 +65,7 @@ def test_production_color_L3_every_step_vs_oracle(operators):
     path = sim.ctx.path_info()
     assert path["viscous"] == "multi-kernel" and path["pressure"] == "mg-pcg", path
     assert path["proj_k"] == 24 and path["reseeds"] >= 2, path
-    assert path["visc_extrap_order"] == 3, path
+    assert path["visc_extrap_order"] == 5, path
     print(f"L3 production path ({operators}), 48 steps: max |u - oracle| = {worst_u:.2e}, "
           f"max |c - oracle| = {worst_c:.2e}")
     sim.close()
