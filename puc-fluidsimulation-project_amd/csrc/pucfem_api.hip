@@ -1388,7 +1388,7 @@ struct Ctx {
   hipStream_t st_sl = nullptr;
   hipEvent_t ev_u = nullptr, ev_sl = nullptr;
   bool sl_overlap = true, sl_pending = false;
-  int sl_prio = 0;
+  int sl_prio = 0, sl_cus = 0;
   double* part_mx = nullptr;  // k_mix2 partials (part_b belongs to the solvers of the main stream)
   double* part_fd = nullptr;  // final-divergence partials (part_d: the main stream's)
   struct StreamSwap {  // run the enclosed launches on the other stream (restored on unwind)
@@ -1429,7 +1429,13 @@ struct Ctx {
     }
     if (ovl) {
       if (!st_sl) {
-        if (sl_prio != 0) {  // measurement knob: 1 = the side stream at the lowest priority, -1 = highest
+        if (sl_cus > 0) {  // measurement knob: the side stream's waves on the first sl_cus compute units
+          int ncu = 0;
+          HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+          std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+          for (int k = 0; k < std::min(sl_cus, ncu); ++k) mask[(size_t)k / 32] |= 1u << (k % 32);
+          HIPCHK(hipExtStreamCreateWithCUMask(&st_sl, (uint32_t)mask.size(), mask.data()));
+        } else if (sl_prio != 0) {  // measurement knob: 1 = the side stream at the lowest priority, -1 = highest
           int lo = 0, hi = 0;
           HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
           HIPCHK(hipStreamCreateWithPriority(&st_sl, hipStreamNonBlocking, sl_prio > 0 ? lo : hi));
@@ -2594,6 +2600,7 @@ void build(Ctx& c) {
   c.part_fd = c.dalloc<double>(2 * MAXB);
   if (const char* e = std::getenv("PUCFEM_SL_OVERLAP")) c.sl_overlap = std::atoi(e) != 0;  // 0: one stream
   if (const char* e = std::getenv("PUCFEM_SL_PRIO")) c.sl_prio = std::atoi(e);
+  if (const char* e = std::getenv("PUCFEM_SL_CUS")) c.sl_cus = std::atoi(e);
   c.part_u = c.dalloc<double>(2 * MAXB);
   c.yr_own = c.dalloc<double>(2);
   c.yr_all = c.dalloc<double>(2 * c.world);
