@@ -184,6 +184,10 @@ int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count)
 int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count);
 
 /* ---- time stepping: nsteps iterations of the scheme's loop body ------------------- */
+/* Within one call, single-rank StokesColor with the semi-Lagrangian dye runs each step's dye tail
+   (final divergence, advection, mixing sums) on a second stream overlapped with the next step's
+   solves (PUCFEM_SL_OVERLAP=0: one stream); the call returns with all of it complete, so fields and
+   stats read afterwards are those of the last step, as with one stream. */
 int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats /* nsteps entries or NULL */);
 
 /* ---- unit operations (reference-named shims and parity tests) --------------------- */
