@@ -438,7 +438,7 @@ struct Ctx {
   // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that, ...;
   // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. VINC_MAX, default 5 (round 2, L7 driver
   // command with the Chebyshev solve: 77 / 71 / 67 viscous steps per 20 steps for orders 3 / 4 / 5,
-  // 106.1 / 107.0 / 107.2 steps/s, r5e; L7, 40 steps,
+  // 106.1 / 107.0 / 107.2 steps/s, r5e; orders 6 / 7: 64 steps, within the spread, r6e; L7, 40 steps,
   // round 1: viscous iterations per step 5 / 4 / 3 / 2-3 for orders 0-3, 17.47 / 16.82 / 16.12 /
   // 15.75 ms per step)
   float* dvinc[2 * VINC_MAX] = {};

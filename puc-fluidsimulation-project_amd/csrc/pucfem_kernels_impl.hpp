@@ -973,11 +973,11 @@ __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const 
 // warm start u^n + a polynomial extrapolation of the viscous increment u* - u from the last steps
 // (it changes smoothly from step to step): d = (d_1x, d_1y, d_2x, ...) the last `order` increments,
 // newest first; u^n + d_1 (order 1), + 2 d_1 - d_2 (2), + 3 d_1 - 3 d_2 + d_3 (3), and the binomial
-// rows 4 d_1 - 6 d_2 + 4 d_3 - d_4 (4), 5 d_1 - 10 d_2 + 10 d_3 - 5 d_4 + d_5 (5)
+// rows 4 d_1 - 6 d_2 + 4 d_3 - d_4 (4), 5 d_1 - 10 d_2 + 10 d_3 - 5 d_4 + d_5 (5), ... (6, 7)
 // The increments are stored in fp32: they only shape the warm start, which the solve corrects to its
 // rtol (1e-12 relative residual); an fp32-rounded increment moves the start by ~1e-7 of the increment,
 // far below the extrapolation's own error.  Halves the increments' share of k_visc_prep / k_visc_fin.
-constexpr int VINC_MAX = 5;  // highest extrapolation order
+constexpr int VINC_MAX = 7;  // highest extrapolation order
 struct VincDev {
   const float* d[2 * VINC_MAX];
   int order;
@@ -1008,6 +1008,12 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
     } else if (D.order == 5) {
       ga += 5.0 * (e[0] - e[6]) + 10.0 * (e[4] - e[2]) + e[8];
       gb += 5.0 * (e[1] - e[7]) + 10.0 * (e[5] - e[3]) + e[9];
+    } else if (D.order == 6) {
+      ga += 6.0 * (e[0] + e[8]) - 15.0 * (e[2] + e[6]) + 20.0 * e[4] - e[10];
+      gb += 6.0 * (e[1] + e[9]) - 15.0 * (e[3] + e[7]) + 20.0 * e[5] - e[11];
+    } else if (D.order == 7) {
+      ga += 7.0 * (e[0] - e[10]) + 21.0 * (e[8] - e[2]) + 35.0 * (e[4] - e[6]) + e[12];
+      gb += 7.0 * (e[1] - e[11]) + 21.0 * (e[9] - e[3]) + 35.0 * (e[5] - e[7]) + e[13];
     }
     stnt(yx + i, sq[i] * ga);
     stnt(yy + i, sq[i] * gb);
