@@ -153,7 +153,9 @@ int pucfem_ctx_create(int32_t device, void** out_ctx);
 int pucfem_rccl_unique_id(uint8_t* out_id /* PUCFEM_UNIQUE_ID_BYTES */);
 int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const uint8_t* unique_id,
                            void** out_ctx);
-/* A unique id that starts with the 16 bytes "PUCFEM-LOCALCOMM" selects the in-process test backend:
+/* world = 1 with a real unique id creates an RCCL communicator of one rank: the context then runs the
+   multi-rank data path (all-reduced dots, broadcasts, the dye range exchange) through RCCL on one GPU.
+   A unique id that starts with the 16 bytes "PUCFEM-LOCALCOMM" selects the in-process test backend:
    `world` contexts created from host threads of ONE process exchange data with device-to-device
    copies instead of RCCL (multi-rank validation on a one-GPU machine). */
 int pucfem_ctx_destroy(void* ctx);
@@ -214,6 +216,10 @@ int pucfem_apply_bc(void* ctx, int32_t which, double* u);
 int pucfem_dye_step(void* ctx, const double* c, const double* u, double* c_out, int32_t* iters);
 /* mixing_index (StokesColor.py:391-403) over marker==0 nodes: out = (I, mu, var) */
 int pucfem_mixing_index(void* ctx, const double* c, double* out3);
+/* mixing_index(c, mass, mask) (StokesColor.py:391-403) with arbitrary node weights w (N, caller order): the
+   reference's c[mask], mass[mask] is w = mass on the mask and 0 elsewhere (repeated mask entries count
+   repeatedly); out = (I, mu, var) */
+int pucfem_mixing_index_w(void* ctx, const double* c, const double* w, double* out3);
 
 /* ---- measurement ------------------------------------------------------------------ */
 /* HIP-event timing of each kernel class on the context's stream (bench.py roofline).
@@ -227,8 +233,9 @@ int pucfem_timing_enable(void* ctx, int32_t on);
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);
-/* micro-benchmark of the dominant kernel (k_cg_dir) variants on the pressure operator:
-   variant 0 plain loop, 1 unrolled, 2 non-temporal, 3 unrolled + non-temporal; average ms/launch */
+/* micro-benchmark of the pressure CG's SpMV + direction kernel (k_cg_dir; the round-1 roofline kernel,
+   kept for A/B measurements) on the pressure operator: variant 0 plain loop, 1 unrolled, 2 non-temporal,
+   3 unrolled + non-temporal; average ms/launch */
 int pucfem_bench_dir(void* ctx, int32_t variant, int32_t nblocks, int32_t iters, double* ms_out);
 /* timing of one kernel on the context's finest-level data (bench.py's roofline cross-check):
    kernel 0 = k_cheb general step (fp32 V-cycle), 1 = k_resid, 2 = k_cg_dir<1> of the pressure CG.
@@ -252,8 +259,15 @@ int pucfem_info(void* ctx, int64_t* out12);
 int pucfem_path_info(void* ctx, int64_t* out8);
 /* multi-rank data flow of the last step: out[0] dye values this rank received in the wide halo before
    the semi-Lagrangian step, out[1] the values a full all-gather of the dye would have received
-   (N - n_own), out[2] values all-reduced for the StokesFood tracers (3 x tracers), out[3] reserved */
+   (N - n_own), out[2] values all-reduced for the StokesFood tracers (3 x tracers), out[3] the data-path
+   backend (0 none: single rank, 1 LocalComm test backend, 2 RCCL) */
 int pucfem_comm_info(void* ctx, int64_t* out4);
+/* Communicator self-test on the library stream (RCCL's first contact in a run): sum and max all-reduces
+   of 8 values and one grouped ring exchange (rank -> rank + 1; a send to itself on one rank), checked
+   against their known results: out = (|sum err|, |max err|, |recv err|, backend 1 LocalComm / 2 RCCL).
+   The replaced reference sites are the dot products inside the np.linalg.solve calls
+   (StokesColor.py:544-545, 555, 569), which become all-reduced CG dots on multi-rank runs. */
+int pucfem_comm_selftest(void* ctx, double* out4);
 /* The viscous Chebyshev iteration's interval for the Jacobi-scaled A_visc (StokesColor.py:471-475):
    out2 = [lo, hi], lo = max(1 - R, 1 / max_i a_ii), hi = 1 + R, R the Gershgorin radius.  Every
    eigenvalue lies inside (tests/test_host_assembly.py checks it against scipy's eigensolver). */

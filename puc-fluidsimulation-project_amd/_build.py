@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = ["csrc/pucfem_api.hip", "csrc/pucfem_host.cpp"]
 DEPS = SRC + ["csrc/pucfem_host.hpp", "csrc/pucfem_kernels.hpp", "csrc/pucfem_kernels_impl.hpp",
-              "csrc/pucfem_comm.hpp"]
+              "csrc/pucfem_comm.hpp", "csrc/pucfem_lattice.hpp"]
 
 
 def hipcc():

@@ -84,6 +84,8 @@ SIGNATURES = {
     "pucfem_visc_interval": ([_P, ct.POINTER(ct.c_double)], ct.c_int),
     "pucfem_tracer_step": ([_P, _D, ct.c_double, ct.c_int32], ct.c_int),
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
+    "pucfem_mixing_index_w": ([_P, _D, _D, _D], ct.c_int),
+    "pucfem_comm_selftest": ([_P, _D], ct.c_int),
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),
     "pucfem_timing_get": ([_P, ct.c_int32, _D, _I64, _D], ct.c_int),
     "pucfem_sync": ([_P], ct.c_int),

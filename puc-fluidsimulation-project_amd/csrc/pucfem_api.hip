@@ -264,7 +264,11 @@ struct Ctx {
   int device = -1;
   bool host_only = true;
   int rank = 0, world = 1;
+  // the data-path communicator: RCCL (or the LocalComm test backend) on multi-rank runs; also RCCL on a
+  // ONE-rank context created from a real unique id (pucfem_ctx_create_dist with world 1), which then
+  // takes every multi-rank code path -- all-reduces, broadcasts, the dye range exchange -- through RCCL
   std::unique_ptr<Comm> comm;
+  bool dist() const { return comm != nullptr; }
   hipStream_t st = nullptr;
   std::vector<void*> allocs;
   Timer timer;
@@ -562,21 +566,21 @@ struct Ctx {
     double* buf = redbuf + 8 * slot;
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
     KCHK();
-    if (world > 1) comm->allreduce(buf, nv, is_max, st);
+    if (dist()) comm->allreduce(buf, nv, is_max, st);
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
   void reduce_into(double* part, int nb, int nv, bool is_max, int slot, int stride = MAXB) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, vals + slot);
     KCHK();
-    if (world > 1)
+    if (dist())
       comm->allreduce(vals + slot, nv, is_max, st);
   }
   // refresh the ghost entries of up to two local vectors
   void halo(double* a, double* b = nullptr) { halo_lp(lp, dsend, dsendbuf, nsend, a, b); }
   template <typename T>
   void halo_lp(const LocalPlan& P, const int32_t* sidx, T* sbuf, i64 ns, T* a, T* b = nullptr) {
-    if (world == 1 || (P.send_peer.empty() && P.recv_peer.empty())) return;
+    if (!dist() || (P.send_peer.empty() && P.recv_peer.empty())) return;
     if (ns > 0) {
       hipLaunchKernelGGL(k_pack<T>, dim3(grid_ew(ns)), dim3(BS), 0, st, ns, sidx, a, b, sbuf);
       KCHK();
@@ -603,7 +607,7 @@ struct Ctx {
   // own segment is current: its SL wrote it).  Replaces the all-gather of the whole field (SURVEY.md
   // §8e: the departure distance bounds the gather).
   void dye_halo(const double* vy, double dt) {
-    if (world == 1) return;
+    if (!dist()) return;
     const i64 n = lp.n_own;
     const int nb = nb_rows(n);
     // every rank's range of back-traced y (StokesColor.py:361-372), all-gathered as a max-reduction
@@ -651,7 +655,7 @@ struct Ctx {
   }
   // full replica <- every rank's owned segment (internal numbering is rank-contiguous)
   void allgather_full(double* full) {
-    if (world == 1) return;
+    if (!dist()) return;
     comm->group_start();
     for (int r = 0; r < world; ++r) {
       const i64 o = row_start[r], n = row_start[r + 1] - row_start[r];
@@ -664,7 +668,7 @@ struct Ctx {
   template <int NR>
   int cg(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
          double tol, int maxit, int which) {
-    if (world == 1 && block_cg && !hf.items && A.nrows <= (int64_t)CGB_THREADS * CGB_MAXR) {
+    if (!dist() && block_cg && !hf.items && A.nrows <= (int64_t)CGB_THREADS * CGB_MAXR) {
       const size_t vec = (size_t)NR * A.nrows * sizeof(double);
       const size_t mat = (size_t)A.padded * (sizeof(double) + sizeof(int32_t));
       const bool mat_lds = vec + mat <= (size_t)150 * 1024;
@@ -761,7 +765,8 @@ struct Ctx {
 
   // Chebyshev iteration for the Jacobi-scaled viscous system (k_vcheb): y (warm start, overwritten only
   // through the double buffer) and b as for cg<NR>; the converged iterate is returned in out[] (y itself
-  // or the alternate buffer cg_pb).  Same stopping rule as the CG: <r, r> <= tol^2 <b, b>.
+  // or the alternate buffer cg_pb).  Target: the CG's test <r, r> <= tol^2 <b, b>, met through the a-priori
+  // residual bound of the interval (below).
   template <int NR>
   int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
             double tol, int maxit, int which, double* out[NR]) {
@@ -1005,7 +1010,7 @@ struct Ctx {
     mg_halo(L, B.res);
     MgLevel& C = mg[l - 1];
     MgBufs<T>& CB = bufs<T>(C);
-    const bool gather = C.rep && !L.rep && world > 1;  // into the finest replicated level
+    const bool gather = C.rep && !L.rep && dist();  // into the finest replicated level
     T* cb = gather ? CB.b + L.r_r0 : CB.b;
     // restriction: entries (value + column), fine residual read once, coarse rhs written
     const FaceDev frs = L.hR.full(), fpr = L.hPr.full();
@@ -1176,7 +1181,7 @@ struct Ctx {
       project_guess(4, bvy, yvy);
     }
     double* yo[2] = {yvx, yvy};  // the converged iterate (the Chebyshev double buffer may hold it)
-    const bool cheb = visc_solver == 0 && visc_R < 0.25 && !(world == 1 && block_cg && !fVisc.items &&
+    const bool cheb = visc_solver == 0 && visc_R < 0.25 && !(!dist() && block_cg && !fVisc.items &&
                                                              dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
     if (cheb) iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo);
     else iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
@@ -1270,7 +1275,7 @@ struct Ctx {
     mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, 2 * m + 4, 0, proj_d);
     KCHK();
-    if (world > 1) comm->allreduce(proj_d, 2 * m + 4, false, st);
+    if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
     QMat qm{};
     int kq = m;
     if (m == op.kmax) kq = proj_reseed(which, m, qm);  // full: X' = Q X, the dots follow as Q a, Q c
@@ -1422,7 +1427,7 @@ struct Ctx {
     // the final u and c, write final_div, c_new and their own partials) run on a side stream,
     // overlapped with the next step's viscous solve and first pressure solve; the main stream waits
     // for them before its next write to u (sl_join above)
-    const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && world == 1;
+    const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && !dist();
     if (!ovl) {
       div(ux, uy, final_div, false);
       reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
@@ -1481,7 +1486,7 @@ struct Ctx {
       KCHK();
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-      } else if (world > 1) {  // the replica keeps its (halo) values; only the owned segment is new
+      } else if (dist()) {  // the replica keeps its (halo) values; only the owned segment is new
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
       } else {
         std::swap(c_full, c_new);
@@ -1580,7 +1585,7 @@ struct Ctx {
     }
     if (!has_tgrid) throw Error(PUCFEM_ESTATE, "tracer grid not built (scheme is not STOKES_FOOD)");
     double *fx = ux, *fy = uy;
-    if (world > 1) {
+    if (dist()) {
       // no replica of u: each rank interpolates the tracers in its own triangles from its owned and
       // ghost values (placed at their global ids), then one all-reduce of 3 x ntr values hands every
       // rank all the velocities (StokesFood's 488 tracers: ~12 KB per step instead of the whole u)
@@ -2033,14 +2038,14 @@ void build(Ctx& c) {
   require(prm.scheme >= 0 && prm.scheme <= 3, "bad scheme");
   const bool stokes = prm.scheme == PUCFEM_STOKES_COLOR || prm.scheme == PUCFEM_STOKES_FOOD;
   const bool literal = !stokes;
-  require(!(literal && c.world > 1), "heat / Poisson literal operators run on one rank");
+  require(!(literal && c.dist()), "heat / Poisson literal operators run on one rank");
   require(!stokes || prm.sl_k == KNN, "sl_k must be 10 (PointLocator.find default)");
   HostMesh& m = c.mesh;
   // lattice operators: a multigrid hierarchy of >= 2 red refinements (face interiors exist)
   c.lattice = stokes && prm.precond == 1 && c.mg_levels >= 2 && prm.assembled == 0;
   c.dye_impl = prm.scheme == PUCFEM_STOKES_COLOR && prm.dye_scheme == 1;
   require(prm.dye_scheme == 0 || prm.dye_scheme == 1, "dye_scheme must be 0 (semi-Lagrangian) or 1 (implicit)");
-  require(!c.dye_impl || c.world == 1, "the implicit dye variant runs on one rank");
+  require(!c.dye_impl || !c.dist(), "the implicit dye variant runs on one rank");
   if (c.lattice) {
     build_macro(c.coarse, prm.nstrips, c.mg_levels, c.macro);
     lattice_ordering(m, c.macro, c.mg_levels, c.ord, c.lat_fine);
@@ -2145,7 +2150,7 @@ void build(Ctx& c) {
     }
     // replicated coarse levels (multi-rank): level 0 always, then every level up to mg_rep_nodes
     const i64 rep_max = prm.mg_rep_nodes > 0 ? prm.mg_rep_nodes : 300000;
-    for (int l = 0; l < Lv; ++l) c.mg[l].rep = c.world > 1 && (l == 0 || c.mg[l].mesh.N <= rep_max);
+    for (int l = 0; l < Lv; ++l) c.mg[l].rep = c.dist() && (l == 0 || c.mg[l].mesh.N <= rep_max);
     for (int l = 1; l < Lv; ++l) c.mg[l].rep = c.mg[l].rep && c.mg[l - 1].rep;
     for (int l = 0; l <= Lv; ++l) {
       MgLevel& L = c.mg[l];
@@ -2210,7 +2215,7 @@ void build(Ctx& c) {
       }
     }
   }
-  if (stokes && c.world > 1) {  // wide-halo tables of the dye replica (Ctx::dye_halo)
+  if (stokes && c.dist()) {  // wide-halo tables of the dye replica (Ctx::dye_halo)
     const i64 S = (i64)c.ord.strip_ptr.size() - 1;
     c.strip_ylo.assign(S, INFINITY);
     c.strip_yhi.assign(S, -INFINITY);
@@ -2446,14 +2451,14 @@ void build(Ctx& c) {
     }
   }
   c.block_cg = c.prm.solver_path != 1;
-  c.dense = stokes && c.world == 1 && N <= DENSE_MAX && c.prm.precond != 1 && c.prm.solver_path != 1;
+  c.dense = stokes && !c.dist() && N <= DENSE_MAX && c.prm.precond != 1 && c.prm.solver_path != 1;
   clk.mark("device: A_visc, pressure, multigrid");
   // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
   // small meshes need no better start)
   // (a basis needs room for the re-seeded span and one new direction: at least 3)
   auto proj_size = [](int k) { return k <= 0 ? 0 : std::max(3, std::min(k, (int)PROJ_MAX)); };
   c.proj_k = c.use_mg && !c.dense ? proj_size(c.prm.proj_k) : 0;
-  const bool block_visc = c.world == 1 && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
+  const bool block_visc = !c.dist() && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
   c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
   for (int w = 1; w <= 4; ++w) {
     const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
@@ -2739,7 +2744,7 @@ void build(Ctx& c) {
     c.c_full = c.dalloc<double>(N);
     c.c_new = c.dalloc<double>(N);
     c.dnotfound = c.dalloc<int32_t>(no);
-    if (c.world > 1) {
+    if (c.dist()) {
       c.ufx = c.dalloc<double>(N);
       c.ufy = c.dalloc<double>(N);
       if (c.lp.n_ghost > 0) c.dghost_global = c.upload(c.lp.ghost_global);
@@ -2816,9 +2821,10 @@ int pucfem_ctx_create_dist(int32_t device, int32_t rank, int32_t world, const ui
     require(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
     c.rank = rank;
     c.world = world;
-    if (world > 1 && !c.host_only) {
-      static const char kLocal[] = "PUCFEM-LOCALCOMM";
-      if (std::memcmp(uid, kLocal, sizeof(kLocal) - 1) == 0) {
+    static const char kLocal[] = "PUCFEM-LOCALCOMM";
+    const bool local = std::memcmp(uid, kLocal, sizeof(kLocal) - 1) == 0;
+    if (!c.host_only && (world > 1 || !local)) {
+      if (local) {
         // test backend: W ranks as W contexts (host threads) of one process
         c.comm = std::make_unique<LocalComm>(std::string((const char*)uid, PUCFEM_UNIQUE_ID_BYTES), world, rank);
       } else {
@@ -2994,7 +3000,7 @@ int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count)
           c.trx = c.dalloc<double>(n);
           c.try_ = c.dalloc<double>(n);
           c.trs = c.dalloc<double>(n);
-          if (c.world > 1) c.trv = c.dalloc<double>(3 * n);
+          if (c.dist()) c.trv = c.dalloc<double>(3 * n);
         }
         std::vector<double> x(n), y(n);
         for (i64 k = 0; k < n; ++k) {
@@ -3197,7 +3203,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1, "pucfem_apply is single-rank");
+    require(!c.dist(), "pucfem_apply is single-rank");
     const i64 N = c.mesh.N;
     auto perm_in = [&](const double* src, int ncomp, double* d0, double* d1) {
       std::vector<double> a(N), b(N);
@@ -3309,7 +3315,7 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1, "pucfem_solve is single-rank");
+    require(!c.dist(), "pucfem_solve is single-rank");
     const i64 N = c.mesh.N;
     int it = 0;
     // standalone solves run on scratch buffers with their own iteration-hint slots (3, 4) and no
@@ -3399,7 +3405,7 @@ int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, d
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1 && c.has_cgrid, "sl_advect needs a single-rank Stokes context");
+    require(!c.dist() && c.has_cgrid, "sl_advect needs a single-rank Stokes context");
     const i64 N = c.mesh.N;
     std::vector<double> a(N), bx(N), by(N);
     for (i64 g = 0; g < N; ++g) {
@@ -3432,7 +3438,7 @@ int pucfem_apply_bc(void* ctx, int32_t which, double* u) {
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1 && (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD),
+    require(!c.dist() && (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD),
             "apply_bc needs a single-rank Stokes context");
     require(which >= 1 && which <= 3, "apply_bc: which must be 1 (periodic), 2 (Dirichlet) or 3 (both)");
     const i64 N = c.mesh.N;
@@ -3498,7 +3504,7 @@ int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1, "tracer_step unit op is single-rank");
+    require(!c.dist(), "tracer_step unit op is single-rank");
     require(c.has_tgrid, "tracer_step needs a STOKES_FOOD context (the tracer grid)");
     const i64 N = c.mesh.N;
     std::vector<double> bx(N), by(N);
@@ -3513,42 +3519,62 @@ int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
   });
 }
 
+// (I, mu, var) of c with the node weights w (device, internal order) over the N nodes of a single-rank
+// context: the two weighted sums, then the weighted variance about mu (k_mix2), then k_stats
+static void mixing_on(Ctx& c, const double* cin, const double* w, double* out3) {
+  const i64 N = c.mesh.N;
+  std::vector<double> a(N);
+  for (i64 g = 0; g < N; ++g) a[g] = cin[c.ord.new2old[g]];
+  double* cf = c.cg_pa[0];
+  HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+  const int nb = c.nb_rows(N);
+  // part_a[0..] = sum w c (the second dot, w w, is not used)
+  hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, w, (const double*)cf, w, w, c.part_a);
+  KCHK();
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_a, nb, MAXB, 1, 0, c.vals + 2);
+  std::vector<double> ones(N, 1.0);
+  double* on = c.cg_pb[0];
+  HIPCHK(hipMemcpyAsync(on, ones.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+  hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, w, (const double*)on, (const double*)nullptr,
+                     (const double*)nullptr, c.part_b);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
+  hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, w, c.vals + 2, 1, 1, c.part_c);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
+  HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
+  double* rec = c.vals + 8;
+  hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec, 7);
+  KCHK();
+  double h[8];
+  HIPCHK(hipMemcpyAsync(h, rec, sizeof(double) * 7, hipMemcpyDeviceToHost, c.st));
+  HIPCHK(hipStreamSynchronize(c.st));
+  out3[0] = h[2];
+  out3[1] = h[3];
+  out3[2] = h[4];
+}
+
 int pucfem_mixing_index(void* ctx, const double* cin, double* out3) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
     c.need_dev();
     c.need_built();
-    require(c.world == 1, "mixing_index unit op is single-rank");
+    require(!c.dist(), "mixing_index unit op is single-rank");
+    mixing_on(c, cin, c.dwmix, out3);
+  });
+}
+
+int pucfem_mixing_index_w(void* ctx, const double* cin, const double* w, double* out3) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    c.need_built();
+    require(!c.dist(), "mixing_index unit op is single-rank");
+    require(w != nullptr, "mixing_index_w: weights");
     const i64 N = c.mesh.N;
     std::vector<double> a(N);
-    for (i64 g = 0; g < N; ++g) a[g] = cin[c.ord.new2old[g]];
-    double* cf = c.cg_pa[0];
-    HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    // pass 1 (sum w c, sum w) reusing the SL partial layout
-    const int nb = c.nb_rows(N);
-    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, (const double*)c.dwmix, (const double*)cf,
-                       (const double*)c.dwmix, (const double*)c.dwmix, c.part_a);
-    KCHK();
-    // part_a[0] = sum w c, part_a[MAXB] = sum w^2 -> recompute sum w separately
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_a, nb, MAXB, 1, 0, c.vals + 2);
-    std::vector<double> ones(N, 1.0);
-    double* on = c.cg_pb[0];
-    HIPCHK(hipMemcpyAsync(on, ones.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, (const double*)c.dwmix, (const double*)on,
-                       (const double*)nullptr, (const double*)nullptr, c.part_b);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
-    hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, c.dwmix, c.vals + 2, 1, 1, c.part_c);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
-    HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
-    double* rec = c.vals + 8;
-    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, c.st, c.vals, rec, 7);
-    KCHK();
-    double h[8];
-    HIPCHK(hipMemcpyAsync(h, rec, sizeof(double) * 7, hipMemcpyDeviceToHost, c.st));
-    HIPCHK(hipStreamSynchronize(c.st));
-    out3[0] = h[2];
-    out3[1] = h[3];
-    out3[2] = h[4];
+    for (i64 g = 0; g < N; ++g) a[g] = w[c.ord.new2old[g]];
+    double* dw = c.cg_q[0];
+    HIPCHK(hipMemcpyAsync(dw, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    mixing_on(c, cin, dw, out3);
   });
 }
 
@@ -3619,7 +3645,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     for (int k = 0; k < 8; ++k) o[k] = 0;
     const bool stokes = c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD;
     if (!stokes) return;
-    const bool block = c.world == 1 && c.block_cg && c.lp.n_own <= (i64)CGB_THREADS * CGB_MAXR;
+    const bool block = !c.dist() && c.block_cg && c.lp.n_own <= (i64)CGB_THREADS * CGB_MAXR;
     o[0] = c.dense ? 0 : (block ? 1 : 2);
     o[1] = c.dense ? 0 : (c.use_mg ? 3 : (block ? 1 : 2));
     o[2] = c.n_reseed;
@@ -3646,10 +3672,52 @@ int pucfem_comm_info(void* ctx, int64_t* o) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
     c.need_built();
-    o[0] = c.world > 1 ? c.dye_halo_values : 0;
-    o[1] = c.world > 1 ? c.mesh.N - c.lp.n_own : 0;
-    o[2] = c.world > 1 ? 3 * (int64_t)c.ntr : 0;
-    o[3] = 0;
+    o[0] = c.dist() ? c.dye_halo_values : 0;
+    o[1] = c.dist() ? c.mesh.N - c.lp.n_own : 0;
+    o[2] = c.dist() ? 3 * (int64_t)c.ntr : 0;
+    o[3] = !c.comm ? 0 : (dynamic_cast<NcclComm*>(c.comm.get()) ? 2 : 1);
+  });
+}
+
+// Communicator self-test on the library stream: an all-reduce (sum and max) of 8 values and one grouped
+// ring exchange (send to rank + 1, receive from rank - 1; on one rank a send to itself), checked on the
+// device values.  out[0] = |sum - expected|, out[1] = |max - expected|, out[2] = |received - expected|,
+// out[3] = backend (1 LocalComm, 2 RCCL).
+int pucfem_comm_selftest(void* ctx, double* out4) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    require(c.dist(), "comm_selftest needs a context created by pucfem_ctx_create_dist with a communicator");
+    const int W = c.world, R = c.rank;
+    constexpr int n = 8;
+    std::vector<double> h(3 * n);
+    for (int k = 0; k < n; ++k) {
+      h[k] = (R + 1) * (k + 1.0);      // sum over ranks: (k + 1) W (W + 1) / 2
+      h[n + k] = R + 0.25 * k;         // max over ranks: W - 1 + 0.25 k
+      h[2 * n + k] = 1000.0 * R + k;   // sent to rank + 1
+    }
+    double* d = c.dalloc<double>(4 * n);
+    HIPCHK(hipMemcpyAsync(d, h.data(), sizeof(double) * 3 * n, hipMemcpyHostToDevice, c.st));
+    c.comm->allreduce(d, n, false, c.st);
+    c.comm->allreduce(d + n, n, true, c.st);
+    c.comm->group_start();
+    c.comm->send(d + 2 * n, n, (R + 1) % W, c.st);
+    c.comm->recv(d + 3 * n, n, (R + W - 1) % W, c.st);
+    c.comm->group_end(c.st);
+    std::vector<double> g(4 * n);
+    HIPCHK(hipMemcpyAsync(g.data(), d, sizeof(double) * 4 * n, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipStreamSynchronize(c.st));
+    double e0 = 0, e1 = 0, e2 = 0;
+    const int from = (R + W - 1) % W;
+    for (int k = 0; k < n; ++k) {
+      e0 = std::max(e0, std::fabs(g[k] - (k + 1.0) * W * (W + 1) / 2.0));
+      e1 = std::max(e1, std::fabs(g[n + k] - (W - 1 + 0.25 * k)));
+      e2 = std::max(e2, std::fabs(g[3 * n + k] - (1000.0 * from + k)));
+    }
+    out4[0] = e0;
+    out4[1] = e1;
+    out4[2] = e2;
+    out4[3] = dynamic_cast<NcclComm*>(c.comm.get()) ? 2 : 1;
   });
 }
 
@@ -3815,7 +3883,7 @@ int pucfem_host_lattice_apply(void* ctx, int32_t level, int32_t kind, const doub
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
     c.need_built();
-    require(c.lattice && c.world == 1, "needs a single-rank context with lattice operators");
+    require(c.lattice && !c.dist(), "needs a single-rank context with lattice operators");
     const int Lv = c.mg_levels;
     require(level >= 0 && level <= Lv, "level out of range");
     require(kind >= 0 && kind <= 6 && kind != 4, "kind");

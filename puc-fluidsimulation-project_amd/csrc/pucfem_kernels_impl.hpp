@@ -798,11 +798,12 @@ __global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, con
 // iteration on that interval converges at a guaranteed rate (T_k(1 / R) ~ (2 / R)^k / 2: ~100x per step)
 // with no inner products.  One kernel per step:
 //   r = b - A^ x_in;  d = c1 d + c2 r;  x_out = x_in + d;  partial <r, r> (and <b, b> at the first step)
-// The residual test of x_in follows the kernel (k_cgr_ctl); the iterate that passed is x_in, kept intact
-// by the double buffer.  first: c1 = 0 (d is not read).
+// Only the first step writes partials (<r_0, r_0>, <b, b>); the host derives the step count K from the
+// residual bound |r_K| <= |r_0| / T_K(sigma) (Ctx::vcheb) and runs steps 1 .. K-1 without reductions.
+// first: c1 = 0 (d is not read).
 // d, the Chebyshev increment, is stored in fp32: x_out = x_in + d takes the fp64 value, and the next
-// step's d = c1 d + c2 r only damps the stored one (c1 < 1; the residual test runs on the fp64 x), so the
-// rounding perturbs the polynomial by ~1e-7 of a shrinking correction -- 16 of the 80 B/row saved
+// step's d = c1 d + c2 r only damps the stored one (c1 < 1), so the rounding perturbs the polynomial by
+// ~1e-7 of a shrinking correction -- 16 of the 80 B/row saved
 template <int NR>
 struct ChebVecs {
   const double* xin[NR];

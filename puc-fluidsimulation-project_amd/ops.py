@@ -38,7 +38,10 @@ def context_for(nodes, triangles, dt=0.05, nu=0.1, bc: SquirmerBC | None = None,
 
 
 def _stokes_context(mesh: Mesh, dt, nu, bc: SquirmerBC, device=0):
-    k = ("stokes", mesh.N, mesh.T, hash(mesh.coords.tobytes()), hash(mesh.triangles.tobytes()), dt, nu, bc.B1, bc.B2)
+    # the Dirichlet set and values depend on the markers and the squirmer geometry, not only on the mesh
+    k = ("stokes", mesh.N, mesh.T, hash(mesh.coords.tobytes()), hash(mesh.triangles.tobytes()),
+         hash(np.ascontiguousarray(mesh.markers).tobytes()), dt, nu, bc.B1, bc.B2, tuple(bc.center),
+         tuple(bc.outer_value), bc.capture_radius, bc.squirmer_radius)
     ctx = _cache.get(k)
     if ctx is None:
         ctx = Context(device)
@@ -47,7 +50,7 @@ def _stokes_context(mesh: Mesh, dt, nu, bc: SquirmerBC, device=0):
         ctx.set_pairs(0, pairs)
         ctx.set_pairs(1, pairs)
         ctx.set_dirichlet(nodes, vals)
-        ctx.build("color", dt, nu, Tolerances())
+        ctx.build("color", dt, nu, Tolerances(), capture=bc.capture_radius, center=bc.center)
         _cache[k] = ctx
     return ctx
 
@@ -93,19 +96,33 @@ def _apply_bc(u, mesh, bc, which):
 
 
 def mixing_index(c, mass, mask=None, mesh: Mesh | None = None):
-    """StokesColor.py:391-403: (I, mu, var) of c weighted by `mass` over `mask`, on the device.
-    The device reduction's weights are the mesh's lumped mass over its marker==0 nodes (the only
-    weights the reference passes, StokesColor.py:497/:580); other weights are refused."""
+    """StokesColor.py:391-403: (I, mu, var) of c weighted by `mass` over `mask` (None: every node), on
+    the device.  The reference's c[mask], mass[mask] becomes the node weights w = mass on the mask and 0
+    elsewhere (an index mask with repeats counts a node repeatedly, a boolean mask selects), so any
+    weights and mask the reference accepts are accepted here."""
     mesh = _mesh_or_global(mesh)
-    M = buildLumpedMassMatrix(mesh.coords, mesh.triangles)
-    want = np.where(mesh.markers == 0)[0]
-    mask = np.arange(mesh.N) if mask is None else np.asarray(mask)
-    if not (np.array_equal(np.asarray(mass), M) and np.array_equal(np.sort(mask), want)):
-        raise ValueError("mixing_index: mass must be buildLumpedMassMatrix(mesh) and mask the marker==0 nodes")
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    mass = np.asarray(mass, dtype=np.float64)
+    if c.shape != (mesh.N,) or mass.shape != (mesh.N,):
+        raise ValueError(f"mixing_index: c and mass must have shape ({mesh.N},)")
+    if mask is None:
+        w = mass
+    else:
+        m = np.asarray(mask)
+        if m.dtype == bool:
+            if m.shape != (mesh.N,):
+                raise ValueError(f"mixing_index: a boolean mask must have shape ({mesh.N},)")
+            w = np.where(m, mass, 0.0)
+        else:
+            m = m.astype(np.int64).ravel()
+            m = np.where(m < 0, m + mesh.N, m)  # numpy's negative indices
+            if m.size and (m.min() < 0 or m.max() >= mesh.N):
+                raise IndexError("mixing_index: mask index out of range")
+            w = np.bincount(m, minlength=mesh.N).astype(np.float64) * mass
     ctx = _stokes_context(mesh, 0.05, 0.1, _globals.get("bc") or SquirmerBC())
     out = np.zeros(3)
-    _lib.check(ctx.L.pucfem_mixing_index(ctx.h, _lib.dptr(np.ascontiguousarray(c, dtype=np.float64)),
-                                         _lib.dptr(out)), ctx.h)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    _lib.check(ctx.L.pucfem_mixing_index_w(ctx.h, _lib.dptr(c), _lib.dptr(w), _lib.dptr(out)), ctx.h)
     return float(out[0]), float(out[1]), float(out[2])
 
 

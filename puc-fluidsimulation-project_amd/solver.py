@@ -106,6 +106,7 @@ class Context:
     """One libpucfem context (one GPU, or host-only with device=-1)."""
 
     def __init__(self, device=0, dist=None):
+        self.h = None  # close() (and __del__) must work when creation fails below
         L = _lib.lib()
         p = ct.c_void_p()
         if dist is None:
@@ -119,7 +120,7 @@ class Context:
         self.device = device
 
     def close(self):
-        if self.h:
+        if getattr(self, "h", None):
             self.L.pucfem_ctx_destroy(self.h)
             self.h = None
 
@@ -236,7 +237,14 @@ class Context:
         """Multi-rank data flow of the last step (pucfem_comm_info)."""
         o = (ct.c_int64 * 4)()
         self._c(self.L.pucfem_comm_info(self.h, o))
-        return dict(dye_halo_values=o[0], allgather_values=o[1], tracer_allreduce_values=o[2])
+        return dict(dye_halo_values=o[0], allgather_values=o[1], tracer_allreduce_values=o[2],
+                    backend={0: None, 1: "local", 2: "rccl"}[o[3]])
+
+    def comm_selftest(self):
+        """All-reduce + ring send/recv check of the context's communicator (pucfem_comm_selftest)."""
+        o = (ct.c_double * 4)()
+        self._c(self.L.pucfem_comm_selftest(self.h, o))
+        return dict(sum_err=o[0], max_err=o[1], recv_err=o[2], backend={1: "local", 2: "rccl"}[int(o[3])])
 
     def timing(self, on):
         self._c(self.L.pucfem_timing_enable(self.h, int(on)))

@@ -7,6 +7,8 @@ literal reference at its pressure noise floor (1e-2 in u, SURVEY.md §8c (iii));
 conditions, mixing index and semi-Lagrangian step bit-exact or at rounding.
 """
 import numpy as np
+
+import oracle as O
 import pytest
 
 from conftest import has_gpu, load_pkg
@@ -91,8 +93,16 @@ def test_mixing_index_and_short_semilagrange_signature(golden):
     M = pf.buildLumpedMassMatrix(mesh.coords, mesh.triangles)
     I, mu, var = pf.mixing_index(c, M, mask=np.where(mesh.markers == 0)[0])
     np.testing.assert_allclose([I, mu, var], g["mixing_sl_small"], rtol=1e-12, atol=0)
+    # any weights and masks the reference accepts (StokesColor.py:397-403): no mask (every node), a
+    # boolean mask, other weights, an index mask with repeats -- against the oracle's restatement
+    rng = np.random.default_rng(3)
+    w = rng.uniform(0.5, 2.0, mesh.N)
+    idx = rng.integers(0, mesh.N, mesh.N // 3)
+    for mass, mask in ((M, None), (2 * M, mesh.markers == 0), (w, None), (w, idx)):
+        got = pf.mixing_index(c, mass, mask=mask)
+        np.testing.assert_allclose(got, O.mixing_index(c, mass, mask=mask), rtol=1e-12, atol=1e-15)
     with pytest.raises(ValueError):
-        pf.mixing_index(c, 2 * M, mask=np.where(mesh.markers == 0)[0])
+        pf.mixing_index(c[:-1], M)
 
 
 def test_frame_recorder_on_a_run(tmp_path):
