@@ -321,7 +321,7 @@ def test_mg_pressure_solve_matches_oracle(golden, single):
     sim.close()
 
 
-@pytest.mark.parametrize("order", ["3", "4", "5"])
+@pytest.mark.parametrize("order", ["3", "4", "5", "6", "7"])
 def test_viscous_extrapolated_start_same_steps(monkeypatch, order):
     """The viscous solve starts from u^n plus an extrapolation of the last viscous increments (order 5
     by default) instead of u^n: only the start changes, so 16 steps equal the plain warm-started run to
