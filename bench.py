@@ -101,6 +101,13 @@ def main():
         td.all_reduce(t, op=td.ReduceOp.MAX)
         return float(t.item())
 
+    def allsum(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.SUM)
+        return float(t.item())
+
     t_setup = time.time()
     mesh = pf.load_mesh("fine", refine=a.level)
     # the production settings (the configuration tests/test_gpu_production.py checks against the
@@ -129,11 +136,13 @@ def main():
     sim.ctx.timing(0 if a.no_kernel_timing else (1 if a.kernel_table or a.precond != "mg" else 2))
     barrier()
     sim.ctx.sync()
+    n0, b0 = sim.ctx.counters()
     t0 = time.perf_counter()
     stats = sim.step(a.steps)
     sim.ctx.sync()
     barrier()
     dt_local = time.perf_counter() - t0
+    n1, b1 = sim.ctx.counters()
     elapsed = allmax(dt_local)
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
     names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl",
@@ -162,9 +171,15 @@ def main():
                     sim.ctx.h)
             batch[nm] = {"ms_batch": mb.value, "ms_each_event": me.value, "bytes": by.value,
                          "GBps_batch": by.value / (mb.value * 1e-3) / 1e9}
-    cg_iters = sum(2 * s.it_visc + s.it_p + s.it_p2 for s in stats)  # viscous CG is 2-RHS
-    cg_iter_launches = sum(s.it_visc + s.it_p + s.it_p2 for s in stats)
+    # CG iterations: the two pressure PCGs (+ the viscous solve when it is a 2-RHS CG); the production
+    # viscous solve is a Chebyshev iteration, whose steps are reported apart
+    path = sim.ctx.path_info()
+    visc_cheb = path["viscous_iteration"] == "chebyshev"
+    cg_iters = sum(s.it_p + s.it_p2 + (0 if visc_cheb else 2 * s.it_visc) for s in stats)
+    visc_steps = sum(s.it_visc for s in stats)
     steps_per_s = a.steps / elapsed
+    launches_per_step = (n1 - n0) / a.steps
+    bytes_per_step = allsum(b1 - b0) / a.steps
     rec = {
         "metric": "Stokes timesteps/sec (and CG iters/sec) on mesh_fine & 10M-node mesh, 1/2/4/8 GPU",
         "value": steps_per_s,
@@ -194,8 +209,11 @@ def main():
             "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
         },
         "cg_iters_per_s": cg_iters / elapsed,
-        "cg_iters_per_step": {"visc_2rhs": [s.it_visc for s in stats], "p": [s.it_p for s in stats],
-                              "p2": [s.it_p2 for s in stats]},
+        "cg_iters_counted": "pressure PCG iterations (both solves)" + ("" if visc_cheb else " + 2 x viscous CG iterations"),
+        "visc_cheb_steps_per_s": visc_steps / elapsed if visc_cheb else None,
+        "cg_iters_per_step": {("visc_cheb_steps" if visc_cheb else "visc_2rhs"): [s.it_visc for s in stats],
+                              "p": [s.it_p for s in stats], "p2": [s.it_p2 for s in stats]},
+        "launches_per_step": launches_per_step,
         "diagnostics": {"max_div_star": stats[-1].max_div_star, "max_final_div": stats[-1].max_final_div,
                         "mix_var": stats[-1].mix_var},
         "setup_s": t_setup,
@@ -224,36 +242,68 @@ def main():
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kd["achieved_GBps"] / HBM_PEAK_GBS,
                            "traffic": traffic, "bytes_per_launch": kd["bytes_per_launch"],
                            "avg_launch_ms": kd["avg_launch_ms"], "launches_timed": kd["launches_timed"]}
+    # step roofline: the algorithmic bytes of EVERY kernel of the timed steps (the library's per-launch
+    # counts, pucfem_counters; all ranks) / the step time -- the step's distance from its HBM floor
+    step_gbs = bytes_per_step / (1e-3 * rec["ms_per_step"]) / 1e9
+    rec.setdefault("roofline", {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"})["step"] = {
+        "bytes_per_step": bytes_per_step, "ms_per_step": rec["ms_per_step"], "achieved": step_gbs,
+        "frac": step_gbs / HBM_PEAK_GBS / world, "floor_ms_per_step": bytes_per_step / (HBM_PEAK_GBS * 1e9 * world) * 1e3,
+        "counted": "every kernel's algorithmic bytes (vectors once per row read or written, stored operators per entry)"}
     rec["kernels"] = ktab
     rec["kernel_batch"] = batch
+    sim.close()
+    if rank == 0 and world == 1 and not a.no_secondary and a.level > 5:
+        rec["l5"] = gpu_l5(pf, tol)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats)
+        rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats, rec.get("l5"))
     if rank == 0 and world == 1 and not a.no_secondary:
         rec["mesh_fine"] = secondary_fine(pf, a.fine_steps)
-    sim.close()
     if rank == 0:
         print(json.dumps(rec))
     if world > 1:
         td.destroy_process_group()
 
 
-def cpu_baseline(pf, level, stats):
+def gpu_l5(pf, tol, warmup=5, steps=20):
+    """The same step on the GPU at L5 (mesh_fine x5, 894,208 nodes: BASELINE configs[3]'s mesh and the
+    size the CPU baseline is measured at), with the production settings and the driver's schedule
+    (5 warm-up steps, 20 timed): the GPU side of a same-configuration GPU / CPU ratio."""
+    m = pf.load_mesh("fine", refine=5)
+    sim = pf.StokesSimulation(m, pf.SquirmerBC(), 0.05, "color", tol=tol)
+    sim.step(warmup)
+    sim.ctx.sync()
+    n0, b0 = sim.ctx.counters()
+    t = time.perf_counter()
+    st = sim.step(steps)
+    sim.ctx.sync()
+    el = time.perf_counter() - t
+    n1, b1 = sim.ctx.counters()
+    sim.close()
+    ms = 1e3 * el / steps
+    return {"mesh": "mesh_fine x5", "nodes": m.N, "warmup": warmup, "steps": steps, "steps_per_s": steps / el,
+            "ms_per_step": ms, "launches_per_step": (n1 - n0) / steps,
+            "step_roofline_frac": (b1 - b0) / steps / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "cg_iters_last_step": [st[-1].it_visc, st[-1].it_p, st[-1].it_p2]}
+
+
+def cpu_baseline(pf, level, stats, l5=None):
     """The CPU sparse restatement (oracle/fem_ref.py StokesRef, the reference's step
     with scipy sparse direct solves in place of its dense LU) timed DIRECTLY on this host at L5 (mesh_fine
     x5, 894,208 nodes, BASELINE configs[3]'s mesh): one untimed step, then 2 timed steps (the bounded
     sample, ~10 s of CPU work on the GPU box's host).  The factorisation setup is reported, not timed.
-    SuperLU's solves and the numpy element loops run on one core; nproc is reported beside it.  The
-    benchmarked mesh (L7) is too large for the direct solves' fill-in, so the L5 rate is reported as
-    measured and, for the ratio, scaled linearly in the node count to L7 (a lower bound on the CPU cost:
-    the sparse LU solves grow faster than linearly)."""
-    import os
-
+    Threads: the element loops (divergence, gradient), the semi-Lagrangian k-NN query and per-node tests
+    run on `cores` threads (the box's CPU share, at most 16), the two viscous SuperLU solves on two; the
+    pressure SuperLU solves are single-threaded (SuperLU).  The benchmarked mesh (L7) is too large for the
+    direct solves' fill-in, so the L5 rate is reported as measured -- beside the GPU's own L5 rate (same
+    configuration: `same_config_ratio`) -- and, for the headline, scaled linearly in the node count to L7
+    (a lower bound on the CPU cost: the sparse LU solves grow faster than linearly)."""
     import oracle as O
 
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
     lv = min(level, 5)
     m = pf.load_mesh("fine", refine=lv)
     t = time.perf_counter()
-    ref = O.StokesRef(m.coords, m.markers, m.triangles, 0.05, 0.1, -2.0, 0.0, "color")
+    ref = O.StokesRef(m.coords, m.markers, m.triangles, 0.05, 0.1, -2.0, 0.0, "color", workers=cores)
     t_setup = time.perf_counter() - t
     u, c = ref.initial()
     out = ref.step(u, c)  # first step outside the timing (warm caches)
@@ -266,13 +316,18 @@ def cpu_baseline(pf, level, stats):
     sps = n / (time.perf_counter() - t)
     n_full = stats_nodes(pf, level)
     scale = m.N / n_full
-    return {"value": sps * scale, "unit": "timesteps/s", "cores": 1, "kind": "port",
-            "label": "CPU sparse restatement", "nproc": os.cpu_count(),
-            "measured": {"mesh": f"mesh_fine x{lv}", "nodes": m.N, "steps_per_s": sps, "setup_s": t_setup},
-            "sample": (f"CPU sparse restatement (oracle StokesRef: scipy SuperLU solves, numpy element loops, "
-                       f"KDTree SL; 1 core of nproc={os.cpu_count()}) timed directly on mesh_fine x{lv} "
-                       f"({m.N} nodes): {n} steps at {sps:.4f} steps/s after one untimed step, factorisation "
-                       f"setup {t_setup:.1f}s excluded; value scaled x{scale:.5f} (node ratio) to x{level}")}
+    rec = {"value": sps * scale, "unit": "timesteps/s", "cores": cores, "kind": "port",
+           "label": "CPU sparse restatement", "nproc": os.cpu_count(),
+           "measured": {"mesh": f"mesh_fine x{lv}", "nodes": m.N, "steps_per_s": sps, "setup_s": t_setup},
+           "sample": (f"CPU sparse restatement (oracle StokesRef: scipy SuperLU solves, numpy element loops, "
+                      f"KDTree SL; element loops / SL / viscous solves on up to {cores} threads, pressure "
+                      f"SuperLU single-threaded; nproc={os.cpu_count()}) timed directly on mesh_fine x{lv} "
+                      f"({m.N} nodes): {n} steps at {sps:.4f} steps/s after one untimed step, factorisation "
+                      f"setup {t_setup:.1f}s excluded; value scaled x{scale:.5f} (node ratio) to x{level}")}
+    if l5 is not None and lv == 5:
+        rec["same_config"] = {"mesh": "mesh_fine x5", "gpu_steps_per_s": l5["steps_per_s"], "cpu_steps_per_s": sps,
+                              "ratio": l5["steps_per_s"] / sps}
+    return rec
 
 
 def stats_nodes(pf, level):

@@ -233,6 +233,12 @@ int pucfem_timing_enable(void* ctx, int32_t on);
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);
+/* cumulative counters of the calling thread / context since its creation (bench.py's step roofline):
+   launches = kernel launches issued by this thread through the library; bytes = the algorithmic bytes of
+   the context's launched kernels (each vector counted once per row it is read or written, stored operators
+   per entry; kernels launched after their solve had converged, which do no work, are not counted) --
+   the HBM floor of the work the steps did.  Replaces nothing in the reference (measurement only). */
+int pucfem_counters(void* ctx, int64_t* launches, double* bytes);
 /* micro-benchmark of the pressure CG's SpMV + direction kernel (k_cg_dir; the round-1 roofline kernel,
    kept for A/B measurements) on the pressure operator: variant 0 plain loop, 1 unrolled, 2 non-temporal,
    3 unrolled + non-temporal; average ms/launch */

@@ -28,6 +28,23 @@ H = 1.0
 L = 1.0
 
 
+def _chunks(n, workers):
+    """[0, n) in `workers` contiguous ranges."""
+    b = np.linspace(0, n, workers + 1).astype(np.int64)
+    return [(int(b[k]), int(b[k + 1])) for k in range(workers) if b[k + 1] > b[k]]
+
+
+def _threaded(fn, n, workers):
+    """fn(lo, hi) over `workers` contiguous ranges of [0, n) on a thread pool (numpy's array kernels
+    release the GIL); returns the per-range results in range order.  workers <= 1: one call."""
+    if workers <= 1:
+        return [fn(0, n)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(workers) as ex:
+        return list(ex.map(lambda r: fn(*r), _chunks(n, workers)))
+
+
 # ----------------------------------------------------------------------------- mesh I/O
 def read_node(path, dtype=np.float64):
     """StokesColor.py:54-78 (fp64) / poisson.py:27-56 (fp32, :40): header N, then N lines id x y marker."""
@@ -155,8 +172,20 @@ def div_area_sum(X, T):
     return S
 
 
-def divergence(X, T, u):
-    """StokesColor.py:130-165 calculate_divergence: lumped nodal divergence / (area_sum + 1e-12)."""
+def divergence(X, T, u, workers=1):
+    """StokesColor.py:130-165 calculate_divergence: lumped nodal divergence / (area_sum + 1e-12).
+    workers > 1 (the CPU baseline's timing leg only): the triangle loop in contiguous chunks on threads,
+    per-chunk node sums added in chunk order -- the same arithmetic, node sums associated differently."""
+    if workers > 1:
+        parts = _threaded(lambda a, b: _divergence_sums(X, T[a:b], u), T.shape[0], workers)
+        ds = sum(p[0] for p in parts)
+        asum = sum(p[1] for p in parts)
+        return ds / (asum + 1e-12)
+    ds, asum = _divergence_sums(X, T, u)
+    return ds / (asum + 1e-12)
+
+
+def _divergence_sums(X, T, u):
     x1, y1, x2, y2, x3, y3 = _xy(X, T)
     det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2)
     ok = np.abs(det) >= 1e-14
@@ -172,11 +201,21 @@ def divergence(X, T, u):
     # reference order: for each triangle, for p in tri: div_sum[p] += lump; area_sum[p] += area/3
     np.add.at(ds, T[ok].ravel(), np.repeat(lump[ok], 3))
     np.add.at(asum, T[ok].ravel(), np.repeat((area / 3.0)[ok], 3))
-    return ds / (asum + 1e-12)
+    return ds, asum
 
 
-def gradient(X, T, p):
-    """StokesColor.py:224-263 calculate_gradiant: lumped nodal gradient / (area_sum + 1e-12)."""
+def gradient(X, T, p, workers=1):
+    """StokesColor.py:224-263 calculate_gradiant: lumped nodal gradient / (area_sum + 1e-12).
+    workers > 1: as divergence."""
+    if workers > 1:
+        parts = _threaded(lambda a, b: _gradient_sums(X, T[a:b], p), T.shape[0], workers)
+        sx, sy, asum = (sum(q[k] for q in parts) for k in range(3))
+    else:
+        sx, sy, asum = _gradient_sums(X, T, p)
+    return sx / (asum + 1e-12), sy / (asum + 1e-12)
+
+
+def _gradient_sums(X, T, p):
     x1, y1, x2, y2, x3, y3 = _xy(X, T)
     det = x1 * (y2 - y3) + x2 * (y3 - y1) + x3 * (y1 - y2)
     ok = np.abs(det) >= 1e-14
@@ -193,7 +232,7 @@ def gradient(X, T, p):
     np.add.at(sx, idx, np.repeat((gx * a3)[ok], 3))
     np.add.at(sy, idx, np.repeat((gy * a3)[ok], 3))
     np.add.at(asum, idx, np.repeat(a3[ok], 3))
-    return sx / (asum + 1e-12), sy / (asum + 1e-12)
+    return sx, sy, asum
 
 
 def fem_system_fp32(X32, T, g_source):
@@ -374,7 +413,7 @@ def centroids(X, T):
     return np.mean(X[T], axis=1)
 
 
-def sl_advect(c, u, dt, X, T, tree=None, k=10):
+def sl_advect(c, u, dt, X, T, tree=None, k=10, workers=1):
     """StokesColor.py:347-389 advect_semilagrange with PointLocator.find (:314-345): back-trace,
     x wrapped mod 1, y clamped to [1e-12, 1-1e-12], first of the k nearest centroids whose
     barycentric weights are all >= 0, periodic-dx interpolation, not found -> keep c[n]."""
@@ -384,21 +423,28 @@ def sl_advect(c, u, dt, X, T, tree=None, k=10):
     yb = X[:, 1] - dt * u[:, 1] * 1.0
     yb = np.where(yb < 0.0, 1e-12, yb)
     yb = np.where(yb > 1.0, 1.0 - 1e-12, yb)
-    _, idx = tree.query(np.stack([xb, yb], 1), k=k)
+    # workers > 1 (the CPU baseline's timing leg): the k-NN query and the per-node tests on threads --
+    # every node is independent, so the result is the same
+    _, idx = tree.query(np.stack([xb, yb], 1), k=k, workers=workers)
     N = X.shape[0]
     found = -np.ones(N, dtype=np.int64)
-    for kk in range(k):
-        t = idx[:, kk]
-        i, j, l_ = T[t, 0], T[t, 1], T[t, 2]
-        x1, y1, x2, y2, x3, y3 = X[i, 0], X[i, 1], X[j, 0], X[j, 1], X[l_, 0], X[l_, 1]
-        det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1)
-        okd = np.abs(det) >= 1e-14
-        sd = np.where(okd, det, 1.0)
-        w1 = ((x2 - xb) * (y3 - yb) - (x3 - xb) * (y2 - yb)) / sd
-        w2 = ((x3 - xb) * (y1 - yb) - (x1 - xb) * (y3 - yb)) / sd
-        w3 = 1.0 - w1 - w2
-        hit = okd & (w1 >= 0.0) & (w2 >= 0.0) & (w3 >= 0.0) & (found < 0)
-        found[hit] = t[hit]
+
+    def first_hit(a, b):
+        xq, yq, fd = xb[a:b], yb[a:b], found[a:b]
+        for kk in range(k):
+            t = idx[a:b, kk]
+            i, j, l_ = T[t, 0], T[t, 1], T[t, 2]
+            x1, y1, x2, y2, x3, y3 = X[i, 0], X[i, 1], X[j, 0], X[j, 1], X[l_, 0], X[l_, 1]
+            det = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1)
+            okd = np.abs(det) >= 1e-14
+            sd = np.where(okd, det, 1.0)
+            w1 = ((x2 - xq) * (y3 - yq) - (x3 - xq) * (y2 - yq)) / sd
+            w2 = ((x3 - xq) * (y1 - yq) - (x1 - xq) * (y3 - yq)) / sd
+            w3 = 1.0 - w1 - w2
+            hit = okd & (w1 >= 0.0) & (w2 >= 0.0) & (w3 >= 0.0) & (fd < 0)
+            fd[hit] = t[hit]
+
+    _threaded(first_hit, N, workers)
 
     def dx(a, b):
         d = a - b
@@ -497,7 +543,10 @@ class StokesRef:
     """StokesColor.py:437-586 / StokesFood.py:357-505: one operator-split step with the
     symmetric-merged pressure (PressureSolver).  ``scheme`` 'color' advects dye, 'food' moves tracers."""
 
-    def __init__(self, X, mk, T, dt, nu, B1, B2, scheme="color"):
+    def __init__(self, X, mk, T, dt, nu, B1, B2, scheme="color", workers=1):
+        # workers > 1: bench.py's CPU-baseline timing leg (element loops, SL and the two viscous solves on
+        # threads); the parity tests use the default single-threaded path
+        self.workers = workers
         self.X, self.mk, self.T = X, mk, T
         self.N = X.shape[0]
         self.dt, self.nu = dt, nu
@@ -528,27 +577,32 @@ class StokesRef:
 
     def step(self, u, c=None, tracers=None, status=None):
         X, T, dt = self.X, self.T, self.dt
+        W = self.workers
         us = np.zeros_like(u)
-        us[:, 0] = self.lu_v.solve(u[:, 0] + dt * 0.0)
-        us[:, 1] = self.lu_v.solve(u[:, 1] + dt * 0.0)
+        if W > 1:
+            cols = _threaded(lambda a, b: self.lu_v.solve(u[:, a] + dt * 0.0), 2, 2)
+            us[:, 0], us[:, 1] = cols[0], cols[1]
+        else:
+            us[:, 0] = self.lu_v.solve(u[:, 0] + dt * 0.0)
+            us[:, 1] = self.lu_v.solve(u[:, 1] + dt * 0.0)
         self.bc(us)
-        div_s = divergence(X, T, us)
+        div_s = divergence(X, T, us, W)
         p = self.ps.solve(-(1.0 / dt) * div_s)
-        gx, gy = gradient(X, T, p)
+        gx, gy = gradient(X, T, p, W)
         un = np.empty_like(u)
         un[:, 0] = us[:, 0] - dt * gx
         un[:, 1] = us[:, 1] - dt * gy
         self.bc(un)
-        div_u = divergence(X, T, un)
+        div_u = divergence(X, T, un, W)
         p2 = self.ps.solve(-(1.0 / dt) * div_u)
-        g2x, g2y = gradient(X, T, p2)
+        g2x, g2y = gradient(X, T, p2, W)
         I = self.interior
         un[I, 0] -= dt * g2x[I]
         un[I, 1] -= dt * g2y[I]
-        fdiv = divergence(X, T, un)
+        fdiv = divergence(X, T, un, W)
         out = dict(u_star=us, div_u_star=div_s, p=p, div_u=div_u, p2=p2, final_div=fdiv, u=un)
         if c is not None:
-            c2, nf = sl_advect(c, un, dt, X, T, self.tree)
+            c2, nf = sl_advect(c, un, dt, X, T, self.tree, workers=W)
             out["c"] = c2
             out["sl_notfound"] = nf
             out["mixing"] = mixing_index(c2, self.M, mask=self.mask_inner)

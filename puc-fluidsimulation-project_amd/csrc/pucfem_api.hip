@@ -30,6 +30,18 @@
 using namespace pucfem;
 using namespace pucfem::dev;
 
+// Kernel launches of this thread (pucfem_counters): every launch of the library goes through
+// hipLaunchKernelGGL (redefined here to count) or Ctx::klaunch.
+namespace {
+thread_local int64_t g_nlaunch = 0;
+}
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(kernelName, ...) \
+  do {                                      \
+    ++g_nlaunch;                            \
+    hipLaunchKernelGGLInternal((kernelName), __VA_ARGS__); \
+  } while (0)
+
 // LocalComm reduction (fixed rank order -> identical result on every rank)
 __global__ void pucfem::k_comm_reduce(int world, int is_max, size_t n, const double* const* bufs, double* out) {
   for (size_t i = threadIdx.x; i < n; i += blockDim.x) {
@@ -79,9 +91,9 @@ struct DevSell {
 };
 
 // A lattice operator's face part on the host (pucfem_lattice.hpp): the FaceDev image and its work
-// items.  Partial-producing launches cap the face blocks (the partial arrays hold MAXB blocks in all),
-// the others give every item a block.
-constexpr int32_t FACE_PART_BLOCKS = 4096;
+// items.  Partial-producing launches cap the face blocks (the partial arrays hold MAXB blocks in all;
+// at L7 every item still gets its own block), the others give every item a block.
+constexpr int32_t FACE_PART_BLOCKS = MAXB - 8192;
 struct HFace {
   FaceDev d{};
   int32_t items = 0;
@@ -226,20 +238,20 @@ void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* 
 // k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size
 template <int M>
 void mdot2_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* b, const double* av,
-                  const double* v, const int32_t* master_of, double* part) {
-  hipLaunchKernelGGL(k_mdot2<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, b, av, v, master_of, part);
+                  const double* v, const int32_t* master_of, double* part, RedOut ro) {
+  hipLaunchKernelGGL(k_mdot2<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, b, av, v, master_of, part, ro);
 }
 using Mdot2Fn = void (*)(hipStream_t, int, int64_t, const ProjT*, int64_t, const double*, const double*,
-                         const double*, const int32_t*, double*);
+                         const double*, const int32_t*, double*, RedOut);
 template <int... M>
 constexpr std::array<Mdot2Fn, sizeof...(M)> mdot2_table(std::integer_sequence<int, M...>) {
   return {&mdot2_launch<M>...};
 }
 void mdot2_on(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, int m, const double* b, const double* av,
-              const double* v, const int32_t* master_of, double* part) {
+              const double* v, const int32_t* master_of, double* part, RedOut ro) {
   static constexpr auto tab = mdot2_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
   if (m < 0 || m > PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
-  tab[m](s, nb, n, X, ld, b, av, v, master_of, part);
+  tab[m](s, nb, n, X, ld, b, av, v, master_of, part, ro);
 }
 template <int M>
 void pcomb_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* K, const double* v,
@@ -272,6 +284,10 @@ struct Ctx {
   hipStream_t st = nullptr;
   std::vector<void*> allocs;
   Timer timer;
+  // algorithmic bytes of the launched kernels (pucfem_counters: the step's HBM floor): each vector
+  // counted once per row it is read or written, stored operators per entry; launches that find their
+  // solve already converged (no work) are taken back once the host learns the iteration count
+  double algo_bytes = 0.0;
 
   // ---- inputs
   HostMesh mesh;
@@ -515,7 +531,7 @@ struct Ctx {
     if (!built) throw Error(PUCFEM_ESTATE, "pucfem_build_operators has not been called");
   }
 
-  static int nb_for(i64 nslices) { return (int)std::max<i64>(1, std::min<i64>(MAXB, (nslices + 3) / 4)); }
+  static int nb_for(i64 nslices) { return (int)std::max<i64>(1, std::min<i64>(EWB, (nslices + 3) / 4)); }
   // grid of the V-cycle kernels that produce no partials (more waves in flight than MAXB blocks)
   int mg_nb_max = 16384;
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
@@ -530,8 +546,10 @@ struct Ctx {
   // rocprofv3 reports it, without the command-processor gap a separately recorded event adds.
   template <typename... KArgs, typename... Args>
   void klaunch(int cls, double bytes, void (*kernel)(KArgs...), dim3 g, dim3 b, Args... args) {
+    algo_bytes += bytes;
     if (timer.on && cls >= 0 && ((timer.mask >> cls) & 1u)) {
       hipEvent_t a = timer.get(), e = timer.get();
+      ++g_nlaunch;
       hipExtLaunchKernelGGL(kernel, g, b, 0, st, a, e, 0, args...);
       timer.pend.push_back({cls, a, e, bytes});
       if (timer.pend.size() > 4096) timer.flush();  // bounded number of live events
@@ -541,22 +559,44 @@ struct Ctx {
   }
   // k_sl over rows [row0, row0 + n) of the full replica c (cout: the new values), either locator
   void sl_launch(int nb, i64 row0, i64 n, const double* vx, const double* vy, double dt, const double* cf, double* cn,
-                 const double* w, int32_t* nf) {
+                 const double* w, int32_t* nf, RedOut ro = RedOut{}) {
     const MeshDev M{mx, my, mtri, mesh.T};
     if (lat_sl) {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
       klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
-              dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
+              dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
     } else {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
       klaunch(8, 0.0, k_sl_slow<LocDev>, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt,
-              cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
+              cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
     }
   }
 
 
+
+  // ------------------------------------------------------------------ fused reductions
+  // The step's partial-producing kernels reduce their own partials (RedOut: the last block to finish
+  // sums them, pucfem_kernels.hpp) instead of a k_reduce launch after them.  One ticket counter per
+  // launch site (a site's launches are ordered on its stream; the dye stream's sites have their own).
+  // Off by default (PUCFEM_FUSED_RED=1 turns it on, a measurement knob): at L7 the fused path ran 101.4
+  // steps/s against 107.2 with k_reduce (r8a/r8b, same box type): under streaming load each block's
+  // write-through partial store and returned ticket (two memory round trips in the block's tail) cost
+  // 10-25 us per producer launch, more than the 9-14 us k_reduce launch they remove.
+  enum { CNT_VCHEB, CNT_INIT, CNT_RZ, CNT_DIR, CNT_UPD, CNT_DIV, CNT_MDOT, CNT_MIX, CNT_SL, CNT_DYE_DIV = 16,
+         CNT_DYE_SL, CNT_DYE_MIX, CNT_N = 32 };
+  unsigned* dcnt = nullptr;
+  bool fused_red = std::getenv("PUCFEM_FUSED_RED") && std::atoi(std::getenv("PUCFEM_FUSED_RED")) != 0;
+  RedOut ro(double* out, int cnt, int nv, int stride = MAXB, unsigned maxmask = 0u, double* out1 = nullptr) const {
+    if (!fused_red || !dcnt) return RedOut{};
+    return RedOut{out, out1, dcnt + cnt, nv, stride, maxmask};
+  }
+  // after a fused reduction into out[0..nv): the all-reduce across ranks
+  void red_done(double* out, int nv, bool is_max) {
+    if (dist()) comm->allreduce(out, nv, is_max, st);
+  }
+  RedOut ro_rz{};  // the finest level's last smoothing step (<r, z>), set by pcg_mg around precondition()
 
   // ------------------------------------------------------------------ communication
   // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
@@ -712,9 +752,10 @@ struct Ctx {
     if (NR == 2) halo(y[0], y[1]);
     else halo(y[0]);
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    algo_bytes += (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 32.0 * NR * (double)A.own();
     with_c16(A, [&](auto c16) {
       hipLaunchKernelGGL((k_cg_init<NR, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, A.view(), fc, val, v,
-                         lp.n_ghost, part_a, part_b, (float*)nullptr, 1);
+                         lp.n_ghost, part_a, part_b, (float*)nullptr, 1, RedOut{});
     });
     KCHK();
     Red rr = reduce_global(part_a, nb, NR, false, 0);
@@ -732,8 +773,12 @@ struct Ctx {
     // host convergence checks: the first after as many iterations as the last solve took (the control
     // test after each update lets the check see convergence without a further launch)
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
+    std::vector<double> bmark;  // algo_bytes at the start of each iteration of the current chunk
     for (;;) {
+      const int it0 = it;
+      bmark.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
+        bmark.push_back(algo_bytes);
         // HIP-event timing samples every 8th iteration (bounded event count for long solves)
         const bool samp = (it & 7) == 0;
         with_c16(A, [&](auto c16) {
@@ -753,6 +798,8 @@ struct Ctx {
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       if (timer.on) timer.flush();
+      // iterations from the converged one on were launched but did no work
+      if (h_ctl[0] && h_ctl[1] >= it0 && h_ctl[1] < it) algo_bytes = bmark[h_ctl[1] - it0];
       if (h_ctl[0]) break;
       chunk = std::max(1, std::min(64, it / 8));
     }
@@ -800,10 +847,13 @@ struct Ctx {
         v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
       }
       // timing class 9; the first step reads no d (4 B/row per right-hand side less)
+      // step 0 reduces its own partials (fused): |r_0|^2 into redbuf[0 .. NR), |b|^2 into redbuf[NR .. 2 NR)
+      const RedOut r0 = it == 0 ? ro(redbuf, CNT_VCHEB, 2 * NR) : RedOut{};
+      double* pb = it == 0 ? (r0.out ? part_a + NR * MAXB : part_b) : (double*)nullptr;
       with_c16(A, [&](auto c16) {
         klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
                 dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl,
-                it == 0 ? part_a : (double*)nullptr, it == 0 ? part_b : (double*)nullptr);
+                it == 0 ? part_a : (double*)nullptr, pb, r0);
       });
       KCHK();
       halo_x(xb);
@@ -816,8 +866,13 @@ struct Ctx {
     // [visc_lo, 1 + visc_R], which tests/test_host_assembly.py checks against the spectrum; the
     // adaptive test it replaces needed one extra step per solve to see the passing residual.)
     step(0, 0.0, 1.0 / theta);
-    Red rr = reduce_global(part_a, nb, NR, false, 0);
-    Red bb = reduce_global(part_b, nb, NR, false, 1);
+    Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
+    if (ro(redbuf, CNT_VCHEB, 2 * NR).out) {
+      red_done(redbuf, 2 * NR, false);
+    } else {
+      rr = reduce_global(part_a, nb, NR, false, 0);
+      bb = reduce_global(part_b, nb, NR, false, 1);
+    }
     HIPCHK(hipMemcpyAsync(h_pinned, rr.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(h_pinned + 8, bb.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
     hipEvent_t have_r0 = timer.get();
@@ -943,13 +998,14 @@ struct Ctx {
           else zo = z;
           if (toz)
             klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
-                    (const T*)B.dinv, b, xi, zo, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+                    (const T*)B.dinv, b, xi, zo, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part,
+                    rd ? ro_rz : RedOut{});
           else if (finest)
             klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
-                    (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+                    (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{});
           else
             klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), fc, val, (const T*)B.dinv, b,
-                    xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part);
+                    xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{});
         });
       });
       KCHK();
@@ -976,6 +1032,7 @@ struct Ctx {
       if constexpr (std::is_same<T, TB>::value) {
         // coarsest: dense pseudo-inverse (replicated on every rank of a multi-rank run)
         const i64 N0 = (i64)L.ord.new2old.size();
+        algo_bytes += 8.0 * (double)N0 * (double)N0 + 2.0 * sizeof(T) * (double)N0;
         hipLaunchKernelGGL(k_dense_mv<T>, dim3((unsigned)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0,
                            dAinv, b, xa, ctl);
         KCHK();
@@ -1072,16 +1129,28 @@ struct Ctx {
     // keeps r0 in pav (its "first direction" output; pcg_mg's directions live elsewhere)
     const bool keep_r0 = proj_k > 0 && (which == 1 || which == 2);
     if (keep_r0) vi.po[0] = pav[which];
+    algo_bytes += (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
+                  (24.0 + (mg_single ? 4.0 : 0.0) + (keep_r0 ? 8.0 : 0.0)) * (double)n;
+    // fused reductions: <r, r> -> redbuf slot 0, <b, b> -> slot 1 (as k_reduce would place them)
+    const RedOut ri = ro(redbuf, CNT_INIT, 2, MAXB, 0u, redbuf + 8);
     with_c16(dPp, [&](auto c16) {
       hipLaunchKernelGGL((k_cg_init<1, decltype(c16)::value>), dim3(nb), dim3(BS), 0, st, dPp.view(), fc, dKp_raw, vi,
-                         lp.n_ghost, part_a, part_b, r32o, keep_r0 ? 1 : 0);
+                         lp.n_ghost, part_a, ri.out ? part_a + MAXB : part_b, r32o, keep_r0 ? 1 : 0, ri);
     });
     KCHK();
-    Red rr = reduce_global(part_a, nb, 1, false, 0);
-    Red bb = reduce_global(part_b, nb, 1, false, 1);
+    Red rr{redbuf, 1, 1}, bb{redbuf + 8, 1, 1};
+    if (ri.out) {
+      red_done(redbuf, 1, false);
+      red_done(redbuf + 8, 1, false);
+    } else {
+      rr = reduce_global(part_a, nb, 1, false, 0);
+      bb = reduce_global(part_b, nb, 1, false, 1);
+    }
+    const RedOut rdir = ro(redbuf + 16, CNT_DIR, 1), rupd = ro(redbuf, CNT_UPD, 1);
     const double tol2 = tol * tol;
     // (iteration, first timing sample): samples from the converged iteration on are dropped
     std::vector<std::pair<int, size_t>> marks;
+    std::vector<std::pair<int, double>> bmarks;  // (iteration, algo_bytes at its start) of the current chunk
     hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
     KCHK();
     // direction: z (4 B in the fp32 cycle) and p_old gathered once, p and q written
@@ -1096,30 +1165,39 @@ struct Ctx {
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 1 ? last_it[which] - 1 : (last_it[which] ? 1 : 4)));
     for (bool first = true;; first = false) {
       if (!first) marks.clear();  // the previous chunk's samples are flushed
+      bmarks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
         marks.push_back({it, timer.pend.size()});  // this iteration's V-cycle works iff not converged at it
+        bmarks.push_back({it, algo_bytes});
+        ro_rz = ro(redbuf + 32, CNT_RZ, 1);
         precondition();
-        Red rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
+        ro_rz = RedOut{};
+        Red rz{redbuf + 32, 1, 1};
+        if (ro(redbuf + 32, CNT_RZ, 1).out) red_done(redbuf + 32, 1, false);
+        else rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
         if (mg_single) mg_halo(mg.back(), z32);
         else halo(z);
         with_c16(dPp, [&](auto c16) {
           if (mg_single)
             klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
                     (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl,
-                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride, rdir);
           else
             klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value>, dim3(nb), dim3(BS), dPp.view(), fc,
                     (const double*)dKp_raw, v, lp.n_ghost, rz.p, rz.nb, rz.stride, bb.p, bb.nb, bb.stride, scal, ctl,
-                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride);
+                    it, maxit, tol2, part_c, rr.p, rr.nb, rr.stride, rdir);
         });
         KCHK();
-        Red pq = reduce_global(part_c, nb, 1, false, 2);
+        Red pq{redbuf + 16, 1, 1};
+        if (rdir.out) red_done(redbuf + 16, 1, false);
+        else pq = reduce_global(part_c, nb, 1, false, 2);
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
         klaunch(2, bytes_upd, k_cg_upd<1>, dim3(nbu), dim3(BS), vu, n, pq.p, pq.nb, pq.stride,
-                (const double*)scal, (const int*)ctl, part_a, r32o);
+                (const double*)scal, (const int*)ctl, part_a, r32o, rupd);
         KCHK();
-        rr = reduce_global(part_a, nbu, 1, false, 0);
+        if (rupd.out) rr = Red{redbuf, 1, 1}, red_done(redbuf, 1, false);
+        else rr = reduce_global(part_a, nbu, 1, false, 0);
         hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, 1);
         KCHK();
         std::swap(v.po[0], v.pn[0]);
@@ -1135,6 +1213,12 @@ struct Ctx {
             }
         timer.flush();
       }
+      if (h_ctl[0])  // the bytes of the iterations that found the solve converged did not move
+        for (auto& bm : bmarks)
+          if (bm.first >= h_ctl[1]) {
+            algo_bytes = bm.second;
+            break;
+          }
       if (h_ctl[0]) break;
       chunk = it < 8 ? 1 : std::min(16, it / 4);
     }
@@ -1171,6 +1255,7 @@ struct Ctx {
     VincDev vd{};
     vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
     for (int k = 0; k < 2 * VINC_MAX; ++k) vd.d[k] = dvinc[k];
+    algo_bytes += (64.0 + 8.0 * vd.order) * (double)n;  // u, s, sq, the increments read; b, y written
     hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
     KCHK();
     double* y[2] = {yvx, yvy};
@@ -1191,6 +1276,7 @@ struct Ctx {
     }
     if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
       const int last = 2 * (visc_extrap - 1);
+      algo_bytes += 64.0 * (double)n;  // s, y, u read; u*, the fp32 increment written
       hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yo[0], yo[1], ux, uy, usx, usy,
                          dvinc[last], dvinc[last + 1]);
       for (int k = last; k >= 2; k -= 2) {
@@ -1199,6 +1285,7 @@ struct Ctx {
       }
       have_vinc = std::min(have_vinc + 1, visc_extrap);
     } else {
+      algo_bytes += 40.0 * (double)n;
       hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yo[0], yo[1], usx, usy,
                          (const int32_t*)nullptr);
     }
@@ -1209,21 +1296,24 @@ struct Ctx {
   }
   // grid of k_div (its partials: max |div|, sum braw)
   int div_grid() const { return grid_part(fK.part(), dP); }
-  void div(const double* ax, const double* ay, double* out, bool rhs, double* part = nullptr) {
+  void div(const double* ax, const double* ay, double* out, bool rhs, double* part = nullptr, RedOut r = RedOut{}) {
     const FaceDev fc = fK.part();
     with_c16(dP, [&](auto c16) {
       klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
               k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
-              rhs ? braw : (double*)nullptr, part ? part : part_d);
+              rhs ? braw : (double*)nullptr, part ? part : part_d, r);
     });
     KCHK();
   }
-  int pressure(double* yst, double* pout, int which) {  // StokesColor.py:554-555 (restated)
+  // sb_fused: the preceding k_div reduced sum(braw) into redbuf slot 3 itself (div_rhs)
+  int pressure(double* yst, double* pout, int which, bool sb_fused = false) {  // StokesColor.py:554-555 (restated)
     const int nb = div_grid();
-    Red sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
+    Red sb{redbuf + 24, 1, 1};
+    if (!sb_fused) sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
     const i64 n = lp.n_own;
     const double* sc = (use_mg || dense) ? nullptr : dsp;  // MG and dense paths solve the unscaled system
+    algo_bytes += 24.0 * (double)n;  // braw, slave_of, master_of read; bh written
     hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
                        sb.p, sb.nb, 1.0 / (double)n_free, bh);
     KCHK();
@@ -1244,6 +1334,7 @@ struct Ctx {
       const double* b[1] = {bh};
       it = cg<1>(dPp, HFace{}, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
     }
+    algo_bytes += (20.0 + (sc ? 8.0 : 0.0)) * (double)n;  // master_of, y (, s) read; p written
     hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
                        (double*)nullptr, dmaster_of);
     KCHK();
@@ -1272,8 +1363,10 @@ struct Ctx {
       return;
     }
     const int nb = grid_ew(n);
-    mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, 2 * m + 4, 0, proj_d);
+    algo_bytes += (4.0 * m + 24.0) * (double)n;  // k_mdot2: X (fp32), b, A v, v
+    const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
+    mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part, rmd);
+    if (!rmd.out) hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, 2 * m + 4, 0, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
     QMat qm{};
@@ -1283,6 +1376,7 @@ struct Ctx {
                        1.0 / (double)n_free, proj_coef);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
+    algo_bytes += (4.0 * kq + 32.0) * (double)n;  // k_pcomb: X, v read; the new direction, x0, y written
     pcomb_on(st, nb, n, projX[which], nloc, kq, proj_coef, pv[which], op.null_free, projX[which] + (i64)kq * nloc, y,
              proj_x0[which]);
     H.coef_m = kq;
@@ -1347,6 +1441,7 @@ struct Ctx {
     for (int i = 0; i < kq; ++i)
       for (int j = 0; j < m; ++j) qm.q[i][j] = Q[i][j];
     const i64 n = lp.n_own;
+    algo_bytes += 4.0 * (double)(m + kq) * (double)n;
     hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], nloc, m, qm, kq,
                        projXalt[which]);
     KCHK();
@@ -1367,6 +1462,7 @@ struct Ctx {
     double *v = pv[which], *av = pav[which];
     if (r_final) {  // v = y - x0 and A v = r0 - r_final in one pass
       const bool whole = proj_m[which] == 0;
+      algo_bytes += 48.0 * (double)n;
       hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], v,
                          whole ? b : (const double*)av, r_final, av);
       KCHK();
@@ -1377,6 +1473,16 @@ struct Ctx {
       spmv_on(st, *op.A, op.fc, op.val, v, av);
     }
     proj_pend[which] = true;
+  }
+  // k_div with the pressure right-hand side; max |div| into maxout (a vals slot, or scratch), sum(braw)
+  // into redbuf slot 3 (pressure's sb) -- fused when enabled (returns whether it was)
+  bool div_rhs(const double* ax, const double* ay, double* out, double* maxout) {
+    const RedOut r = ro(maxout, CNT_DIV, 2, MAXB, 1u, redbuf + 24);
+    div(ax, ay, out, true, nullptr, r);
+    if (!r.out) return false;
+    if (maxout != redbuf + 40) red_done(maxout, 1, true);  // (redbuf slot 5: an unrecorded maximum)
+    red_done(redbuf + 24, 1, false);
+    return true;
   }
   void grad_proj(const double* pp, int mode) {
     const FaceDev fc = fK.full();
@@ -1409,18 +1515,19 @@ struct Ctx {
   }
 
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
+  RedOut sl_ro{};
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
-    div(usx, usy, div_star, true);
-    reduce_into(part_d, div_grid(), 1, true, 0);  // max |div u*|
-    const int itp = pressure(yp, p, 1);
+    const bool f1 = div_rhs(usx, usy, div_star, vals);  // max |div u*| -> vals[0]
+    if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
+    const int itp = pressure(yp, p, 1, f1);
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
     grad_proj(p, 0);
     bc(ux, uy);
     halo(ux, uy);
-    div(ux, uy, div_u, true);
-    const int itp2 = pressure(yp2, p2, 2);
+    const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
+    const int itp2 = pressure(yp2, p2, 2, f2);
     grad_proj(p2, 1);
     halo(ux, uy);
     // single-rank explicit dye: the final-divergence record and the advection of this step (they read
@@ -1429,8 +1536,10 @@ struct Ctx {
     // for them before its next write to u (sl_join above)
     const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && !dist();
     if (!ovl) {
-      div(ux, uy, final_div, false);
-      reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
+      const RedOut r = ro(vals + 1, CNT_DIV, 1, MAXB, 1u);
+      div(ux, uy, final_div, false, nullptr, r);
+      if (r.out) red_done(vals + 1, 1, true);
+      else reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     }
     if (ovl) {
       if (!st_sl) {
@@ -1456,18 +1565,22 @@ struct Ctx {
       HIPCHK(hipStreamWaitEvent(st_sl, ev_u, 0));
       {
         StreamSwap sw(st, st_sl);
-        div(ux, uy, final_div, false, part_fd);
-        reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
+        const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
+        div(ux, uy, final_div, false, part_fd, rf);
+        if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
         const int nb = nb_sl(lp.n_own);
-        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
+        const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
+        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
         KCHK();
         std::swap(c_full, c_new);
-        reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+        if (!rs.out) reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
         const int nbm = nb_rows(lp.n_own);
+        algo_bytes += 16.0 * (double)lp.n_own;  // c, w
+        const RedOut rm = ro(vals + 5, CNT_DYE_MIX, 1);
         hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
-                           part_mx);
+                           part_mx, rm);
         KCHK();
-        reduce_into(part_mx, nbm, 1, false, 5);
+        if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
         KCHK();
       }
@@ -1481,7 +1594,8 @@ struct Ctx {
                            (const double*)dwmix, part_sl);
       } else {
         dye_halo(uy, prm.dt);
-        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr);
+        sl_ro = ro(vals + 2, CNT_SL, 3, SLB);
+        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, sl_ro);
       }
       KCHK();
       if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
@@ -1491,11 +1605,16 @@ struct Ctx {
       } else {
         std::swap(c_full, c_new);
       }
-      reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+      if (sl_ro.out) red_done(vals + 2, 3, false);
+      else reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+      sl_ro = RedOut{};
       const int nbm = nb_rows(lp.n_own);
-      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx);
+      algo_bytes += 16.0 * (double)lp.n_own;
+      const RedOut rm = ro(vals + 5, CNT_MIX, 1);
+      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx, rm);
       KCHK();
-      reduce_into(part_mx, nbm, 1, false, 5);
+      if (rm.out) red_done(vals + 5, 1, false);
+      else reduce_into(part_mx, nbm, 1, false, 5);
     } else {
       tracer_advance(prm.dt);
     }
@@ -2617,6 +2736,7 @@ void build(Ctx& c) {
   c.scal = c.dalloc<double>(32);
   c.ctl = c.dalloc<int>(4);
   c.redbuf = c.dalloc<double>(8 * 64);
+  c.dcnt = c.dalloc<unsigned>(Ctx::CNT_N);
   c.vals = c.dalloc<double>(16);
   c.bicg_sc = c.dalloc<double>(16);
   if (literal || c.dye_impl) {
@@ -3275,7 +3395,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         perm_in(x, 2, t0, t1);
         with_c16(c.dP, [&](auto c16) {
           hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(c.div_grid()), dim3(BS), 0, c.st, c.dP.view(),
-                             c.fK.part(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d);
+                             c.fK.part(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d, RedOut{});
         });
         KCHK();
         perm_out(y, 1, o0, nullptr);
@@ -3538,7 +3658,7 @@ static void mixing_on(Ctx& c, const double* cin, const double* w, double* out3) 
   hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, c.st, N, w, (const double*)on, (const double*)nullptr,
                      (const double*)nullptr, c.part_b);
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_b, nb, MAXB, 1, 0, c.vals + 3);
-  hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, w, c.vals + 2, 1, 1, c.part_c);
+  hipLaunchKernelGGL(k_mix2, dim3(nb), dim3(BS), 0, c.st, (int64_t)0, N, cf, w, c.vals + 2, 1, 1, c.part_c, RedOut{});
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, c.st, c.part_c, nb, MAXB, 1, 0, c.vals + 5);
   HIPCHK(hipMemsetAsync(c.vals + 6, 0, 2 * sizeof(double), c.st));
   double* rec = c.vals + 8;
@@ -3607,6 +3727,14 @@ int pucfem_timing_get(void* ctx, int32_t k, double* ms, int64_t* n, double* byte
     *ms = c.timer.ms[k];
     *n = c.timer.n[k];
     *bytes = c.timer.n[k] ? c.timer.bytes[k] / (double)c.timer.n[k] : 0.0;
+  });
+}
+
+int pucfem_counters(void* ctx, int64_t* launches, double* bytes) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    *launches = g_nlaunch;
+    *bytes = c.algo_bytes;
   });
 }
 
@@ -4049,31 +4177,31 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(ff.nb + 8), dim3(BS), 0, c.st, a, e, 0,
                                   none, ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
                                   (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
-                                  (const double*)nullptr, (double*)nullptr);
+                                  (const double*)nullptr, (double*)nullptr, RedOut{});
             break;
           case 4:  // the SELL (skeleton) part alone
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(c.nb_mg(A.nslices)), dim3(BS), 0, c.st,
                                   a, e, 0, A.view(), FaceDev{}, (const float*)B.Aval, (const float*)B.dinv,
                                   (const float*)c.r32, (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1,
-                                  (const int*)nullptr, (const double*)nullptr, (double*)nullptr);
+                                  (const int*)nullptr, (const double*)nullptr, (double*)nullptr, RedOut{});
             break;
           case 5:  // k_cg_dir, the face part alone
             hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(fpt.nb + 8), dim3(BS), 0, c.st, a, e, 0, none, fpt,
                                   (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
                                   (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
-                                  (const double*)nullptr, 0, 0);
+                                  (const double*)nullptr, 0, 0, RedOut{});
             break;
           case 6:  // k_cg_dir, the SELL (skeleton) part alone
             hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(Ctx::nb_for(A.nslices)), dim3(BS), 0, c.st, a, e, 0,
                                   A.view(), FaceDev{}, (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one,
                                   1, 1, (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
-                                  (const double*)nullptr, 0, 0);
+                                  (const double*)nullptr, 0, 0, RedOut{});
             break;
           case 0:
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0,
                                   A.view(), ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
                                   (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
-                                  (const double*)nullptr, (double*)nullptr);
+                                  (const double*)nullptr, (double*)nullptr, RedOut{});
             break;
           case 1:
             hipExtLaunchKernelGGL(k_resid<float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0, A.view(),
@@ -4084,7 +4212,7 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
             hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(nb), dim3(BS), 0, c.st, a, e, 0, A.view(), fpt,
                                   (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
                                   (const double*)one, 1, 1, c.scal, ctl0, 1, 1 << 30, 0.0, c.part_c,
-                                  (const double*)nullptr, 0, 0);
+                                  (const double*)nullptr, 0, 0, RedOut{});
         }
       });
       KCHK();
@@ -4108,7 +4236,7 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
           hipLaunchKernelGGL((k_cheb<float, float, float, float, C16, 0>), dim3(c.grid_full(Lc.hA.full(), Lc.dA)), dim3(BS),
                              0, c.st, Lc.dA.view(), Lc.hA.full(), (const float*)Lc.f32.Aval, (const float*)Lc.f32.dinv,
                              (const float*)Lc.f32.b, (const float*)nullptr, Lc.f32.x2, Lc.f32.d, 0.3, 0.7, 0.0, 2,
-                             (const int*)nullptr, (const double*)nullptr, (double*)nullptr);
+                             (const int*)nullptr, (const double*)nullptr, (double*)nullptr, RedOut{});
         });
         KCHK();
       }

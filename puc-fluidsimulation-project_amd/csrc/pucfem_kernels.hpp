@@ -19,7 +19,11 @@ namespace pucfem {
 namespace dev {
 
 constexpr int BS = 256;     // threads per block
-constexpr int MAXB = 8192;  // max blocks of a partial-producing launch (= partial stride)
+// max blocks of a partial-producing launch (= partial stride): a lattice kernel's full grid (one block per
+// 1,024-row face item, dealt XCD-contiguously, plus the skeleton SELL blocks: ~15.3k at L7) fits, so the
+// kernels that produce partials get the same item mapping as the others
+constexpr int MAXB = 32768;
+constexpr int EWB = 8192;   // max blocks of a row-wise (SELL / elementwise) grid
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
 constexpr int SLB = 4096;   // max blocks (= partial stride) of the semi-Lagrangian kernel
 #ifndef PUCFEM_FACE_RPT
@@ -130,6 +134,72 @@ __device__ __forceinline__ double reduce_partials_max(const double* p, int nb, d
   double a = 0.0;
   for (int i = threadIdx.x; i < nb; i += BS) a = fmax(a, p[i]);
   return block_max(a, sh);
+}
+
+// ---- in-kernel reduction of a launch's per-block partials (replaces the one-block k_reduce launch
+// that followed every partial-producing kernel, and its kernel boundary).  Every block's thread 0
+// stores the block's partials write-through (agent-scope relaxed atomic stores: `sc1`, no L2 copy
+// kept), drains them (s_waitcnt vmcnt(0)) and draws a ticket from an agent-scope counter; the block
+// drawing the last ticket reads every partial with `sc1` loads (agent-scope relaxed atomic loads, so no
+// stale L1 / L2 line can serve them) in block order, reduces them in a fixed order, writes the values
+// and resets the counter.  MI355X_MICROARCH.md "inter-workgroup visibility": the R1 counter form
+// (every handed-off byte stored sc1 and drained before the ticket, every load of it sc1).
+// Deterministic: for a given grid the combination order is fixed, whichever block finishes last.
+struct RedOut {
+  double* out;       // value v -> out[v]; null: no in-kernel reduction (the partials stay for k_reduce)
+  double* out1;      // non-null: value 1 -> out1[0] instead (k_div: a max and a sum with different homes)
+  unsigned* cnt;     // ticket counter, 0 between launches
+  int nv;            // values
+  int stride;        // partial stride (value v of block b at part[v * stride + b])
+  unsigned maxmask;  // bit v: value v is a maximum (of values >= 0), else a sum
+};
+__device__ __forceinline__ void red_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double red_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Called by every thread of every block after thread 0 stored the block's partials with red_store
+// (and, as every block must, with no early return before it).  sh: >= 4 doubles of LDS.
+// all_waves: partials were stored by several waves (each drains its stores before the barrier).
+__device__ __forceinline__ void red_finish(const RedOut& R, const double* part, double* sh, bool all_waves = false) {
+  if (!R.out) return;
+  __shared__ int last;
+  if (all_waves) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partials have left the CU
+    const unsigned t = __hip_atomic_fetch_add(R.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction) the loads stay below the ticket
+  const int nb = gridDim.x;
+  for (int v = 0; v < R.nv; ++v) {
+    const bool mx = (R.maxmask >> v) & 1u;
+    const double* p = part + (int64_t)v * R.stride;
+    double a = 0.0;
+    for (int i = threadIdx.x; i < nb; i += BS) {
+      const double x = red_load(p + i);
+      a = mx ? fmax(a, x) : a + x;
+    }
+    const double r = mx ? block_max(a, sh) : block_sum(a, sh);
+    if (threadIdx.x == 0) {
+      if (v == 1 && R.out1) R.out1[0] = r;
+      else R.out[v] = r;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(R.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// thread 0: partial of value v of this block
+__device__ __forceinline__ void red_part(const RedOut& R, double* part, int v, double x) {
+  if (R.out) red_store(part + (int64_t)v * R.stride + blockIdx.x, x);
+  else part[(int64_t)v * R.stride + blockIdx.x] = x;
 }
 
 // wave index inside the block as a wave-uniform (scalar) value: slice indices derived from it stay

@@ -184,7 +184,8 @@ __device__ __forceinline__ double cg_rg(const CgVecs<NR>& v, int c, int64_t j) {
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                 int64_t n_ghost, double* part_rr, double* part_bb,
-                                                float* __restrict__ r32 = nullptr, int write_p = 0) {
+                                                float* __restrict__ r32 = nullptr, int write_p = 0,
+                                                RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   double rr[NR], bb[NR];
 #pragma unroll
@@ -264,10 +265,16 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
     const double t = block_sum(rr[c], sh);
     const double u = block_sum(bb[c], sh);
     if (threadIdx.x == 0) {
-      part_rr[c * MAXB + blockIdx.x] = t;
-      part_bb[c * MAXB + blockIdx.x] = u;
+      if (ro.out) {  // fused reduction: <r, r> values 0 .. NR-1, <b, b> values NR .. 2 NR - 1 of part_rr
+        red_part(ro, part_rr, c, t);
+        red_part(ro, part_rr, NR + c, u);
+      } else {
+        part_rr[c * MAXB + blockIdx.x] = t;
+        part_bb[c * MAXB + blockIdx.x] = u;
+      }
     }
   }
+  red_finish(ro, part_rr, sh);
 }
 
 // One SELL slice of q = A^ (r + beta p_old): WMAX > 0 unrolls the entry loop (all index/value
@@ -339,7 +346,8 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
                                                int* ctl, int it, int maxit, double tol2, double* part_pq,
-                                               const double* part_cv = nullptr, int nb_cv = 0, int stride_cv = 0) {
+                                               const double* part_cv = nullptr, int nb_cv = 0, int stride_cv = 0,
+                                               RedOut ro = RedOut{}) {
   // part_rr: numerator of beta (<r,r> for CG, <r,z> for preconditioned CG); part_cv (if given):
   // <r,r> for the convergence test; part_bb: <b,b>.
   __shared__ double sh[4];
@@ -438,14 +446,15 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
     const double t = block_sum(pq[c], sh);
-    if (threadIdx.x == 0) part_pq[c * MAXB + blockIdx.x] = t;
+    if (threadIdx.x == 0) red_part(ro, part_pq, c, t);
   }
+  red_finish(ro, part_pq, sh);
 }
 
 template <int NR>
 __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, const double* part_pq, int nb_pq,
                                                int stride_pq, const double* scal, const int* ctl, double* part_rr,
-                                               float* __restrict__ r32 = nullptr) {
+                                               float* __restrict__ r32 = nullptr, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   if (ctl[0]) return;
   double alpha[NR], rr[NR];
@@ -470,8 +479,9 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
     const double t = block_sum(rr[c], sh);
-    if (threadIdx.x == 0) part_rr[c * MAXB + blockIdx.x] = t;
+    if (threadIdx.x == 0) red_part(ro, part_rr, c, t);
   }
+  red_finish(ro, part_rr, sh);
 }
 
 // ----------------------------------------------------------------------------- solution projection
@@ -517,7 +527,7 @@ template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
                                               const double* __restrict__ v, const int32_t* __restrict__ master_of,
-                                              double* part) {
+                                              double* part, RedOut ro) {
   constexpr int NA = 2 * M + 4;
   __shared__ double sh[NA][4];
   double acc[NA];
@@ -547,8 +557,8 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
     if ((threadIdx.x & 63) == 0) sh[i][threadIdx.x >> 6] = t;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NA; i += BS)
-    part[(int64_t)i * MAXB + blockIdx.x] = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
+  for (int i = threadIdx.x; i < NA; i += BS) red_part(ro, part, i, (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]));
+  red_finish(ro, part, sh[0], true);  // (several waves stored partials)
 }
 
 // pass 1 -> coefficients (one thread).  D: the reduced dots of k_mdot2 over m vectors; kq >= 0: the
@@ -814,7 +824,7 @@ struct ChebVecs {
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
                                               double c1, double c2, int first, const int* ctl, double* part_rr,
-                                              double* part_bb) {
+                                              double* part_bb, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   if (ctl[0]) return;
   double rr[NR], bb[NR];
@@ -919,12 +929,18 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
 #pragma unroll
   for (int c = 0; c < NR; ++c) {
     const double t1 = block_sum(rr[c], sh);
-    if (threadIdx.x == 0) part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
-    if (part_bb) {
-      const double t2 = block_sum(bb[c], sh);
-      if (threadIdx.x == 0) part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
+    const double t2 = part_bb ? block_sum(bb[c], sh) : 0.0;
+    if (threadIdx.x == 0) {
+      if (ro.out) {  // fused reduction: |r_0|^2 values 0 .. NR-1, |b|^2 values NR .. 2 NR - 1 of part_rr
+        red_part(ro, part_rr, c, t1);
+        red_part(ro, part_rr, NR + c, t2);
+      } else {
+        part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
+        if (part_bb) part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
+      }
     }
   }
+  red_finish(ro, part_rr, sh);
 }
 
 // the recurrence CG's control after an update: converged (1), maxit (2), not finite (3); it = the
@@ -1043,7 +1059,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
                                             const double* __restrict__ gy, const double* __restrict__ ux,
                                             const double* __restrict__ uy, const double* __restrict__ as1,
                                             double* __restrict__ div, const double* __restrict__ mp, double negidt,
-                                            double* __restrict__ braw, double* part) {
+                                            double* __restrict__ braw, double* part, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   double mx = 0.0, sb = 0.0;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
@@ -1131,9 +1147,10 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
   const double t = block_max(mx, sh);
   const double u = block_sum(sb, sh);
   if (threadIdx.x == 0) {
-    part[blockIdx.x] = t;
-    part[MAXB + blockIdx.x] = u;
+    red_part(ro, part, 0, t);
+    red_part(ro, part, 1, u);
   }
+  red_finish(ro, part, sh);
 }
 
 // pressure RHS of the merged, range-projected, scaled system (oracle PressureSolver.rhs):
@@ -1811,7 +1828,8 @@ __global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int
                                                 const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                                 const double* __restrict__ c, double* __restrict__ cout,
                                                 const double* __restrict__ wmix, int32_t* notfound, double* part,
-                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt) {
+                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt,
+                                                RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   double swc = 0.0, nnf = 0.0;
   int64_t r0, r1;
@@ -1839,10 +1857,17 @@ __global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int
     swc += (wmix ? wmix[i] : 0.0) * cn;
   }
   const double a = block_sum(swc, sh), d = block_sum(nnf, sh);
-  if (threadIdx.x == 0) {
-    part[blockIdx.x] += a;
-    part[2 * SLB + blockIdx.x] += d;
+  if (threadIdx.x == 0) {  // k_sl's partials of this block (the same grid) plus this pass's
+    if (ro.out) {
+      red_part(ro, part, 0, part[blockIdx.x] + a);
+      red_part(ro, part, 1, part[SLB + blockIdx.x]);
+      red_part(ro, part, 2, part[2 * SLB + blockIdx.x] + d);
+    } else {
+      part[blockIdx.x] += a;
+      part[2 * SLB + blockIdx.x] += d;
+    }
   }
+  red_finish(ro, part, sh);
 }
 
 // the locator's answer for every row's own node (q = its node after the x wrap: zero velocity), once
@@ -1980,7 +2005,7 @@ __global__ __launch_bounds__(BS) void k_wsum(int64_t row0, int64_t n, const doub
 // mixing_index second pass (StokesColor.py:399-401): partial sum w (c - mu)^2, mu from pass 1.
 __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const double* __restrict__ c,
                                              const double* __restrict__ wmix, const double* part1, int nb1,
-                                             int stride1, double* part) {
+                                             int stride1, double* part, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   const double swc = reduce_partials(part1, nb1, sh);
   const double sw = reduce_partials(part1 + stride1, nb1, sh);
@@ -1993,7 +2018,8 @@ __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const doub
     acc += wmix[i] * (d * d);
   }
   const double t = block_sum(acc, sh);
-  if (threadIdx.x == 0) part[blockIdx.x] = t;
+  if (threadIdx.x == 0) red_part(ro, part, 0, t);
+  red_finish(ro, part, sh);
 }
 
 // ----------------------------------------------------------------------------- tracers
@@ -2566,7 +2592,7 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
                                              const T* __restrict__ dinv, const TB* __restrict__ b,
                                              const T* __restrict__ xin, TO* __restrict__ xout, T* __restrict__ d,
                                              double c1, double c2, double c20, int mode, const int* ctl,
-                                             const double* __restrict__ rdot, double* part) {
+                                             const double* __restrict__ rdot, double* part, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   if (ctl && ctl[0]) return;
   const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
@@ -2586,7 +2612,8 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
 #undef PUCFEM_CHEB
   if (rdot) {
     const double t = block_sum(acc_rz, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = t;
+    if (threadIdx.x == 0) red_part(ro, part, 0, t);
+    red_finish(ro, part, sh);
   }
 }
 

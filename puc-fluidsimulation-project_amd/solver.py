@@ -254,6 +254,13 @@ class Context:
         self._c(self.L.pucfem_timing_get(self.h, kclass, ct.byref(ms), ct.byref(n), ct.byref(b)))
         return ms.value, n.value, b.value
 
+    def counters(self):
+        """(kernel launches of this thread, algorithmic bytes of the context's kernels), cumulative
+        (pucfem_counters): differences over a timed region give launches and the HBM floor per step."""
+        n, b = ct.c_int64(), ct.c_double()
+        self._c(self.L.pucfem_counters(self.h, ct.byref(n), ct.byref(b)))
+        return n.value, b.value
+
     def sync(self):
         self._c(self.L.pucfem_sync(self.h))
 
