@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--mg-post", type=int, default=3, help="Chebyshev post-smoothing degree")
     ap.add_argument("--mg-ratio", type=float, default=15.0, help="Chebyshev interval [lmax / ratio, lmax]")
     ap.add_argument("--mg-kind", type=int, default=1, choices=[1, 4], help="Chebyshev smoother of the first / fourth kind")
-    ap.add_argument("--proj-k", type=int, default=24,
+    ap.add_argument("--proj-k", type=int, default=16,
                     help="pressure initial guess: A-projection onto the last K solutions (0: warm start only)")
     ap.add_argument("--proj-k-visc", type=int, default=0, help="the same for the viscous solve (0: warm start)")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],

@@ -274,6 +274,10 @@ int pucfem_comm_info(void* ctx, int64_t* out4);
    The replaced reference sites are the dot products inside the np.linalg.solve calls
    (StokesColor.py:544-545, 555, 569), which become all-reduced CG dots on multi-rank runs. */
 int pucfem_comm_selftest(void* ctx, double* out4);
+/* cumulative data-path traffic of this rank's communicator (zeros without one): out[0] all-reduce calls,
+   [1] all-reduced values, [2] point-to-point sends, [3] bytes sent, [4] grouped launches (group_start),
+   [5] broadcasts (DESIGN.md §7's per-step counts; measurement only) */
+int pucfem_comm_counters(void* ctx, int64_t* out6);
 /* The viscous Chebyshev iteration's interval for the Jacobi-scaled A_visc (StokesColor.py:471-475):
    out2 = [lo, hi], lo = max(1 - R, 1 / max_i a_ii), hi = 1 + R, R the Gershgorin radius.  Every
    eigenvalue lies inside (tests/test_host_assembly.py checks it against scipy's eigensolver). */

@@ -89,6 +89,7 @@ SIGNATURES = {
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),
     "pucfem_timing_get": ([_P, ct.c_int32, _D, _I64, _D], ct.c_int),
     "pucfem_counters": ([_P, _I64, _D], ct.c_int),
+    "pucfem_comm_counters": ([_P, _I64], ct.c_int),
     "pucfem_sync": ([_P], ct.c_int),
     "pucfem_bench_dir": ([_P, ct.c_int32, ct.c_int32, ct.c_int32, _D], ct.c_int),
     "pucfem_bench_kernel": ([_P, ct.c_int32, ct.c_int32, _D, _D, _D], ct.c_int),

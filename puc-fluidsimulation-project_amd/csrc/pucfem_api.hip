@@ -412,6 +412,16 @@ struct Ctx {
   // lies in [1 - visc_R, 1 + visc_R] (the Chebyshev viscous solve's interval)
   double visc_R = 1.0, visc_lo = 0.0;
   int visc_solver = 0;  // 0 = Chebyshev iteration when visc_R < 0.25 (multi-kernel path), 1 = CG
+  // a-posteriori check of the Chebyshev bound (vcheb): the last step of a solve also reduces |r_{k}|^2 of
+  // the iterate it starts from (k = K - 1), copied to h_pinned[32 ..]; the next solve compares it with
+  // |r_0| / T_k(sigma) -- a spectrum outside [visc_lo, 1 + visc_R] (a wrong interval) breaks the bound.  A
+  // violation switches the viscous solves to the CG (visc_check_fail counts them, pucfem_path_info)
+  struct ViscCheck {
+    bool pending = false;
+    int nr = 0;
+    double bound2[2] = {0.0, 0.0}, floor2[2] = {0.0, 0.0};
+  } vcc;
+  int visc_check_fail = 0;
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
   static FaceDev nof() { return FaceDev{}; }
 
@@ -838,7 +848,7 @@ struct Ctx {
     const double bytes = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                          32.0 * NR * (double)A.own();
     // One step: x_out = x_in + d, d = c1 d + c2 (b - A^ x_in); the first step also yields |r_0| and |b|.
-    auto step = [&](int it, double c1, double c2) {
+    auto step = [&](int it, double c1, double c2, bool check = false) {
       ChebVecs<NR> v;
       for (int c = 0; c < NR; ++c) {
         v.xin[c] = xa[c];
@@ -850,10 +860,11 @@ struct Ctx {
       // step 0 reduces its own partials (fused): |r_0|^2 into redbuf[0 .. NR), |b|^2 into redbuf[NR .. 2 NR)
       const RedOut r0 = it == 0 ? ro(redbuf, CNT_VCHEB, 2 * NR) : RedOut{};
       double* pb = it == 0 ? (r0.out ? part_a + NR * MAXB : part_b) : (double*)nullptr;
+      // check: the post-check's |r_it|^2 partials (part_c)
+      double* pr = it == 0 ? part_a : (check ? part_c : (double*)nullptr);
       with_c16(A, [&](auto c16) {
         klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
-                dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl,
-                it == 0 ? part_a : (double*)nullptr, pb, r0);
+                dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, pr, pb, r0);
       });
       KCHK();
       halo_x(xb);
@@ -891,6 +902,14 @@ struct Ctx {
     advance(std::max(1, last_it[which] - 1));
     HIPCHK(hipEventSynchronize(have_r0));
     timer.pool.push_back(have_r0);
+    if (vcc.pending) {  // the previous solve's post-check (its copy preceded step 0 on the stream)
+      vcc.pending = false;
+      for (int c = 0; c < vcc.nr; ++c)
+        if (!(h_pinned[32 + c] <= vcc.bound2[c] * 1.0201 + vcc.floor2[c])) {
+          ++visc_check_fail;
+          visc_solver = 1;  // the interval does not hold the spectrum: CG from the next solve on
+        }
+    }
     int K = 1;  // x_1 exists now; x_0 (y) is the answer when r_0 already passes
     bool pass0 = true;
     for (int c = 0; c < NR; ++c) {
@@ -915,6 +934,31 @@ struct Ctx {
       for (int c = 0; c < NR; ++c) out[c] = y[c];
       last_it[which] = 0;
       return 0;
+    }
+    if (done < K) {
+      advance(K - 1);
+      // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check
+      const double rho = 1.0 / (2.0 * sigma - rho_old);
+      step(done, rho * rho_old, 2.0 * rho / delta, true);
+      rho_old = rho;
+      const int kc = done;
+      ++done;
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, (const double*)part_c, nb, MAXB, NR, 0, redbuf + 48);
+      KCHK();
+      if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
+      HIPCHK(hipMemcpyAsync(h_pinned + 32, redbuf + 48, NR * sizeof(double), hipMemcpyDeviceToHost, st));
+      double tm = 1.0, tk = sigma;  // T_kc(sigma)
+      for (int k = 1; k < kc; ++k) {
+        const double tn = 2.0 * sigma * tk - tm;
+        tm = tk;
+        tk = tn;
+      }
+      vcc.pending = true;
+      vcc.nr = NR;
+      for (int c = 0; c < NR; ++c) {
+        vcc.bound2[c] = h_pinned[c] / (tk * tk);
+        vcc.floor2[c] = 1e-28 * h_pinned[8 + c];  // rounding: |r| ~ 1e-14 |b| is as far as it resolves
+      }
     }
     advance(K);  // (steps beyond K, already launched, only reduce the residual further)
     for (int c = 0; c < NR; ++c) out[c] = xa[c];  // x_done, done >= K
@@ -1019,6 +1063,10 @@ struct Ctx {
   // PUCFEM_MG_POST_COARSE; 0: the finest level's)
   int mg_pre_coarse = std::getenv("PUCFEM_MG_PRE_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_PRE_COARSE")) : 0;
   int mg_post_coarse = std::getenv("PUCFEM_MG_POST_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_POST_COARSE")) : 0;
+  // levels of at most PUCFEM_MG_TINY_ROWS rows (measurement knob, default 0: none) smooth with
+  // PUCFEM_MG_TINY_DEG steps before and after: their launches are latency-bound (~6 us for ~1 us of work)
+  int64_t mg_tiny_rows = std::getenv("PUCFEM_MG_TINY_ROWS") ? std::atoll(std::getenv("PUCFEM_MG_TINY_ROWS")) : 0;
+  int mg_tiny_deg = std::getenv("PUCFEM_MG_TINY_DEG") ? std::max(1, std::atoi(std::getenv("PUCFEM_MG_TINY_DEG"))) : 1;
   template <typename T, typename TB>
   T* vcycle(int l, const TB* b, const double* rdot, double* part) {
     MgLevel& L = mg[l];
@@ -1041,7 +1089,8 @@ struct Ctx {
         throw Error(PUCFEM_ESTATE, "multigrid hierarchy has a single level");
       }
     }
-    const int pre = finest || mg_pre_coarse <= 0 ? prm.mg_degree : mg_pre_coarse;
+    const bool tiny = !finest && (int64_t)A.own() <= mg_tiny_rows;
+    const int pre = tiny ? mg_tiny_deg : (finest || mg_pre_coarse <= 0 ? prm.mg_degree : mg_pre_coarse);
     if constexpr (std::is_same<T, TB>::value) {
       // coarse levels: the fused first smoothing step reads b at ghost columns
       if (pre >= 2) mg_halo(L, const_cast<T*>(b));
@@ -1094,7 +1143,7 @@ struct Ctx {
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
     return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part,
-                            finest || mg_post_coarse <= 0 ? post : mg_post_coarse);
+                            tiny ? mg_tiny_deg : (finest || mg_post_coarse <= 0 ? post : mg_post_coarse));
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
@@ -2246,6 +2295,8 @@ void build(Ctx& c) {
     // than Gershgorin's 1 - R)
     c.visc_lo = std::max(1.0 - c.visc_R, 1.0 / *std::max_element(cd.begin(), cd.end()));
     if (const char* e = std::getenv("PUCFEM_VISC_SOLVER")) c.visc_solver = std::atoi(e);  // 1: CG (measurement)
+    // test knob: a deliberately wrong (too short) interval [visc_lo, 1 + s R], for the post-check's test
+    if (const char* e = std::getenv("PUCFEM_VISC_R_SCALE")) c.visc_R *= std::atof(e);
   }
   clk.mark("A_visc");
   // partition + local plan
@@ -3782,7 +3833,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
-           (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0);
+           (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0);
   });
 }
 
@@ -3804,6 +3855,20 @@ int pucfem_comm_info(void* ctx, int64_t* o) {
     o[1] = c.dist() ? c.mesh.N - c.lp.n_own : 0;
     o[2] = c.dist() ? 3 * (int64_t)c.ntr : 0;
     o[3] = !c.comm ? 0 : (dynamic_cast<NcclComm*>(c.comm.get()) ? 2 : 1);
+  });
+}
+
+int pucfem_comm_counters(void* ctx, int64_t* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    for (int k = 0; k < 6; ++k) o[k] = 0;
+    if (!c.comm) return;
+    o[0] = c.comm->n_allreduce;
+    o[1] = c.comm->v_allreduce;
+    o[2] = c.comm->n_msg;
+    o[3] = c.comm->b_msg;
+    o[4] = c.comm->n_group;
+    o[5] = c.comm->n_bcast;
   });
 }
 

@@ -30,6 +30,11 @@ template <> constexpr Dt dt_of<double>() { return Dt::F64; }
 template <> constexpr Dt dt_of<float>() { return Dt::F32; }
 
 struct Comm {
+  // traffic counters of this rank (pucfem_comm_counters): all-reduce calls and values, point-to-point
+  // sends / broadcasts (messages) and their bytes, grouped launches
+  int64_t n_allreduce = 0, v_allreduce = 0, n_msg = 0, b_msg = 0, n_group = 0, n_bcast = 0;
+  void count_ar(size_t n) { ++n_allreduce; v_allreduce += (int64_t)n; }
+  void count_msg(size_t bytes) { ++n_msg; b_msg += (int64_t)bytes; }
   virtual ~Comm() {}
   virtual void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) = 0;
   virtual void group_start() = 0;
@@ -53,17 +58,23 @@ struct NcclComm : Comm {
     if (c) (void)ncclCommDestroy(c);
   }
   void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) override {
+    count_ar(n);
     nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, is_max ? ncclMax : ncclSum, c, st), "allreduce");
   }
-  void group_start() override { nccl_check(ncclGroupStart(), "group start"); }
+  void group_start() override {
+    ++n_group;
+    nccl_check(ncclGroupStart(), "group start");
+  }
   static ncclDataType_t nt(Dt t) { return t == Dt::F64 ? ncclDouble : ncclFloat; }
   void send(const void* p, size_t n, Dt t, int peer, hipStream_t st) override {
+    count_msg(n * dt_size(t));
     nccl_check(ncclSend(p, n, nt(t), peer, c, st), "send");
   }
   void recv(void* p, size_t n, Dt t, int peer, hipStream_t st) override {
     nccl_check(ncclRecv(p, n, nt(t), peer, c, st), "recv");
   }
   void bcast(void* p, size_t n, Dt t, int root, hipStream_t st) override {
+    ++n_bcast;
     nccl_check(ncclBroadcast(p, p, n, nt(t), root, c, st), "broadcast");
   }
   void group_end(hipStream_t) override { nccl_check(ncclGroupEnd(), "group end"); }
@@ -146,6 +157,7 @@ struct LocalComm : Comm {
     if (e != hipSuccess) throw std::runtime_error(std::string("LocalComm HIP: ") + hipGetErrorString(e));
   }
   void allreduce(double* buf, size_t n, bool is_max, hipStream_t st) override {
+    count_ar(n);
     if (world > 64) throw std::runtime_error("LocalComm supports <= 64 ranks");
     if (n > cap) {  // this rank's output buffer only: no other rank touches it
       chk(hipStreamSynchronize(st));
@@ -171,14 +183,19 @@ struct LocalComm : Comm {
     chk(hipMemcpyAsync(buf, tmp, n * sizeof(double), hipMemcpyDeviceToDevice, st));
     S->barrier();
   }
-  void group_start() override { pending.clear(); }
+  void group_start() override {
+    ++n_group;
+    pending.clear();
+  }
   void send(const void* p, size_t n, Dt t, int peer, hipStream_t) override {
+    count_msg(n * dt_size(t));
     pending.push_back({0, const_cast<void*>(p), n * dt_size(t), peer});
   }
   void recv(void* p, size_t n, Dt t, int peer, hipStream_t) override {
     pending.push_back({1, p, n * dt_size(t), peer});
   }
   void bcast(void* p, size_t n, Dt t, int root, hipStream_t) override {
+    ++n_bcast;
     pending.push_back({2, p, n * dt_size(t), root});
   }
   void group_end(hipStream_t st) override {

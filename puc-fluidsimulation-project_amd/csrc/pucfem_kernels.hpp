@@ -196,10 +196,10 @@ __device__ __forceinline__ void red_finish(const RedOut& R, const double* part, 
   }
   if (threadIdx.x == 0) __hip_atomic_store(R.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// thread 0: partial of value v of this block
+// thread 0: partial of value v of this block (stride R.stride when fused, else MAXB: the k_reduce layout)
 __device__ __forceinline__ void red_part(const RedOut& R, double* part, int v, double x) {
   if (R.out) red_store(part + (int64_t)v * R.stride + blockIdx.x, x);
-  else part[(int64_t)v * R.stride + blockIdx.x] = x;
+  else part[(int64_t)v * MAXB + blockIdx.x] = x;
 }
 
 // wave index inside the block as a wave-uniform (scalar) value: slice indices derived from it stay

@@ -83,13 +83,15 @@ class Tolerances:
     @classmethod
     def production(cls, **kw):
         """The settings bench.py measures (and the production-path parity tests check): multigrid-
-        preconditioned pressure CG with the fp32 V-cycle, the 24-direction projected pressure guess,
+        preconditioned pressure CG with the fp32 V-cycle, the 16-direction projected pressure guess,
         int16 column deltas, the extrapolated viscous start, pressure rtol PRODUCTION_RTOL_PRES."""
         # V(3,3) Chebyshev smoothing on [lmax / 15, lmax]: measured at L7 against V(2,2) / ratio 10 and the
         # neighbouring choices (DESIGN.md §5; driver command 90.7 -> 97.6 steps/s)
         base = dict(rtol_visc=1e-12, rtol_pres=PRODUCTION_RTOL_PRES, precond="mg", mg_single=True,
                     mg_f16_vals=False, index16=True, mg_degree=3, mg_post=3, mg_ratio=15.0, mg_kind=1,
-                    proj_k=24, proj_k_visc=0)
+                    proj_k=16, proj_k_visc=0)
+        # proj_k 16: the driver command on one box, twice each (r8d): 24 -> 106.8 / 107.0, 16 -> 107.1 / 108.5,
+        # 12 -> 105.6 / 105.6, 8 -> 99.8 / 100.0 steps/s; pressure iterations 72 / 72 / 76 / 83
         base.update(kw)
         return cls(**base)
 
@@ -225,7 +227,8 @@ class Context:
         return dict(viscous=visc[o[0]], pressure=pres[o[1]], reseeds=o[2], basis_p=o[3], basis_p2=o[4],
                     visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7] & 1),
                     sl_locator="lattice" if o[7] & 2 else "records",
-                    viscous_iteration="chebyshev" if o[7] & 4 else "cg")
+                    viscous_iteration="chebyshev" if o[7] & 4 else "cg",
+                    visc_check_failed=bool(o[7] & 8))
 
     def visc_interval(self):
         """[lo, hi] of the viscous Chebyshev iteration (pucfem_visc_interval)."""
@@ -239,6 +242,13 @@ class Context:
         self._c(self.L.pucfem_comm_info(self.h, o))
         return dict(dye_halo_values=o[0], allgather_values=o[1], tracer_allreduce_values=o[2],
                     backend={0: None, 1: "local", 2: "rccl"}[o[3]])
+
+    def comm_counters(self):
+        """Cumulative communicator traffic of this rank (pucfem_comm_counters)."""
+        o = (ct.c_int64 * 6)()
+        self._c(self.L.pucfem_comm_counters(self.h, o))
+        return dict(allreduce_calls=o[0], allreduce_values=o[1], sends=o[2], send_bytes=o[3], groups=o[4],
+                    broadcasts=o[5])
 
     def comm_selftest(self):
         """All-reduce + ring send/recv check of the context's communicator (pucfem_comm_selftest)."""

@@ -341,6 +341,25 @@ def test_viscous_extrapolated_start_same_steps(monkeypatch, order):
     b.close()
 
 
+def test_viscous_chebyshev_post_check(monkeypatch):
+    """The Chebyshev viscous solve takes its step count from the a-priori residual bound of its interval;
+    the last step of each solve also reduces the residual of the iterate it starts from, and the next
+    solve checks it against that bound.  With the true interval the check never fires; with a
+    deliberately short one (PUCFEM_VISC_R_SCALE) it fires and the viscous solves switch to the CG."""
+    mesh = pf.load_mesh("fine", refine=2)
+    a = stokes(mesh)
+    monkeypatch.setenv("PUCFEM_VISC_R_SCALE", "0.3")  # read when the operators are built
+    b = stokes(mesh)
+    a.step(12)
+    b.step(12)
+    pa, pb = a.ctx.path_info(), b.ctx.path_info()
+    assert pa["viscous_iteration"] == "chebyshev" and not pa["visc_check_failed"]
+    assert pb["visc_check_failed"] and pb["viscous_iteration"] == "cg"
+    assert np.isfinite(b.u).all()
+    a.close()
+    b.close()
+
+
 def test_projected_pressure_guess_same_steps():
     """Successive-RHS projection (Fischer) only changes the pressure CG's initial guess: 24 steps with
     a 3-vector basis (several restarts) equal the warm-started run to the CG tolerance, and once the

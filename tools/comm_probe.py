@@ -1,5 +1,8 @@
 """Per-rank multi-GPU data flow of the StokesColor step on W LocalComm ranks (one GPU, one process):
-the wide dye halo each rank receives vs a full all-gather, after each of S steps.
+the wide dye halo each rank receives vs a full all-gather, after each of S steps, and per step the
+communicator's traffic (pucfem_comm_counters: all-reduce calls and values, point-to-point sends and
+bytes, grouped launches, broadcasts), the pressure / viscous iteration counts and the kernel launches.
+The same call sequence runs over RCCL on W GPUs (NcclComm), so the counts are the production path's.
   python tools/comm_probe.py LEVEL W STEPS"""
 import os
 import sys
@@ -22,8 +25,13 @@ def worker(r):
         sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", 0, pf.Tolerances.production(),
                                   dist=(r, world, uid))
         for k in range(steps):
-            sim.step(1)
+            c0, (n0, _) = sim.ctx.comm_counters(), sim.ctx.counters()
+            st = sim.step(1)[0]
+            c1, (n1, _) = sim.ctx.comm_counters(), sim.ctx.counters()
             rows[r][k] = sim.ctx.comm_info()
+            rows[r][k]["traffic"] = {key: c1[key] - c0[key] for key in c1}
+            rows[r][k]["traffic"]["launches"] = n1 - n0
+            rows[r][k]["its"] = (st.it_visc, st.it_p, st.it_p2)
         sim.close()
     except Exception as e:  # pragma: no cover
         errs.append((r, repr(e)))
@@ -41,3 +49,9 @@ for k in range(steps):
     a = [rows[r][k]["allgather_values"] for r in range(world)]
     print(f"step {k}: dye halo values per rank {h} (max {max(h) * 8 / 1e6:.2f} MB) vs all-gather "
           f"{max(a) * 8 / 1e6:.2f} MB")
+    t = [rows[r][k]["traffic"] for r in range(world)]
+    mx = {key: max(x[key] for x in t) for key in t[0]}
+    print(f"        iterations visc/p/p2 {rows[0][k]['its']}; per rank (max over ranks): "
+          f"{mx['allreduce_calls']} all-reduces ({mx['allreduce_values']} values), {mx['sends']} sends "
+          f"({mx['send_bytes'] / 1e6:.2f} MB), {mx['broadcasts']} broadcasts, {mx['groups']} groups, "
+          f"{mx['launches']} kernel launches")
