@@ -2797,12 +2797,16 @@ void build(Ctx& c) {
   // full-mesh replica in internal numbering
   {
     std::vector<double> X(N), Y(N);
-    for (i64 g = 0; g < N; ++g) {
-      X[g] = m.x[c.ord.new2old[g]];
-      Y[g] = m.y[c.ord.new2old[g]];
-    }
+    parallel_for(N, [&](i64 g0, i64 g1) {
+      for (i64 g = g0; g < g1; ++g) {
+        X[g] = m.x[c.ord.new2old[g]];
+        Y[g] = m.y[c.ord.new2old[g]];
+      }
+    });
     std::vector<i32> tri(3 * m.T);
-    for (i64 k = 0; k < 3 * m.T; ++k) tri[k] = c.ord.old2new[m.tri[k]];
+    parallel_for(3 * m.T, [&](i64 k0, i64 k1) {
+      for (i64 k = k0; k < k1; ++k) tri[k] = c.ord.old2new[m.tri[k]];
+    });
     c.mx = c.upload(X);
     c.my = c.upload(Y);
     c.mtri = c.upload(tri);
@@ -2838,14 +2842,40 @@ void build(Ctx& c) {
         c.has_tgrid = true;
       }
       clk.mark("SL: centroid / triangle grids");
-      const std::vector<float> rho2 = centroid_knn_radius2(G, cx, cy, KNN);
-      clk.mark("SL: centroid 10-NN radii");
-      const float* drv2 = c.upload(knn_radius2(G, X, Y, KNN + 1, false));
-      std::vector<double> xy(2 * (size_t)N);
-      for (i64 i = 0; i < N; ++i) {
-        xy[2 * i] = X[i];
-        xy[2 * i + 1] = Y[i];
+      // fast-accept radii (k-NN of every centroid among the centroids, of every vertex among the
+      // centroids): on the device (k_knn_radius2, bit-identical to the host's knn_radius2, which
+      // PUCFEM_KNN_HOST=1 selects -- the cross-check of tests/test_gpu_parity.py)
+      const bool knn_host = std::getenv("PUCFEM_KNN_HOST") && std::atoi(std::getenv("PUCFEM_KNN_HOST"));
+      const bool knn_ok = (i64)G.item.size() - 1 >= KNN && (i64)G.item.size() >= KNN + 1;
+      std::vector<float> rho2;
+      const float* drho2 = nullptr;
+      const float* drv2 = nullptr;
+      if (knn_host || !knn_ok) {
+        rho2 = centroid_knn_radius2(G, cx, cy, KNN);
+        drho2 = c.upload(rho2);
+        clk.mark("SL: centroid 10-NN radii");
+        drv2 = c.upload(knn_radius2(G, X, Y, KNN + 1, false));
+      } else {
+        float* r2 = c.dalloc<float>(m.T);
+        hipLaunchKernelGGL(k_knn_radius2, dim3((unsigned)std::min<i64>(65536, (m.T + BS - 1) / BS)), dim3(BS), 0, c.st,
+                           c.cgrid, c.cgrid.px, c.cgrid.py, c.cgrid.item, (int64_t)m.T, KNN, 1, r2);
+        KCHK();
+        float* v2 = c.dalloc<float>(N);
+        hipLaunchKernelGGL(k_knn_radius2, dim3((unsigned)std::min<i64>(65536, (N + BS - 1) / BS)), dim3(BS), 0, c.st,
+                           c.cgrid, (const double*)c.mx, (const double*)c.my, (const int32_t*)nullptr, (int64_t)N,
+                           KNN + 1, 0, v2);
+        KCHK();
+        drho2 = r2;
+        drv2 = v2;
+        clk.mark("SL: centroid 10-NN radii");
       }
+      std::vector<double> xy(2 * (size_t)N);
+      parallel_for(N, [&](i64 i0, i64 i1) {
+        for (i64 i = i0; i < i1; ++i) {
+          xy[2 * i] = X[i];
+          xy[2 * i + 1] = Y[i];
+        }
+      });
       const double2* dxy = reinterpret_cast<const double2*>(c.upload(xy));
       clk.mark("SL: vertex 11-NN radii");
       const int probe = std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0;
@@ -2874,7 +2904,7 @@ void build(Ctx& c) {
           for (i64 k = 0; k < LL.F; ++k) home[LL.face_start[f] + k] = (i32)f;
         c.llgrid = LatLocDev{mg.nx, mg.ny, mg.x0, mg.y0, 1.0 / mg.hx, 1.0 / mg.hy, mg.start, mg.item,
                              reinterpret_cast<const lat::SlFace*>(c.upload(sf)), c.upload(cells), dxy,
-                             c.upload(rho2), drv2, c.upload(home), nullptr, LL.n, probe};
+                             drho2, drv2, c.upload(home), nullptr, LL.n, probe};
         // zero-velocity rows (walls): the answer for the row's own node, once
         int32_t* dself = c.dalloc<int32_t>(N);
         hipLaunchKernelGGL(k_sl_self<LatLocDev>, dim3(2048), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, m.T},
@@ -2893,6 +2923,11 @@ void build(Ctx& c) {
         }
         std::stable_sort(p2t.begin(), p2t.end(), [&](i32 a, i32 b) { return vmin[a] < vmin[b]; });
         for (i64 p = 0; p < m.T; ++p) t2p[p2t[p]] = (i32)p;
+        if (rho2.empty()) {  // the device radii, in triangle order, for the record permutation below
+          rho2.resize(m.T);
+          HIPCHK(hipMemcpyAsync(rho2.data(), drho2, sizeof(float) * m.T, hipMemcpyDeviceToHost, c.st));
+          HIPCHK(hipStreamSynchronize(c.st));
+        }
         std::vector<int32_t> rec(4 * (size_t)m.T);  // SlTri records (pucfem_kernels_impl.hpp)
         std::vector<float> rho2p(m.T);
         for (i64 p = 0; p < m.T; ++p) {

@@ -812,24 +812,35 @@ bool spd_inverse(std::vector<double>& A, i64 n) {
       A[i * n + j] = s / d;
     }
   }
-  // Linv (lower) into W
-  std::vector<double> W(n * n, 0.0);
-  for (i64 j = 0; j < n; ++j) {
-    W[j * n + j] = 1.0 / A[j * n + j];
-    for (i64 i = j + 1; i < n; ++i) {
-      double s = 0.0;
-      for (i64 k = j; k < i; ++k) s -= A[i * n + k] * W[k * n + j];
-      W[i * n + j] = s / A[i * n + i];
+  // Linv (lower): column j of W = L^-1 by forward substitution, columns independent -> threads; stored
+  // transposed (Wt[j][i] = W[i][j]) so both loops below read contiguous rows.  Same operations in the
+  // same order as the column-by-column loop: the inverse is bit-identical to the serial one.
+  std::vector<double> Wt(n * n, 0.0);
+  parallel_for(n, [&](i64 j0, i64 j1) {
+    for (i64 j = j0; j < j1; ++j) {
+      double* w = Wt.data() + j * n;
+      w[j] = 1.0 / A[j * n + j];
+      for (i64 i = j + 1; i < n; ++i) {
+        double s = 0.0;
+        for (i64 k = j; k < i; ++k) s -= A[i * n + k] * w[k];
+        w[i] = s / A[i * n + i];
+      }
     }
-  }
-  // inv = W^T W
+  });
+  // inv = W^T W: inv[i][j] = sum_{k >= i} W[k][i] W[k][j] (j <= i), rows independent -> threads
+  parallel_for(n, [&](i64 i0, i64 i1) {
+    for (i64 i = i0; i < i1; ++i) {
+      const double* wi = Wt.data() + i * n;
+      for (i64 j = 0; j <= i; ++j) {
+        const double* wj = Wt.data() + j * n;
+        double s = 0.0;
+        for (i64 k = i; k < n; ++k) s += wi[k] * wj[k];
+        A[i * n + j] = s;
+      }
+    }
+  });
   for (i64 i = 0; i < n; ++i)
-    for (i64 j = 0; j <= i; ++j) {
-      double s = 0.0;
-      for (i64 k = i; k < n; ++k) s += W[k * n + i] * W[k * n + j];
-      A[i * n + j] = s;
-      A[j * n + i] = s;
-    }
+    for (i64 j = 0; j < i; ++j) A[j * n + i] = A[i * n + j];
   return true;
 }
 

@@ -1367,6 +1367,54 @@ __device__ __forceinline__ int32_t gcell(double v, double v0, double hv, int32_t
   if (f >= (double)n) return n - 1;
   return (int32_t)f;
 }
+// Squared distance from query q to its k-th nearest grid point (the semi-Lagrangian fast-accept radii,
+// pucfem_host.cpp knn_radius2 restated for the device, operation for operation, so the tables are
+// bit-identical): ring search over the grid cells, ascending k smallest distances, stop once every
+// unvisited cell is farther than the k-th; rounded DOWN to fp32.  Query e: (qx[e], qy[e]); its own id
+// qid[e] (self: the grid point with that id is skipped; qid null: id e) and out[id].
+constexpr int KNN_MAX = 16;
+__global__ __launch_bounds__(BS) void k_knn_radius2(GridDev G, const double* __restrict__ qx,
+                                                    const double* __restrict__ qy, const int32_t* __restrict__ qid,
+                                                    int64_t nq, int k, int self, float* __restrict__ out) {
+  for (int64_t e = (int64_t)blockIdx.x * BS + threadIdx.x; e < nq; e += (int64_t)gridDim.x * BS) {
+    const double x = qx[e], y = qy[e];
+    const int32_t id = qid ? qid[e] : (int32_t)e;
+    double best[KNN_MAX];
+    for (int p = 0; p < k; ++p) best[p] = INFINITY;
+    const int32_t ci = gcell(x, G.x0, G.hx, G.nx), cj = gcell(y, G.y0, G.hy, G.ny);
+    for (int32_t r = 0;; ++r) {
+      const int32_t jlo = max(cj - r, 0), jhi = min(cj + r, G.ny - 1);
+      for (int32_t j = jlo; j <= jhi; ++j) {
+        const bool edge = j == cj - r || j == cj + r;
+        for (int32_t i = ci - r; i <= ci + r; i += (edge || r == 0) ? 1 : 2 * r) {
+          if (i < 0 || i >= G.nx) continue;
+          const int64_t c = (int64_t)j * G.nx + i;
+          for (int32_t q = G.start[c]; q < G.start[c + 1]; ++q) {
+            if (self && G.item[q] == id) continue;
+            const double dx = G.px[q] - x, dy = G.py[q] - y, d = dx * dx + dy * dy;
+            if (d >= best[k - 1]) continue;
+            int p = k - 1;
+            while (p > 0 && best[p - 1] > d) {
+              best[p] = best[p - 1];
+              --p;
+            }
+            best[p] = d;
+          }
+        }
+      }
+      double dmin = INFINITY;
+      if (ci - r > 0) dmin = fmin(dmin, x - (G.x0 + (ci - r) * G.hx));
+      if (ci + r < G.nx - 1) dmin = fmin(dmin, G.x0 + (ci + r + 1) * G.hx - x);
+      if (cj - r > 0) dmin = fmin(dmin, y - (G.y0 + (cj - r) * G.hy));
+      if (cj + r < G.ny - 1) dmin = fmin(dmin, G.y0 + (cj + r + 1) * G.hy - y);
+      if (dmin == INFINITY || (dmin > 0 && best[k - 1] < dmin * dmin * (1.0 - 1e-9))) break;
+    }
+    float f = (float)best[k - 1];
+    if ((double)f > best[k - 1]) f = nextafterf(f, 0.0f);
+    out[id] = f;
+  }
+}
+
 __device__ __forceinline__ bool knn_less(double d, int32_t i, double bd, int32_t bi) {
   return d < bd || (d == bd && i < bi);
 }

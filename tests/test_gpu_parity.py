@@ -360,6 +360,24 @@ def test_viscous_chebyshev_post_check(monkeypatch):
     b.close()
 
 
+@pytest.mark.parametrize("records", ["0", "1"])
+def test_knn_radii_device_equals_host(monkeypatch, records):
+    """The semi-Lagrangian fast-accept radii (k-NN distances of every centroid and vertex) are built on
+    the device (k_knn_radius2) as the host's knn_radius2 builds them: 6 StokesColor steps at L3 with
+    either table are bit-identical, with the lattice locator and with the record locator."""
+    mesh = pf.load_mesh("fine", refine=3)
+    monkeypatch.setenv("PUCFEM_SL_RECORDS", records)
+    a = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.setenv("PUCFEM_KNN_HOST", "1")
+    b = stokes(mesh, tol=S.Tolerances.production())
+    assert a.ctx.path_info()["sl_locator"] == ("records" if records == "1" else "lattice")
+    sa, sb = a.step(6), b.step(6)
+    assert np.array_equal(a.u, b.u) and np.array_equal(a.c, b.c)
+    assert [s.sl_notfound for s in sa] == [s.sl_notfound for s in sb]
+    a.close()
+    b.close()
+
+
 def test_projected_pressure_guess_same_steps():
     """Successive-RHS projection (Fischer) only changes the pressure CG's initial guess: 24 steps with
     a 3-vector basis (several restarts) equal the warm-started run to the CG tolerance, and once the
