@@ -612,16 +612,23 @@ struct Ctx {
   // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
   // the all-reduce across ranks): consumers read one scalar instead of re-reducing up to MAXB
   // partials in each of their blocks
+  int red_threads = std::getenv("PUCFEM_RED_THREADS") ? std::atoi(std::getenv("PUCFEM_RED_THREADS")) : RB;
+  void launch_reduce(const double* part, int nb, int stride, int nv, bool is_max, double* out) {
+    if (red_threads == 256)
+      hipLaunchKernelGGL(k_reduce_t<256>, dim3(1), dim3(256), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
+    else
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
+  }
   Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
     double* buf = redbuf + 8 * slot;
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, MAXB, nv, is_max ? 1 : 0, buf);
+    launch_reduce(part, nb, MAXB, nv, is_max, buf);
     KCHK();
     if (dist()) comm->allreduce(buf, nv, is_max, st);
     return Red{buf, 1, 1};
   }
   // reduce partials into vals[slot..slot+nv) (+ all-reduce)
   void reduce_into(double* part, int nb, int nv, bool is_max, int slot, int stride = MAXB) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, vals + slot);
+    launch_reduce(part, nb, stride, nv, is_max, vals + slot);
     KCHK();
     if (dist())
       comm->allreduce(vals + slot, nv, is_max, st);
@@ -824,9 +831,18 @@ struct Ctx {
   // through the double buffer) and b as for cg<NR>; the converged iterate is returned in out[] (y itself
   // or the alternate buffer cg_pb).  Target: the CG's test <r, r> <= tol^2 <b, b>, met through the a-priori
   // residual bound of the interval (below).
+  // fin (optional, NR = 2): the viscous finish (k_visc_fin: u* = S y, the fp32 increment u* - u) for the
+  // solve's last step to do in place of its x_out; *fin_done tells whether it did
+  struct ViscFin {
+    const double* s;
+    const double* u[2];
+    double* us[2];
+    float* inc[2];
+  };
   template <int NR>
   int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
-            double tol, int maxit, int which, double* out[NR]) {
+            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr) {
+    if (fin_done) *fin_done = false;
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
     double* xa[NR];
@@ -848,13 +864,19 @@ struct Ctx {
     const double bytes = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                          32.0 * NR * (double)A.own();
     // One step: x_out = x_in + d, d = c1 d + c2 (b - A^ x_in); the first step also yields |r_0| and |b|.
-    auto step = [&](int it, double c1, double c2, bool check = false) {
-      ChebVecs<NR> v;
+    auto step = [&](int it, double c1, double c2, bool check = false, bool fin = false) {
+      ChebVecs<NR> v{};
       for (int c = 0; c < NR; ++c) {
         v.xin[c] = xa[c];
         v.xout[c] = xb[c];
         v.b[c] = b[c];
         v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
+        if (fin) {
+          v.s = vfin->s;
+          v.u[c] = vfin->u[c];
+          v.us[c] = vfin->us[c];
+          v.inc[c] = vfin->inc[c];
+        }
       }
       // timing class 9; the first step reads no d (4 B/row per right-hand side less)
       // step 0 reduces its own partials (fused): |r_0|^2 into redbuf[0 .. NR), |b|^2 into redbuf[NR .. 2 NR)
@@ -867,6 +889,10 @@ struct Ctx {
                 dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, pr, pb, r0);
       });
       KCHK();
+      if (fin) {  // the solve's output is u* (haloed by viscous()), x_out was not written
+        algo_bytes += 12.0 * NR * (double)A.own();  // + s, u read and u*, the increment written - d, x_out
+        return;
+      }
       halo_x(xb);
       for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
     };
@@ -939,10 +965,12 @@ struct Ctx {
       advance(K - 1);
       // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check
       const double rho = 1.0 / (2.0 * sigma - rho_old);
-      step(done, rho * rho_old, 2.0 * rho / delta, true);
+      const bool fuse = vfin != nullptr && NR == 2;
+      step(done, rho * rho_old, 2.0 * rho / delta, true, fuse);
       rho_old = rho;
       const int kc = done;
       ++done;
+      if (fuse) *fin_done = true;
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, (const double*)part_c, nb, MAXB, NR, 0, redbuf + 48);
       KCHK();
       if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
@@ -1290,6 +1318,8 @@ struct Ctx {
                        bc_gather ? (const double*)dbctmp : nullptr, ndir, ddnode, ddval, dir_ncomp, a, b);
     KCHK();
   }
+  // PUCFEM_VISC_FUSE_FIN=0 (measurement knob): k_visc_fin as its own launch after the solve
+  bool visc_fuse_fin = !(std::getenv("PUCFEM_VISC_FUSE_FIN") && std::atoi(std::getenv("PUCFEM_VISC_FUSE_FIN")) == 0);
   int viscous(int& iters) {  // StokesColor.py:540-547
     const i64 n = lp.n_own;
     if (dense) {  // u* = A_visc^-1 (u + DT * 0)
@@ -1317,17 +1347,25 @@ struct Ctx {
     double* yo[2] = {yvx, yvy};  // the converged iterate (the Chebyshev double buffer may hold it)
     const bool cheb = visc_solver == 0 && visc_R < 0.25 && !(!dist() && block_cg && !fVisc.items &&
                                                              dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
-    if (cheb) iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo);
+    // with the extrapolated start the solve's last Chebyshev step also does k_visc_fin's work
+    const int last = 2 * (visc_extrap - 1);
+    bool fin_done = false;
+    ViscFin vf{};
+    const bool fuse = ext && !proj && visc_fuse_fin;
+    if (fuse) vf = ViscFin{dsv, {ux, uy}, {usx, usy}, {dvinc[last], dvinc[last + 1]}};
+    if (cheb) iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr,
+                               &fin_done);
     else iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
     if (proj) {
       project_update(3, yo[0]);
       project_update(4, yo[1]);
     }
     if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
-      const int last = 2 * (visc_extrap - 1);
-      algo_bytes += 64.0 * (double)n;  // s, y, u read; u*, the fp32 increment written
-      hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yo[0], yo[1], ux, uy, usx, usy,
-                         dvinc[last], dvinc[last + 1]);
+      if (!fin_done) {
+        algo_bytes += 64.0 * (double)n;  // s, y, u read; u*, the fp32 increment written
+        hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yo[0], yo[1], ux, uy, usx, usy,
+                           dvinc[last], dvinc[last + 1]);
+      }
       for (int k = last; k >= 2; k -= 2) {
         std::swap(dvinc[k], dvinc[k - 2]);
         std::swap(dvinc[k + 1], dvinc[k - 1]);
@@ -1415,7 +1453,7 @@ struct Ctx {
     algo_bytes += (4.0 * m + 24.0) * (double)n;  // k_mdot2: X (fp32), b, A v, v
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
     mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part, rmd);
-    if (!rmd.out) hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, proj_part, nb, MAXB, 2 * m + 4, 0, proj_d);
+    if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
     QMat qm{};

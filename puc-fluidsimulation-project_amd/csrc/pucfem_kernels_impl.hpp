@@ -820,6 +820,12 @@ struct ChebVecs {
   double* xout[NR];
   const double* b[NR];
   float* d[NR];
+  // the solve's last step with k_visc_fin folded in (us[0] non-null): instead of d and x_out it writes
+  // u* = s x_out and the fp32 increment u* - u (the same operations as k_visc_fin: bit-identical)
+  const double* s;
+  const double* u[NR];
+  double* us[NR];
+  float* inc[NR];
 };
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
@@ -830,11 +836,18 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
   double rr[NR], bb[NR];
 #pragma unroll
   for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
+  const bool fin = v.us[0] != nullptr;
   auto finish = [&](int c, int64_t row, double ax, double x0, double br, double dr) {
     const double r = br - ax;
     const double dn = first ? c2 * r : c1 * dr + c2 * r;
-    stnt(v.d[c] + row, (float)dn);
-    stnt(v.xout[c] + row, x0 + dn);
+    if (fin) {
+      const double a = v.s[row] * (x0 + dn);
+      stnt(v.us[c] + row, a);
+      stnt(v.inc[c] + row, (float)(a - v.u[c][row]));
+    } else {
+      stnt(v.d[c] + row, (float)dn);
+      stnt(v.xout[c] + row, x0 + dn);
+    }
     rr[c] += r * r;
     bb[c] += br * br;
   };
@@ -2306,7 +2319,8 @@ __global__ void k_asm(int64_t n, const int64_t* __restrict__ ptr, const int32_t*
 // partials are L2 / MALL misses; a dependent load chain per thread would take nb / RB round trips).
 // Fixed combination order: deterministic for a given nb.
 constexpr int RB = 1024, RU = 8;
-__global__ __launch_bounds__(RB) void k_reduce(const double* part, int nb, int stride, int nv, int is_max, double* out) {
+template <int RB>
+__global__ __launch_bounds__(RB) void k_reduce_t(const double* part, int nb, int stride, int nv, int is_max, double* out) {
   __shared__ double sh[RB / 64];
   for (int v = 0; v < nv; ++v) {
     const double* p = part + (int64_t)v * stride;
@@ -2334,6 +2348,9 @@ __global__ __launch_bounds__(RB) void k_reduce(const double* part, int nb, int s
     }
   }
 }
+// the step's reductions: 1,024 threads (RB); 256 (k_reduce_t<256>, PUCFEM_RED_THREADS=256) schedules on a
+// CU with fewer free wave slots while the dye stream's kernels occupy the chip (measurement knob)
+constexpr auto k_reduce = k_reduce_t<RB>;
 
 template <typename T>
 __global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const T* __restrict__ a, const T* __restrict__ b,
