@@ -502,6 +502,7 @@ struct Ctx {
       if (st_sl) (void)hipStreamSynchronize(st_sl);
       if (ev_u) (void)hipEventDestroy(ev_u);
       if (ev_sl) (void)hipEventDestroy(ev_sl);
+      if (ev_gate) (void)hipEventDestroy(ev_gate);
       if (st_sl) (void)hipStreamDestroy(st_sl);
       if (st) (void)hipStreamDestroy(st);
     }
@@ -1603,9 +1604,55 @@ struct Ctx {
 
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
   RedOut sl_ro{};
+  // The dye tail of a step (final-divergence record, semi-Lagrangian advection, mixing sums, its part of
+  // the step record) on the side stream, after the main stream's event `gate`.  PUCFEM_SL_DELAY=1
+  // (a measurement knob): the tail of step n is enqueued after step n+1's viscous solve and waits for it, so it runs
+  // beside the first pressure solve (whose coarse multigrid levels are latency-bound and leave HBM
+  // bandwidth idle) instead of beside the bandwidth-bound viscous Chebyshev steps; 0 (default): right after
+  // step n.  A/B on one box (r8j): 107.6 / 108.5 (0) against 108.3 / 108.4 steps/s (1) -- the viscous
+  // steps speed up (441 -> 345 us) by what the semi-Lagrangian pass loses beside the pressure solve
+  // (698 -> 937 us): the step is bound by the bytes both streams move, not by where the tail sits.
+  bool sl_delay = std::getenv("PUCFEM_SL_DELAY") && std::atoi(std::getenv("PUCFEM_SL_DELAY")) != 0;
+  double* sl_deferred_rec = nullptr;  // a tail waiting for the next step's viscous solve (its step record)
+  hipEvent_t ev_gate = nullptr;
+  void dye_tail(double* rec) {
+    HIPCHK(hipEventRecord(ev_gate, st));
+    HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
+    {
+      StreamSwap sw(st, st_sl);
+      const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
+      div(ux, uy, final_div, false, part_fd, rf);
+      if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
+      const int nb = nb_sl(lp.n_own);
+      const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
+      sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
+      KCHK();
+      std::swap(c_full, c_new);
+      if (!rs.out) reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+      const int nbm = nb_rows(lp.n_own);
+      algo_bytes += 16.0 * (double)lp.n_own;  // c, w
+      const RedOut rm = ro(vals + 5, CNT_DYE_MIX, 1);
+      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
+                         part_mx, rm);
+      KCHK();
+      if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
+      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
+      KCHK();
+    }
+    HIPCHK(hipEventRecord(ev_sl, st_sl));
+    sl_pending = true;
+  }
+  // a deferred tail goes now (behind whatever the main stream holds)
+  void dye_flush() {
+    if (!sl_deferred_rec) return;
+    double* r = sl_deferred_rec;
+    sl_deferred_rec = nullptr;
+    dye_tail(r);
+  }
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
+    dye_flush();  // the previous step's deferred dye tail, beside the pressure solve below
     const bool f1 = div_rhs(usx, usy, div_star, vals);  // max |div u*| -> vals[0]
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
     const int itp = pressure(yp, p, 1, f1);
@@ -1645,34 +1692,12 @@ struct Ctx {
         }
         HIPCHK(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_sl, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
       }
       hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);  // max |div u*|
       KCHK();
-      HIPCHK(hipEventRecord(ev_u, st));
-      HIPCHK(hipStreamWaitEvent(st_sl, ev_u, 0));
-      {
-        StreamSwap sw(st, st_sl);
-        const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
-        div(ux, uy, final_div, false, part_fd, rf);
-        if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
-        const int nb = nb_sl(lp.n_own);
-        const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
-        sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
-        KCHK();
-        std::swap(c_full, c_new);
-        if (!rs.out) reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
-        const int nbm = nb_rows(lp.n_own);
-        algo_bytes += 16.0 * (double)lp.n_own;  // c, w
-        const RedOut rm = ro(vals + 5, CNT_DYE_MIX, 1);
-        hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
-                           part_mx, rm);
-        KCHK();
-        if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
-        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
-        KCHK();
-      }
-      HIPCHK(hipEventRecord(ev_sl, st_sl));
-      sl_pending = true;
+      if (sl_delay) sl_deferred_rec = rec;  // enqueued by the next step after its viscous solve (dye_flush)
+      else dye_tail(rec);
     } else if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       if (dye_impl) {
@@ -3375,9 +3400,11 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
+          c.dye_flush();  // the last step's deferred dye tail
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
+          c.sl_deferred_rec = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
           throw;
