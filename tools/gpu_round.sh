@@ -24,6 +24,10 @@ rm -rf /tmp/prof_$TAG
 step rocprof_stats 900 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG/stats -o run --output-format csv -- \
   python "$ROOT/bench.py" $BARGS
 find /tmp/prof_$TAG/stats -name "*stats*.csv" -exec cp {} "$OUT/" \;
+# per-kernel time over the bench's timed window (the driver schedule: --warmup W --steps K in BARGS)
+TR=$(find /tmp/prof_$TAG/stats -name "*kernel_trace.csv" | head -1)
+W=$(echo " $BARGS" | sed -n 's/.* --warmup \([0-9]*\).*/\1/p'); K=$(echo " $BARGS" | sed -n 's/.* --steps \([0-9]*\).*/\1/p')
+[ -n "$TR" ] && python "$ROOT/tools/trace_window.py" "$TR" --warmup ${W:-20} --steps ${K:-20} --top 80 > "$OUT/step_window.txt"
 if [ -z "$SKIP_PMC" ]; then
   step pmc_fetch 900 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d /tmp/prof_$TAG/fetch -o run --output-format csv -- \
     python "$ROOT/bench.py" $BARGS --steps 1 --warmup 1 --no-cpu-baseline --no-secondary

@@ -7,11 +7,10 @@ Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--level 7 --world 1]
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's memory-side request
 counters, FETCH_SIZE under-reports wide streaming reads by exactly 2x on gfx950, and other access
 widths must be calibrated on a known byte count in one's own access pattern.  The guide's
-corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_visc_fin, a pure 8-B/lane
-elementwise kernel whose algorithmic traffic is exactly 40 B/row read (s, yx, yy, ux, uy) and 24 B/row
-written (u*x, u*y in fp64, the two increments in fp32; 32 B/row before the increments went to fp32),
-nrows from the bench line.  (k_visc_prep, the check of
-round 1, reads 32-80 B/row depending on the extrapolation order of the step, so it no longer is one.)  Raw counter values are kept next
+corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_diff2 (the projection update of
+the pressure solves), a pure 8-B/lane elementwise kernel whose algorithmic traffic is exactly 32 B/row
+read (y, x0, A v or b, r_final) and 16 B/row written (v, A v), nrows from the bench line.  (Rounds 1-2
+checked k_visc_fin, which round 3 folded into the viscous solve's last step.)  Raw counter values are kept next
 to the corrected bytes.  Caveat: the L2 is write-back, so up to ~32 MiB of one kernel's dirty lines
 are evicted (and counted) during the next kernel.
 """
@@ -73,18 +72,18 @@ def main():
         except Exception:
             pass
     # gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a
-    # streaming read, WRITE_SIZE counts streaming stores exactly; both in KiB.  Checked on k_visc_fin,
-    # a pure elementwise kernel with exactly 40 B/row read (s, yx, yy, ux, uy) and 24 B/row written
-    # (usx, usy fp64; dx, dy fp32): the corrected values must equal the algorithmic bytes.
+    # streaming read, WRITE_SIZE counts streaming stores exactly; both in KiB.  Checked on k_diff2,
+    # a pure elementwise kernel with exactly 32 B/row read and 16 B/row written (all fp64): the
+    # corrected values must equal the algorithmic bytes.
     res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
     fr, fw = 2.0 * 1024.0, 1.0 * 1024.0
     check = None
-    cal = [k for k in kern if short(k[0]).endswith("k_visc_fin")]
+    cal = [k for k in kern if short(k[0]).endswith("k_diff2")]
     if cal and nrows and fetch.get(cal[0]) and write.get(cal[0]):
         f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
         w_avg = sum(write[cal[0]]) / len(write[cal[0]])
-        check = {"kernel": "k_visc_fin", "nrows": nrows, "algorithmic_read": 40.0 * nrows,
-                 "corrected_read": f_avg * fr, "algorithmic_write": 24.0 * nrows, "corrected_write": w_avg * fw}
+        check = {"kernel": "k_diff2", "nrows": nrows, "algorithmic_read": 32.0 * nrows,
+                 "corrected_read": f_avg * fr, "algorithmic_write": 16.0 * nrows, "corrected_write": w_avg * fw}
     res["calibration"] = {"read_bytes_per_unit": fr, "write_bytes_per_unit": fw,
                           "note": "FETCH_SIZE x2 KiB, WRITE_SIZE x1 KiB (guide's gfx950 corrections)",
                           "check": check}
@@ -108,7 +107,9 @@ def main():
                     ("k_cg_dir", [k for k in res["kernels"] if k.startswith("k_cg_dir<1,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
                     ("k_cg_dir<2>", [k for k in res["kernels"] if k.startswith("k_cg_dir<2,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
                     ("k_sl", [k for k in res["kernels"] if k.startswith("k_sl") and not k.startswith("k_sl_") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_sl_slow", [k for k in res["kernels"] if k.startswith("k_sl_slow") and "hbm_bytes_per_launch" in res["kernels"][k]])):
+                    ("k_sl_slow", [k for k in res["kernels"] if k.startswith("k_sl_slow") and "hbm_bytes_per_launch" in res["kernels"][k]]),
+                    ("k_vcheb<2>", [k for k in res["kernels"] if k.startswith("k_vcheb<2,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
+                    ("k_div", [k for k in res["kernels"] if k.startswith("k_div<") and "hbm_bytes_per_launch" in res["kernels"][k]])):
         if ks:
             n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
