@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--mg-post", type=int, default=3, help="Chebyshev post-smoothing degree")
     ap.add_argument("--mg-ratio", type=float, default=15.0, help="Chebyshev interval [lmax / ratio, lmax]")
     ap.add_argument("--mg-kind", type=int, default=1, choices=[1, 4], help="Chebyshev smoother of the first / fourth kind")
-    ap.add_argument("--proj-k", type=int, default=16,
+    ap.add_argument("--proj-separate", action="store_true",
+                    help="a projection basis per pressure solve instead of one shared by both")
+    ap.add_argument("--proj-k", type=int, default=32,
                     help="pressure initial guess: A-projection onto the last K solutions (0: warm start only)")
     ap.add_argument("--proj-k-visc", type=int, default=0, help="the same for the viscous solve (0: warm start)")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
@@ -115,7 +117,8 @@ def main():
     tol = pf.Tolerances.production(precond=a.precond, mg_single=not a.mg_double,
                                    mg_f16_vals={"f16": True, "f32": False, "coarse-f16": "coarse"}[a.mg_vals],
                                    index16=not a.index32, mg_degree=a.mg_pre, mg_post=a.mg_post, mg_ratio=a.mg_ratio,
-                                   mg_kind=a.mg_kind, proj_k=a.proj_k, proj_k_visc=a.proj_k_visc)
+                                   mg_kind=a.mg_kind, proj_k=a.proj_k, proj_k_visc=a.proj_k_visc,
+                                   proj_shared=not a.proj_separate)
     if a.rtol_pres is not None:
         tol.rtol_pres = a.rtol_pres
     a.rtol_pres = tol.rtol_pres
@@ -204,7 +207,8 @@ def main():
             "dt": 0.05, "nu": 0.1, "B1": -2.0, "B2": 0.0,
             "rtol_pres": a.rtol_pres, "rtol_visc": 1e-12, "pressure_precond": sim.ctx.precond,
             "mg_cheb": {"kind": a.mg_kind, "pre": a.mg_pre, "post": a.mg_post, "ratio": a.mg_ratio},
-            "pressure_guess": f"projection onto up to {a.proj_k} solution directions" if a.proj_k else "previous solution",
+            "pressure_guess": (f"projection onto up to {a.proj_k} solution directions"
+                               + (" per solve" if a.proj_separate else " shared by both solves")) if a.proj_k else "previous solution",
             "viscous_guess": f"projection onto up to {a.proj_k_visc} solution directions" if a.proj_k_visc else "u^n",
             "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
         },

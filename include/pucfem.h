@@ -101,6 +101,9 @@ typedef struct pucfem_params {
                           pattern and the K / Gx / Gy / lumped-mass values of every level (buildStiffnessMatrix,
                           buildLumpedMassMatrix and the divergence / gradient coefficients, StokesColor.py:98-128,
                           130-284) are assembled on the device, bit-identical to the host assembly; 1 = host C++ */
+  int32_t proj_shared; /* 1 = the two pressure solves of a step project onto ONE basis of up to proj_k
+                          directions that collects the solutions of both (the same merged operator: one
+                          A-orthonormal basis serves both); 0 = a basis per solve */
 } pucfem_params;
 
 /* per-step diagnostics, the values the reference prints (StokesColor.py:586, StokesFood.py:505) */

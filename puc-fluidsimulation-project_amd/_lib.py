@@ -39,7 +39,7 @@ class Params(ct.Structure):
         ("mg_single", ct.c_int32), ("mg_rep_nodes", ct.c_int64), ("mg_f32_vals", ct.c_int32),
         ("idx32", ct.c_int32), ("proj_k", ct.c_int32), ("proj_k_visc", ct.c_int32), ("mg_kind", ct.c_int32),
         ("solver_path", ct.c_int32), ("assembled", ct.c_int32), ("dye_scheme", ct.c_int32),
-        ("dye_diffusivity", ct.c_double), ("assembly", ct.c_int32),
+        ("dye_diffusivity", ct.c_double), ("assembly", ct.c_int32), ("proj_shared", ct.c_int32),
     ]
 
 

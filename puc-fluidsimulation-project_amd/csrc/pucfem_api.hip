@@ -1185,6 +1185,12 @@ struct Ctx {
     }
   }
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
+  // prm.proj_shared: both pressure solves of a step project onto ONE basis (the same merged operator, so
+  // one A-orthonormal basis serves both) that collects the solutions of both -- slot 1 for both; else a
+  // basis per solve.  Separate bases stop improving at 16 directions; a shared one keeps improving up to
+  // PROJ_MAX = 32 (r8l: 72 -> 63 pressure iterations over the driver window, +2 % steps/s)
+  bool proj_shared = false;  // prm.proj_shared (PUCFEM_PROJ_SHARED=0/1 overrides it: a measurement knob)
+  int proj_slot(int which) const { return proj_shared && which == 2 ? 1 : which; }
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
     const FaceDev fc = fP.part();
     const int nb = grid_part(fc, dPp);  // also the grid of the V-cycle's last smoothing step (<r, z> partials)
@@ -1206,7 +1212,7 @@ struct Ctx {
     // the projection's update takes A (y - x0) = r0 - r_final from the CG's residuals: k_cg_init
     // keeps r0 in pav (its "first direction" output; pcg_mg's directions live elsewhere)
     const bool keep_r0 = proj_k > 0 && (which == 1 || which == 2);
-    if (keep_r0) vi.po[0] = pav[which];
+    if (keep_r0) vi.po[0] = pav[proj_slot(which)];
     algo_bytes += (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
                   (24.0 + (mg_single ? 4.0 : 0.0) + (keep_r0 ? 8.0 : 0.0)) * (double)n;
     // fused reductions: <r, r> -> redbuf slot 0, <b, b> -> slot 1 (as k_reduce would place them)
@@ -1407,7 +1413,7 @@ struct Ctx {
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
-    if (proj) project_guess(which, bh, yst);
+    if (proj) project_guess(proj_slot(which), bh, yst);
     int it;
     if (dense) {
       hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
@@ -1416,7 +1422,7 @@ struct Ctx {
       it = 0;
     } else if (use_mg) {
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
-      if (proj) project_update(which, yst, bh, cg_r[0]);
+      if (proj) project_update(proj_slot(which), yst, bh, cg_r[0]);
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
@@ -2691,6 +2697,8 @@ void build(Ctx& c) {
   // (a basis needs room for the re-seeded span and one new direction: at least 3)
   auto proj_size = [](int k) { return k <= 0 ? 0 : std::max(3, std::min(k, (int)PROJ_MAX)); };
   c.proj_k = c.use_mg && !c.dense ? proj_size(c.prm.proj_k) : 0;
+  c.proj_shared = c.prm.proj_shared != 0;
+  if (const char* e = std::getenv("PUCFEM_PROJ_SHARED")) c.proj_shared = std::atoi(e) != 0;
   const bool block_visc = !c.dist() && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
   c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
   for (int w = 1; w <= 4; ++w) {

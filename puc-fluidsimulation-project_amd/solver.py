@@ -67,6 +67,7 @@ class Tolerances:
     mg_kind: int = 1  # smoother: 1 = Chebyshev on [lmax/mg_ratio, lmax], 4 = fourth-kind Chebyshev
     proj_k: int = 24  # pressure initial guess: A-projection onto up to proj_k solution directions (0: warm start)
     proj_k_visc: int = 0  # the same for the viscous solve's two components (measured: no net gain at L7)
+    proj_shared: bool = False  # both pressure solves of a step project onto one shared basis
     # "auto": small meshes (<= 1500 nodes, one rank) solve with precomputed dense inverses and meshes of
     # <= 4096 nodes with a one-workgroup CG; "iterative": the large-mesh multi-kernel CG path on every mesh
     solver_path: str = "auto"
@@ -83,15 +84,18 @@ class Tolerances:
     @classmethod
     def production(cls, **kw):
         """The settings bench.py measures (and the production-path parity tests check): multigrid-
-        preconditioned pressure CG with the fp32 V-cycle, the 16-direction projected pressure guess,
+        preconditioned pressure CG with the fp32 V-cycle, the pressure guess projected onto one basis of
+        up to 32 directions shared by both pressure solves,
         int16 column deltas, the extrapolated viscous start, pressure rtol PRODUCTION_RTOL_PRES."""
         # V(3,3) Chebyshev smoothing on [lmax / 15, lmax]: measured at L7 against V(2,2) / ratio 10 and the
         # neighbouring choices (DESIGN.md §5; driver command 90.7 -> 97.6 steps/s)
         base = dict(rtol_visc=1e-12, rtol_pres=PRODUCTION_RTOL_PRES, precond="mg", mg_single=True,
                     mg_f16_vals=False, index16=True, mg_degree=3, mg_post=3, mg_ratio=15.0, mg_kind=1,
-                    proj_k=16, proj_k_visc=0)
-        # proj_k 16: the driver command on one box, twice each (r8d): 24 -> 106.8 / 107.0, 16 -> 107.1 / 108.5,
-        # 12 -> 105.6 / 105.6, 8 -> 99.8 / 100.0 steps/s; pressure iterations 72 / 72 / 76 / 83
+                    proj_k=32, proj_shared=True, proj_k_visc=0)
+        # separate bases per solve (r8d, one box, twice each): 24 -> 106.8 / 107.0, 16 -> 107.1 / 108.5,
+        # 12 -> 105.6 / 105.6, 8 -> 99.8 / 100.0 steps/s, pressure iterations 72 / 72 / 76 / 83 (saturated
+        # at 16); ONE basis shared by both solves keeps improving with its size (r8l): 16 -> 105.1 / 105.4
+        # (73 iterations), 24 -> 106.9 / 107.1 (68), 32 -> 109.5 / 110.1 (63) against separate 16: 107.6 / 107.8
         base.update(kw)
         return cls(**base)
 
@@ -177,7 +181,7 @@ class Context:
                         mg_kind=tol.mg_kind, solver_path={"auto": 0, "iterative": 1}[tol.solver_path],
                         assembled={"auto": 0, "assembled": 1}[tol.operators],
                         dye_scheme={"semilagrange": 0, "implicit": 1}[tol.dye], dye_diffusivity=tol.dye_diffusivity,
-                        assembly={"auto": 0, "device": 0, "host": 1}[tol.assembly])
+                        assembly={"auto": 0, "device": 0, "host": 1}[tol.assembly], proj_shared=int(tol.proj_shared))
         self.precond = "mg" if mg else "jacobi"
         self._c(self.L.pucfem_build_operators(self.h, ct.byref(p)))
 

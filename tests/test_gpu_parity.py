@@ -378,12 +378,14 @@ def test_knn_radii_device_equals_host(monkeypatch, records):
     b.close()
 
 
-def test_projected_pressure_guess_same_steps():
+@pytest.mark.parametrize("shared", [False, True])
+def test_projected_pressure_guess_same_steps(shared):
     """Successive-RHS projection (Fischer) only changes the pressure CG's initial guess: 24 steps with
     a 3-vector basis (several restarts) equal the warm-started run to the CG tolerance, and once the
-    flow is steady the projected guesses need fewer iterations."""
+    flow is steady the projected guesses need fewer iterations -- with a basis per pressure solve and
+    with one basis shared by both solves of a step."""
     mesh = pf.load_mesh("fine", refine=2)
-    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", proj_k=3))
+    a = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", proj_k=3, proj_shared=shared))
     b = stokes(mesh, tol=S.Tolerances(rtol_pres=1e-12, precond="mg", proj_k=0))
     sa, sb = a.step(24), b.step(24)
     assert np.abs(a.u - b.u).max() < 1e-8

@@ -2,7 +2,7 @@
 
 bench.py measures Tolerances.production(): the multi-kernel Jacobi-scaled viscous CG<2> with the
 extrapolated warm start, the multigrid-preconditioned pressure CG with the fp32 V-cycle, the
-16-direction projected pressure guess (re-seeded when full), int16 SELL column deltas and the
+pressure guess projected onto a 32-direction basis shared by both solves (re-seeded when full), int16 SELL column deltas and the
 locate-then-rank semi-Lagrangian kernel.  mesh_fine itself takes the small-mesh direct path, so these
 tests run refined meshes (L2 = 17k, L3 = 69k nodes) where none of the small-mesh shortcuts apply, and
 compare against oracle.StokesRef (exact sparse solves of the same pressure restatement) along
@@ -36,7 +36,7 @@ def _need_gpu():
 @pytest.mark.parametrize("operators", ["auto", "assembled"])
 def test_production_color_L3_every_step_vs_oracle(operators):
     """48 StokesColor steps on mesh_fine x3 (69,632 nodes) with the bench's exact settings: the
-    projection bases fill (16 directions per pressure solve) and are re-seeded at least twice.
+    projection basis fills (32 directions shared by both pressure solves) and are re-seeded at least twice.
     operators 'auto' is the production path (matrix-free lattice stencils on the face interiors,
     SELL rows on the skeleton); 'assembled' the stored SELL operators (int16 column deltas) for every row."""
     mesh = pf.load_mesh("fine", refine=3)
@@ -64,7 +64,7 @@ def test_production_color_L3_every_step_vs_oracle(operators):
         assert abs(st.mix_var - out["mixing"][2]) < 1e-9, k
     path = sim.ctx.path_info()
     assert path["viscous"] == "multi-kernel" and path["pressure"] == "mg-pcg", path
-    assert path["proj_k"] == 16 and path["reseeds"] >= 2, path
+    assert path["proj_k"] == 32 and path["reseeds"] >= 2, path
     assert path["visc_extrap_order"] == 5, path
     print(f"L3 production path ({operators}), 48 steps: max |u - oracle| = {worst_u:.2e}, "
           f"max |c - oracle| = {worst_c:.2e}")

@@ -117,7 +117,7 @@ def test_production_partitioned_L3_vs_oracle(world):
     assert not errs, errs
     assert all(o is not None for o in out)
     assert sum(o["info"]["n_own"] for o in out) == mesh.N
-    assert all(o["path"]["pressure"] == "mg-pcg" and o["path"]["proj_k"] == 16 for o in out)
+    assert all(o["path"]["pressure"] == "mg-pcg" and o["path"]["proj_k"] == 32 for o in out)
     ref = O.StokesRef(mesh.coords, mesh.markers, mesh.triangles, 0.05, 0.1, -2.0, 0.0, "color")
     u, c = ref.initial()
     for _ in range(12):
