@@ -73,7 +73,7 @@ typedef struct pucfem_params {
   double mg_ratio;     /* Chebyshev interval [lmax / mg_ratio, lmax] (10) */
   int32_t mg_post;     /* post-smoothing steps (0: same as mg_degree) */
   int32_t mg_single;   /* 1: fp32 V-cycle (values, vectors, halos) inside the fp64 CG */
-  int64_t mg_rep_nodes; /* multi-rank: coarse levels up to this many nodes are replicated (0: 300000) */
+  int64_t mg_rep_nodes; /* multi-rank: coarse levels up to this many nodes are replicated (0: 1000000) */
   int32_t mg_f32_vals; /* fp32 cycle: 0 = level operators stored in fp16 when every value is representable
                           (arithmetic stays fp32), 1 = all stored in fp32, 2 = the finest in fp32 and
                           the coarser levels in fp16 */

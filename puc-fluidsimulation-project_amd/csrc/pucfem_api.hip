@@ -2388,7 +2388,10 @@ void build(Ctx& c) {
       for (int r = 0; r <= c.world; ++r) L.rs[r] = L.ord.strip_ptr[cut[r]];
     }
     // replicated coarse levels (multi-rank): level 0 always, then every level up to mg_rep_nodes
-    const i64 rep_max = prm.mg_rep_nodes > 0 ? prm.mg_rep_nodes : 300000;
+    // default 1M: at L7 L5 (894k) and below are replicated.  Counted at W = 8 (tools/comm_probe.py, r8n):
+    // grouped exchanges per PCG iteration 25 -> 17, per step 264-385 -> 184-265, for each rank smoothing
+    // the whole L5 (latency-bound launches either way: ~11 against ~6 us)
+    const i64 rep_max = prm.mg_rep_nodes > 0 ? prm.mg_rep_nodes : 1000000;
     for (int l = 0; l < Lv; ++l) c.mg[l].rep = c.dist() && (l == 0 || c.mg[l].mesh.N <= rep_max);
     for (int l = 1; l < Lv; ++l) c.mg[l].rep = c.mg[l].rep && c.mg[l - 1].rep;
     for (int l = 0; l <= Lv; ++l) {

@@ -3,7 +3,7 @@ the wide dye halo each rank receives vs a full all-gather, after each of S steps
 communicator's traffic (pucfem_comm_counters: all-reduce calls and values, point-to-point sends and
 bytes, grouped launches, broadcasts), the pressure / viscous iteration counts and the kernel launches.
 The same call sequence runs over RCCL on W GPUs (NcclComm), so the counts are the production path's.
-  python tools/comm_probe.py LEVEL W STEPS"""
+  python tools/comm_probe.py LEVEL W STEPS [MG_REP_NODES]"""
 import os
 import sys
 import threading
@@ -14,6 +14,7 @@ from conftest import load_pkg  # noqa: E402
 
 pf = load_pkg()
 level, world, steps = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (5, 8, 6)))
+rep_nodes = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # coarse levels up to this size replicated (0: default)
 mesh = pf.load_mesh("fine", refine=level)
 uid = b"PUCFEM-LOCALCOMM" + os.urandom(112)
 rows = [[None] * steps for _ in range(world)]
@@ -22,8 +23,8 @@ errs = []
 
 def worker(r):
     try:
-        sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", 0, pf.Tolerances.production(),
-                                  dist=(r, world, uid))
+        sim = pf.StokesSimulation(mesh, pf.SquirmerBC(), 0.05, "color", 0,
+                                  pf.Tolerances.production(mg_rep_nodes=rep_nodes), dist=(r, world, uid))
         for k in range(steps):
             c0, (n0, _) = sim.ctx.comm_counters(), sim.ctx.counters()
             st = sim.step(1)[0]
@@ -43,7 +44,7 @@ for t in th:
 for t in th:
     t.join()
 assert not errs, errs
-print(f"L{level} N={mesh.N} W={world}")
+print(f"L{level} N={mesh.N} W={world} mg_rep_nodes={rep_nodes or 'default'}")
 for k in range(steps):
     h = [rows[r][k]["dye_halo_values"] for r in range(world)]
     a = [rows[r][k]["allgather_values"] for r in range(world)]
