@@ -460,8 +460,9 @@ struct Ctx {
   } proj_hist[5];
   int proj_keep = std::getenv("PUCFEM_PROJ_KEEP")
                       ? std::max(2, std::min(PROJ_KEEP_MAX, std::atoi(std::getenv("PUCFEM_PROJ_KEEP"))))
-                      : 8;
+                      : 16;
   double *proj_part = nullptr, *proj_d = nullptr, *proj_coef = nullptr;
+  double* dqm = nullptr;  // re-seed coefficients (QMat) on the device
   bool proj_pend[5] = {false, false, false, false, false};  // v / A v wait for the next guess
   double *pv[5] = {}, *pav[5] = {};
   // viscous warm start u^n + a polynomial extrapolation of the increments u* - u of the last steps:
@@ -1466,7 +1467,8 @@ struct Ctx {
     QMat qm{};
     int kq = m;
     if (m == op.kmax) kq = proj_reseed(which, m, qm);  // full: X' = Q X, the dots follow as Q a, Q c
-    hipLaunchKernelGGL(k_pcoef, dim3(1), dim3(64), 0, st, (const double*)proj_d, m, qm, m == op.kmax ? kq : -1,
+    hipLaunchKernelGGL(k_pcoef, dim3(1), dim3(64), 0, st, (const double*)proj_d, m, (const double*)dqm,
+                       m == op.kmax ? kq : -1,
                        1.0 / (double)n_free, proj_coef);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
@@ -1534,9 +1536,12 @@ struct Ctx {
     const int kq = (int)Q.size();
     for (int i = 0; i < kq; ++i)
       for (int j = 0; j < m; ++j) qm.q[i][j] = Q[i][j];
+    // (pageable source: the copy is staged before the call returns)
+    HIPCHK(hipMemcpyAsync(dqm, &qm, sizeof(QMat), hipMemcpyHostToDevice, st));
     const i64 n = lp.n_own;
     algo_bytes += 4.0 * (double)(m + kq) * (double)n;
-    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], nloc, m, qm, kq,
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], nloc, m,
+                       (const double*)dqm, kq,
                        projXalt[which]);
     KCHK();
     std::swap(projX[which], projXalt[which]);
@@ -2721,6 +2726,7 @@ void build(Ctx& c) {
         c.pav[w] = c.dalloc<double>(c.nloc);
       }
     c.proj_part = c.dalloc<double>((i64)Ctx::NCOEF * MAXB);
+    c.dqm = c.dalloc<double>((i64)sizeof(QMat) / (i64)sizeof(double));
     c.proj_d = c.dalloc<double>(Ctx::NCOEF);
     c.proj_coef = c.dalloc<double>(Ctx::NCOEF);
   }

@@ -8,6 +8,21 @@
 namespace pucfem {
 namespace dev {
 
+// row-group sizes of face kernels (rows per thread loaded together, face_rows_k): compile-time, so A/B
+// builds (tools/build_variant.sh) can measure them; the defaults are the measured choices
+#ifndef PUCFEM_INIT_K
+#define PUCFEM_INIT_K 2
+#endif
+#ifndef PUCFEM_VCHEB_K
+#define PUCFEM_VCHEB_K 2
+#endif
+#ifndef PUCFEM_DIV_K
+#define PUCFEM_DIV_K 2
+#endif
+#ifndef PUCFEM_GRADP_K
+#define PUCFEM_GRADP_K 4
+#endif
+
 // ----------------------------------------------------------------------------- lattice face rows
 // fn(F, lf, t, i, j) for the interior rows of the face part that block b of nbf runs (work items: chunks
 // of BS consecutive rows of one face; the item index is block-uniform, so the face table entry and
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // groups of K rows per thread, every gathered value of a group loaded first (face_rows_k)
-    constexpr int K = face_k(NR == 1 ? 4 : 2);
+    constexpr int K = face_k(NR == 1 ? PUCFEM_INIT_K : 2);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -495,13 +510,14 @@ constexpr int PROJ_MAX = 32;
 // combinations are formed in fp64.  Halves the two passes over the basis (2 m vector reads per solve).
 using ProjT = float;
 
-// basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X
-constexpr int PROJ_KEEP_MAX = 8;
+// basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X.
+// Q: the re-seed coefficients in device memory, row-major [PROJ_KEEP_MAX][PROJ_MAX] (block-uniform loads)
+constexpr int PROJ_KEEP_MAX = 16;
 struct QMat {
   double q[PROJ_KEEP_MAX][PROJ_MAX];
 };
-__global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restrict__ X, int64_t ld, int m, QMat Q,
-                                               int kq, ProjT* __restrict__ out) {
+__global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restrict__ X, int64_t ld, int m,
+                                               const double* __restrict__ Q, int kq, ProjT* __restrict__ out) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
     double acc[PROJ_KEEP_MAX];
 #pragma unroll
@@ -509,7 +525,7 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
     for (int j = 0; j < m; ++j) {
       const double x = (double)X[j * ld + r];
 #pragma unroll
-      for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] += Q.q[i][j] * x;
+      for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] += Q[i * PROJ_MAX + j] * x;
     }
 #pragma unroll
     for (int i = 0; i < PROJ_KEEP_MAX; ++i)
@@ -566,7 +582,8 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
 // [a (m'), c (m'), s, mu, alpha] with a_i = <X_i, b>, c_i = <X_i, A v>,
 // s = (<v, A v> - |c|^2)^-1/2 (0 when v lies in span X to 1e-10 relative: a null direction),
 // mu = sum_free v / n_free, alpha = <X_m, b> = s (<v, b> - mu sum_free b - <c, a>).
-__global__ void k_pcoef(const double* __restrict__ D, int m, QMat Q, int kq, double inv_nfree, double* K) {
+__global__ void k_pcoef(const double* __restrict__ D, int m, const double* __restrict__ Q, int kq, double inv_nfree,
+                        double* K) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int mp = kq >= 0 ? kq : m;
   double q = 0.0, ca = 0.0;
@@ -574,8 +591,8 @@ __global__ void k_pcoef(const double* __restrict__ D, int m, QMat Q, int kq, dou
     double a = 0.0, c = 0.0;
     if (kq >= 0) {
       for (int j = 0; j < m; ++j) {
-        a += Q.q[i][j] * D[j];
-        c += Q.q[i][j] * D[m + j];
+        a += Q[i * PROJ_MAX + j] * D[j];
+        c += Q[i * PROJ_MAX + j] * D[m + j];
       }
     } else {
       a = D[i];
@@ -852,7 +869,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
     bb[c] += br * br;
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    constexpr int K = face_k(NR == 1 ? 4 : 2);
+    constexpr int K = face_k(NR == 1 ? 4 : PUCFEM_VCHEB_K);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -1078,7 +1095,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
     // groups of 2 rows per thread, the 24 gathered values of a group loaded first
-    constexpr int K = face_k(2);
+    constexpr int K = face_k(PUCFEM_DIV_K);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -1198,7 +1215,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
   const double* by = MODE == 0 ? usy : uy;
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
     // interior rows are never Dirichlet nodes
-    constexpr int K = face_k(4);
+    constexpr int K = face_k(PUCFEM_GRADP_K);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
