@@ -98,14 +98,21 @@ struct HFace {
   FaceDev d{};
   int32_t items = 0;
   int64_t rows = 0;  // face-interior rows (algorithmic bytes)
+  // PUCFEM_FACE_SEQ=1 (measurement knob): one block per face running its chunks in order (FaceDev::seq)
+  static bool face_seq() {
+    static const bool on = std::getenv("PUCFEM_FACE_SEQ") && std::atoi(std::getenv("PUCFEM_FACE_SEQ")) != 0;
+    return on;
+  }
   FaceDev part() const {
     FaceDev f = d;
     f.nb = std::min(items, FACE_PART_BLOCKS);
+    if (face_seq() && d.cpf > 1 && d.nf <= FACE_PART_BLOCKS) f.nb = d.nf, f.seq = 1;
     return f;
   }
   FaceDev full() const {
     FaceDev f = d;
     f.nb = items;
+    if (face_seq() && d.cpf > 1) f.nb = d.nf, f.seq = 1;
     return f;
   }
 };

@@ -68,6 +68,8 @@ struct FaceDev {
   float rinv;                // 1 / (n - 1)
   int32_t nb;                // blocks on the face part
   int32_t op;                // 0 = stiffness-type stencil (K, merged pressure, level operators), 1 = scaled A_visc
+  int32_t seq;               // 1: nb = nf and block f runs face f's chunks in order (the halo rows a chunk shares
+                             // with the previous one are still in L2); 0: one block per chunk item
 };
 
 template <class T>

@@ -29,6 +29,21 @@ namespace dev {
 // the coefficient record are scalar loads)
 template <class Fn>
 __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
+  if (fc.seq) {  // block b: face b, its chunks in order
+    const lat::FaceTab F = fc.tab[b];
+    for (int32_t ch = 0; ch < fc.cpf; ++ch) {
+      const int32_t t0 = ch * (BS * FACE_RPT) + (int32_t)threadIdx.x;
+      for (int32_t r = 0; r < FACE_RPT; ++r) {
+        const int32_t t = t0 + r * BS;
+        if (t < fc.F) {
+          int32_t i, j;
+          lat::coords(t, fc.n, fc.rinv, i, j);
+          fn(F, b, t, i, j);
+        }
+      }
+    }
+    return;
+  }
   const int32_t items = fc.nf * fc.cpf;
   // one block per item (launches without partials): consecutive chunks of a face run on one XCD
   // (blocks are dealt round-robin over the 8 XCDs), so the rows a chunk shares with its neighbours
@@ -62,6 +77,27 @@ __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t 
 template <int K, class Fn>
 __device__ __forceinline__ void face_rows_k(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
   static_assert(FACE_RPT % K == 0, "group size divides the rows per thread");
+  if (fc.seq) {  // block b: face b, its chunks in order (face_rows)
+    const lat::FaceTab F = fc.tab[b];
+    for (int32_t ch = 0; ch < fc.cpf; ++ch) {
+      const int32_t t0 = ch * (BS * FACE_RPT) + (int32_t)threadIdx.x;
+#pragma unroll
+      for (int32_t g = 0; g < FACE_RPT; g += K) {
+        if (t0 + g * BS >= fc.F) break;
+        int32_t t[K], i[K], j[K];
+        bool ok[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          const int32_t tt = t0 + (g + r) * BS;
+          ok[r] = tt < fc.F;
+          t[r] = ok[r] ? tt : fc.F - 1;
+          lat::coords(t[r], fc.n, fc.rinv, i[r], j[r]);
+        }
+        fn(F, b, t, i, j, ok);
+      }
+    }
+    return;
+  }
   const int32_t items = fc.nf * fc.cpf;
   if (nbf == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows)
     const int32_t x = b & 7, q = items >> 3, rem = items & 7;
