@@ -1231,20 +1231,32 @@ struct Ctx {
     });
     KCHK();
     Red rr{redbuf, 1, 1}, bb{redbuf + 8, 1, 1};
+    const double tol2 = tol * tol;
+    // single rank with k_reduce: the reduction of <b, b> (and, per iteration, of <r, r>) also runs the
+    // convergence test (k_reduce_conv: one launch instead of k_reduce + k_conv; multi-rank runs test after
+    // the all-reduce)
+    const bool merged_conv = !dist() && !ri.out;
     if (ri.out) {
       red_done(redbuf, 1, false);
       red_done(redbuf + 8, 1, false);
     } else {
       rr = reduce_global(part_a, nb, 1, false, 0);
-      bb = reduce_global(part_b, nb, 1, false, 1);
+      if (merged_conv) {
+        hipLaunchKernelGGL(k_reduce_conv, dim3(1), dim3(RB), 0, st, (const double*)part_b, nb, MAXB, redbuf + 8,
+                           (const double*)rr.p, (const double*)(redbuf + 8), tol2, ctl, 0);
+        KCHK();
+      } else {
+        bb = reduce_global(part_b, nb, 1, false, 1);
+      }
     }
     const RedOut rdir = ro(redbuf + 16, CNT_DIR, 1), rupd = ro(redbuf, CNT_UPD, 1);
-    const double tol2 = tol * tol;
     // (iteration, first timing sample): samples from the converged iteration on are dropped
     std::vector<std::pair<int, size_t>> marks;
     std::vector<std::pair<int, double>> bmarks;  // (iteration, algo_bytes at its start) of the current chunk
-    hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
-    KCHK();
+    if (!merged_conv) {
+      hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
+      KCHK();
+    }
     // direction: z (4 B in the fp32 cycle) and p_old gathered once, p and q written
     const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
                              (mg_single ? 28.0 : 32.0) * (double)n;
@@ -1289,8 +1301,14 @@ struct Ctx {
                 (const double*)scal, (const int*)ctl, part_a, r32o, rupd);
         KCHK();
         if (rupd.out) rr = Red{redbuf, 1, 1}, red_done(redbuf, 1, false);
-        else rr = reduce_global(part_a, nbu, 1, false, 0);
-        hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, 1);
+        else if (!merged_conv) rr = reduce_global(part_a, nbu, 1, false, 0);
+        if (merged_conv) {
+          rr = Red{redbuf, 1, 1};
+          hipLaunchKernelGGL(k_reduce_conv, dim3(1), dim3(RB), 0, st, (const double*)part_a, nbu, MAXB, redbuf,
+                             (const double*)redbuf, (const double*)bb.p, tol2, ctl, it + 1);
+        } else {
+          hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, it + 1, 1);
+        }
         KCHK();
         std::swap(v.po[0], v.pn[0]);
       }

@@ -2401,6 +2401,38 @@ __global__ __launch_bounds__(RB) void k_reduce_t(const double* part, int nb, int
     }
   }
 }
+// one sum (k_reduce_t's order) into out[0], then k_conv's test on rr / bb (either may be out): the PCG's
+// reduction of <r, r> and its convergence test in one launch (single rank: no all-reduce in between)
+__global__ __launch_bounds__(RB) void k_reduce_conv(const double* part, int nb, int stride, double* out,
+                                                    const double* rr, const double* bb, double tol2, int* ctl,
+                                                    int it) {
+  __shared__ double sh[RB / 64];
+  double a[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) a[u] = 0.0;
+  for (int b0 = threadIdx.x; b0 < nb; b0 += RB * RU) {
+    double t[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) t[u] = b0 + u * RB < nb ? part[b0 + u * RB] : 0.0;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) a[u] += t[u];
+  }
+  double x = a[0];
+#pragma unroll
+  for (int u = 1; u < RU; ++u) x += a[u];
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double y = sh[0];
+    for (int w = 1; w < RB / 64; ++w) y += sh[w];
+    out[0] = y;
+    if (ctl[0] == 0 && rr[0] <= tol2 * bb[0]) {  // k_conv
+      ctl[0] = 1;
+      ctl[1] = it;
+    }
+  }
+}
 // the step's reductions: 1,024 threads (RB); 256 (k_reduce_t<256>, PUCFEM_RED_THREADS=256) schedules on a
 // CU with fewer free wave slots while the dye stream's kernels occupy the chip (measurement knob)
 constexpr auto k_reduce = k_reduce_t<RB>;
