@@ -80,8 +80,21 @@ __device__ __forceinline__ T ldnt(const T* p) {
 // L2 busy with the input vectors, and ordinary stores of the outputs allocate L2 lines that then have
 // to be written back; the streaming store halves the time of a gather kernel with two fp64 outputs
 // (tools/face_lab.hip: 119 -> 61 us for the 14M-row direction kernel, the same bytes as a pure copy).
+// PUCFEM_STORE_SC1 (A/B build): write-through `sc1` stores instead, which do not keep the line in the XCD's
+// L2 (MI355X_MICROARCH.md store table) -- more of the 4 MB L2 for the gathered vectors' halo rows
 template <class T>
 __device__ __forceinline__ void stnt(T* p, T v) {
+#ifdef PUCFEM_STORE_SC1
+  if constexpr (sizeof(T) == 8) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  } else if constexpr (sizeof(T) == 4) {
+    __hip_atomic_store(reinterpret_cast<unsigned int*>(p), __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+#endif
   __builtin_nontemporal_store(v, p);
 }
 // column of entry e of the slice whose first row is `base`.  C16: the operator's band fits int16, so
