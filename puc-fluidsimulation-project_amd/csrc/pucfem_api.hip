@@ -429,6 +429,13 @@ struct Ctx {
     double bound2[2] = {0.0, 0.0}, floor2[2] = {0.0, 0.0};
   } vcc;
   int visc_check_fail = 0;
+  // step pairs of the viscous Chebyshev solve (k_vcheb_pair, single rank with a face part): PUCFEM_VISC_PAIR=0
+  // runs every step as its own k_vcheb (a measurement knob); the pair's third x buffer and second d
+  // buffer are allocated on first use
+  bool visc_pair = !(std::getenv("PUCFEM_VISC_PAIR") && std::atoi(std::getenv("PUCFEM_VISC_PAIR")) == 0);
+  int64_t visc_pairs = 0;  // pairs launched (pucfem_path_info)
+  double* vp_x[2] = {nullptr, nullptr};
+  float* vp_d[2] = {nullptr, nullptr};
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
   static FaceDev nof() { return FaceDev{}; }
 
@@ -856,9 +863,24 @@ struct Ctx {
     const int nb = grid_part(fc, A);
     double* xa[NR];
     double* xb[NR];
+    double* xc[NR];  // step pairs: x_{a+2} (k_vcheb_pair)
+    float* dcur[NR];  // the fp32 increments d (in place for single steps)
+    float* dalt[NR];  // step pairs: d_{a+2}
+    // step pairs (k_vcheb_pair): NR = 2, one rank, a face part of lattice size <= VP_HALO
+    const bool pairs = visc_pair && NR == 2 && !dist() && hf.items > 0 && fc.n <= VP_HALO &&
+                       nb_for(A.nslices) + hf.items <= MAXB;  // (the check's partials of both halves)
+    if (pairs && !vp_x[0]) {
+      for (int c = 0; c < 2; ++c) {
+        vp_x[c] = dalloc<double>(nloc);
+        vp_d[c] = dalloc<float>(nloc);
+      }
+    }
     for (int c = 0; c < NR; ++c) {
       xa[c] = y[c];
       xb[c] = cg_pb[c];
+      xc[c] = pairs ? vp_x[c] : nullptr;
+      dcur[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
+      dalt[c] = pairs ? vp_d[c] : nullptr;
     }
     auto halo_x = [&](double* const* x) {
       if (NR == 2) halo(x[0], x[1]);
@@ -879,7 +901,7 @@ struct Ctx {
         v.xin[c] = xa[c];
         v.xout[c] = xb[c];
         v.b[c] = b[c];
-        v.d[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
+        v.d[c] = dcur[c];
         if (fin) {
           v.s = vfin->s;
           v.u[c] = vfin->u[c];
@@ -905,6 +927,70 @@ struct Ctx {
       halo_x(xb);
       for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
     };
+    // Two steps a, a + 1 in three launches: the skeleton rows' step a (k_vcheb on the SELL part alone),
+    // both steps on the face interiors (k_vcheb_pair: x_{a+1} in LDS), the skeleton rows' step a + 1.
+    // check: the |r_{a+1}|^2 partials of both halves in part_c (SELL blocks first); fin: step a + 1 is
+    // the solve's last and writes u* and the increment.  Returns the partial count.
+    const int nbs = nb_for(A.nslices);
+    const double bytes_sk = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
+                            32.0 * NR * (double)(A.own() - hf.rows);
+    auto pair_step = [&](double c1a, double c2a, double c1b, double c2b, bool check, bool fin) {
+      if constexpr (NR == 2) {
+        FaceDev fs = fc;
+        fs.nb = 0;
+        ChebVecs<NR> v1{}, v2{};
+        VPairVecs p{};
+        for (int c = 0; c < NR; ++c) {
+          v1.xin[c] = xa[c];
+          v1.xout[c] = xb[c];
+          v1.b[c] = b[c];
+          v1.d[c] = dcur[c];
+          v2.xin[c] = xb[c];
+          v2.xout[c] = xc[c];
+          v2.b[c] = b[c];
+          v2.d[c] = dcur[c];
+          v2.dout[c] = dalt[c];
+          p.xa[c] = xa[c];
+          p.xb[c] = xb[c];
+          p.xc[c] = xc[c];
+          p.b[c] = b[c];
+          p.da[c] = dcur[c];
+          p.dc[c] = dalt[c];
+          if (fin) {
+            v2.s = p.s = vfin->s;
+            v2.u[c] = p.u[c] = vfin->u[c];
+            v2.us[c] = p.us[c] = vfin->us[c];
+            v2.inc[c] = p.inc[c] = vfin->inc[c];
+          }
+        }
+        // face rows: x_a, b, d_a read, x_{a+2}, d_{a+2} written (fin: + s, u read, u*, the increment
+        // written - x, d), x_{a+1} written at the rows next to the skeleton (3 (n - 3) per face)
+        const double bnd_rows = fc.n > 3 ? 3.0 * (fc.n - 3) * (double)fc.nf : 0.0;
+        const double bytes_f = (32.0 * NR + (fin ? 12.0 * NR : 0.0)) * (double)hf.rows + 8.0 * NR * bnd_rows;
+        const double fin_sk = fin ? 12.0 * NR * (double)(A.own() - hf.rows) : 0.0;
+        double* pc = check ? part_c : nullptr;
+        with_c16(A, [&](auto c16) {
+          klaunch(-1, bytes_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a,
+                  c2a, 0, (const int*)ctl, (double*)nullptr, (double*)nullptr, RedOut{});
+          KCHK();
+          klaunch(-1, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
+                  (int32_t)nbs);
+          KCHK();
+          klaunch(-1, bytes_sk + fin_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
+                  c1b, c2b, 0, (const int*)ctl, pc, (double*)nullptr, RedOut{});
+          KCHK();
+        });
+        ++visc_pairs;
+        if (fin) return;
+        for (int c = 0; c < NR; ++c) {  // x_{a+2} is current; x_a, x_{a+1} are free
+          double* t = xa[c];
+          xa[c] = xc[c];
+          xc[c] = xb[c];
+          xb[c] = t;
+          std::swap(dcur[c], dalt[c]);
+        }
+      }
+    };
     // Step 0 gives r_0 = b - A^ x_0.  The residual polynomial of the Chebyshev iteration on an interval
     // holding the spectrum is bounded by 1 / T_k(sigma) there, so |r_k| <= |r_0| / T_k(sigma): the step
     // count K that meets the CG's test |r_K| <= rtol |b| is known after step 0, and steps 1 .. K-1 run with
@@ -927,14 +1013,33 @@ struct Ctx {
     // (one fewer than its count): the round trip hides behind them
     double rho_old = 1.0 / sigma;
     int done = 1;
+    // (step pairs: two steps per pass while at least two are due)
+    auto pair_coefs = [&](double& c1a, double& c2a, double& c1b, double& c2b) {
+      const double ra = 1.0 / (2.0 * sigma - rho_old), rb = 1.0 / (2.0 * sigma - ra);
+      c1a = ra * rho_old;
+      c2a = 2.0 * ra / delta;
+      c1b = rb * ra;
+      c2b = 2.0 * rb / delta;
+      rho_old = rb;
+    };
     auto advance = [&](int upto) {
-      for (; done < upto; ++done) {
+      while (done < upto) {
+        if (pairs && upto - done >= 2) {
+          double c1a, c2a, c1b, c2b;
+          pair_coefs(c1a, c2a, c1b, c2b);
+          pair_step(c1a, c2a, c1b, c2b, false, false);
+          done += 2;
+          continue;
+        }
         const double rho = 1.0 / (2.0 * sigma - rho_old);
         step(done, rho * rho_old, 2.0 * rho / delta);
         rho_old = rho;
+        ++done;
       }
     };
-    advance(std::max(1, last_it[which] - 1));
+    // with step pairs only whole pairs go ahead of the round trip, and at least the last two steps
+    // wait for it (so that they can run as one pair with the finish)
+    advance(pairs ? 1 + 2 * std::max(0, (last_it[which] - 3) / 2) : std::max(1, last_it[which] - 1));
     HIPCHK(hipEventSynchronize(have_r0));
     timer.pool.push_back(have_r0);
     if (vcc.pending) {  // the previous solve's post-check (its copy preceded step 0 on the stream)
@@ -971,16 +1076,29 @@ struct Ctx {
       return 0;
     }
     if (done < K) {
-      advance(K - 1);
-      // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check
-      const double rho = 1.0 / (2.0 * sigma - rho_old);
+      // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check; with
+      // step pairs it is the second step of a pair when an even number of steps is left
       const bool fuse = vfin != nullptr && NR == 2;
-      step(done, rho * rho_old, 2.0 * rho / delta, true, fuse);
-      rho_old = rho;
-      const int kc = done;
-      ++done;
+      const bool last_pair = pairs && (K - done) % 2 == 0;
+      advance(last_pair ? K - 2 : K - 1);
+      int kc, nck;
+      if (last_pair) {
+        double c1a, c2a, c1b, c2b;
+        pair_coefs(c1a, c2a, c1b, c2b);
+        pair_step(c1a, c2a, c1b, c2b, true, fuse);
+        kc = done + 1;
+        done += 2;
+        nck = nbs + (int)hf.items;
+      } else {
+        const double rho = 1.0 / (2.0 * sigma - rho_old);
+        step(done, rho * rho_old, 2.0 * rho / delta, true, fuse);
+        rho_old = rho;
+        kc = done;
+        ++done;
+        nck = nb;
+      }
       if (fuse) *fin_done = true;
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, (const double*)part_c, nb, MAXB, NR, 0, redbuf + 48);
+      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, (const double*)part_c, nck, MAXB, NR, 0, redbuf + 48);
       KCHK();
       if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
       HIPCHK(hipMemcpyAsync(h_pinned + 32, redbuf + 48, NR * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -3975,7 +4093,8 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[5] = c.dvinc[0] && !c.proj_k_visc ? std::min(c.have_vinc, c.visc_extrap) : 0;
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
-           (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0);
+           (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
+           (c.visc_pairs ? 16 : 0);
   });
 }
 

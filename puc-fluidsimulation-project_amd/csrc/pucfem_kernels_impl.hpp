@@ -879,6 +879,8 @@ struct ChebVecs {
   const double* u[NR];
   double* us[NR];
   float* inc[NR];
+  // non-null: the new d goes here instead of in place (the skeleton half of a step pair, k_vcheb_pair)
+  float* dout[NR];
 };
 template <int NR, bool C16>
 __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
@@ -898,7 +900,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
       stnt(v.us[c] + row, a);
       stnt(v.inc[c] + row, (float)(a - v.u[c][row]));
     } else {
-      stnt(v.d[c] + row, (float)dn);
+      stnt((v.dout[c] ? v.dout[c] : v.d[c]) + row, (float)dn);
       stnt(v.xout[c] + row, x0 + dn);
     }
     rr[c] += r * r;
@@ -1007,6 +1009,174 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
     }
   }
   red_finish(ro, part_rr, sh);
+}
+
+// Two Chebyshev steps of the viscous solve (steps a and a + 1, both right-hand sides) on the face
+// interiors in one pass: temporal blocking with the intermediate iterate in LDS.  A block owns one work
+// item (BS * FACE_RPT consecutive rows of one face); it runs step a on its rows and on the in-face
+// neighbours of its rows outside them (every in-face neighbour is within n - 1 offsets, so the window
+// [t0 - n, t1 + n) holds them: ~25 % redundant rows at L7), keeps x_{a+1} in LDS and runs step a + 1 on its
+// own rows from there.  The skeleton rows' x_{a+1} come from the SELL-only launch of step a that precedes
+// this one (k_vcheb with nb = 0); the SELL-only launch of step a + 1 that follows reads x_{a+1} at the face
+// rows next to the skeleton, which this kernel writes (xb at the boundary rows).  The operations per row
+// are k_vcheb's (same stencil order, d rounded to fp32 between the steps), so the result is the same as
+// two k_vcheb steps.  x_a, b, d_a are read and x_{a+2}, d_{a+2} written once: 64 B/row for two steps
+// instead of 128 (d_{a+2} goes to a second buffer: neighbouring blocks still read d_a in their windows).
+struct VPairVecs {
+  const double* xa[2];  // x_a (every row)
+  double* xb[2];        // x_{a+1}: read at skeleton rows, written at the face rows next to the skeleton
+  double* xc[2];        // x_{a+2}
+  const double* b[2];
+  const float* da[2];   // d_a
+  float* dc[2];         // d_{a+2}
+  // the solve's last step (us[0] non-null): u* = s x_{a+2} and the fp32 increment instead of xc, dc
+  const double* s;
+  const double* u[2];
+  double* us[2];
+  float* inc[2];
+};
+constexpr int VP_HALO = 256;  // window rows on each side: n <= VP_HALO (lattice size of the face)
+constexpr int VP_W = BS * FACE_RPT + 2 * VP_HALO;
+constexpr int VP_WK = (VP_W + BS - 1) / BS;
+#ifndef PUCFEM_VP_G
+#define PUCFEM_VP_G 1
+#endif
+constexpr int VP_G = PUCFEM_VP_G;  // rows of a thread loaded together (compile-time: an A/B knob)
+static_assert(VP_WK % VP_G == 0, "the window rows of a thread go in groups");
+#ifdef PUCFEM_VP_WPE
+#define PUCFEM_VP_ATTR __attribute__((amdgpu_waves_per_eu(PUCFEM_VP_WPE, 8)))
+#else
+#define PUCFEM_VP_ATTR
+#endif
+__global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
+                                                   double c2b, const int* ctl, double* part_rr, int32_t part_off) {
+  __shared__ double lx[2][VP_W];
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  const int32_t items = fc.nf * fc.cpf;
+  int32_t it = blockIdx.x;
+  if ((int32_t)gridDim.x == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows)
+    const int32_t x = it & 7, q = items >> 3, rem = items & 7;
+    it = x * q + (x < rem ? x : rem) + (it >> 3);
+  }
+  const int32_t lf = it / fc.cpf;
+  const lat::FaceTab F = fc.tab[lf];
+  const int32_t n = fc.n;
+  const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT), t1 = min(t0 + BS * FACE_RPT, fc.F);
+  const int32_t w0 = max(0, t0 - n), nw = min(fc.F, t1 + n) - w0;
+  const bool fin = v.us[0] != nullptr;
+  // step a on the window; b and the fp32 d_{a+1} of the rows stay in registers for step a + 1.  Rows
+  // go in groups of VP_G with every load of the group first (k_vcheb's row groups); a row past the
+  // window is clamped to the window's first row (a valid address; not stored)
+  double bt[VP_WK][2];
+  float dt[VP_WK][2];
+#pragma unroll
+  for (int k0 = 0; k0 < VP_WK; k0 += VP_G) {
+    if (k0 * BS >= nw) break;
+    int32_t nb[VP_G][6];
+    bool in[VP_G][6], ok[VP_G];
+    int64_t row[VP_G];
+    double xv[VP_G][2][7], br[VP_G][2], dr[VP_G][2];
+#pragma unroll
+    for (int r = 0; r < VP_G; ++r) {
+      const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
+      ok[r] = w < nw;
+      const int32_t t = w0 + (ok[r] ? w : 0);
+      int32_t i, j;
+      lat::coords(t, n, fc.rinv, i, j);
+      lat::neighbours(F, n, t, i, j, nb[r], in[r]);
+      row[r] = F.base + t;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        xv[r][c][6] = v.xa[c][row[r]];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) xv[r][c][q] = v.xa[c][nb[r][q]];
+        br[r][c] = v.b[c][row[r]];
+        dr[r][c] = (double)v.da[c][row[r]];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < VP_G; ++r) {
+      double a[7];
+      face_kcoefs(fc, lf, nb[r], in[r], a);
+      const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double ax = a[0] * xv[r][c][6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[r][c][q];
+        const double rs = br[r][c] - ax;
+        const double dn = c1a * dr[r][c] + c2a * rs;
+        if (ok[r]) lx[c][w] = xv[r][c][6] + dn;
+        bt[k0 + r][c] = br[r][c];
+        dt[k0 + r][c] = (float)dn;
+      }
+    }
+  }
+  __syncthreads();
+  // step a + 1 on the item's own rows (in groups as above)
+  double rr[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < VP_WK; k0 += VP_G) {
+    if (k0 * BS >= nw) break;
+    int32_t nb[VP_G][6];
+    bool in[VP_G][6], ok[VP_G];
+    int32_t wr[VP_G];
+    double xv[VP_G][2][7];
+#pragma unroll
+    for (int r = 0; r < VP_G; ++r) {
+      const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
+      ok[r] = w < nw && w0 + w >= t0 && w0 + w < t1;
+      wr[r] = ok[r] ? w : t0 - w0;
+      const int32_t t = w0 + wr[r];
+      int32_t i, j;
+      lat::coords(t, n, fc.rinv, i, j);
+      lat::neighbours(F, n, t, i, j, nb[r], in[r]);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        xv[r][c][6] = lx[c][wr[r]];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int32_t lw = min(max(nb[r][q] - F.base - w0, 0), nw - 1);
+          xv[r][c][q] = in[r][q] ? lx[c][lw] : v.xb[c][nb[r][q]];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < VP_G; ++r) {
+      if (!ok[r]) continue;
+      double a[7];
+      face_kcoefs(fc, lf, nb[r], in[r], a);
+      const int64_t row = F.base + w0 + wr[r];
+      bool bnd = false;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) bnd = bnd || !in[r][q];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double ax = a[0] * xv[r][c][6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[r][c][q];
+        const double rs = bt[k0 + r][c] - ax;
+        const double dn = c1b * (double)dt[k0 + r][c] + c2b * rs;
+        if (bnd) v.xb[c][row] = xv[r][c][6];
+        if (fin) {
+          const double au = v.s[row] * (xv[r][c][6] + dn);
+          stnt(v.us[c] + row, au);
+          stnt(v.inc[c] + row, (float)(au - v.u[c][row]));
+        } else {
+          stnt(v.dc[c] + row, (float)dn);
+          stnt(v.xc[c] + row, xv[r][c][6] + dn);
+        }
+        rr[c] += rs * rs;
+      }
+    }
+  }
+  if (!part_rr) return;  // the solve's last step: |r_{a+1}|^2 partials for the a-posteriori check
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const double t = block_sum(rr[c], sh);
+    if (threadIdx.x == 0) part_rr[(int64_t)c * MAXB + part_off + blockIdx.x] = t;
+  }
 }
 
 // the recurrence CG's control after an update: converged (1), maxit (2), not finite (3); it = the

@@ -232,7 +232,8 @@ class Context:
                     visc_extrap_order=o[5], proj_k=o[6], lattice=bool(o[7] & 1),
                     sl_locator="lattice" if o[7] & 2 else "records",
                     viscous_iteration="chebyshev" if o[7] & 4 else "cg",
-                    visc_check_failed=bool(o[7] & 8))
+                    visc_check_failed=bool(o[7] & 8),
+                    visc_step_pairs=bool(o[7] & 16))
 
     def visc_interval(self):
         """[lo, hi] of the viscous Chebyshev iteration (pucfem_visc_interval)."""

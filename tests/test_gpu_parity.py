@@ -360,6 +360,23 @@ def test_viscous_chebyshev_post_check(monkeypatch):
     b.close()
 
 
+@pytest.mark.parametrize("refine", [3, 5])
+def test_viscous_step_pairs_equal_single_steps(monkeypatch, refine):
+    """Two Chebyshev viscous steps in one pass on the face interiors (k_vcheb_pair, x_{a+1} in LDS, the
+    skeleton rows in their own launches) do k_vcheb's operations row by row: the production run at L3 /
+    L5 with step pairs is bit-identical to the one that runs every step as its own k_vcheb."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    a = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.setenv("PUCFEM_VISC_PAIR", "0")
+    b = stokes(mesh, tol=S.Tolerances.production())
+    sa, sb = a.step(8), b.step(8)
+    assert a.ctx.path_info()["visc_step_pairs"] and not b.ctx.path_info()["visc_step_pairs"]
+    assert [(s.it_visc, s.it_p, s.it_p2) for s in sa] == [(s.it_visc, s.it_p, s.it_p2) for s in sb]
+    assert np.array_equal(a.u, b.u) and np.array_equal(a.c, b.c)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("records", ["0", "1"])
 def test_knn_radii_device_equals_host(monkeypatch, records):
     """The semi-Lagrangian fast-accept radii (k-NN distances of every centroid and vertex) are built on
