@@ -136,7 +136,7 @@ struct Timer {
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
-  static constexpr int NCLS = 10;
+  static constexpr int NCLS = 11;
   double ms[NCLS] = {};
   double bytes[NCLS] = {};
   int64_t n[NCLS] = {};
@@ -436,6 +436,13 @@ struct Ctx {
   int64_t visc_pairs = 0;  // pairs launched (pucfem_path_info)
   double* vp_x[2] = {nullptr, nullptr};
   float* vp_d[2] = {nullptr, nullptr};
+  // step pairs of the finest level's smoothing in the fp32 V-cycle (k_cheb_pair, single rank):
+  // PUCFEM_MG_PAIR=0 runs every step as its own k_cheb (a measurement knob); a third x buffer and a second
+  // d buffer of the finest level are allocated on first use
+  bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
+  int64_t mg_pairs = 0;
+  float* mgp_x = nullptr;
+  float* mgp_d = nullptr;
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
   static FaceDev nof() { return FaceDev{}; }
 
@@ -1151,7 +1158,8 @@ struct Ctx {
     T* cur = xin;
     deg = std::max(1, deg);
     const bool finest = &L == &mg.back();
-    double c20 = 0.0;
+    // the step coefficients: d = c1 d + c2 Dinv (b - A x)
+    std::vector<double> c1s(deg), c2s(deg);
     for (int k = 0; k < deg; ++k) {
       double c1 = 0.0, c2 = 1.0 / theta;
       if (prm.mg_kind == 4) {
@@ -1163,6 +1171,22 @@ struct Ctx {
         c2 = 2.0 * rho / delta;
         rho_old = rho;
       }
+      c1s[k] = c1;
+      c2s[k] = c2;
+    }
+    // step pairs (k_cheb_pair) on the finest level of the fp32 cycle, one rank: two steps per pass on the
+    // face interiors; not the step that writes z / the <r, z> partials
+    bool pairs = false;
+    if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
+      pairs = mg_pair && finest && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
+    if (pairs && !mgp_x) {
+      mgp_x = dalloc<float>(L.nloc);
+      mgp_d = dalloc<float>(L.nloc);
+    }
+    T* dcur = B.d;  // the current d (a pair writes its d to the other buffer)
+    double c20 = 0.0;
+    for (int k = 0; k < deg; ++k) {
+      const double c1 = c1s[k], c2 = c2s[k];
       // zero initial guess and >= 2 steps: step 0 is folded into step 1 (mode 2; b's ghosts are
       // current, see vcycle)
       const bool fuse = cur == nullptr && k == 0 && deg >= 2;
@@ -1171,6 +1195,60 @@ struct Ctx {
         continue;
       }
       const int mode = (cur == nullptr && k == 0) ? 0 : (cur == nullptr ? 2 : 1);
+      if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value) {
+        const bool next_last = k + 1 == deg - 1;
+        if (pairs && mode != 0 && k + 1 < deg && !(next_last && (tozr || rdot))) {
+          // steps k, k + 1: x_a = cur (mode 1) -> x_{a+1} in p1 (skeleton rows, the face rows next to
+          // them) -> x_{a+2} in p2; d_a = dcur -> d_{a+2} in the other d buffer
+          float* p1 = mode == 2 ? xa : (cur == xa ? xb : xa);
+          float* p2 = mode == 2 ? xb : mgp_x;
+          if (mode == 1 && cur == mgp_x) {  // (cur is the extra buffer after an earlier pair)
+            p1 = xa;
+            p2 = xb;
+          }
+          float* dn = dcur == B.d ? mgp_d : B.d;
+          FaceDev fs = hf.full();
+          fs.nb = 0;
+          const int nbs = nb_mg(A.nslices);
+          // skeleton rows: the SELL part of a k_cheb step (bytes as in the single step, SELL rows only)
+          const double sk_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + 2.0 * sizeof(T);
+          const double bytes_sk = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz +
+                                  (double)A.nrows * (sk_row + A.row_bytes());
+          const double bytes_sk1 = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz +
+                                   (double)A.nrows * (5.0 * sizeof(T) + sizeof(TB) + A.row_bytes());
+          // face rows: x_a and d_a (mode 1) and b read once, x_{a+2} and d_{a+2} written, x_{a+1} at the
+          // 3 (n - 3) rows per face next to the skeleton
+          const double bnd_rows = hf.d.n > 3 ? 3.0 * (hf.d.n - 3) * (double)hf.d.nf : 0.0;
+          const double bytes_f = (double)hf.rows * ((mode == 1 ? 8.0 : 0.0) + 4.0 + 8.0) + 4.0 * bnd_rows;
+          MgPairVecs pv{(const float*)b, (const float*)B.dinv, (const float*)cur, p1, p2, (const float*)dcur, dn};
+          B.with_vals([&](auto* val) {
+            using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
+            with_c16(A, [&](auto c16) {
+              constexpr bool C = decltype(c16)::value;
+              klaunch(-1, bytes_sk, k_cheb<T, TB, T, VT, C, 1>, dim3(nbs), dim3(BS), A.view(), fs, val,
+                      (const T*)B.dinv, b, (const T*)(mode == 1 ? cur : nullptr), p1, dcur, c1, c2, c20, mode,
+                      (const int*)ctl, (const double*)nullptr, (double*)nullptr, RedOut{}, (T*)nullptr);
+              KCHK();
+              if (mode == 1)
+                klaunch(10, bytes_f, k_cheb_pair<1>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
+                        (float)c20, (float)c1s[k + 1], (float)c2s[k + 1], (const int*)ctl);
+              else
+                klaunch(10, bytes_f, k_cheb_pair<2>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
+                        (float)c20, (float)c1s[k + 1], (float)c2s[k + 1], (const int*)ctl);
+              KCHK();
+              klaunch(-1, bytes_sk1, k_cheb<T, TB, T, VT, C, 1>, dim3(nbs), dim3(BS), A.view(), fs, val,
+                      (const T*)B.dinv, b, (const T*)p1, p2, dcur, c1s[k + 1], c2s[k + 1], c20, 1, (const int*)ctl,
+                      (const double*)nullptr, (double*)nullptr, RedOut{}, dn);
+              KCHK();
+            });
+          });
+          ++mg_pairs;
+          cur = p2;
+          dcur = dn;
+          ++k;
+          continue;
+        }
+      }
       T* out = (cur == xa) ? xb : xa;
       if (mode == 1) mg_halo(L, cur);
       const bool last = k == deg - 1;
@@ -1197,14 +1275,15 @@ struct Ctx {
           else zo = z;
           if (toz)
             klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
-                    (const T*)B.dinv, b, xi, zo, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part,
-                    rd ? ro_rz : RedOut{});
+                    (const T*)B.dinv, b, xi, zo, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part,
+                    rd ? ro_rz : RedOut{}, (T*)nullptr);
           else if (finest)
             klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
-                    (const T*)B.dinv, b, xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{});
+                    (const T*)B.dinv, b, xi, out, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{},
+                    (T*)nullptr);
           else
             klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), fc, val, (const T*)B.dinv, b,
-                    xi, out, B.d, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{});
+                    xi, out, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{}, (T*)nullptr);
         });
       });
       KCHK();
@@ -4018,7 +4097,7 @@ int pucfem_timing_enable(void* ctx, int32_t on) {
     c.timer.flush();
     require(on >= 0 && on <= 2, "timing mode");
     c.timer.on = on != 0;
-    c.timer.mask = on == 2 ? 1u : ~0u;
+    c.timer.mask = on == 2 ? (1u | (1u << 10)) : ~0u;  // mode 2: the roofline kernels (k_cheb, k_cheb_pair)
     for (int k = 0; k < Timer::NCLS; ++k) {
       c.timer.ms[k] = 0;
       c.timer.bytes[k] = 0;
@@ -4094,7 +4173,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
-           (c.visc_pairs ? 16 : 0);
+           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0);
   });
 }
 
@@ -4503,13 +4582,15 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(ff.nb + 8), dim3(BS), 0, c.st, a, e, 0,
                                   none, ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
                                   (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
-                                  (const double*)nullptr, (double*)nullptr, RedOut{});
+                                  (const double*)nullptr, (double*)nullptr, RedOut{},
+                                  (float*)nullptr);
             break;
           case 4:  // the SELL (skeleton) part alone
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(c.nb_mg(A.nslices)), dim3(BS), 0, c.st,
                                   a, e, 0, A.view(), FaceDev{}, (const float*)B.Aval, (const float*)B.dinv,
                                   (const float*)c.r32, (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1,
-                                  (const int*)nullptr, (const double*)nullptr, (double*)nullptr, RedOut{});
+                                  (const int*)nullptr, (const double*)nullptr, (double*)nullptr, RedOut{},
+                                  (float*)nullptr);
             break;
           case 5:  // k_cg_dir, the face part alone
             hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(fpt.nb + 8), dim3(BS), 0, c.st, a, e, 0, none, fpt,
@@ -4527,7 +4608,8 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
             hipExtLaunchKernelGGL(k_cheb<float, float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0,
                                   A.view(), ff, (const float*)B.Aval, (const float*)B.dinv, (const float*)c.r32,
                                   (const float*)B.x, B.x2, B.d, 0.3, 0.7, 0.0, 1, (const int*)nullptr,
-                                  (const double*)nullptr, (double*)nullptr, RedOut{});
+                                  (const double*)nullptr, (double*)nullptr, RedOut{},
+                                  (float*)nullptr);
             break;
           case 1:
             hipExtLaunchKernelGGL(k_resid<float, float, float, C16, 2>, dim3(nb_mg), dim3(BS), 0, c.st, a, e, 0, A.view(),

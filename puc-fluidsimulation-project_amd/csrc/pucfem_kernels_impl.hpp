@@ -2821,7 +2821,8 @@ template <int MODE, bool RD, typename T, typename TB, typename TO, typename VT, 
 __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, const VT* __restrict__ val,
                                           const T* __restrict__ dinv, const TB* __restrict__ b,
                                           const T* __restrict__ xin, TO* __restrict__ xout, T* __restrict__ d,
-                                          T tc1, T tc2, T tc20, const double* __restrict__ rdot, double& acc_rz) {
+                                          T tc1, T tc2, T tc20, const double* __restrict__ rdot, double& acc_rz,
+                                          T* __restrict__ dout) {
   // the step's row update from A x (ax), the row's 1 / diag, b and (mode 1) x_in and d
   auto finish = [&](int64_t row, T ax, T di, T brow, T xrow, T drow, double rrow) {
     T dn, xo;
@@ -2834,7 +2835,7 @@ __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, c
       dn = tc1 * d1 + tc2 * di * (brow - ax);
       xo = x1 + dn;
     }
-    stnt(d + row, dn);
+    stnt((dout ? dout : d) + row, dn);
     stnt(xout + row, (TO)xo);
     if constexpr (RD) acc_rz += rrow * (double)xo;
   };
@@ -2912,13 +2913,14 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
                                              const T* __restrict__ dinv, const TB* __restrict__ b,
                                              const T* __restrict__ xin, TO* __restrict__ xout, T* __restrict__ d,
                                              double c1, double c2, double c20, int mode, const int* ctl,
-                                             const double* __restrict__ rdot, double* part, RedOut ro = RedOut{}) {
+                                             const double* __restrict__ rdot, double* part, RedOut ro = RedOut{},
+                                             T* __restrict__ dout = nullptr) {
   __shared__ double sh[4];
   if (ctl && ctl[0]) return;
   const T tc1 = (T)c1, tc2 = (T)c2, tc20 = (T)c20;
   double acc_rz = 0.0;
 #define PUCFEM_CHEB(M, R) \
-  cheb_body<M, R, T, TB, TO, VT, C16>(A, fc, val, dinv, b, xin, xout, d, tc1, tc2, tc20, rdot, acc_rz)
+  cheb_body<M, R, T, TB, TO, VT, C16>(A, fc, val, dinv, b, xin, xout, d, tc1, tc2, tc20, rdot, acc_rz, dout)
   if (mode == 1) {
     if (rdot) PUCFEM_CHEB(1, true);
     else PUCFEM_CHEB(1, false);
@@ -2934,6 +2936,110 @@ __global__ __launch_bounds__(BS) void k_cheb(SellDev A, FaceDev fc, const VT* __
     const double t = block_sum(acc_rz, sh);
     if (threadIdx.x == 0) red_part(ro, part, 0, t);
     red_finish(ro, part, sh);
+  }
+}
+
+// Two smoothing steps of the fp32 V-cycle's finest level on the face interiors in one pass (the viscous
+// k_vcheb_pair's scheme: step a on the item's rows and their in-face neighbours, x_{a+1} in LDS, step a + 1
+// on the item's rows; the skeleton rows run in k_cheb launches on the SELL part alone before and after,
+// and this kernel writes x_{a+1} at the face rows next to the skeleton for the second of them).  Step a is
+// mode MA of cheb_body (1: general, 2: the fused first two steps from x = 0), step a + 1 mode 1; the
+// arithmetic per row is cheb_body's, so the result is bit-identical to two k_cheb launches.
+struct MgPairVecs {
+  const float* b;
+  const float* dinv;  // 1 / diag at skeleton columns (mode 2)
+  const float* xa;    // x_a (mode 1)
+  float* xb;          // x_{a+1}: read at skeleton rows, written at the face rows next to the skeleton
+  float* xc;          // x_{a+2}
+  const float* da;    // d_a (mode 1)
+  float* dc;          // d_{a+2}
+};
+template <int MA>
+__global__ __launch_bounds__(BS) void k_cheb_pair(FaceDev fc, MgPairVecs v, float c1a, float c2a, float c20, float c1b,
+                                                  float c2b, const int* ctl) {
+  __shared__ float lx[VP_W];
+  if (ctl && ctl[0]) return;
+  const int32_t items = fc.nf * fc.cpf;
+  int32_t it = blockIdx.x;
+  if ((int32_t)gridDim.x == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows)
+    const int32_t x = it & 7, q = items >> 3, rem = items & 7;
+    it = x * q + (x < rem ? x : rem) + (it >> 3);
+  }
+  const int32_t lf = it / fc.cpf;
+  const lat::FaceTab F = fc.tab[lf];
+  const int32_t n = fc.n;
+  const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT), t1 = min(t0 + BS * FACE_RPT, fc.F);
+  const int32_t w0 = max(0, t0 - n), nw = min(fc.F, t1 + n) - w0;
+  const float di = fc.coef32[lf * lat::NCOEF + lat::C_DINV];
+  float a[7];
+  {
+    int32_t nb0[6];
+    bool in0[6];
+    int32_t i, j;
+    lat::coords(t0, n, fc.rinv, i, j);
+    lat::neighbours(F, n, t0, i, j, nb0, in0);
+    face_kcoefs(fc, lf, nb0, in0, a);  // (the K stencil: one set per face)
+  }
+  float bt[VP_WK], dt[VP_WK];
+#pragma unroll
+  for (int k = 0; k < VP_WK; ++k) {
+    const int32_t w = (int32_t)threadIdx.x + k * BS;
+    bt[k] = dt[k] = 0.0f;
+    if (w < nw) {
+      const int32_t t = w0 + w;
+      int32_t i, j, nb[6];
+      bool in[6];
+      lat::coords(t, n, fc.rinv, i, j);
+      lat::neighbours(F, n, t, i, j, nb, in);
+      const int64_t row = F.base + t;
+      const float brow = v.b[row];
+      float g[6], x1, d1, ax;
+      if constexpr (MA == 1) {
+        x1 = v.xa[row];
+        d1 = v.da[row];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) g[q] = v.xa[nb[q]];
+        ax = a[0] * x1;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) g[q] = c20 * (in[q] ? di : v.dinv[nb[q]]) * v.b[nb[q]];
+        ax = a[0] * (c20 * di * brow);
+        x1 = c20 * di * brow;
+        d1 = x1;
+      }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) ax += a[1 + q] * g[q];
+      const float dn = c1a * d1 + c2a * di * (brow - ax);
+      lx[w] = x1 + dn;
+      bt[k] = brow;
+      dt[k] = dn;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < VP_WK; ++k) {
+    const int32_t w = (int32_t)threadIdx.x + k * BS;
+    const int32_t t = w0 + w;
+    if (w < nw && t >= t0 && t < t1) {
+      int32_t i, j, nb[6];
+      bool in[6];
+      lat::coords(t, n, fc.rinv, i, j);
+      lat::neighbours(F, n, t, i, j, nb, in);
+      const int64_t row = F.base + t;
+      const float xr = lx[w];
+      float ax = a[0] * xr;
+      bool bnd = false;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int32_t lw = min(max(nb[q] - F.base - w0, 0), nw - 1);
+        ax += a[1 + q] * (in[q] ? lx[lw] : v.xb[nb[q]]);
+        bnd = bnd || !in[q];
+      }
+      const float dn = c1b * dt[k] + c2b * di * (bt[k] - ax);
+      if (bnd) v.xb[row] = xr;
+      stnt(v.dc + row, dn);
+      stnt(v.xc + row, xr + dn);
+    }
   }
 }
 

@@ -361,16 +361,18 @@ def test_viscous_chebyshev_post_check(monkeypatch):
 
 
 @pytest.mark.parametrize("refine", [3, 5])
-def test_viscous_step_pairs_equal_single_steps(monkeypatch, refine):
-    """Two Chebyshev viscous steps in one pass on the face interiors (k_vcheb_pair, x_{a+1} in LDS, the
-    skeleton rows in their own launches) do k_vcheb's operations row by row: the production run at L3 /
-    L5 with step pairs is bit-identical to the one that runs every step as its own k_vcheb."""
+@pytest.mark.parametrize("knob,key", [("PUCFEM_VISC_PAIR", "visc_step_pairs"), ("PUCFEM_MG_PAIR", "mg_step_pairs")])
+def test_step_pairs_equal_single_steps(monkeypatch, refine, knob, key):
+    """Two Chebyshev steps in one pass on the face interiors (x_{a+1} in LDS, the skeleton rows in their
+    own launches): the viscous solve's (k_vcheb_pair) and the finest multigrid level's smoothing
+    (k_cheb_pair) do k_vcheb's / k_cheb's operations row by row, so the production run at L3 / L5 with
+    step pairs is bit-identical to the one that runs every step as its own launch."""
     mesh = pf.load_mesh("fine", refine=refine)
     a = stokes(mesh, tol=S.Tolerances.production())
-    monkeypatch.setenv("PUCFEM_VISC_PAIR", "0")
+    monkeypatch.setenv(knob, "0")
     b = stokes(mesh, tol=S.Tolerances.production())
     sa, sb = a.step(8), b.step(8)
-    assert a.ctx.path_info()["visc_step_pairs"] and not b.ctx.path_info()["visc_step_pairs"]
+    assert a.ctx.path_info()[key] and not b.ctx.path_info()[key]
     assert [(s.it_visc, s.it_p, s.it_p2) for s in sa] == [(s.it_visc, s.it_p, s.it_p2) for s in sb]
     assert np.array_equal(a.u, b.u) and np.array_equal(a.c, b.c)
     a.close()
