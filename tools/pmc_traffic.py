@@ -109,7 +109,10 @@ def main():
                     ("k_sl", [k for k in res["kernels"] if k.startswith("k_sl") and not k.startswith("k_sl_") and "hbm_bytes_per_launch" in res["kernels"][k]]),
                     ("k_sl_slow", [k for k in res["kernels"] if k.startswith("k_sl_slow") and "hbm_bytes_per_launch" in res["kernels"][k]]),
                     ("k_vcheb<2>", [k for k in res["kernels"] if k.startswith("k_vcheb<2,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_div", [k for k in res["kernels"] if k.startswith("k_div<") and "hbm_bytes_per_launch" in res["kernels"][k]])):
+                    ("k_div", [k for k in res["kernels"] if k.startswith("k_div<") and "hbm_bytes_per_launch" in res["kernels"][k]]),
+                    # step pairs (both modes of the multigrid pair: the bench's class 10 averages them too)
+                    ("k_cheb_pair", [k for k in res["kernels"] if k.startswith("k_cheb_pair<") and "hbm_bytes_per_launch" in res["kernels"][k]]),
+                    ("k_vcheb_pair", [k for k in res["kernels"] if k.startswith("k_vcheb_pair") and "hbm_bytes_per_launch" in res["kernels"][k]])):
         if ks:
             n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
