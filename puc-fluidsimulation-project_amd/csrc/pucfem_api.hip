@@ -441,6 +441,11 @@ struct Ctx {
   // d buffer of the finest level are allocated on first use
   bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
   int64_t mg_pairs = 0;
+  // k_visc_prep folded into the viscous solve's first step (k_vcheb_first): PUCFEM_VISC_FIRST=1 (measurement
+  // knob; off by default: r9i measured 100.3 against 110.3 steps/s -- the window recomputes y's 64 B/row of
+  // inputs on 25 % more rows, so the fusion saves no bytes)
+  bool visc_first = std::getenv("PUCFEM_VISC_FIRST") && std::atoi(std::getenv("PUCFEM_VISC_FIRST")) != 0;
+  int64_t visc_firsts = 0;
   float* mgp_x = nullptr;
   float* mgp_d = nullptr;
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
@@ -864,7 +869,8 @@ struct Ctx {
   };
   template <int NR>
   int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
-            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr) {
+            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr,
+            const VFirstVecs* vfirst = nullptr) {
     if (fin_done) *fin_done = false;
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
@@ -1004,13 +1010,35 @@ struct Ctx {
     // no residual checks, no reductions and no host round trip.  (The bound is rigorous for the interval
     // [visc_lo, 1 + visc_R], which tests/test_host_assembly.py checks against the spectrum; the
     // adaptive test it replaces needed one extra step per solve to see the passing residual.)
-    step(0, 0.0, 1.0 / theta);
+    int nb0 = nb;  // the first step's partial count
+    if (vfirst) {  // (NR = 2) k_visc_prep folded into the first step: y is never written
+      if constexpr (NR == 2) {
+        FaceDev ff = fc;
+        ff.nb = hf.items;
+        nb0 = ((nb_for(A.nslices) + 7) & ~7) + hf.items;
+        const double bytes0 = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
+                              (72.0 + 8.0 * vfirst->D.order) * (double)A.own();
+        VFirstVecs vf = *vfirst;
+        for (int c = 0; c < 2; ++c) {
+          vf.xout[c] = xb[c];
+          vf.d[c] = dcur[c];
+        }
+        with_c16(A, [&](auto c16) {
+          klaunch(9, bytes0, k_vcheb_first<decltype(c16)::value>, dim3(nb0), dim3(BS), A.view(), ff, val, vf,
+                  1.0 / theta, (const int*)ctl, part_a, part_b);
+        });
+        KCHK();
+        for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
+      }
+    } else {
+      step(0, 0.0, 1.0 / theta);
+    }
     Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
-    if (ro(redbuf, CNT_VCHEB, 2 * NR).out) {
+    if (!vfirst && ro(redbuf, CNT_VCHEB, 2 * NR).out) {
       red_done(redbuf, 2 * NR, false);
     } else {
-      rr = reduce_global(part_a, nb, NR, false, 0);
-      bb = reduce_global(part_b, nb, NR, false, 1);
+      rr = reduce_global(part_a, nb0, NR, false, 0);
+      bb = reduce_global(part_b, nb0, NR, false, 1);
     }
     HIPCHK(hipMemcpyAsync(h_pinned, rr.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(h_pinned + 8, bb.p, NR * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1564,9 +1592,24 @@ struct Ctx {
     VincDev vd{};
     vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
     for (int k = 0; k < 2 * VINC_MAX; ++k) vd.d[k] = dvinc[k];
-    algo_bytes += (64.0 + 8.0 * vd.order) * (double)n;  // u, s, sq, the increments read; b, y written
-    hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
-    KCHK();
+    const bool cheb0 = visc_solver == 0 && visc_R < 0.25 && !(!dist() && block_cg && !fVisc.items &&
+                                                              dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
+    // k_visc_prep folded into the Chebyshev solve's first step (k_vcheb_first; one rank, lattice faces)
+    const bool first_fused = visc_first && cheb0 && ext && proj_k_visc == 0 && !dist() && fVisc.items > 0 &&
+                             fVisc.d.n <= VP_HALO && !fused_red &&
+                             ((nb_for(dP.nslices) + 7) & ~7) + fVisc.items <= MAXB;
+    VFirstVecs vfv{};
+    auto prep = [&] {
+      algo_bytes += (64.0 + 8.0 * vd.order) * (double)n;  // u, s, sq, the increments read; b, y written
+      hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
+      KCHK();
+    };
+    if (first_fused) {
+      vfv = VFirstVecs{dsv, dsqv, {ux, uy}, vd, {bvx, bvy}, {nullptr, nullptr}, {nullptr, nullptr}};
+      ++visc_firsts;
+    } else {
+      prep();
+    }
     double* y[2] = {yvx, yvy};
     const double* b[2] = {bvx, bvy};
     const bool proj = proj_k_visc > 0;
@@ -1583,9 +1626,13 @@ struct Ctx {
     ViscFin vf{};
     const bool fuse = ext && !proj && visc_fuse_fin;
     if (fuse) vf = ViscFin{dsv, {ux, uy}, {usx, usy}, {dvinc[last], dvinc[last + 1]}};
-    if (cheb) iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr,
-                               &fin_done);
-    else iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    if (cheb) {
+      iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr, &fin_done,
+                       first_fused ? &vfv : nullptr);
+      if (first_fused && iters == 0) prep();  // y itself passed the test: it is the answer, so write it
+    } else {
+      iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
+    }
     if (proj) {
       project_update(3, yo[0]);
       project_update(4, yo[1]);
@@ -4173,7 +4220,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
-           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0);
+           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.visc_firsts ? 64 : 0);
   });
 }
 

@@ -1235,6 +1235,36 @@ struct VincDev {
   const float* d[2 * VINC_MAX];
   int order;
 };
+// the warm start's unscaled value at row i (u + the extrapolated increment), both components
+__device__ __forceinline__ void visc_start(const VincDev& D, int64_t i, double a, double b, double& ga, double& gb) {
+  ga = a;
+  gb = b;
+  double e[2 * VINC_MAX];
+#pragma unroll
+  for (int k = 0; k < 2 * VINC_MAX; ++k) e[k] = k < 2 * D.order ? (double)D.d[k][i] : 0.0;
+  if (D.order == 1) {
+    ga += e[0];
+    gb += e[1];
+  } else if (D.order == 2) {
+    ga += 2.0 * e[0] - e[2];
+    gb += 2.0 * e[1] - e[3];
+  } else if (D.order == 3) {
+    ga += 3.0 * (e[0] - e[2]) + e[4];
+    gb += 3.0 * (e[1] - e[3]) + e[5];
+  } else if (D.order == 4) {
+    ga += 4.0 * (e[0] + e[4]) - 6.0 * e[2] - e[6];
+    gb += 4.0 * (e[1] + e[5]) - 6.0 * e[3] - e[7];
+  } else if (D.order == 5) {
+    ga += 5.0 * (e[0] - e[6]) + 10.0 * (e[4] - e[2]) + e[8];
+    gb += 5.0 * (e[1] - e[7]) + 10.0 * (e[5] - e[3]) + e[9];
+  } else if (D.order == 6) {
+    ga += 6.0 * (e[0] + e[8]) - 15.0 * (e[2] + e[6]) + 20.0 * e[4] - e[10];
+    gb += 6.0 * (e[1] + e[9]) - 15.0 * (e[3] + e[7]) + 20.0 * e[5] - e[11];
+  } else if (D.order == 7) {
+    ga += 7.0 * (e[0] - e[10]) + 21.0 * (e[8] - e[2]) + 35.0 * (e[4] - e[6]) + e[12];
+    gb += 7.0 * (e[1] - e[11]) + 21.0 * (e[9] - e[3]) + 35.0 * (e[5] - e[7]) + e[13];
+  }
+}
 __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
                             const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy,
                             VincDev D) {
@@ -1242,32 +1272,8 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
     const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
     stnt(bx + i, s[i] * a);
     stnt(by + i, s[i] * b);
-    double ga = a, gb = b;
-    double e[2 * VINC_MAX];
-#pragma unroll
-    for (int k = 0; k < 2 * VINC_MAX; ++k) e[k] = k < 2 * D.order ? (double)D.d[k][i] : 0.0;
-    if (D.order == 1) {
-      ga += e[0];
-      gb += e[1];
-    } else if (D.order == 2) {
-      ga += 2.0 * e[0] - e[2];
-      gb += 2.0 * e[1] - e[3];
-    } else if (D.order == 3) {
-      ga += 3.0 * (e[0] - e[2]) + e[4];
-      gb += 3.0 * (e[1] - e[3]) + e[5];
-    } else if (D.order == 4) {
-      ga += 4.0 * (e[0] + e[4]) - 6.0 * e[2] - e[6];
-      gb += 4.0 * (e[1] + e[5]) - 6.0 * e[3] - e[7];
-    } else if (D.order == 5) {
-      ga += 5.0 * (e[0] - e[6]) + 10.0 * (e[4] - e[2]) + e[8];
-      gb += 5.0 * (e[1] - e[7]) + 10.0 * (e[5] - e[3]) + e[9];
-    } else if (D.order == 6) {
-      ga += 6.0 * (e[0] + e[8]) - 15.0 * (e[2] + e[6]) + 20.0 * e[4] - e[10];
-      gb += 6.0 * (e[1] + e[9]) - 15.0 * (e[3] + e[7]) + 20.0 * e[5] - e[11];
-    } else if (D.order == 7) {
-      ga += 7.0 * (e[0] - e[10]) + 21.0 * (e[8] - e[2]) + 35.0 * (e[4] - e[6]) + e[12];
-      gb += 7.0 * (e[1] - e[11]) + 21.0 * (e[9] - e[3]) + 35.0 * (e[5] - e[7]) + e[13];
-    }
+    double ga, gb;
+    visc_start(D, i, a, b, ga, gb);
     stnt(yx + i, sq[i] * ga);
     stnt(yy + i, sq[i] * gb);
   }
@@ -1283,6 +1289,154 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double
     stnt(usy + i, b);
     stnt(dx + i, (float)(a - ux[i]));
     stnt(dy + i, (float)(b - uy[i]));
+  }
+}
+
+// The viscous solve's first Chebyshev step with k_visc_prep folded in (one rank, extrapolated start):
+// the start y = sq (u + extrapolated increment) is a per-row function of u, sq and the stored
+// increments, so it is never written.  Face items compute y on their window [t0 - n, t1 + n) into LDS
+// (k_vcheb_pair's window) and the step on their own rows; y at a skeleton column and, in the SELL
+// blocks, y at every column is evaluated where it is needed.  Writes b = s u, x_1 = y + c2 (b - A^ y),
+// d_1 and the <r_0, r_0>, <b, b> partials.  Every value is computed as k_visc_prep + k_vcheb (first)
+// compute it, so the step is bit-identical to the two launches; 72 + 8 order B/row instead of
+// 104 + 8 order + 56.
+struct VFirstVecs {
+  const double* s;
+  const double* sq;
+  const double* u[2];
+  VincDev D;
+  double* b[2];     // s u (written)
+  double* xout[2];  // x_1
+  float* d[2];      // d_1
+};
+template <bool C16>
+__global__ __launch_bounds__(BS) void k_vcheb_first(SellDev A, FaceDev fc, const double* __restrict__ val,
+                                                    VFirstVecs v, double c2, const int* ctl, double* part_rr,
+                                                    double* part_bb) {
+  __shared__ double lx[2][VP_W];
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  auto ystart = [&](int64_t j, double& ya, double& yb) {
+    const double a = v.u[0][j] + 0.0, b = v.u[1][j] + 0.0;
+    double ga, gb;
+    visc_start(v.D, j, a, b, ga, gb);
+    const double q = v.sq[j];
+    ya = q * ga;
+    yb = q * gb;
+  };
+  double rr[2] = {0.0, 0.0}, bb[2] = {0.0, 0.0};
+  auto finish = [&](int c, int64_t row, double ax, double x0, double br) {
+    const double r = br - ax;
+    const double dn = c2 * r;
+    stnt(v.d[c] + row, (float)dn);
+    stnt(v.xout[c] + row, x0 + dn);
+    stnt(v.b[c] + row, br);
+    rr[c] += r * r;
+    bb[c] += br * br;
+  };
+  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+    const int32_t items = fc.nf * fc.cpf;
+    int32_t it = (int32_t)blockIdx.x - ((int32_t)gridDim.x - fc.nb);
+    if (fc.nb == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows; the SELL blocks are 8k)
+      const int32_t x = it & 7, q = items >> 3, rem = items & 7;
+      it = x * q + (x < rem ? x : rem) + (it >> 3);
+    }
+    const int32_t lf = it / fc.cpf;
+    const lat::FaceTab F = fc.tab[lf];
+    const int32_t n = fc.n;
+    const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT), t1 = min(t0 + BS * FACE_RPT, fc.F);
+    const int32_t w0 = max(0, t0 - n), nw = min(fc.F, t1 + n) - w0;
+    // (b = s u of the rows stays in registers for the step: u and s are read once per row)
+    double bt[VP_WK][2];
+#pragma unroll
+    for (int k = 0; k < VP_WK; ++k) {
+      const int32_t w = (int32_t)threadIdx.x + k * BS;
+      bt[k][0] = bt[k][1] = 0.0;
+      if (w < nw) {
+        const int64_t j = F.base + w0 + w;
+        const double a = v.u[0][j] + 0.0, b = v.u[1][j] + 0.0;
+        double ga, gb;
+        visc_start(v.D, j, a, b, ga, gb);
+        const double q = v.sq[j], sr = v.s[j];
+        lx[0][w] = q * ga;
+        lx[1][w] = q * gb;
+        bt[k][0] = sr * a;
+        bt[k][1] = sr * b;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < VP_WK; ++k) {
+      const int32_t w = (int32_t)threadIdx.x + k * BS;
+      const int32_t t = w0 + w;
+      if (w < nw && t >= t0 && t < t1) {
+        int32_t i, j, nb[6];
+        bool in[6];
+        lat::coords(t, n, fc.rinv, i, j);
+        lat::neighbours(F, n, t, i, j, nb, in);
+        double a[7];
+        face_kcoefs(fc, lf, nb, in, a);
+        const int64_t row = F.base + t;
+        double xv[2][7];
+        xv[0][6] = lx[0][w];
+        xv[1][6] = lx[1][w];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          if (in[q]) {
+            const int32_t lw = min(max(nb[q] - F.base - w0, 0), nw - 1);
+            xv[0][q] = lx[0][lw];
+            xv[1][q] = lx[1][lw];
+          } else {
+            ystart(nb[q], xv[0][q], xv[1][q]);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const double br = bt[k][c];
+          double ax = a[0] * xv[c][6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[c][q];
+          finish(c, row, ax, xv[c][6], br);
+        }
+      }
+    }
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t s = s0 + wv; s < s1; s += 4) {
+      const int64_t row = sell_row(A, s, lane);
+      const int64_t rw = row >= 0 ? row : 0;
+      double acc[2] = {0.0, 0.0}, x0[2], br[2];
+      ystart(rw, x0[0], x0[1]);
+      const double sr = v.s[rw];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) br[c] = sr * (v.u[c][rw] + 0.0);
+      const int64_t off = A.off[s];
+      const int w = A.w[s];
+      const int32_t base = (int32_t)(s * 64);
+      for (int k = 0; k < w; ++k) {
+        const int64_t e = off + (int64_t)k * 64 + lane;
+        const double av = ldnt(val + e);
+        double ya, yb;
+        ystart(sell_col<C16>(A, e, base), ya, yb);
+        acc[0] += av * ya;
+        acc[1] += av * yb;
+      }
+      if (row >= 0) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) finish(c, row, acc[c], x0[c], br[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const double t1 = block_sum(rr[c], sh);
+    const double t2 = block_sum(bb[c], sh);
+    if (threadIdx.x == 0) {
+      part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
+      part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
+    }
   }
 }
 
