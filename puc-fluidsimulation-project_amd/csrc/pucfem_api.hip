@@ -2341,19 +2341,36 @@ void build_mg_host(Ctx& c, SetupClock& clk) {
   if (c.lattice) F.latl = std::move(c.lat_fine);
   F.dof = c.dof;
   F.master_of = c.master_of;
-  for (int l = 1; l <= Lv; ++l) {
-    MgLevel& L = c.mg[l];
-    const MgLevel& C = c.mg[l - 1];
-    build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
-    transpose(L.Pr, C.mesh.N, L.R);
-  }
-  clk.mark("  mg: transfers");
+  // the transfers of every level (serial builders, one thread per level) and the lmax estimates (each
+  // parallel inside) read only what the level operators above produced: they run concurrently
   // the finest level's power iteration runs on the device at the end of build() (single rank)
   c.lmax_dev = c.world == 1 && !c.host_only;
-  for (int l = 0; l <= Lv; ++l)
-    c.mg[l].lmax = l == Lv && c.lmax_dev ? lmax_estimate(c.Pp, false, &c.lmax_dinv)
-                                         : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
-  clk.mark("  mg: lmax estimates");
+  {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(Lv + 1);
+    for (int l = 1; l <= Lv; ++l)
+      th.emplace_back([&c, &err, l] {
+        try {
+          MgLevel& L = c.mg[l];
+          const MgLevel& C = c.mg[l - 1];
+          build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
+          transpose(L.Pr, C.mesh.N, L.R);
+        } catch (...) {
+          err[l] = std::current_exception();
+        }
+      });
+    try {
+      for (int l = 0; l <= Lv; ++l)
+        c.mg[l].lmax = l == Lv && c.lmax_dev ? lmax_estimate(c.Pp, false, &c.lmax_dinv)
+                                             : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
+    } catch (...) {
+      err[0] = std::current_exception();
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+  clk.mark("  mg: transfers + lmax estimates");
 }
 
 // ------------------------------------------------------------------ operator build
