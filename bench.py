@@ -61,6 +61,9 @@ def parse():
                     help="time the steps without per-launch kernel events (no roofline block)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--fine-steps", type=int, default=200)
+    ap.add_argument("--steady-after", type=int, default=100,
+                    help="steady-state leg: the same run continued to this step, then --steady-steps timed (0: off)")
+    ap.add_argument("--steady-steps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -148,10 +151,13 @@ def main():
     n1, b1 = sim.ctx.counters()
     elapsed = allmax(dt_local)
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
-    names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_div/k_grad_proj", "k_sl",
+    names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_grad_proj", "k_sl",
              "k_resid (MG residual, finest level)", "k_transfer (restriction from finest)",
              "k_transfer (prolongation to finest)", "k_sl_slow (general locate + rank count)",
-             "k_vcheb (viscous Chebyshev step)", "k_cheb_pair (two MG smoothing steps, finest level)"]
+             "k_vcheb (viscous Chebyshev step, whole grid)", "k_cheb_pair (two MG smoothing steps, finest level)",
+             "k_div (divergence + pressure rhs)", "k_vcheb_pair (two viscous Chebyshev steps, face rows)",
+             "k_visc_prep (viscous rhs + extrapolated start)", "k_mdot2 (projection multi-dot)",
+             "k_pcomb (projection combination)"]
     ktab = {}
     for k, nm in enumerate(names):
         ms, n, b = sim.ctx.timing_get(k)
@@ -225,19 +231,17 @@ def main():
                     "ms_per_step": [1e3 * s for s, _ in startup], "pressure_cg_iters": [i for _, i in startup]}
         if startup else None,
     }
-    # roofline of the dominant kernel: the finest-level Chebyshev smoother step (k_cheb) when the
-    # pressure is multigrid-preconditioned, else the CG SpMV+direction kernel (k_cg_dir).  Algorithmic
-    # bytes per launch for k_cheb in the fp32 cycle = (value + column bytes) * nnz -- 2 + 2 with fp16
-    # values and int16 column deltas, 4 + 4 without -- + per row 4 B each for x (gathered once), dinv,
-    # d read, d write, x write + 8 B fp64 rhs (the CG residual), plus 8 B r for <r, z> and fp64 z on the
-    # last post-smoothing step; (8 + column bytes) * nnz + 32*NRHS*N for k_cg_dir.  The library counts
-    # them per launch (tstop); timed with HIP events on the library stream.
-    # (with step pairs the finest level's smoothing runs mostly in k_cheb_pair: the class with the larger
-    # share of the timed region is the roofline kernel)
-    dom = names[0] if names[0] in ktab else names[1]
-    if names[10] in ktab and (dom not in ktab or ktab[names[10]]["launches_timed"] * ktab[names[10]]["avg_launch_ms"]
-                              > ktab[dom]["launches_timed"] * ktab[dom]["avg_launch_ms"]):
-        dom = names[10]
+    # roofline of the dominant kernel: the timed class with the largest share of the timed region (every
+    # class with a share of the step is timed with per-launch events: viscous Chebyshev steps and pairs,
+    # divergence, semi-Lagrangian, the finest smoother, the PCG kernels, the projection passes).  Algorithmic
+    # bytes per launch are the library's own counts: vectors once per row read or
+    # written, stored operators per entry; timed with HIP events taken by each launch's dispatch on the
+    # stream it runs on.
+    dom = max(ktab, key=lambda k: ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"]) if ktab else None
+    ms_step = 1e3 * elapsed / a.steps
+    for k in ktab:  # share of the timed region (the dye stream's kernels overlap the main stream's)
+        ktab[k]["ms_per_step"] = ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"] / a.steps
+        ktab[k]["share"] = ktab[k]["ms_per_step"] / ms_step
     if dom in ktab:
         kd = ktab[dom]
         traffic = None
@@ -247,7 +251,8 @@ def main():
                 traffic = json.load(open(pmc)).get(f"L{a.level}_n{world}", {}).get(dom.split()[0])
             except Exception:
                 traffic = None
-        rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "achieved": kd["achieved_GBps"],
+        rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "kernel_share": kd["share"],
+                           "achieved": kd["achieved_GBps"],
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kd["achieved_GBps"] / HBM_PEAK_GBS,
                            "traffic": traffic, "bytes_per_launch": kd["bytes_per_launch"],
                            "avg_launch_ms": kd["avg_launch_ms"], "launches_timed": kd["launches_timed"]}
@@ -260,13 +265,19 @@ def main():
         "counted": "every kernel's algorithmic bytes (vectors once per row read or written, stored operators per entry)"}
     rec["kernels"] = ktab
     rec["kernel_batch"] = batch
+    if a.steady_after > 0:
+        rec["steady"] = steady_leg(sim, a.warmup + a.steps, a.steady_after, a.steady_steps, barrier, allmax, allsum,
+                                   world)
     sim.close()
     if rank == 0 and world == 1 and not a.no_secondary and a.level > 5:
         rec["l5"] = gpu_l5(pf, tol)
+    if rank == 0 and world == 1 and not a.no_secondary:
+        rec["food_l5"] = gpu_food_l5(pf, tol)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(pf, a.level, stats, rec.get("l5"))
     if rank == 0 and world == 1 and not a.no_secondary:
         rec["mesh_fine"] = secondary_fine(pf, a.fine_steps)
+        rec["heat_fine"] = heat_fine(pf)
     if rank == 0:
         print(json.dumps(rec))
     if world > 1:
@@ -293,6 +304,81 @@ def gpu_l5(pf, tol, warmup=5, steps=20):
             "ms_per_step": ms, "launches_per_step": (n1 - n0) / steps,
             "step_roofline_frac": (b1 - b0) / steps / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
             "cg_iters_last_step": [st[-1].it_visc, st[-1].it_p, st[-1].it_p2]}
+
+
+def steady_leg(sim, done, after, steps, barrier, allmax, allsum, world):
+    """Past the start-up transient: the benchmarked run continued (untimed) to step `after`, then `steps`
+    timed steps -- the rate of the reference's long runs (StokesColor.py:44: 6000 steps), where the
+    pressure solves take 1-2 iterations.  Same schedule and tolerances as the headline; no kernel events."""
+    if after > done:
+        sim.step(after - done)
+    barrier()
+    sim.ctx.sync()
+    n0, b0 = sim.ctx.counters()
+    t = time.perf_counter()
+    st = sim.step(steps)
+    sim.ctx.sync()
+    barrier()
+    el = allmax(time.perf_counter() - t)
+    n1, b1 = sim.ctx.counters()
+    ms = 1e3 * el / steps
+    return {"after_steps": max(after, done), "steps": steps, "steps_per_s": steps / el, "ms_per_step": ms,
+            "launches_per_step": (n1 - n0) / steps,
+            "step_roofline_frac": allsum(b1 - b0) / steps / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9 * world),
+            "cg_iters_per_step": {"visc": [s.it_visc for s in st], "p": [s.it_p for s in st],
+                                  "p2": [s.it_p2 for s in st]}}
+
+
+def gpu_food_l5(pf, tol, warmup=5, steps=20):
+    """BASELINE configs[3]: the StokesFood pusher (B1=-2, B2=-5, nu=1, DT=0.01; StokesFood.py:441-505, the
+    488 tracers at :482-499) on L5 (894,208 nodes), production settings, 5 warm-up steps and 20 timed."""
+    m = pf.load_mesh("fine", refine=5)
+    sim = pf.StokesSimulation(m, pf.SquirmerBC(B2=-5.0, nu=1.0), 0.01, "food", tol=tol)
+    sim.step(warmup)
+    sim.ctx.sync()
+    n0, b0 = sim.ctx.counters()
+    t = time.perf_counter()
+    st = sim.step(steps)
+    sim.ctx.sync()
+    el = time.perf_counter() - t
+    n1, b1 = sim.ctx.counters()
+    path = sim.ctx.path_info()
+    sim.close()
+    ms = 1e3 * el / steps
+    return {"workload": "StokesFood pusher (B1=-2, B2=-5, nu=1, DT=0.01), mesh_fine x5, 488 tracers",
+            "nodes": m.N, "warmup": warmup, "steps": steps, "steps_per_s": steps / el, "ms_per_step": ms,
+            "launches_per_step": (n1 - n0) / steps,
+            "step_roofline_frac": (b1 - b0) / steps / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "viscous_iteration": path.get("viscous_iteration"), "eaten_after": st[-1].eaten,
+            "cg_iters_last_step": [st[-1].it_visc, st[-1].it_p, st[-1].it_p2]}
+
+
+def heat_fine(pf, steps=600):
+    """BASELINE configs[1]: heatEq.py's 600 backward-Euler steps (heatEq.py:320-325) on mesh_fine, GPU
+    against the oracle's HeatLiteral (scipy splu, factorised once) on this host; both end states compared."""
+    import numpy as np
+
+    import oracle as O
+
+    mesh = pf.load_mesh("fine")
+    h = pf.HeatSimulation(mesh)
+    h.ctx.sync()
+    t = time.perf_counter()
+    h.step(steps)
+    h.ctx.sync()
+    gpu = steps / (time.perf_counter() - t)
+    ug = h.u
+    h.close()
+    m32 = mesh.as_fp32()
+    ref = O.HeatLiteral(m32.coords, m32.markers, m32.triangles)
+    u = ref.initial()
+    t = time.perf_counter()
+    for _ in range(steps):
+        u = ref.step(u)
+    cpu = steps / (time.perf_counter() - t)
+    return {"workload": f"heatEq.py backward Euler, mesh_fine ({mesh.N} nodes), {steps} steps",
+            "gpu_steps_per_s": gpu, "cpu_oracle_steps_per_s": cpu, "cpu_oracle_kind": "port (scipy splu, 1 thread)",
+            "ratio_vs_oracle": gpu / cpu, "max_abs_diff_u600": float(np.abs(ug - u).max())}
 
 
 def cpu_baseline(pf, level, stats, l5=None):

@@ -98,21 +98,14 @@ struct HFace {
   FaceDev d{};
   int32_t items = 0;
   int64_t rows = 0;  // face-interior rows (algorithmic bytes)
-  // PUCFEM_FACE_SEQ=1 (measurement knob): one block per face running its chunks in order (FaceDev::seq)
-  static bool face_seq() {
-    static const bool on = std::getenv("PUCFEM_FACE_SEQ") && std::atoi(std::getenv("PUCFEM_FACE_SEQ")) != 0;
-    return on;
-  }
   FaceDev part() const {
     FaceDev f = d;
     f.nb = std::min(items, FACE_PART_BLOCKS);
-    if (face_seq() && d.cpf > 1 && d.nf <= FACE_PART_BLOCKS) f.nb = d.nf, f.seq = 1;
     return f;
   }
   FaceDev full() const {
     FaceDev f = d;
     f.nb = items;
-    if (face_seq() && d.cpf > 1) f.nb = d.nf, f.seq = 1;
     return f;
   }
 };
@@ -136,7 +129,10 @@ struct Timer {
   std::vector<hipEvent_t> pool;
   struct Pend { int cls; hipEvent_t a, b; double bytes; };
   std::vector<Pend> pend;
-  static constexpr int NCLS = 11;
+  // classes: 0 k_cheb (finest), 1 k_cg_dir, 2 k_cg_upd, 3 k_grad_proj, 4 k_sl, 5 k_resid (finest), 6 / 7 the
+  // finest level's restriction / prolongation, 8 k_sl_slow, 9 k_vcheb (whole-grid steps), 10 k_cheb_pair,
+  // 11 k_div, 12 k_vcheb_pair, 13 k_visc_prep, 14 k_mdot2, 15 k_pcomb
+  static constexpr int NCLS = 16;
   double ms[NCLS] = {};
   double bytes[NCLS] = {};
   int64_t n[NCLS] = {};
@@ -242,40 +238,27 @@ template <> MgBufs<double>& bufs<double>(MgLevel& L) { return L.f64; }
 template <> MgBufs<float>& bufs<float>(MgLevel& L) { return L.f32; }
 
 void spmv_on(hipStream_t st, const DevSell& A, const FaceDev& fc, const double* val, const double* x, double* y);
-// k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size
-template <int M>
-void mdot2_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* b, const double* av,
-                  const double* v, const int32_t* master_of, double* part, RedOut ro) {
-  hipLaunchKernelGGL(k_mdot2<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, b, av, v, master_of, part, ro);
-}
-using Mdot2Fn = void (*)(hipStream_t, int, int64_t, const ProjT*, int64_t, const double*, const double*,
-                         const double*, const int32_t*, double*, RedOut);
+// k_mdot2 / k_pcomb for basis size m (0..PROJ_MAX): one instance per size, picked from a table (every
+// instance has the same signature, so the launch goes through Ctx::klaunch like any other kernel)
+using Mdot2K = decltype(&k_mdot2<0>);
+using PcombK = decltype(&k_pcomb<0>);
 template <int... M>
-constexpr std::array<Mdot2Fn, sizeof...(M)> mdot2_table(std::integer_sequence<int, M...>) {
-  return {&mdot2_launch<M>...};
+constexpr std::array<Mdot2K, sizeof...(M)> mdot2_table(std::integer_sequence<int, M...>) {
+  return {&k_mdot2<M>...};
 }
-void mdot2_on(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, int m, const double* b, const double* av,
-              const double* v, const int32_t* master_of, double* part, RedOut ro) {
+template <int... M>
+constexpr std::array<PcombK, sizeof...(M)> pcomb_table(std::integer_sequence<int, M...>) {
+  return {&k_pcomb<M>...};
+}
+Mdot2K mdot2_kernel(int m) {
   static constexpr auto tab = mdot2_table(std::make_integer_sequence<int, PROJ_MAX + 1>{});
   if (m < 0 || m > PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
-  tab[m](s, nb, n, X, ld, b, av, v, master_of, part, ro);
+  return tab[m];
 }
-template <int M>
-void pcomb_launch(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, const double* K, const double* v,
-                  const int32_t* master_of, ProjT* xm, double* y, double* x0) {
-  hipLaunchKernelGGL(k_pcomb<M>, dim3(nb), dim3(BS), 0, s, n, X, ld, K, v, master_of, xm, y, x0);
-}
-using PcombFn = void (*)(hipStream_t, int, int64_t, const ProjT*, int64_t, const double*, const double*,
-                         const int32_t*, ProjT*, double*, double*);
-template <int... M>
-constexpr std::array<PcombFn, sizeof...(M)> pcomb_table(std::integer_sequence<int, M...>) {
-  return {&pcomb_launch<M>...};
-}
-void pcomb_on(hipStream_t s, int nb, int64_t n, const ProjT* X, int64_t ld, int m, const double* K, const double* v,
-              const int32_t* master_of, ProjT* xm, double* y, double* x0) {
+PcombK pcomb_kernel(int m) {
   static constexpr auto tab = pcomb_table(std::make_integer_sequence<int, PROJ_MAX>{});
   if (m < 0 || m >= PROJ_MAX) throw Error(PUCFEM_EINVAL, "projection basis size out of range");
-  tab[m](s, nb, n, X, ld, K, v, master_of, xm, y, x0);
+  return tab[m];
 }
 
 struct Ctx {
@@ -441,11 +424,6 @@ struct Ctx {
   // d buffer of the finest level are allocated on first use
   bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
   int64_t mg_pairs = 0;
-  // k_visc_prep folded into the viscous solve's first step (k_vcheb_first): PUCFEM_VISC_FIRST=1 (measurement
-  // knob; off by default: r9i measured 100.3 against 110.3 steps/s -- the window recomputes y's 64 B/row of
-  // inputs on 25 % more rows, so the fusion saves no bytes)
-  bool visc_first = std::getenv("PUCFEM_VISC_FIRST") && std::atoi(std::getenv("PUCFEM_VISC_FIRST")) != 0;
-  int64_t visc_firsts = 0;
   float* mgp_x = nullptr;
   float* mgp_d = nullptr;
   double* dwsk = nullptr;  // scaled A_visc skeleton column weights
@@ -640,12 +618,9 @@ struct Ctx {
   // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
   // the all-reduce across ranks): consumers read one scalar instead of re-reducing up to MAXB
   // partials in each of their blocks
-  int red_threads = std::getenv("PUCFEM_RED_THREADS") ? std::atoi(std::getenv("PUCFEM_RED_THREADS")) : RB;
   void launch_reduce(const double* part, int nb, int stride, int nv, bool is_max, double* out) {
-    if (red_threads == 256)
-      hipLaunchKernelGGL(k_reduce_t<256>, dim3(1), dim3(256), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
-    else
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
+    // one block per value (k_reduce_t); a 256-thread reduce measured equal in round 3 (r8i)
+    hipLaunchKernelGGL(k_reduce, dim3(std::max(1, nv)), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
   }
   Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
     double* buf = redbuf + 8 * slot;
@@ -699,7 +674,7 @@ struct Ctx {
     // of a 2 W vector holding (1 - min, max) in each rank's slot
     hipLaunchKernelGGL(k_yrange, dim3(nb), dim3(BS), 0, st, n, my + lp.r0, vy, dt, part_u);
     KCHK();
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_u, nb, MAXB, 2, 1, yr_own);
+    hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_u, nb, MAXB, 2, 1, yr_own);
     hipLaunchKernelGGL(k_place2, dim3(1), dim3(64), 0, st, world, rank, (const double*)yr_own, yr_all);
     KCHK();
     comm->allreduce(yr_all, 2 * (size_t)world, true, st);
@@ -869,8 +844,7 @@ struct Ctx {
   };
   template <int NR>
   int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
-            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr,
-            const VFirstVecs* vfirst = nullptr) {
+            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr) {
     if (fin_done) *fin_done = false;
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
@@ -986,7 +960,7 @@ struct Ctx {
           klaunch(-1, bytes_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a,
                   c2a, 0, (const int*)ctl, (double*)nullptr, (double*)nullptr, RedOut{});
           KCHK();
-          klaunch(-1, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
+          klaunch(12, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
                   (int32_t)nbs);
           KCHK();
           klaunch(-1, bytes_sk + fin_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
@@ -1010,31 +984,10 @@ struct Ctx {
     // no residual checks, no reductions and no host round trip.  (The bound is rigorous for the interval
     // [visc_lo, 1 + visc_R], which tests/test_host_assembly.py checks against the spectrum; the
     // adaptive test it replaces needed one extra step per solve to see the passing residual.)
-    int nb0 = nb;  // the first step's partial count
-    if (vfirst) {  // (NR = 2) k_visc_prep folded into the first step: y is never written
-      if constexpr (NR == 2) {
-        FaceDev ff = fc;
-        ff.nb = hf.items;
-        nb0 = ((nb_for(A.nslices) + 7) & ~7) + hf.items;
-        const double bytes0 = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
-                              (72.0 + 8.0 * vfirst->D.order) * (double)A.own();
-        VFirstVecs vf = *vfirst;
-        for (int c = 0; c < 2; ++c) {
-          vf.xout[c] = xb[c];
-          vf.d[c] = dcur[c];
-        }
-        with_c16(A, [&](auto c16) {
-          klaunch(9, bytes0, k_vcheb_first<decltype(c16)::value>, dim3(nb0), dim3(BS), A.view(), ff, val, vf,
-                  1.0 / theta, (const int*)ctl, part_a, part_b);
-        });
-        KCHK();
-        for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
-      }
-    } else {
-      step(0, 0.0, 1.0 / theta);
-    }
+    const int nb0 = nb;  // the first step's partial count
+    step(0, 0.0, 1.0 / theta);
     Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
-    if (!vfirst && ro(redbuf, CNT_VCHEB, 2 * NR).out) {
+    if (ro(redbuf, CNT_VCHEB, 2 * NR).out) {
       red_done(redbuf, 2 * NR, false);
     } else {
       rr = reduce_global(part_a, nb0, NR, false, 0);
@@ -1133,7 +1086,7 @@ struct Ctx {
         nck = nb;
       }
       if (fuse) *fin_done = true;
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, (const double*)part_c, nck, MAXB, NR, 0, redbuf + 48);
+      hipLaunchKernelGGL(k_reduce, dim3(NR), dim3(RB), 0, st, (const double*)part_c, nck, MAXB, NR, 0, redbuf + 48);
       KCHK();
       if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
       HIPCHK(hipMemcpyAsync(h_pinned + 32, redbuf + 48, NR * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1321,14 +1274,8 @@ struct Ctx {
   }
   // z = M^-1 r on level l (b = r_l); the finest level passes rdot = r for the <r, z> partials and
   // writes z (fp64) directly from its last smoothing step
-  // smoothing degrees below the finest level (measurement knobs PUCFEM_MG_PRE_COARSE /
-  // PUCFEM_MG_POST_COARSE; 0: the finest level's)
-  int mg_pre_coarse = std::getenv("PUCFEM_MG_PRE_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_PRE_COARSE")) : 0;
-  int mg_post_coarse = std::getenv("PUCFEM_MG_POST_COARSE") ? std::atoi(std::getenv("PUCFEM_MG_POST_COARSE")) : 0;
-  // levels of at most PUCFEM_MG_TINY_ROWS rows (measurement knob, default 0: none) smooth with
-  // PUCFEM_MG_TINY_DEG steps before and after: their launches are latency-bound (~6 us for ~1 us of work)
-  int64_t mg_tiny_rows = std::getenv("PUCFEM_MG_TINY_ROWS") ? std::atoll(std::getenv("PUCFEM_MG_TINY_ROWS")) : 0;
-  int mg_tiny_deg = std::getenv("PUCFEM_MG_TINY_DEG") ? std::max(1, std::atoi(std::getenv("PUCFEM_MG_TINY_DEG"))) : 1;
+  // (every level smooths with the finest level's degrees: fewer steps on the latency-bound coarse levels
+  // cost more pressure iterations than their launches save, round 3 r8e / r8f)
   template <typename T, typename TB>
   T* vcycle(int l, const TB* b, const double* rdot, double* part) {
     MgLevel& L = mg[l];
@@ -1351,8 +1298,7 @@ struct Ctx {
         throw Error(PUCFEM_ESTATE, "multigrid hierarchy has a single level");
       }
     }
-    const bool tiny = !finest && (int64_t)A.own() <= mg_tiny_rows;
-    const int pre = tiny ? mg_tiny_deg : (finest || mg_pre_coarse <= 0 ? prm.mg_degree : mg_pre_coarse);
+    const int pre = prm.mg_degree;
     if constexpr (std::is_same<T, TB>::value) {
       // coarse levels: the fused first smoothing step reads b at ghost columns
       if (pre >= 2) mg_halo(L, const_cast<T*>(b));
@@ -1405,7 +1351,7 @@ struct Ctx {
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
     return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part,
-                            tiny ? mg_tiny_deg : (finest || mg_post_coarse <= 0 ? post : mg_post_coarse));
+                            post);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
@@ -1592,24 +1538,12 @@ struct Ctx {
     VincDev vd{};
     vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
     for (int k = 0; k < 2 * VINC_MAX; ++k) vd.d[k] = dvinc[k];
-    const bool cheb0 = visc_solver == 0 && visc_R < 0.25 && !(!dist() && block_cg && !fVisc.items &&
-                                                              dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
-    // k_visc_prep folded into the Chebyshev solve's first step (k_vcheb_first; one rank, lattice faces)
-    const bool first_fused = visc_first && cheb0 && ext && proj_k_visc == 0 && !dist() && fVisc.items > 0 &&
-                             fVisc.d.n <= VP_HALO && !fused_red &&
-                             ((nb_for(dP.nslices) + 7) & ~7) + fVisc.items <= MAXB;
-    VFirstVecs vfv{};
-    auto prep = [&] {
-      algo_bytes += (64.0 + 8.0 * vd.order) * (double)n;  // u, s, sq, the increments read; b, y written
-      hipLaunchKernelGGL(k_visc_prep, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, dsqv, ux, uy, bvx, bvy, yvx, yvy, vd);
-      KCHK();
-    };
-    if (first_fused) {
-      vfv = VFirstVecs{dsv, dsqv, {ux, uy}, vd, {bvx, bvy}, {nullptr, nullptr}, {nullptr, nullptr}};
-      ++visc_firsts;
-    } else {
-      prep();
-    }
+    // (k_visc_prep folded into the solve's first step was measured 9 % slower in round 3, r9i: the window
+    // recomputes the start's 64 B/row of inputs on 25 % more rows, so the fusion saved no bytes)
+    // u, s, sq, the increments read; b, y written
+    klaunch(13, (64.0 + 8.0 * vd.order) * (double)n, k_visc_prep, dim3(grid_ew(n)), dim3(BS), (int64_t)n,
+            (const double*)dsv, (const double*)dsqv, (const double*)ux, (const double*)uy, bvx, bvy, yvx, yvy, vd);
+    KCHK();
     double* y[2] = {yvx, yvy};
     const double* b[2] = {bvx, bvy};
     const bool proj = proj_k_visc > 0;
@@ -1627,9 +1561,7 @@ struct Ctx {
     const bool fuse = ext && !proj && visc_fuse_fin;
     if (fuse) vf = ViscFin{dsv, {ux, uy}, {usx, usy}, {dvinc[last], dvinc[last + 1]}};
     if (cheb) {
-      iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr, &fin_done,
-                       first_fused ? &vfv : nullptr);
-      if (first_fused && iters == 0) prep();  // y itself passed the test: it is the answer, so write it
+      iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr, &fin_done);
     } else {
       iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
     }
@@ -1663,7 +1595,7 @@ struct Ctx {
   void div(const double* ax, const double* ay, double* out, bool rhs, double* part = nullptr, RedOut r = RedOut{}) {
     const FaceDev fc = fK.part();
     with_c16(dP, [&](auto c16) {
-      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
+      klaunch(11, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
               k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
               rhs ? braw : (double*)nullptr, part ? part : part_d, r);
@@ -1727,9 +1659,11 @@ struct Ctx {
       return;
     }
     const int nb = grid_ew(n);
-    algo_bytes += (4.0 * m + 24.0) * (double)n;  // k_mdot2: X (fp32), b, A v, v
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
-    mdot2_on(st, nb, n, projX[which], nloc, m, b, pav[which], pv[which], op.null_free, proj_part, rmd);
+    // k_mdot2: X (fp32), b, A v, v read
+    klaunch(14, (4.0 * m + 24.0) * (double)n, mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
+            (const ProjT*)projX[which], (int64_t)nloc, b, (const double*)pav[which], (const double*)pv[which],
+            op.null_free, proj_part, rmd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
@@ -1741,9 +1675,11 @@ struct Ctx {
                        1.0 / (double)n_free, proj_coef);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
-    algo_bytes += (4.0 * kq + 32.0) * (double)n;  // k_pcomb: X, v read; the new direction, x0, y written
-    pcomb_on(st, nb, n, projX[which], nloc, kq, proj_coef, pv[which], op.null_free, projX[which] + (i64)kq * nloc, y,
-             proj_x0[which]);
+    // k_pcomb: X, v read; the new direction, x0, y written
+    klaunch(15, (4.0 * kq + 32.0) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
+            (const ProjT*)projX[which], (int64_t)nloc, (const double*)proj_coef, (const double*)pv[which], op.null_free,
+            projX[which] + (i64)kq * nloc, y, proj_x0[which]);
+    KCHK();
     H.coef_m = kq;
     proj_m[which] = kq + 1;
     proj_pend[which] = false;
@@ -1867,7 +1803,6 @@ struct Ctx {
   hipStream_t st_sl = nullptr;
   hipEvent_t ev_u = nullptr, ev_sl = nullptr;
   bool sl_overlap = true, sl_pending = false;
-  int sl_prio = 0, sl_cus = 0;
   double* part_mx = nullptr;  // k_mix2 partials (part_b belongs to the solvers of the main stream)
   double* part_fd = nullptr;  // final-divergence partials (part_d: the main stream's)
   struct StreamSwap {  // run the enclosed launches on the other stream (restored on unwind)
@@ -1885,15 +1820,9 @@ struct Ctx {
   // one StokesColor / StokesFood step (StokesColor.py:537-586, StokesFood.py:441-505)
   RedOut sl_ro{};
   // The dye tail of a step (final-divergence record, semi-Lagrangian advection, mixing sums, its part of
-  // the step record) on the side stream, after the main stream's event `gate`.  PUCFEM_SL_DELAY=1
-  // (a measurement knob): the tail of step n is enqueued after step n+1's viscous solve and waits for it, so it runs
-  // beside the first pressure solve (whose coarse multigrid levels are latency-bound and leave HBM
-  // bandwidth idle) instead of beside the bandwidth-bound viscous Chebyshev steps; 0 (default): right after
-  // step n.  A/B on one box (r8j): 107.6 / 108.5 (0) against 108.3 / 108.4 steps/s (1) -- the viscous
-  // steps speed up (441 -> 345 us) by what the semi-Lagrangian pass loses beside the pressure solve
-  // (698 -> 937 us): the step is bound by the bytes both streams move, not by where the tail sits.
-  bool sl_delay = std::getenv("PUCFEM_SL_DELAY") && std::atoi(std::getenv("PUCFEM_SL_DELAY")) != 0;
-  double* sl_deferred_rec = nullptr;  // a tail waiting for the next step's viscous solve (its step record)
+  // the step record) on the side stream, after the main stream's event `gate`.  (Round 3 measured the
+  // tail enqueued after the next step's viscous solve instead, beside the pressure solve: the time moved
+  // between the streams, the step rate stayed, r8j.)
   hipEvent_t ev_gate = nullptr;
   void dye_tail(double* rec) {
     HIPCHK(hipEventRecord(ev_gate, st));
@@ -1922,17 +1851,9 @@ struct Ctx {
     HIPCHK(hipEventRecord(ev_sl, st_sl));
     sl_pending = true;
   }
-  // a deferred tail goes now (behind whatever the main stream holds)
-  void dye_flush() {
-    if (!sl_deferred_rec) return;
-    double* r = sl_deferred_rec;
-    sl_deferred_rec = nullptr;
-    dye_tail(r);
-  }
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
-    dye_flush();  // the previous step's deferred dye tail, beside the pressure solve below
     const bool f1 = div_rhs(usx, usy, div_star, vals);  // max |div u*| -> vals[0]
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
     const int itp = pressure(yp, p, 1, f1);
@@ -1957,27 +1878,16 @@ struct Ctx {
     }
     if (ovl) {
       if (!st_sl) {
-        if (sl_cus > 0) {  // measurement knob: the side stream's waves on the first sl_cus compute units
-          int ncu = 0;
-          HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-          std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-          for (int k = 0; k < std::min(sl_cus, ncu); ++k) mask[(size_t)k / 32] |= 1u << (k % 32);
-          HIPCHK(hipExtStreamCreateWithCUMask(&st_sl, (uint32_t)mask.size(), mask.data()));
-        } else if (sl_prio != 0) {  // measurement knob: 1 = the side stream at the lowest priority, -1 = highest
-          int lo = 0, hi = 0;
-          HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-          HIPCHK(hipStreamCreateWithPriority(&st_sl, hipStreamNonBlocking, sl_prio > 0 ? lo : hi));
-        } else {
-          HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
-        }
+        // (stream priorities and CU masks for the side stream were measured and changed nothing or lost,
+        // rounds 2-3: r4d, r6c)
+        HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_sl, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
       }
       hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);  // max |div u*|
       KCHK();
-      if (sl_delay) sl_deferred_rec = rec;  // enqueued by the next step after its viscous solve (dye_flush)
-      else dye_tail(rec);
+      dye_tail(rec);
     } else if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       if (dye_impl) {
@@ -2036,7 +1946,7 @@ struct Ctx {
       hipLaunchKernelGGL(k_vmul, dim3(ge), dim3(BS), 0, st, n, (const double*)y, dinv, y);
       hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, (const double*)x, (const double*)x, (const double*)y,
                          (const double*)y, part_a);
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, redbuf);
+      hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, redbuf);
       KCHK();
       HIPCHK(hipMemcpyAsync(h_pinned, redbuf, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -2153,7 +2063,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(bicg_sc, init, sizeof(init), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, b, b, (const double*)r, (const double*)r, part_a);
     KCHK();
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, bicg_sc + 8);
+    hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, bicg_sc + 8);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_pinned, bicg_sc + 8, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -3140,8 +3050,6 @@ void build(Ctx& c) {
   c.part_mx = c.dalloc<double>(MAXB);
   c.part_fd = c.dalloc<double>(2 * MAXB);
   if (const char* e = std::getenv("PUCFEM_SL_OVERLAP")) c.sl_overlap = std::atoi(e) != 0;  // 0: one stream
-  if (const char* e = std::getenv("PUCFEM_SL_PRIO")) c.sl_prio = std::atoi(e);
-  if (const char* e = std::getenv("PUCFEM_SL_CUS")) c.sl_cus = std::atoi(e);
   c.part_u = c.dalloc<double>(2 * MAXB);
   c.yr_own = c.dalloc<double>(2);
   c.yr_all = c.dalloc<double>(2 * c.world);
@@ -3703,11 +3611,9 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
-          c.dye_flush();  // the last step's deferred dye tail
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
-          c.sl_deferred_rec = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
           throw;
@@ -4161,7 +4067,9 @@ int pucfem_timing_enable(void* ctx, int32_t on) {
     c.timer.flush();
     require(on >= 0 && on <= 2, "timing mode");
     c.timer.on = on != 0;
-    c.timer.mask = on == 2 ? (1u | (1u << 10)) : ~0u;  // mode 2: the roofline kernels (k_cheb, k_cheb_pair)
+    // mode 2: the kernel classes with a share of the step (the roofline kernel is the largest of them); mode 1
+    // adds the finest level's residual and transfers
+    c.timer.mask = on == 2 ? ~((1u << 5) | (1u << 6) | (1u << 7)) : ~0u;
     for (int k = 0; k < Timer::NCLS; ++k) {
       c.timer.ms[k] = 0;
       c.timer.bytes[k] = 0;
@@ -4237,7 +4145,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
-           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.visc_firsts ? 64 : 0);
+           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0);
   });
 }
 

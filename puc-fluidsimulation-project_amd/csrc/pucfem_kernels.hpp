@@ -68,8 +68,6 @@ struct FaceDev {
   float rinv;                // 1 / (n - 1)
   int32_t nb;                // blocks on the face part
   int32_t op;                // 0 = stiffness-type stencil (K, merged pressure, level operators), 1 = scaled A_visc
-  int32_t seq;               // 1: nb = nf and block f runs face f's chunks in order (the halo rows a chunk shares
-                             // with the previous one are still in L2); 0: one block per chunk item
 };
 
 template <class T>
@@ -80,21 +78,9 @@ __device__ __forceinline__ T ldnt(const T* p) {
 // L2 busy with the input vectors, and ordinary stores of the outputs allocate L2 lines that then have
 // to be written back; the streaming store halves the time of a gather kernel with two fp64 outputs
 // (tools/face_lab.hip: 119 -> 61 us for the 14M-row direction kernel, the same bytes as a pure copy).
-// PUCFEM_STORE_SC1 (A/B build): write-through `sc1` stores instead, which do not keep the line in the XCD's
-// L2 (MI355X_MICROARCH.md store table) -- more of the 4 MB L2 for the gathered vectors' halo rows
+// (Write-through sc1 stores instead were measured 5 % slower at L7, round 3 r9b.)
 template <class T>
 __device__ __forceinline__ void stnt(T* p, T v) {
-#ifdef PUCFEM_STORE_SC1
-  if constexpr (sizeof(T) == 8) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  } else if constexpr (sizeof(T) == 4) {
-    __hip_atomic_store(reinterpret_cast<unsigned int*>(p), __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-#endif
   __builtin_nontemporal_store(v, p);
 }
 // column of entry e of the slice whose first row is `base`.  C16: the operator's band fits int16, so
@@ -188,12 +174,14 @@ __device__ __forceinline__ void red_finish(const RedOut& R, const double* part, 
   }
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partials have left the CU
-    const unsigned t = __hip_atomic_fetch_add(R.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acquire-release ticket: this block's partials are released with it, and the last block acquires
+    // every other block's (the HIP memory model's guarantee, not only the sc1 stores' hardware behaviour)
+    const unsigned t = __hip_atomic_fetch_add(R.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction) the loads stay below the ticket
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the last block reads after the ticket
   const int nb = gridDim.x;
   for (int v = 0; v < R.nv; ++v) {
     const bool mx = (R.maxmask >> v) & 1u;

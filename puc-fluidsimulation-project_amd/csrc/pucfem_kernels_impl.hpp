@@ -29,21 +29,6 @@ namespace dev {
 // the coefficient record are scalar loads)
 template <class Fn>
 __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
-  if (fc.seq) {  // block b: face b, its chunks in order
-    const lat::FaceTab F = fc.tab[b];
-    for (int32_t ch = 0; ch < fc.cpf; ++ch) {
-      const int32_t t0 = ch * (BS * FACE_RPT) + (int32_t)threadIdx.x;
-      for (int32_t r = 0; r < FACE_RPT; ++r) {
-        const int32_t t = t0 + r * BS;
-        if (t < fc.F) {
-          int32_t i, j;
-          lat::coords(t, fc.n, fc.rinv, i, j);
-          fn(F, b, t, i, j);
-        }
-      }
-    }
-    return;
-  }
   const int32_t items = fc.nf * fc.cpf;
   // one block per item (launches without partials): consecutive chunks of a face run on one XCD
   // (blocks are dealt round-robin over the 8 XCDs), so the rows a chunk shares with its neighbours
@@ -77,27 +62,6 @@ __device__ __forceinline__ void face_rows(const FaceDev& fc, int32_t b, int32_t 
 template <int K, class Fn>
 __device__ __forceinline__ void face_rows_k(const FaceDev& fc, int32_t b, int32_t nbf, Fn&& fn) {
   static_assert(FACE_RPT % K == 0, "group size divides the rows per thread");
-  if (fc.seq) {  // block b: face b, its chunks in order (face_rows)
-    const lat::FaceTab F = fc.tab[b];
-    for (int32_t ch = 0; ch < fc.cpf; ++ch) {
-      const int32_t t0 = ch * (BS * FACE_RPT) + (int32_t)threadIdx.x;
-#pragma unroll
-      for (int32_t g = 0; g < FACE_RPT; g += K) {
-        if (t0 + g * BS >= fc.F) break;
-        int32_t t[K], i[K], j[K];
-        bool ok[K];
-#pragma unroll
-        for (int r = 0; r < K; ++r) {
-          const int32_t tt = t0 + (g + r) * BS;
-          ok[r] = tt < fc.F;
-          t[r] = ok[r] ? tt : fc.F - 1;
-          lat::coords(t[r], fc.n, fc.rinv, i[r], j[r]);
-        }
-        fn(F, b, t, i, j, ok);
-      }
-    }
-    return;
-  }
   const int32_t items = fc.nf * fc.cpf;
   if (nbf == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows)
     const int32_t x = b & 7, q = items >> 3, rem = items & 7;
@@ -1289,154 +1253,6 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double
     stnt(usy + i, b);
     stnt(dx + i, (float)(a - ux[i]));
     stnt(dy + i, (float)(b - uy[i]));
-  }
-}
-
-// The viscous solve's first Chebyshev step with k_visc_prep folded in (one rank, extrapolated start):
-// the start y = sq (u + extrapolated increment) is a per-row function of u, sq and the stored
-// increments, so it is never written.  Face items compute y on their window [t0 - n, t1 + n) into LDS
-// (k_vcheb_pair's window) and the step on their own rows; y at a skeleton column and, in the SELL
-// blocks, y at every column is evaluated where it is needed.  Writes b = s u, x_1 = y + c2 (b - A^ y),
-// d_1 and the <r_0, r_0>, <b, b> partials.  Every value is computed as k_visc_prep + k_vcheb (first)
-// compute it, so the step is bit-identical to the two launches; 72 + 8 order B/row instead of
-// 104 + 8 order + 56.
-struct VFirstVecs {
-  const double* s;
-  const double* sq;
-  const double* u[2];
-  VincDev D;
-  double* b[2];     // s u (written)
-  double* xout[2];  // x_1
-  float* d[2];      // d_1
-};
-template <bool C16>
-__global__ __launch_bounds__(BS) void k_vcheb_first(SellDev A, FaceDev fc, const double* __restrict__ val,
-                                                    VFirstVecs v, double c2, const int* ctl, double* part_rr,
-                                                    double* part_bb) {
-  __shared__ double lx[2][VP_W];
-  __shared__ double sh[4];
-  if (ctl[0]) return;
-  auto ystart = [&](int64_t j, double& ya, double& yb) {
-    const double a = v.u[0][j] + 0.0, b = v.u[1][j] + 0.0;
-    double ga, gb;
-    visc_start(v.D, j, a, b, ga, gb);
-    const double q = v.sq[j];
-    ya = q * ga;
-    yb = q * gb;
-  };
-  double rr[2] = {0.0, 0.0}, bb[2] = {0.0, 0.0};
-  auto finish = [&](int c, int64_t row, double ax, double x0, double br) {
-    const double r = br - ax;
-    const double dn = c2 * r;
-    stnt(v.d[c] + row, (float)dn);
-    stnt(v.xout[c] + row, x0 + dn);
-    stnt(v.b[c] + row, br);
-    rr[c] += r * r;
-    bb[c] += br * br;
-  };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    const int32_t items = fc.nf * fc.cpf;
-    int32_t it = (int32_t)blockIdx.x - ((int32_t)gridDim.x - fc.nb);
-    if (fc.nb == items && items >= 8 * 64) {  // XCD-grouped item order (face_rows; the SELL blocks are 8k)
-      const int32_t x = it & 7, q = items >> 3, rem = items & 7;
-      it = x * q + (x < rem ? x : rem) + (it >> 3);
-    }
-    const int32_t lf = it / fc.cpf;
-    const lat::FaceTab F = fc.tab[lf];
-    const int32_t n = fc.n;
-    const int32_t t0 = (it - lf * fc.cpf) * (BS * FACE_RPT), t1 = min(t0 + BS * FACE_RPT, fc.F);
-    const int32_t w0 = max(0, t0 - n), nw = min(fc.F, t1 + n) - w0;
-    // (b = s u of the rows stays in registers for the step: u and s are read once per row)
-    double bt[VP_WK][2];
-#pragma unroll
-    for (int k = 0; k < VP_WK; ++k) {
-      const int32_t w = (int32_t)threadIdx.x + k * BS;
-      bt[k][0] = bt[k][1] = 0.0;
-      if (w < nw) {
-        const int64_t j = F.base + w0 + w;
-        const double a = v.u[0][j] + 0.0, b = v.u[1][j] + 0.0;
-        double ga, gb;
-        visc_start(v.D, j, a, b, ga, gb);
-        const double q = v.sq[j], sr = v.s[j];
-        lx[0][w] = q * ga;
-        lx[1][w] = q * gb;
-        bt[k][0] = sr * a;
-        bt[k][1] = sr * b;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < VP_WK; ++k) {
-      const int32_t w = (int32_t)threadIdx.x + k * BS;
-      const int32_t t = w0 + w;
-      if (w < nw && t >= t0 && t < t1) {
-        int32_t i, j, nb[6];
-        bool in[6];
-        lat::coords(t, n, fc.rinv, i, j);
-        lat::neighbours(F, n, t, i, j, nb, in);
-        double a[7];
-        face_kcoefs(fc, lf, nb, in, a);
-        const int64_t row = F.base + t;
-        double xv[2][7];
-        xv[0][6] = lx[0][w];
-        xv[1][6] = lx[1][w];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          if (in[q]) {
-            const int32_t lw = min(max(nb[q] - F.base - w0, 0), nw - 1);
-            xv[0][q] = lx[0][lw];
-            xv[1][q] = lx[1][lw];
-          } else {
-            ystart(nb[q], xv[0][q], xv[1][q]);
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const double br = bt[k][c];
-          double ax = a[0] * xv[c][6];
-#pragma unroll
-          for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[c][q];
-          finish(c, row, ax, xv[c][6], br);
-        }
-      }
-    }
-  } else {
-    int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    for (int64_t s = s0 + wv; s < s1; s += 4) {
-      const int64_t row = sell_row(A, s, lane);
-      const int64_t rw = row >= 0 ? row : 0;
-      double acc[2] = {0.0, 0.0}, x0[2], br[2];
-      ystart(rw, x0[0], x0[1]);
-      const double sr = v.s[rw];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) br[c] = sr * (v.u[c][rw] + 0.0);
-      const int64_t off = A.off[s];
-      const int w = A.w[s];
-      const int32_t base = (int32_t)(s * 64);
-      for (int k = 0; k < w; ++k) {
-        const int64_t e = off + (int64_t)k * 64 + lane;
-        const double av = ldnt(val + e);
-        double ya, yb;
-        ystart(sell_col<C16>(A, e, base), ya, yb);
-        acc[0] += av * ya;
-        acc[1] += av * yb;
-      }
-      if (row >= 0) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) finish(c, row, acc[c], x0[c], br[c]);
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const double t1 = block_sum(rr[c], sh);
-    const double t2 = block_sum(bb[c], sh);
-    if (threadIdx.x == 0) {
-      part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
-      part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
-    }
   }
 }
 
@@ -2694,12 +2510,14 @@ __global__ void k_asm(int64_t n, const int64_t* __restrict__ ptr, const int32_t*
 // 1-block reduction of nv partial arrays (sum or max) into out[0..nv): the consumers of a producer
 // kernel's partials read one scalar.  RB threads, each with RU independent loads in flight (the
 // partials are L2 / MALL misses; a dependent load chain per thread would take nb / RB round trips).
-// Fixed combination order: deterministic for a given nb.
+// Fixed combination order: deterministic for a given nb.  Block b reduces values b, b + grid, ...: a
+// launch over nv blocks reduces every value at once (the projection's 2 m + 4 dots were 68 reductions
+// in a row in one block, ~150 us), with the same per-value order as a one-block launch.
 constexpr int RB = 1024, RU = 8;
 template <int RB>
 __global__ __launch_bounds__(RB) void k_reduce_t(const double* part, int nb, int stride, int nv, int is_max, double* out) {
   __shared__ double sh[RB / 64];
-  for (int v = 0; v < nv; ++v) {
+  for (int v = blockIdx.x; v < nv; v += gridDim.x) {
     const double* p = part + (int64_t)v * stride;
     double a[RU];
 #pragma unroll
@@ -2757,8 +2575,7 @@ __global__ __launch_bounds__(RB) void k_reduce_conv(const double* part, int nb, 
     }
   }
 }
-// the step's reductions: 1,024 threads (RB); 256 (k_reduce_t<256>, PUCFEM_RED_THREADS=256) schedules on a
-// CU with fewer free wave slots while the dye stream's kernels occupy the chip (measurement knob)
+// the step's reductions: 1,024 threads (RB)
 constexpr auto k_reduce = k_reduce_t<RB>;
 
 template <typename T>

@@ -361,16 +361,13 @@ def test_viscous_chebyshev_post_check(monkeypatch):
 
 
 @pytest.mark.parametrize("refine", [3, 5])
-@pytest.mark.parametrize("knob,key", [("PUCFEM_VISC_PAIR", "visc_step_pairs"), ("PUCFEM_MG_PAIR", "mg_step_pairs"),
-                                      ("PUCFEM_VISC_FIRST", "visc_first_fused")])
+@pytest.mark.parametrize("knob,key", [("PUCFEM_VISC_PAIR", "visc_step_pairs"), ("PUCFEM_MG_PAIR", "mg_step_pairs")])
 def test_step_pairs_equal_single_steps(monkeypatch, refine, knob, key):
     """Two Chebyshev steps in one pass on the face interiors (x_{a+1} in LDS, the skeleton rows in their
     own launches): the viscous solve's (k_vcheb_pair) and the finest multigrid level's smoothing
     (k_cheb_pair) do k_vcheb's / k_cheb's operations row by row, so the production run at L3 / L5 with
     step pairs is bit-identical to the one that runs every step as its own launch."""
     mesh = pf.load_mesh("fine", refine=refine)
-    if knob == "PUCFEM_VISC_FIRST":  # (off by default: a measurement knob)
-        monkeypatch.setenv(knob, "1")
     a = stokes(mesh, tol=S.Tolerances.production())
     monkeypatch.setenv(knob, "0")
     b = stokes(mesh, tol=S.Tolerances.production())

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Parity at HEAD on the GPU box: the full `-m gpu` suite (verbose, per-test time limit), smoke(),
+# then the driver's bench command. Every step has its own time limit; the script stops at the
+# first failure. Usage: tools/gpu_check_head.sh TAG
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-head}
+OUT="gpurun_out/$TAG"
+mkdir -p "$OUT"
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "=== $name rc=$rc" >&2; tail -n 6 "$OUT/$name.out" >&2; tail -n 4 "$OUT/$name.err" >&2
+  if [ $rc -ne 0 ]; then echo "stop after $name" >&2; exit $rc; fi
+}
+step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS}
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+if [ -z "$SKIP_BENCH" ]; then step bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5; fi
