@@ -225,14 +225,18 @@ int pucfem_mixing_index(void* ctx, const double* c, double* out3);
 int pucfem_mixing_index_w(void* ctx, const double* c, const double* w, double* out3);
 
 /* ---- measurement ------------------------------------------------------------------ */
-/* HIP-event timing of each kernel class on the context's stream (bench.py roofline).
-   on: 0 off, 1 every class, 2 class 0 only (the finest-level smoother: the roofline kernel) */
+/* HIP-event timing of each kernel class (bench.py roofline): the events are taken by each launch's own
+   dispatch, on the stream the kernel runs on.  on: 0 off, 1 every class, 2 every class but 5-7 (the
+   classes with a share of the step; the roofline kernel is the largest of them) */
 int pucfem_timing_enable(void* ctx, int32_t on);
 /* kernel classes: 0 = multigrid Chebyshev smoother on the finest level (k_cheb), 1 = CG SpMV+direction
-   (k_cg_dir), 2 = CG update (k_cg_upd), 3 = div/grad (k_div, k_grad_proj), 4 = semi-Lagrangian (k_sl),
+   (k_cg_dir), 2 = CG update (k_cg_upd), 3 = gradient projection (k_grad_proj), 4 = semi-Lagrangian (k_sl),
    5 = multigrid residual on the finest level (k_resid), 6 = restriction from the finest level,
-   7 = prolongation to the finest level (k_transfer), 8 = the semi-Lagrangian second pass (k_sl_slow: general locate
-   and rank count of the rows off the lattice fast path), 9 = the viscous Chebyshev step (k_vcheb) */
+   7 = prolongation to the finest level (k_transfer), 8 = the semi-Lagrangian second pass (k_sl_slow: general
+   locate and rank count of the rows off the lattice fast path), 9 = the viscous Chebyshev step over the whole
+   grid (k_vcheb), 10 = two finest-level smoothing steps (k_cheb_pair), 11 = divergence (k_div), 12 = two
+   viscous Chebyshev steps on the face rows (k_vcheb_pair), 13 = viscous right-hand side and warm start
+   (k_visc_prep), 14 / 15 = the pressure projection's multi-dot and combination passes (k_mdot2, k_pcomb) */
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);

@@ -378,6 +378,7 @@ struct Ctx {
   // iteration count of the last solve per `which` slot (the next solve's first host check): 0 viscous,
   // 1 / 2 the two pressure solves of a step, 3 / 4 standalone viscous / pressure solves (pucfem_solve)
   int last_it[6] = {0, 0, 0, 0, 0, 0};
+  bool solved_before[6] = {false, false, false, false, false, false};  // last_it[which] holds a real count
   bool lds_attr[3] = {false, false, false};  // k_cg_block<NR>: dynamic-LDS attribute set on this device
   double* solve_tmp = nullptr;  // pucfem_solve scratch (4 x nloc): standalone solves never touch the step state
   int* dits = nullptr;  // per-step iteration counts written by single-workgroup solves (no host sync)
@@ -387,6 +388,9 @@ struct Ctx {
   // precomputed inverses -- the reference's np.linalg.solve, factorised once instead of per call
   bool dense = false;
   double *dVinv = nullptr, *dPinv = nullptr;
+  // small literal operators (heat / Poisson, N <= DENSE_MAX): the inverse of the literal operator
+  // (heatEq.py:321 / poisson.py:283 solve with it every step: np.linalg.solve, factorised once here)
+  double* dLitInv = nullptr;
   // small meshes: one StokesColor/StokesFood step captured once into a hipGraph and replayed
   bool graph_mode = false;
   hipGraphExec_t gexec = nullptr;
@@ -452,8 +456,8 @@ struct Ctx {
   // guess of the same solve orthogonalises v against X, appends it and projects the new right-hand
   // side in one multi-dot and one combination pass over X.  h_coef (pinned) receives each guess's
   // coefficients, read at the next guess to track the coordinates of the recent solutions in the
-  // basis (re-seeding a full basis, proj_reseed).  PUCFEM_PROJ_KEEP (measurement knob, 2..8,
-  // default 8): seeds kept.
+  // basis (re-seeding a full basis, proj_reseed).  PUCFEM_PROJ_KEEP (measurement knob, 2..16,
+  // default 16): seeds kept.
   static constexpr int NCOEF = 2 * PROJ_MAX + 4;
   double* h_coef = nullptr;
   ProjT* projXalt[5] = {};
@@ -618,9 +622,16 @@ struct Ctx {
   // partials of a producer kernel -> nv final values in redbuf slot `slot` (one 1-block kernel, then
   // the all-reduce across ranks): consumers read one scalar instead of re-reducing up to MAXB
   // partials in each of their blocks
+  // the dye stream's reductions run in 256-thread blocks: a 1,024-thread block needs 16 free wave slots on
+  // one CU, which the main stream's kernels rarely leave (the k_sl sums waited ~270 us for a CU, r10a)
+  bool red_small = false;
   void launch_reduce(const double* part, int nb, int stride, int nv, bool is_max, double* out) {
-    // one block per value (k_reduce_t); a 256-thread reduce measured equal in round 3 (r8i)
-    hipLaunchKernelGGL(k_reduce, dim3(std::max(1, nv)), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
+    // one block per value (k_reduce_t)
+    if (red_small)
+      hipLaunchKernelGGL(k_reduce_t<256>, dim3(std::max(1, nv)), dim3(256), 0, st, part, nb, stride, nv,
+                         is_max ? 1 : 0, out);
+    else
+      hipLaunchKernelGGL(k_reduce, dim3(std::max(1, nv)), dim3(RB), 0, st, part, nb, stride, nv, is_max ? 1 : 0, out);
   }
   Red reduce_global(double* part, int nb, int nv, bool is_max, int slot) {
     double* buf = redbuf + 8 * slot;
@@ -1436,9 +1447,20 @@ struct Ctx {
     // an iteration = V-cycle, direction, update, convergence test (k_conv): the host checks right
     // after a test, so a solve that converges at a check launches no V-cycle after it.  The first
     // check comes one iteration before the last solve's count (a no-op iteration costs more than a
-    // check's round trip), then every iteration while the solve is short.
-    int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 1 ? last_it[which] - 1 : (last_it[which] ? 1 : 4)));
-    for (bool first = true;; first = false) {
+    // check's round trip), then every iteration while the solve is short.  Past the start-up transient
+    // the projected guess often passes the test itself (0 iterations): when the last solve took at most
+    // one iteration, the host reads the initial test before launching any (one round trip, where an
+    // iteration of early-exiting launches -- the V-cycle's ~70 -- costs ~0.3 ms of GPU time).
+    const bool seen = solved_before[which];
+    solved_before[which] = true;
+    int chunk = std::max(1, std::min(maxit + 1, !seen ? 4 : (last_it[which] > 1 ? last_it[which] - 1 : 1)));
+    bool done0 = false;
+    if (seen && last_it[which] <= 1) {
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      done0 = h_ctl[0] != 0;
+    }
+    for (bool first = true; !done0; first = false) {
       if (!first) marks.clear();  // the previous chunk's samples are flushed
       bmarks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
@@ -1829,6 +1851,11 @@ struct Ctx {
     HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
     {
       StreamSwap sw(st, st_sl);
+      struct SmallRed {  // (reset on unwind)
+        bool& f;
+        explicit SmallRed(bool& x) : f(x) { f = true; }
+        ~SmallRed() { f = false; }
+      } small_red(red_small);
       const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
       div(ux, uy, final_div, false, part_fd, rf);
       if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
@@ -2256,29 +2283,24 @@ void build_mg_host(Ctx& c, SetupClock& clk) {
   // the finest level's power iteration runs on the device at the end of build() (single rank)
   c.lmax_dev = c.world == 1 && !c.host_only;
   {
-    std::vector<std::thread> th;
-    std::vector<std::exception_ptr> err(Lv + 1);
+    ThreadGroup g;  // joined on every exit path; a level's exception reaches the caller from join()
     for (int l = 1; l <= Lv; ++l)
-      th.emplace_back([&c, &err, l] {
-        try {
-          MgLevel& L = c.mg[l];
-          const MgLevel& C = c.mg[l - 1];
-          build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
-          transpose(L.Pr, C.mesh.N, L.R);
-        } catch (...) {
-          err[l] = std::current_exception();
-        }
+      g.spawn([&c, l] {
+        MgLevel& L = c.mg[l];
+        const MgLevel& C = c.mg[l - 1];
+        build_prolongation(C.mesh.N, L.ea, L.eb, L.ord, C.ord, C.dof, L.master_of, L.Pr);
+        transpose(L.Pr, C.mesh.N, L.R);
       });
+    std::exception_ptr e0;
     try {
       for (int l = 0; l <= Lv; ++l)
         c.mg[l].lmax = l == Lv && c.lmax_dev ? lmax_estimate(c.Pp, false, &c.lmax_dinv)
                                              : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
     } catch (...) {
-      err[0] = std::current_exception();
+      e0 = std::current_exception();
     }
-    for (auto& t : th) t.join();
-    for (auto& e : err)
-      if (e) std::rethrow_exception(e);
+    g.join();
+    if (e0) std::rethrow_exception(e0);
   }
   clk.mark("  mg: transfers + lmax estimates");
 }
@@ -2946,6 +2968,13 @@ void build(Ctx& c) {
     require(spd_inverse(Dp, N), "regularised pressure operator is not SPD");
     c.dVinv = c.upload(Dv);
     c.dPinv = c.upload(Dp);
+  }
+  if (literal && !c.dist() && N <= DENSE_MAX && c.prm.solver_path != 1) {
+    std::vector<double> D(N * N, 0.0);
+    for (i64 r = 0; r < N; ++r)
+      for (i64 k = c.Lit.rowptr[r]; k < c.Lit.rowptr[r + 1]; ++k) D[r * N + c.Lit.col[k]] += c.Lit.val[k];
+    require(lu_inverse(D, N), "literal operator is singular");
+    c.dLitInv = c.upload(D);
   }
   if (literal) {
     dsell(c.sLit, c.Lit, c.dLit);
@@ -3653,9 +3682,18 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
         }
     } else if (c.scheme == PUCFEM_HEAT) {
       // heatEq.py:321-325: u = solve(A, u + DT*b*0); reapply_periodic_u; reapply_dirchlect_u
+      const i64 n = c.lp.n_own;
       for (int s = 0; s < nsteps; ++s) {
-        HIPCHK(hipMemcpyAsync(c.litw[8], c.scalar, sizeof(double) * c.lp.n_own, hipMemcpyDeviceToDevice, c.st));
-        const int it = c.bicgstab(c.scalar, c.litw[8], c.prm.rtol_lin, c.prm.maxit_lin);
+        int it = 0;
+        if (c.dLitInv) {  // small mesh: u = A^-1 u (one launch, no host synchronisation)
+          hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, c.st, n,
+                             (const double*)c.dLitInv, (const double*)c.scalar, c.litw[8], (const int*)nullptr);
+          KCHK();
+          std::swap(c.scalar, c.litw[8]);
+        } else {
+          HIPCHK(hipMemcpyAsync(c.litw[8], c.scalar, sizeof(double) * n, hipMemcpyDeviceToDevice, c.st));
+          it = c.bicgstab(c.scalar, c.litw[8], c.prm.rtol_lin, c.prm.maxit_lin);
+        }
         c.bc(c.scalar, nullptr);
         if (stats) {
           std::memset(&stats[s], 0, sizeof(pucfem_step_stats));
@@ -3667,7 +3705,15 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       // poisson.py:283-285: f = solve(A, b)
       HIPCHK(hipMemcpyAsync(c.bh, c.litb.data(), sizeof(double) * c.lp.n_own, hipMemcpyHostToDevice, c.st));
       HIPCHK(hipMemsetAsync(c.scalar, 0, sizeof(double) * c.lp.n_own, c.st));
-      const int it = c.bicgstab(c.scalar, c.bh, c.prm.rtol_lin, c.prm.maxit_lin);
+      int it = 0;
+      if (c.dLitInv) {
+        hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (c.lp.n_own + 3) / 4)), dim3(BS), 0, c.st,
+                           (int64_t)c.lp.n_own, (const double*)c.dLitInv, (const double*)c.bh, c.scalar,
+                           (const int*)nullptr);
+        KCHK();
+      } else {
+        it = c.bicgstab(c.scalar, c.bh, c.prm.rtol_lin, c.prm.maxit_lin);
+      }
       HIPCHK(hipStreamSynchronize(c.st));
       if (stats) {
         std::memset(&stats[0], 0, sizeof(pucfem_step_stats));

@@ -673,9 +673,9 @@ std::vector<float> knn_radius2(const Grid& G, const std::vector<double>& cx, con
     }
   };
   const int nt = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (int w = 0; w < nt; ++w) th.emplace_back(work, T * w / nt, T * (w + 1) / nt);
-  for (auto& h : th) h.join();
+  ThreadGroup g;
+  for (int w = 0; w < nt; ++w) g.spawn([&work, w, nt, T] { work(T * w / nt, T * (w + 1) / nt); });
+  g.join();
   return out;
 }
 
@@ -796,6 +796,60 @@ void transpose(const Csr& A, i64 ncols, Csr& At) {
       At.col[d] = (i32)r;
       At.val[d] = A.val[k];
     }
+}
+
+bool lu_inverse(std::vector<double>& A, i64 n) {
+  // LU with partial pivoting (row-major, in place: P A = L U, unit lower L), then the inverse column by
+  // column: L y = P e_j, U x = y.  The columns are independent -> threads.
+  std::vector<i64> piv(n);
+  for (i64 k = 0; k < n; ++k) {
+    i64 p = k;
+    double best = std::fabs(A[k * n + k]);
+    for (i64 i = k + 1; i < n; ++i)
+      if (std::fabs(A[i * n + k]) > best) best = std::fabs(A[i * n + k]), p = i;
+    if (!(best > 0.0) || !std::isfinite(best)) return false;
+    piv[k] = p;
+    if (p != k)
+      for (i64 j = 0; j < n; ++j) std::swap(A[k * n + j], A[p * n + j]);
+    const double inv = 1.0 / A[k * n + k];
+    const double* rk = A.data() + k * n;
+    parallel_for(n - k - 1, [&](i64 a, i64 b) {
+      for (i64 i = k + 1 + a; i < k + 1 + b; ++i) {
+        double* ri = A.data() + i * n;
+        const double l = ri[k] * inv;
+        ri[k] = l;
+        if (l != 0.0)
+          for (i64 j = k + 1; j < n; ++j) ri[j] -= l * rk[j];
+      }
+    });
+  }
+  // row permutation of the identity: e_j lands in row perm^-1(j)
+  std::vector<i64> perm(n);
+  std::iota(perm.begin(), perm.end(), (i64)0);
+  for (i64 k = 0; k < n; ++k) std::swap(perm[k], perm[piv[k]]);
+  std::vector<double> inv(n * n, 0.0);  // inverse, transposed (column j in row j)
+  parallel_for(n, [&](i64 j0, i64 j1) {
+    std::vector<double> x(n);
+    for (i64 j = j0; j < j1; ++j) {
+      for (i64 i = 0; i < n; ++i) x[i] = perm[i] == j ? 1.0 : 0.0;
+      for (i64 i = 0; i < n; ++i) {  // L (unit diagonal)
+        double s = x[i];
+        const double* ri = A.data() + i * n;
+        for (i64 k = 0; k < i; ++k) s -= ri[k] * x[k];
+        x[i] = s;
+      }
+      for (i64 i = n - 1; i >= 0; --i) {  // U
+        double s = x[i];
+        const double* ri = A.data() + i * n;
+        for (i64 k = i + 1; k < n; ++k) s -= ri[k] * x[k];
+        x[i] = s / ri[i];
+      }
+      std::copy(x.begin(), x.end(), inv.begin() + j * n);
+    }
+  });
+  for (i64 i = 0; i < n; ++i)
+    for (i64 j = 0; j < n; ++j) A[i * n + j] = inv[j * n + i];
+  return true;
 }
 
 bool spd_inverse(std::vector<double>& A, i64 n) {

@@ -3,9 +3,12 @@
 // exercised by the CPU test-suite through a host-only context.
 #pragma once
 #include <cstdint>
+#include <exception>
+#include <memory>
 #include <string>
 #include <algorithm>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "pucfem_lattice.hpp"
@@ -16,6 +19,35 @@ using i32 = int32_t;
 using i64 = int64_t;
 
 // ----------------------------------------------------------------------------- host threading
+// Threads that are joined on every exit path (a failed spawn unwinds through the destructor instead of
+// destroying joinable threads, which would terminate the process) and whose exceptions reach the caller:
+// join() rethrows the first one.
+struct ThreadGroup {
+  std::vector<std::thread> th;
+  std::vector<std::shared_ptr<std::exception_ptr>> err;  // one heap slot per thread (stable while spawning)
+  template <class F>
+  void spawn(F&& f) {
+    auto slot = std::make_shared<std::exception_ptr>();
+    err.push_back(slot);
+    th.emplace_back([slot, f = std::forward<F>(f)]() mutable {
+      try {
+        f();
+      } catch (...) {
+        *slot = std::current_exception();
+      }
+    });
+  }
+  void wait() {
+    for (auto& t : th)
+      if (t.joinable()) t.join();
+  }
+  void join() {
+    wait();
+    for (auto& e : err)
+      if (*e) std::rethrow_exception(*e);
+  }
+  ~ThreadGroup() { wait(); }
+};
 // f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to 64)
 template <class F>
 void parallel_for(i64 n, F&& f) {
@@ -24,9 +56,9 @@ void parallel_for(i64 n, F&& f) {
     f((i64)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  for (int w = 0; w < nt; ++w) th.emplace_back([&, w] { f(n * w / nt, n * (w + 1) / nt); });
-  for (auto& h : th) h.join();
+  ThreadGroup g;
+  for (int w = 0; w < nt; ++w) g.spawn([&, w] { f(n * w / nt, n * (w + 1) / nt); });
+  g.join();
 }
 // f(chunk, r0, r1) over PAR_CHUNKS fixed chunks of [0, n) (independent of the machine's thread
 // count: per-chunk partial sums combined in chunk order are reproducible everywhere)
@@ -41,9 +73,9 @@ void parallel_chunks(i64 n, F&& f) {
     run(0);
     return;
   }
-  std::vector<std::thread> th;
-  for (int w = 0; w < nt; ++w) th.emplace_back(run, w);
-  for (auto& h : th) h.join();
+  ThreadGroup g;
+  for (int w = 0; w < nt; ++w) g.spawn([&run, w] { run(w); });
+  g.join();
 }
 
 struct HostMesh {
@@ -134,6 +166,8 @@ void build_prolongation(i64 Nc, const std::vector<i32>& edge_a, const std::vecto
 void transpose(const Csr& A, i64 ncols, Csr& At);
 // Dense inverse of a (regularised) SPD matrix, row-major n x n, by Cholesky.  Returns false if not SPD.
 bool spd_inverse(std::vector<double>& A, i64 n);
+// general dense inverse (LU with partial pivoting), in place; false when singular
+bool lu_inverse(std::vector<double>& A, i64 n);
 
 // Local view of one rank: owned rows [r0, r1) + sorted ghost list, local column ids.
 struct LocalPlan {

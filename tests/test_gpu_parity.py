@@ -214,19 +214,24 @@ def test_tracers_vs_reference(m, golden):
     sim.close()
 
 
+@pytest.mark.parametrize("path", ["auto", "iterative"])
 @pytest.mark.parametrize("m", ["mesh1", "mesh21", "fine"])
-def test_poisson_vs_reference(m, golden):
-    """poisson.py end to end: ||f_ref - f_hip||_inf < 1e-10 (north_star)."""
+def test_poisson_vs_reference(m, path, golden):
+    """poisson.py end to end: ||f_ref - f_hip||_inf < 1e-10 (north_star).  The small meshes take the dense
+    path by default (the literal operator's inverse, factorised once); "iterative" forces the BiCGStab
+    kernels of the large-mesh path onto them."""
     g = golden(m)
-    f = pf.poisson_solve(pf.load_mesh(m))
+    f = pf.poisson_solve(pf.load_mesh(m), tol=S.Tolerances(solver_path=path))
     np.testing.assert_allclose(f, g["poisson_f"], rtol=0, atol=1e-10)
 
 
+@pytest.mark.parametrize("path", ["auto", "iterative"])
 @pytest.mark.parametrize("m", ["mesh1", "mesh21", "fine"])
-def test_heat_vs_reference(m, golden):
-    """heatEq.py: u after 1, 10, 600 backward-Euler steps, 1e-10 vs the reference."""
+def test_heat_vs_reference(m, path, golden):
+    """heatEq.py: u after 1, 10, 600 backward-Euler steps, 1e-10 vs the reference (dense inverse by
+    default on these meshes, BiCGStab with solver_path="iterative")."""
     g = golden(m)
-    h = pf.HeatSimulation(pf.load_mesh(m), dt=0.02)
+    h = pf.HeatSimulation(pf.load_mesh(m), dt=0.02, tol=S.Tolerances(solver_path=path))
     done = 0
     for k in (1, 10, 600):
         h.step(k - done)

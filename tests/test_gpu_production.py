@@ -1,7 +1,8 @@
 """Parity of the PRODUCTION (large-mesh) code path against the oracle, step by step.
 
-bench.py measures Tolerances.production(): the multi-kernel Jacobi-scaled viscous CG<2> with the
-extrapolated warm start, the multigrid-preconditioned pressure CG with the fp32 V-cycle, the
+bench.py measures Tolerances.production(): the viscous Chebyshev iteration on the Jacobi-scaled A_visc
+(step count from the residual bound, two steps per pass through LDS, the fifth-order extrapolated warm
+start), the multigrid-preconditioned pressure CG with the fp32 V-cycle, the
 pressure guess projected onto a 32-direction basis shared by both solves (re-seeded when full), int16 SELL column deltas and the
 locate-then-rank semi-Lagrangian kernel.  mesh_fine itself takes the small-mesh direct path, so these
 tests run refined meshes (L2 = 17k, L3 = 69k nodes) where none of the small-mesh shortcuts apply, and
