@@ -421,8 +421,6 @@ struct Ctx {
   // buffer are allocated on first use
   bool visc_pair = !(std::getenv("PUCFEM_VISC_PAIR") && std::atoi(std::getenv("PUCFEM_VISC_PAIR")) == 0);
   int64_t visc_pairs = 0;  // pairs launched (pucfem_path_info)
-  double* vp_x[2] = {nullptr, nullptr};
-  float* vp_d[2] = {nullptr, nullptr};
   // step pairs of the finest level's smoothing in the fp32 V-cycle (k_cheb_pair, single rank):
   // PUCFEM_MG_PAIR=0 runs every step as its own k_cheb (a measurement knob); a third x buffer and a second
   // d buffer of the finest level are allocated on first use
@@ -841,51 +839,54 @@ struct Ctx {
     return h_ctl[1];
   }
 
-  // Chebyshev iteration for the Jacobi-scaled viscous system (k_vcheb): y (warm start, overwritten only
-  // through the double buffer) and b as for cg<NR>; the converged iterate is returned in out[] (y itself
-  // or the alternate buffer cg_pb).  Target: the CG's test <r, r> <= tol^2 <b, b>, met through the a-priori
-  // residual bound of the interval (below).
-  // fin (optional, NR = 2): the viscous finish (k_visc_fin: u* = S y, the fp32 increment u* - u) for the
-  // solve's last step to do in place of its x_out; *fin_done tells whether it did
+  // Chebyshev iteration for the Jacobi-scaled viscous system (k_vcheb), both components at once in the
+  // interleaved (dbl2) vectors: y (warm start, overwritten only through the buffers) and b; the converged
+  // iterate is returned in *out (y itself or one of the x buffers).  Target: the CG's test
+  // <r, r> <= tol^2 <b, b> per component, met through the a-priori residual bound of the interval (below).
+  // fin (optional): the viscous finish (k_visc_fin: u* = S y, the fp32 increment u* - u) for the solve's
+  // last step to do in place of its x_out; *fin_done tells whether it did
   struct ViscFin {
     const double* s;
     const double* u[2];
     double* us[2];
     float* inc[2];
   };
-  template <int NR>
-  int vcheb(const DevSell& A, const HFace& hf, const double* val, double* const y[NR], const double* const b[NR],
-            double tol, int maxit, int which, double* out[NR], const ViscFin* vfin = nullptr, bool* fin_done = nullptr) {
+  // the interleaved vectors of the viscous Chebyshev solve (allocated with the operators): the start / x
+  // buffers, b, and the fp32 increments d (a step pair writes its d to the second buffer)
+  dbl2 *vx2[3] = {nullptr, nullptr, nullptr}, *vb2 = nullptr;
+  flt2* vd2[2] = {nullptr, nullptr};
+  // halo of an interleaved vector (both components of each ghost row)
+  void halo2(dbl2* a) {
+    const LocalPlan& P = lp;
+    if (!dist() || (P.send_peer.empty() && P.recv_peer.empty())) return;
+    if (nsend > 0) {
+      hipLaunchKernelGGL(k_pack<dbl2>, dim3(grid_ew(nsend)), dim3(BS), 0, st, nsend, dsend, (const dbl2*)a,
+                         (const dbl2*)nullptr, reinterpret_cast<dbl2*>(dsendbuf));
+      KCHK();
+    }
+    comm->group_start();
+    for (size_t k = 0; k < P.send_peer.size(); ++k)
+      comm->send(dsendbuf + 2 * P.send_off[k], 2 * P.send_cnt[k], P.send_peer[k], st);
+    for (size_t k = 0; k < P.recv_peer.size(); ++k)
+      comm->recv(reinterpret_cast<double*>(a + P.n_own + P.recv_off[k]), 2 * P.recv_cnt[k], P.recv_peer[k], st);
+    comm->group_end(st);
+  }
+  int vcheb(const DevSell& A, const HFace& hf, const double* val, dbl2* y, const dbl2* b, double tol, int maxit,
+            int which, dbl2** out, const ViscFin* vfin = nullptr, bool* fin_done = nullptr) {
+    constexpr int NR = 2;
     if (fin_done) *fin_done = false;
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
-    double* xa[NR];
-    double* xb[NR];
-    double* xc[NR];  // step pairs: x_{a+2} (k_vcheb_pair)
-    float* dcur[NR];  // the fp32 increments d (in place for single steps)
-    float* dalt[NR];  // step pairs: d_{a+2}
-    // step pairs (k_vcheb_pair): NR = 2, one rank, a face part of lattice size <= VP_HALO
-    const bool pairs = visc_pair && NR == 2 && !dist() && hf.items > 0 && fc.n <= VP_HALO &&
+    // step pairs (k_vcheb_pair): one rank, a face part of lattice size <= VP_HALO
+    const bool pairs = visc_pair && !dist() && hf.items > 0 && fc.n <= VP_HALO &&
                        nb_for(A.nslices) + hf.items <= MAXB;  // (the check's partials of both halves)
-    if (pairs && !vp_x[0]) {
-      for (int c = 0; c < 2; ++c) {
-        vp_x[c] = dalloc<double>(nloc);
-        vp_d[c] = dalloc<float>(nloc);
-      }
-    }
-    for (int c = 0; c < NR; ++c) {
-      xa[c] = y[c];
-      xb[c] = cg_pb[c];
-      xc[c] = pairs ? vp_x[c] : nullptr;
-      dcur[c] = reinterpret_cast<float*>(cg_pa[c]);  // fp32 increments in the fp64 work vector
-      dalt[c] = pairs ? vp_d[c] : nullptr;
-    }
-    auto halo_x = [&](double* const* x) {
-      if (NR == 2) halo(x[0], x[1]);
-      else halo(x[0]);
-    };
-    halo_x(xa);
+    dbl2* xa = y;
+    dbl2* xb = vx2[1];
+    dbl2* xc = vx2[2];  // step pairs: x_{a+2}
+    flt2* dcur = vd2[0];  // the fp32 increments d (in place for single steps)
+    flt2* dalt = vd2[1];  // step pairs: d_{a+2}
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    halo2(xa);
     // the interval [visc_lo, 1 + visc_R]: theta its centre, delta its half-width
     const double hi = 1.0 + visc_R, lo = visc_lo;
     const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo), sigma = theta / delta, tol2 = tol * tol;
@@ -894,14 +895,14 @@ struct Ctx {
                          32.0 * NR * (double)A.own();
     // One step: x_out = x_in + d, d = c1 d + c2 (b - A^ x_in); the first step also yields |r_0| and |b|.
     auto step = [&](int it, double c1, double c2, bool check = false, bool fin = false) {
-      ChebVecs<NR> v{};
-      for (int c = 0; c < NR; ++c) {
-        v.xin[c] = xa[c];
-        v.xout[c] = xb[c];
-        v.b[c] = b[c];
-        v.d[c] = dcur[c];
-        if (fin) {
-          v.s = vfin->s;
+      ChebVecs2 v{};
+      v.xin = xa;
+      v.xout = xb;
+      v.b = b;
+      v.d = dcur;
+      if (fin) {
+        v.s = vfin->s;
+        for (int c = 0; c < NR; ++c) {
           v.u[c] = vfin->u[c];
           v.us[c] = vfin->us[c];
           v.inc[c] = vfin->inc[c];
@@ -914,7 +915,7 @@ struct Ctx {
       // check: the post-check's |r_it|^2 partials (part_c)
       double* pr = it == 0 ? part_a : (check ? part_c : (double*)nullptr);
       with_c16(A, [&](auto c16) {
-        klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<NR, decltype(c16)::value>, dim3(nb),
+        klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<decltype(c16)::value>, dim3(nb),
                 dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, pr, pb, r0);
       });
       KCHK();
@@ -922,72 +923,69 @@ struct Ctx {
         algo_bytes += 12.0 * NR * (double)A.own();  // + s, u read and u*, the increment written - d, x_out
         return;
       }
-      halo_x(xb);
-      for (int c = 0; c < NR; ++c) std::swap(xa[c], xb[c]);
+      halo2(xb);
+      std::swap(xa, xb);
     };
     // Two steps a, a + 1 in three launches: the skeleton rows' step a (k_vcheb on the SELL part alone),
     // both steps on the face interiors (k_vcheb_pair: x_{a+1} in LDS), the skeleton rows' step a + 1.
     // check: the |r_{a+1}|^2 partials of both halves in part_c (SELL blocks first); fin: step a + 1 is
-    // the solve's last and writes u* and the increment.  Returns the partial count.
+    // the solve's last and writes u* and the increment.
     const int nbs = nb_for(A.nslices);
     const double bytes_sk = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                             32.0 * NR * (double)(A.own() - hf.rows);
     auto pair_step = [&](double c1a, double c2a, double c1b, double c2b, bool check, bool fin) {
-      if constexpr (NR == 2) {
-        FaceDev fs = fc;
-        fs.nb = 0;
-        ChebVecs<NR> v1{}, v2{};
-        VPairVecs p{};
+      FaceDev fs = fc;
+      fs.nb = 0;
+      ChebVecs2 v1{}, v2{};
+      VPairVecs p{};
+      v1.xin = xa;
+      v1.xout = xb;
+      v1.b = b;
+      v1.d = dcur;
+      v2.xin = xb;
+      v2.xout = xc;
+      v2.b = b;
+      v2.d = dcur;
+      v2.dout = dalt;
+      p.xa = xa;
+      p.xb = xb;
+      p.xc = xc;
+      p.b = b;
+      p.da = dcur;
+      p.dc = dalt;
+      if (fin) {
+        v2.s = p.s = vfin->s;
         for (int c = 0; c < NR; ++c) {
-          v1.xin[c] = xa[c];
-          v1.xout[c] = xb[c];
-          v1.b[c] = b[c];
-          v1.d[c] = dcur[c];
-          v2.xin[c] = xb[c];
-          v2.xout[c] = xc[c];
-          v2.b[c] = b[c];
-          v2.d[c] = dcur[c];
-          v2.dout[c] = dalt[c];
-          p.xa[c] = xa[c];
-          p.xb[c] = xb[c];
-          p.xc[c] = xc[c];
-          p.b[c] = b[c];
-          p.da[c] = dcur[c];
-          p.dc[c] = dalt[c];
-          if (fin) {
-            v2.s = p.s = vfin->s;
-            v2.u[c] = p.u[c] = vfin->u[c];
-            v2.us[c] = p.us[c] = vfin->us[c];
-            v2.inc[c] = p.inc[c] = vfin->inc[c];
-          }
-        }
-        // face rows: x_a, b, d_a read, x_{a+2}, d_{a+2} written (fin: + s, u read, u*, the increment
-        // written - x, d), x_{a+1} written at the rows next to the skeleton (3 (n - 3) per face)
-        const double bnd_rows = fc.n > 3 ? 3.0 * (fc.n - 3) * (double)fc.nf : 0.0;
-        const double bytes_f = (32.0 * NR + (fin ? 12.0 * NR : 0.0)) * (double)hf.rows + 8.0 * NR * bnd_rows;
-        const double fin_sk = fin ? 12.0 * NR * (double)(A.own() - hf.rows) : 0.0;
-        double* pc = check ? part_c : nullptr;
-        with_c16(A, [&](auto c16) {
-          klaunch(-1, bytes_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a,
-                  c2a, 0, (const int*)ctl, (double*)nullptr, (double*)nullptr, RedOut{});
-          KCHK();
-          klaunch(12, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
-                  (int32_t)nbs);
-          KCHK();
-          klaunch(-1, bytes_sk + fin_sk, k_vcheb<NR, decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
-                  c1b, c2b, 0, (const int*)ctl, pc, (double*)nullptr, RedOut{});
-          KCHK();
-        });
-        ++visc_pairs;
-        if (fin) return;
-        for (int c = 0; c < NR; ++c) {  // x_{a+2} is current; x_a, x_{a+1} are free
-          double* t = xa[c];
-          xa[c] = xc[c];
-          xc[c] = xb[c];
-          xb[c] = t;
-          std::swap(dcur[c], dalt[c]);
+          v2.u[c] = p.u[c] = vfin->u[c];
+          v2.us[c] = p.us[c] = vfin->us[c];
+          v2.inc[c] = p.inc[c] = vfin->inc[c];
         }
       }
+      // face rows: x_a, b, d_a read, x_{a+2}, d_{a+2} written (fin: + s, u read, u*, the increment
+      // written - x, d), x_{a+1} written at the rows next to the skeleton (3 (n - 3) per face)
+      const double bnd_rows = fc.n > 3 ? 3.0 * (fc.n - 3) * (double)fc.nf : 0.0;
+      const double bytes_f = (32.0 * NR + (fin ? 12.0 * NR : 0.0)) * (double)hf.rows + 8.0 * NR * bnd_rows;
+      const double fin_sk = fin ? 12.0 * NR * (double)(A.own() - hf.rows) : 0.0;
+      double* pc = check ? part_c : nullptr;
+      with_c16(A, [&](auto c16) {
+        klaunch(-1, bytes_sk, k_vcheb<decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a, c2a, 0,
+                (const int*)ctl, (double*)nullptr, (double*)nullptr, RedOut{});
+        KCHK();
+        klaunch(12, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
+                (int32_t)nbs);
+        KCHK();
+        klaunch(-1, bytes_sk + fin_sk, k_vcheb<decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
+                c1b, c2b, 0, (const int*)ctl, pc, (double*)nullptr, RedOut{});
+        KCHK();
+      });
+      ++visc_pairs;
+      if (fin) return;
+      // x_{a+2} is current; x_a, x_{a+1} are free
+      dbl2* t = xa;
+      xa = xc;
+      xc = xb;
+      xb = t;
+      std::swap(dcur, dalt);
     };
     // Step 0 gives r_0 = b - A^ x_0.  The residual polynomial of the Chebyshev iteration on an interval
     // holding the spectrum is bounded by 1 / T_k(sigma) there, so |r_k| <= |r_0| / T_k(sigma): the step
@@ -1070,14 +1068,14 @@ struct Ctx {
       K = std::max(K, k);
     }
     if (pass0 && done == 1) {
-      for (int c = 0; c < NR; ++c) out[c] = y[c];
+      *out = y;
       last_it[which] = 0;
       return 0;
     }
     if (done < K) {
       // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check; with
       // step pairs it is the second step of a pair when an even number of steps is left
-      const bool fuse = vfin != nullptr && NR == 2;
+      const bool fuse = vfin != nullptr;
       const bool last_pair = pairs && (K - done) % 2 == 0;
       advance(last_pair ? K - 2 : K - 1);
       int kc, nck;
@@ -1115,7 +1113,7 @@ struct Ctx {
       }
     }
     advance(K);  // (steps beyond K, already launched, only reduce the residual further)
-    for (int c = 0; c < NR; ++c) out[c] = xa[c];  // x_done, done >= K
+    *out = xa;  // x_done, done >= K
     last_it[which] = K;
     return done;
   }
@@ -1560,52 +1558,69 @@ struct Ctx {
     VincDev vd{};
     vd.order = ext ? std::min(have_vinc, visc_extrap) : 0;
     for (int k = 0; k < 2 * VINC_MAX; ++k) vd.d[k] = dvinc[k];
+    const bool proj = proj_k_visc > 0;
+    // the Chebyshev iteration (interleaved vectors); the CG (SoA vectors) when the interval is too wide, the
+    // post-check failed, the operator is small enough for the one-workgroup CG, or the projection guess of
+    // the viscous solve is on (a measurement knob whose bases hold SoA vectors)
+    const bool cheb = visc_solver == 0 && visc_R < 0.25 && !proj &&
+                      !(!dist() && block_cg && !fVisc.items && dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
     // (k_visc_prep folded into the solve's first step was measured 9 % slower in round 3, r9i: the window
     // recomputes the start's 64 B/row of inputs on 25 % more rows, so the fusion saved no bytes)
     // u, s, sq, the increments read; b, y written
-    klaunch(13, (64.0 + 8.0 * vd.order) * (double)n, k_visc_prep, dim3(grid_ew(n)), dim3(BS), (int64_t)n,
-            (const double*)dsv, (const double*)dsqv, (const double*)ux, (const double*)uy, bvx, bvy, yvx, yvy, vd);
+    const double prep_bytes = (64.0 + 8.0 * vd.order) * (double)n;
+    if (cheb)
+      klaunch(13, prep_bytes, k_visc_prep<true>, dim3(grid_ew(n)), dim3(BS), (int64_t)n, (const double*)dsv,
+              (const double*)dsqv, (const double*)ux, (const double*)uy, reinterpret_cast<double*>(vb2),
+              (double*)nullptr, reinterpret_cast<double*>(vx2[0]), (double*)nullptr, vd);
+    else
+      klaunch(13, prep_bytes, k_visc_prep<false>, dim3(grid_ew(n)), dim3(BS), (int64_t)n, (const double*)dsv,
+              (const double*)dsqv, (const double*)ux, (const double*)uy, bvx, bvy, yvx, yvy, vd);
     KCHK();
-    double* y[2] = {yvx, yvy};
-    const double* b[2] = {bvx, bvy};
-    const bool proj = proj_k_visc > 0;
-    if (proj) {  // the warm start u^n is replaced by the projection onto earlier solutions
-      project_guess(3, bvx, yvx);
-      project_guess(4, bvy, yvy);
-    }
-    double* yo[2] = {yvx, yvy};  // the converged iterate (the Chebyshev double buffer may hold it)
-    const bool cheb = visc_solver == 0 && visc_R < 0.25 && !(!dist() && block_cg && !fVisc.items &&
-                                                             dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
     // with the extrapolated start the solve's last Chebyshev step also does k_visc_fin's work
     const int last = 2 * (visc_extrap - 1);
     bool fin_done = false;
-    ViscFin vf{};
-    const bool fuse = ext && !proj && visc_fuse_fin;
-    if (fuse) vf = ViscFin{dsv, {ux, uy}, {usx, usy}, {dvinc[last], dvinc[last + 1]}};
     if (cheb) {
-      iters = vcheb<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0, yo, fuse ? &vf : nullptr, &fin_done);
+      ViscFin vf{};
+      const bool fuse = ext && visc_fuse_fin;
+      if (fuse) vf = ViscFin{dsv, {ux, uy}, {usx, usy}, {dvinc[last], dvinc[last + 1]}};
+      dbl2* yo = vx2[0];  // the converged iterate (one of the solve's buffers)
+      iters = vcheb(dP, fVisc, dKv, vx2[0], vb2, prm.rtol_visc, prm.maxit_visc, 0, &yo, fuse ? &vf : nullptr,
+                    &fin_done);
+      if (!fin_done) {  // u* = S y (and the increment)
+        algo_bytes += (ext ? 64.0 : 40.0) * (double)n;  // s, y (, u) read; u* (, the fp32 increment) written
+        hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, (int64_t)n, (const double*)dsv,
+                           (const dbl2*)yo, (const double*)ux, (const double*)uy, usx, usy,
+                           ext ? dvinc[last] : (float*)nullptr, ext ? dvinc[last + 1] : (float*)nullptr);
+      }
     } else {
+      double* y[2] = {yvx, yvy};
+      const double* b[2] = {bvx, bvy};
+      if (proj) {  // the warm start u^n is replaced by the projection onto earlier solutions
+        project_guess(3, bvx, yvx);
+        project_guess(4, bvy, yvy);
+      }
       iters = cg<2>(dP, fVisc, dKv, y, b, prm.rtol_visc, prm.maxit_visc, 0);
-    }
-    if (proj) {
-      project_update(3, yo[0]);
-      project_update(4, yo[1]);
+      if (proj) {
+        project_update(3, yvx);
+        project_update(4, yvy);
+      }
+      if (ext) {
+        algo_bytes += 64.0 * (double)n;  // s, y, u read; u*, the fp32 increment written
+        hipLaunchKernelGGL(k_visc_fin_soa, dim3(grid_ew(n)), dim3(BS), 0, st, (int64_t)n, (const double*)dsv,
+                           (const double*)yvx, (const double*)yvy, (const double*)ux, (const double*)uy, usx, usy,
+                           dvinc[last], dvinc[last + 1]);
+      } else {
+        algo_bytes += 40.0 * (double)n;
+        hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
+                           (const int32_t*)nullptr);
+      }
     }
     if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
-      if (!fin_done) {
-        algo_bytes += 64.0 * (double)n;  // s, y, u read; u*, the fp32 increment written
-        hipLaunchKernelGGL(k_visc_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, dsv, yo[0], yo[1], ux, uy, usx, usy,
-                           dvinc[last], dvinc[last + 1]);
-      }
       for (int k = last; k >= 2; k -= 2) {
         std::swap(dvinc[k], dvinc[k - 2]);
         std::swap(dvinc[k + 1], dvinc[k - 1]);
       }
       have_vinc = std::min(have_vinc + 1, visc_extrap);
-    } else {
-      algo_bytes += 40.0 * (double)n;
-      hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yo[0], yo[1], usx, usy,
-                         (const int32_t*)nullptr);
     }
     KCHK();
     bc(usx, usy);
@@ -3073,6 +3088,11 @@ void build(Ctx& c) {
     c.cg_pb[q] = c.dalloc<double>(c.nloc);
     c.cg_q[q] = c.dalloc<double>(c.nloc);
   }
+  if (stokes && !c.dense) {  // the viscous Chebyshev solve's interleaved vectors
+    for (auto& x : c.vx2) x = c.dalloc<dbl2>(c.nloc);
+    c.vb2 = c.dalloc<dbl2>(c.nloc);
+    for (auto& d : c.vd2) d = c.dalloc<flt2>(c.nloc);
+  }
   // 6 MAXB: the recurrence CG direction kernel writes 3 dots per right-hand side
   for (double** f : {&c.part_a, &c.part_b, &c.part_c, &c.part_d}) *f = c.dalloc<double>(6 * MAXB);
   c.part_sl = c.dalloc<double>(3 * SLB);
@@ -3857,8 +3877,8 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
       }
       HIPCHK(hipMemcpyAsync(s0, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
       HIPCHK(hipMemcpyAsync(s1, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-      hipLaunchKernelGGL(k_visc_prep, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s1, c.bvx,
-                         c.bvy, c.yvx, c.yvy, VincDev{});
+      hipLaunchKernelGGL(k_visc_prep<false>, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s1,
+                         c.bvx, c.bvy, c.yvx, c.yvy, VincDev{});
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
       const double* bb[2] = {c.bvx, c.bvy};

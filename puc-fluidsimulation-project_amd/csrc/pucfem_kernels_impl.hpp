@@ -831,47 +831,59 @@ __global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, con
 // d, the Chebyshev increment, is stored in fp32: x_out = x_in + d takes the fp64 value, and the next
 // step's d = c1 d + c2 r only damps the stored one (c1 < 1), so the rounding perturbs the polynomial by
 // ~1e-7 of a shrinking correction -- 16 of the 80 B/row saved
-template <int NR>
-struct ChebVecs {
-  const double* xin[NR];
-  double* xout[NR];
-  const double* b[NR];
-  float* d[NR];
+// The solver's vectors interleave the x and y components of u (dbl2: one 16-B gather per neighbour where
+// the two components were two 8-B gathers; round 4 lab, tools/vlayout_lab.hip: the face-row step 215 ->
+// 170 us warm, 252 -> 221 us cold at L7 size); u and u* themselves stay SoA.
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef float flt2 __attribute__((ext_vector_type(2)));
+struct ChebVecs2 {
+  const dbl2* xin;
+  dbl2* xout;
+  const dbl2* b;
+  const flt2* d;
+  // non-null: the new d goes here instead of in place (the skeleton half of a step pair, k_vcheb_pair)
+  flt2* dout;
   // the solve's last step with k_visc_fin folded in (us[0] non-null): instead of d and x_out it writes
   // u* = s x_out and the fp32 increment u* - u (the same operations as k_visc_fin: bit-identical)
   const double* s;
-  const double* u[NR];
-  double* us[NR];
-  float* inc[NR];
-  // non-null: the new d goes here instead of in place (the skeleton half of a step pair, k_vcheb_pair)
-  float* dout[NR];
+  const double* u[2];
+  double* us[2];
+  float* inc[2];
 };
-template <int NR, bool C16>
-__global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs<NR> v,
+template <bool C16>
+__global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs2 v,
                                               double c1, double c2, int first, const int* ctl, double* part_rr,
                                               double* part_bb, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   if (ctl[0]) return;
-  double rr[NR], bb[NR];
-#pragma unroll
-  for (int c = 0; c < NR; ++c) rr[c] = bb[c] = 0.0;
+  double rr[2] = {0.0, 0.0}, bb[2] = {0.0, 0.0};
   const bool fin = v.us[0] != nullptr;
-  auto finish = [&](int c, int64_t row, double ax, double x0, double br, double dr) {
-    const double r = br - ax;
-    const double dn = first ? c2 * r : c1 * dr + c2 * r;
+  flt2* dout = v.dout ? v.dout : const_cast<flt2*>(v.d);
+  // row: r = b - A^ x (both components), d = c1 d + c2 r, x_out = x + d
+  auto finish = [&](int64_t row, dbl2 ax, dbl2 x0, dbl2 br, flt2 dr) {
+    const double r0 = br.x - ax.x, r1 = br.y - ax.y;
+    const double dn0 = first ? c2 * r0 : c1 * (double)dr.x + c2 * r0;
+    const double dn1 = first ? c2 * r1 : c1 * (double)dr.y + c2 * r1;
     if (fin) {
-      const double a = v.s[row] * (x0 + dn);
-      stnt(v.us[c] + row, a);
-      stnt(v.inc[c] + row, (float)(a - v.u[c][row]));
+      const double s = v.s[row];
+      const double a0 = s * (x0.x + dn0), a1 = s * (x0.y + dn1);
+      stnt(v.us[0] + row, a0);
+      stnt(v.us[1] + row, a1);
+      stnt(v.inc[0] + row, (float)(a0 - v.u[0][row]));
+      stnt(v.inc[1] + row, (float)(a1 - v.u[1][row]));
     } else {
-      stnt((v.dout[c] ? v.dout[c] : v.d[c]) + row, (float)dn);
-      stnt(v.xout[c] + row, x0 + dn);
+      const flt2 dn = {(float)dn0, (float)dn1};
+      const dbl2 xo = {x0.x + dn0, x0.y + dn1};
+      stnt(dout + row, dn);
+      stnt(v.xout + row, xo);
     }
-    rr[c] += r * r;
-    bb[c] += br * br;
+    rr[0] += r0 * r0;
+    rr[1] += r1 * r1;
+    bb[0] += br.x * br.x;
+    bb[1] += br.y * br.y;
   };
   if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    constexpr int K = face_k(NR == 1 ? 4 : PUCFEM_VCHEB_K);
+    constexpr int K = face_k(PUCFEM_VCHEB_K);
     face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
@@ -882,29 +894,27 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
       double a[K][7];
 #pragma unroll
       for (int r = 0; r < K; ++r) face_kcoefs(fc, lf, nb[r], in[r], a[r]);
-      double xv[K][NR][7], bv[K][NR], dv[K][NR];
+      dbl2 xv[K][7], bv[K];
+      flt2 dv[K];
 #pragma unroll
       for (int r = 0; r < K; ++r) {
         const int64_t row = F.base + t[r];
+        xv[r][6] = v.xin[row];
+        bv[r] = v.b[row];
+        dv[r] = first ? flt2{0.0f, 0.0f} : v.d[row];
 #pragma unroll
-        for (int c = 0; c < NR; ++c) {
-          xv[r][c][6] = v.xin[c][row];
-          bv[r][c] = v.b[c][row];
-          dv[r][c] = first ? 0.0 : (double)v.d[c][row];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) xv[r][c][k] = v.xin[c][nb[r][k]];
-        }
+        for (int k = 0; k < 6; ++k) xv[r][k] = v.xin[nb[r][k]];
       }
 #pragma unroll
       for (int r = 0; r < K; ++r) {
         if (!ok[r]) continue;
+        double ax0 = a[r][0] * xv[r][6].x, ax1 = a[r][0] * xv[r][6].y;
 #pragma unroll
-        for (int c = 0; c < NR; ++c) {
-          double ax = a[r][0] * xv[r][c][6];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) ax += a[r][1 + k] * xv[r][c][k];
-          finish(c, F.base + t[r], ax, xv[r][c][6], bv[r][c], dv[r][c]);
+        for (int k = 0; k < 6; ++k) {
+          ax0 += a[r][1 + k] * xv[r][k].x;
+          ax1 += a[r][1 + k] * xv[r][k].y;
         }
+        finish(F.base + t[r], dbl2{ax0, ax1}, xv[r][6], bv[r], dv[r]);
       }
     });
   } else {
@@ -914,14 +924,9 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t row = sell_row(A, s, lane);
       const int64_t rw = row >= 0 ? row : 0;
-      double acc[NR], x0[NR], br[NR], dr[NR];
-#pragma unroll
-      for (int c = 0; c < NR; ++c) {
-        x0[c] = v.xin[c][rw];
-        br[c] = v.b[c][rw];
-        dr[c] = first ? 0.0 : (double)v.d[c][rw];
-        acc[c] = 0.0;
-      }
+      const dbl2 x0 = v.xin[rw], br = v.b[rw];
+      const flt2 dr = first ? flt2{0.0f, 0.0f} : v.d[rw];
+      double acc0 = 0.0, acc1 = 0.0;
       const int64_t off = A.off[s];
       const int w = A.w[s];
       const int32_t base = (int32_t)(s * 64);
@@ -938,34 +943,32 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
           }
 #pragma unroll
           for (int k = 0; k < WN; ++k) {
-#pragma unroll
-            for (int c = 0; c < NR; ++c) acc[c] += av[k] * v.xin[c][cj[k]];
+            const dbl2 xj = v.xin[cj[k]];
+            acc0 += av[k] * xj.x;
+            acc1 += av[k] * xj.y;
           }
         } else {
           for (int k = 0; k < w; ++k) {
             const int64_t e = off + (int64_t)k * 64 + lane;
             const double av = ldnt(val + e);
-            const int32_t j = sell_col<C16>(A, e, base);
-#pragma unroll
-            for (int c = 0; c < NR; ++c) acc[c] += av * v.xin[c][j];
+            const dbl2 xj = v.xin[sell_col<C16>(A, e, base)];
+            acc0 += av * xj.x;
+            acc1 += av * xj.y;
           }
         }
       });
-      if (row >= 0) {
-#pragma unroll
-        for (int c = 0; c < NR; ++c) finish(c, row, acc[c], x0[c], br[c], dr[c]);
-      }
+      if (row >= 0) finish(row, dbl2{acc0, acc1}, x0, br, dr);
     }
   }
   if (!part_rr) return;  // steps after the first: no residual norms needed (the step count is known)
 #pragma unroll
-  for (int c = 0; c < NR; ++c) {
+  for (int c = 0; c < 2; ++c) {
     const double t1 = block_sum(rr[c], sh);
     const double t2 = part_bb ? block_sum(bb[c], sh) : 0.0;
     if (threadIdx.x == 0) {
-      if (ro.out) {  // fused reduction: |r_0|^2 values 0 .. NR-1, |b|^2 values NR .. 2 NR - 1 of part_rr
+      if (ro.out) {  // fused reduction: |r_0|^2 values 0 .. 1, |b|^2 values 2 .. 3 of part_rr
         red_part(ro, part_rr, c, t1);
-        red_part(ro, part_rr, NR + c, t2);
+        red_part(ro, part_rr, 2 + c, t2);
       } else {
         part_rr[(int64_t)c * MAXB + blockIdx.x] = t1;
         if (part_bb) part_bb[(int64_t)c * MAXB + blockIdx.x] = t2;
@@ -975,24 +978,20 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
   red_finish(ro, part_rr, sh);
 }
 
-// Two Chebyshev steps of the viscous solve (steps a and a + 1, both right-hand sides) on the face
-// interiors in one pass: temporal blocking with the intermediate iterate in LDS.  A block owns one work
-// item (BS * FACE_RPT consecutive rows of one face); it runs step a on its rows and on the in-face
-// neighbours of its rows outside them (every in-face neighbour is within n - 1 offsets, so the window
-// [t0 - n, t1 + n) holds them: ~25 % redundant rows at L7), keeps x_{a+1} in LDS and runs step a + 1 on its
-// own rows from there.  The skeleton rows' x_{a+1} come from the SELL-only launch of step a that precedes
-// this one (k_vcheb with nb = 0); the SELL-only launch of step a + 1 that follows reads x_{a+1} at the face
-// rows next to the skeleton, which this kernel writes (xb at the boundary rows).  The operations per row
-// are k_vcheb's (same stencil order, d rounded to fp32 between the steps), so the result is the same as
-// two k_vcheb steps.  x_a, b, d_a are read and x_{a+2}, d_{a+2} written once: 64 B/row for two steps
-// instead of 128 (d_{a+2} goes to a second buffer: neighbouring blocks still read d_a in their windows).
+// Step pairs (temporal blocking through LDS): a block owns one work item (BS * FACE_RPT consecutive rows of
+// one face) and runs step a on its rows and on their in-face neighbours (every in-face neighbour of lattice
+// row t lies within n - 1 offsets of t: the window [t0 - n, t1 + n)), keeping x_{a+1} in LDS, then step
+// a + 1 on its own rows.  The skeleton rows run their two steps in k_vcheb launches (SELL part only) before
+// and after; the face kernel writes x_{a+1} at its rows next to the skeleton, which the second one gathers.
+// Row for row k_vcheb's operations in k_vcheb's order (d rounded to fp32 between the steps): bit-identical
+// to two single steps.
 struct VPairVecs {
-  const double* xa[2];  // x_a (every row)
-  double* xb[2];        // x_{a+1}: read at skeleton rows, written at the face rows next to the skeleton
-  double* xc[2];        // x_{a+2}
-  const double* b[2];
-  const float* da[2];   // d_a
-  float* dc[2];         // d_{a+2}
+  const dbl2* xa;  // x_a (every row)
+  dbl2* xb;        // x_{a+1}: read at skeleton rows, written at the face rows next to the skeleton
+  dbl2* xc;        // x_{a+2}
+  const dbl2* b;
+  const flt2* da;  // d_a
+  flt2* dc;        // d_{a+2}
   // the solve's last step (us[0] non-null): u* = s x_{a+2} and the fp32 increment instead of xc, dc
   const double* s;
   const double* u[2];
@@ -1007,14 +1006,9 @@ constexpr int VP_WK = (VP_W + BS - 1) / BS;
 #endif
 constexpr int VP_G = PUCFEM_VP_G;  // rows of a thread loaded together (compile-time: an A/B knob)
 static_assert(VP_WK % VP_G == 0, "the window rows of a thread go in groups");
-#ifdef PUCFEM_VP_WPE
-#define PUCFEM_VP_ATTR __attribute__((amdgpu_waves_per_eu(PUCFEM_VP_WPE, 8)))
-#else
-#define PUCFEM_VP_ATTR
-#endif
-__global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
+__global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
                                                    double c2b, const int* ctl, double* part_rr, int32_t part_off) {
-  __shared__ double lx[2][VP_W];
+  __shared__ dbl2 lx[VP_W];
   __shared__ double sh[4];
   if (ctl[0]) return;
   const int32_t items = fc.nf * fc.cpf;
@@ -1032,15 +1026,16 @@ __global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VP
   // step a on the window; b and the fp32 d_{a+1} of the rows stay in registers for step a + 1.  Rows
   // go in groups of VP_G with every load of the group first (k_vcheb's row groups); a row past the
   // window is clamped to the window's first row (a valid address; not stored)
-  double bt[VP_WK][2];
-  float dt[VP_WK][2];
+  dbl2 bt[VP_WK];
+  flt2 dt[VP_WK];
 #pragma unroll
   for (int k0 = 0; k0 < VP_WK; k0 += VP_G) {
     if (k0 * BS >= nw) break;
     int32_t nb[VP_G][6];
     bool in[VP_G][6], ok[VP_G];
     int64_t row[VP_G];
-    double xv[VP_G][2][7], br[VP_G][2], dr[VP_G][2];
+    dbl2 xv[VP_G][7], br[VP_G];
+    flt2 dr[VP_G];
 #pragma unroll
     for (int r = 0; r < VP_G; ++r) {
       const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
@@ -1050,43 +1045,40 @@ __global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VP
       lat::coords(t, n, fc.rinv, i, j);
       lat::neighbours(F, n, t, i, j, nb[r], in[r]);
       row[r] = F.base + t;
+      xv[r][6] = v.xa[row[r]];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        xv[r][c][6] = v.xa[c][row[r]];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) xv[r][c][q] = v.xa[c][nb[r][q]];
-        br[r][c] = v.b[c][row[r]];
-        dr[r][c] = (double)v.da[c][row[r]];
-      }
+      for (int q = 0; q < 6; ++q) xv[r][q] = v.xa[nb[r][q]];
+      br[r] = v.b[row[r]];
+      dr[r] = v.da[row[r]];
     }
 #pragma unroll
     for (int r = 0; r < VP_G; ++r) {
       double a[7];
       face_kcoefs(fc, lf, nb[r], in[r], a);
       const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
+      double ax0 = a[0] * xv[r][6].x, ax1 = a[0] * xv[r][6].y;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        double ax = a[0] * xv[r][c][6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[r][c][q];
-        const double rs = br[r][c] - ax;
-        const double dn = c1a * dr[r][c] + c2a * rs;
-        if (ok[r]) lx[c][w] = xv[r][c][6] + dn;
-        bt[k0 + r][c] = br[r][c];
-        dt[k0 + r][c] = (float)dn;
+      for (int q = 0; q < 6; ++q) {
+        ax0 += a[1 + q] * xv[r][q].x;
+        ax1 += a[1 + q] * xv[r][q].y;
       }
+      const double dn0 = c1a * (double)dr[r].x + c2a * (br[r].x - ax0);
+      const double dn1 = c1a * (double)dr[r].y + c2a * (br[r].y - ax1);
+      if (ok[r]) lx[w] = dbl2{xv[r][6].x + dn0, xv[r][6].y + dn1};
+      bt[k0 + r] = br[r];
+      dt[k0 + r] = flt2{(float)dn0, (float)dn1};
     }
   }
   __syncthreads();
   // step a + 1 on the item's own rows (in groups as above)
-  double rr[2] = {0.0, 0.0};
+  double rr0 = 0.0, rr1 = 0.0;
 #pragma unroll
   for (int k0 = 0; k0 < VP_WK; k0 += VP_G) {
     if (k0 * BS >= nw) break;
     int32_t nb[VP_G][6];
     bool in[VP_G][6], ok[VP_G];
     int32_t wr[VP_G];
-    double xv[VP_G][2][7];
+    dbl2 xv[VP_G][7];
 #pragma unroll
     for (int r = 0; r < VP_G; ++r) {
       const int32_t w = (int32_t)threadIdx.x + (k0 + r) * BS;
@@ -1096,14 +1088,11 @@ __global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VP
       int32_t i, j;
       lat::coords(t, n, fc.rinv, i, j);
       lat::neighbours(F, n, t, i, j, nb[r], in[r]);
+      xv[r][6] = lx[wr[r]];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        xv[r][c][6] = lx[c][wr[r]];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          const int32_t lw = min(max(nb[r][q] - F.base - w0, 0), nw - 1);
-          xv[r][c][q] = in[r][q] ? lx[c][lw] : v.xb[c][nb[r][q]];
-        }
+      for (int q = 0; q < 6; ++q) {
+        const int32_t lw = min(max(nb[r][q] - F.base - w0, 0), nw - 1);
+        xv[r][q] = in[r][q] ? lx[lw] : v.xb[nb[r][q]];
       }
     }
 #pragma unroll
@@ -1115,31 +1104,37 @@ __global__ __launch_bounds__(BS) PUCFEM_VP_ATTR void k_vcheb_pair(FaceDev fc, VP
       bool bnd = false;
 #pragma unroll
       for (int q = 0; q < 6; ++q) bnd = bnd || !in[r][q];
+      double ax0 = a[0] * xv[r][6].x, ax1 = a[0] * xv[r][6].y;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        double ax = a[0] * xv[r][c][6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ax += a[1 + q] * xv[r][c][q];
-        const double rs = bt[k0 + r][c] - ax;
-        const double dn = c1b * (double)dt[k0 + r][c] + c2b * rs;
-        if (bnd) v.xb[c][row] = xv[r][c][6];
-        if (fin) {
-          const double au = v.s[row] * (xv[r][c][6] + dn);
-          stnt(v.us[c] + row, au);
-          stnt(v.inc[c] + row, (float)(au - v.u[c][row]));
-        } else {
-          stnt(v.dc[c] + row, (float)dn);
-          stnt(v.xc[c] + row, xv[r][c][6] + dn);
-        }
-        rr[c] += rs * rs;
+      for (int q = 0; q < 6; ++q) {
+        ax0 += a[1 + q] * xv[r][q].x;
+        ax1 += a[1 + q] * xv[r][q].y;
       }
+      const double rs0 = bt[k0 + r].x - ax0, rs1 = bt[k0 + r].y - ax1;
+      const double dn0 = c1b * (double)dt[k0 + r].x + c2b * rs0;
+      const double dn1 = c1b * (double)dt[k0 + r].y + c2b * rs1;
+      if (bnd) v.xb[row] = xv[r][6];
+      if (fin) {
+        const double s = v.s[row];
+        const double au0 = s * (xv[r][6].x + dn0), au1 = s * (xv[r][6].y + dn1);
+        stnt(v.us[0] + row, au0);
+        stnt(v.us[1] + row, au1);
+        stnt(v.inc[0] + row, (float)(au0 - v.u[0][row]));
+        stnt(v.inc[1] + row, (float)(au1 - v.u[1][row]));
+      } else {
+        stnt(v.dc + row, flt2{(float)dn0, (float)dn1});
+        stnt(v.xc + row, dbl2{xv[r][6].x + dn0, xv[r][6].y + dn1});
+      }
+      rr0 += rs0 * rs0;
+      rr1 += rs1 * rs1;
     }
   }
   if (!part_rr) return;  // the solve's last step: |r_{a+1}|^2 partials for the a-posteriori check
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const double t = block_sum(rr[c], sh);
-    if (threadIdx.x == 0) part_rr[(int64_t)c * MAXB + part_off + blockIdx.x] = t;
+  const double ta = block_sum(rr0, sh);
+  const double tb = block_sum(rr1, sh);
+  if (threadIdx.x == 0) {
+    part_rr[part_off + blockIdx.x] = ta;
+    part_rr[(int64_t)MAXB + part_off + blockIdx.x] = tb;
   }
 }
 
@@ -1229,30 +1224,54 @@ __device__ __forceinline__ void visc_start(const VincDev& D, int64_t i, double a
     gb += 7.0 * (e[1] - e[11]) + 21.0 * (e[9] - e[3]) + 35.0 * (e[5] - e[7]) + e[13];
   }
 }
+// the viscous right-hand side b = s u and the warm start y = sq (u + extrapolated increment); AOS: b and y
+// interleaved (the Chebyshev solve's dbl2 vectors: bx, yx point at them, by, yy unused), else SoA (the CG)
+template <bool AOS>
 __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const double* __restrict__ sq,
                             const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy,
                             VincDev D) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
-    stnt(bx + i, s[i] * a);
-    stnt(by + i, s[i] * b);
     double ga, gb;
     visc_start(D, i, a, b, ga, gb);
-    stnt(yx + i, sq[i] * ga);
-    stnt(yy + i, sq[i] * gb);
+    if constexpr (AOS) {
+      stnt(reinterpret_cast<dbl2*>(bx) + i, dbl2{s[i] * a, s[i] * b});
+      stnt(reinterpret_cast<dbl2*>(yx) + i, dbl2{sq[i] * ga, sq[i] * gb});
+    } else {
+      stnt(bx + i, s[i] * a);
+      stnt(by + i, s[i] * b);
+      stnt(yx + i, sq[i] * ga);
+      stnt(yy + i, sq[i] * gb);
+    }
   }
 }
-// u* = S y (both components) and the increment u* - u for the next step's warm start
-__global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const double* __restrict__ yx,
-                           const double* __restrict__ yy, const double* __restrict__ ux, const double* __restrict__ uy,
-                           double* __restrict__ usx, double* __restrict__ usy, float* __restrict__ dx,
-                           float* __restrict__ dy) {
+// the same from SoA y (the viscous CG's vectors)
+__global__ void k_visc_fin_soa(int64_t n, const double* __restrict__ s, const double* __restrict__ yx,
+                               const double* __restrict__ yy, const double* __restrict__ ux,
+                               const double* __restrict__ uy, double* __restrict__ usx, double* __restrict__ usy,
+                               float* __restrict__ dx, float* __restrict__ dy) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = s[i] * yx[i], b = s[i] * yy[i];
     stnt(usx + i, a);
     stnt(usy + i, b);
     stnt(dx + i, (float)(a - ux[i]));
     stnt(dy + i, (float)(b - uy[i]));
+  }
+}
+// u* = S y (both components, y interleaved) and, with dx non-null, the increment u* - u for the next
+// step's warm start
+__global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const dbl2* __restrict__ y,
+                           const double* __restrict__ ux, const double* __restrict__ uy, double* __restrict__ usx,
+                           double* __restrict__ usy, float* __restrict__ dx, float* __restrict__ dy) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+    const dbl2 yi = y[i];
+    const double a = s[i] * yi.x, b = s[i] * yi.y;
+    stnt(usx + i, a);
+    stnt(usy + i, b);
+    if (dx) {
+      stnt(dx + i, (float)(a - ux[i]));
+      stnt(dy + i, (float)(b - uy[i]));
+    }
   }
 }
 
