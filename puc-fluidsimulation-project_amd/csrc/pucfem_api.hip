@@ -2505,6 +2505,76 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
 }
 
 
+// Host half of the semi-Lagrangian / replica setup (build): node and triangle tables in internal
+// numbering, the centroid grid, the lattice locator's tables, the initial dye.  It reads only the mesh,
+// the ordering, the macro mesh and the finest lattice level, which nothing writes after the multigrid
+// hierarchy exists, so build() runs it on a thread beside the operator uploads and SELL fills
+// (round 4: ~1.3 s of L7 setup off the critical path); the uploads and kernels stay on the caller.
+struct SlPrep {
+  std::vector<double> X, Y, cx, cy, xy, c0;
+  std::vector<i32> tri, home;
+  Grid G, TG, MG;
+  std::vector<lat::SlFace> sf;
+  std::vector<uint32_t> cells;
+  bool lat_sl = false;
+};
+void sl_prep(const Ctx& c, bool food, SlPrep& P) {
+  const HostMesh& m = c.mesh;
+  const i64 N = m.N;
+  P.X.resize(N);
+  P.Y.resize(N);
+  parallel_for(N, [&](i64 g0, i64 g1) {
+    for (i64 g = g0; g < g1; ++g) {
+      P.X[g] = m.x[c.ord.new2old[g]];
+      P.Y[g] = m.y[c.ord.new2old[g]];
+    }
+  });
+  P.tri.resize(3 * m.T);
+  parallel_for(3 * m.T, [&](i64 k0, i64 k1) {
+    for (i64 k = k0; k < k1; ++k) P.tri[k] = c.ord.old2new[m.tri[k]];
+  });
+  // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
+  P.cx.resize(m.T);
+  P.cy.resize(m.T);
+  parallel_for(m.T, [&](i64 t0, i64 t1) {
+    for (i64 t = t0; t < t1; ++t) {
+      const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
+      P.cx[t] = (m.x[a] + m.x[b] + m.x[d]) / 3;
+      P.cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
+    }
+  });
+  build_centroid_grid(P.cx, P.cy, 2.0, P.G);
+  if (food) build_tri_grid(P.X, P.Y, P.tri, 4.0, P.TG);  // tracer location (StokesFood only)
+  P.xy.resize(2 * (size_t)N);
+  parallel_for(N, [&](i64 i0, i64 i1) {
+    for (i64 i = i0; i < i1; ++i) {
+      P.xy[2 * i] = P.X[i];
+      P.xy[2 * i + 1] = P.Y[i];
+    }
+  });
+  // semi-Lagrangian point location: on a lattice hierarchy the lattice locator (no per-triangle
+  // records); PUCFEM_SL_RECORDS=1 forces the record locator (measurement / cross-check knob)
+  P.lat_sl = c.lattice && !c.mg.empty() && !(std::getenv("PUCFEM_SL_RECORDS") && std::atoi(std::getenv("PUCFEM_SL_RECORDS")));
+  if (P.lat_sl) {
+    try {
+      lattice_locator(c.macro, c.mg.back().latl, m, c.ord, P.sf, P.cells);
+    } catch (const std::exception&) {
+      P.lat_sl = false;  // a hierarchy not numbered face by face: the record locator
+    }
+  }
+  if (P.lat_sl) {
+    build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, P.MG, 1e-6);
+    // home faces: the macro face of every face-interior row (the first face tried)
+    const LatticeLevel& LL = c.mg.back().latl;
+    P.home.assign(N, -1);
+    for (i64 f = 0; f < c.macro.nf; ++f)
+      for (i64 k = 0; k < LL.F; ++k) P.home[LL.face_start[f] + k] = (i32)f;
+  }
+  // initial dye c = 1[x < 0.5] (StokesColor.py:493-495)
+  P.c0.resize(N);
+  for (i64 g = 0; g < N; ++g) P.c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
+}
+
 void build(Ctx& c) {
   SetupClock clk;
   require(c.has_mesh, "mesh not uploaded");
@@ -2566,6 +2636,10 @@ void build(Ctx& c) {
                      prm.scheme == PUCFEM_HEAT ? prm.dt : -1.0, c.Lit, c.litb);
   }
   clk.mark("multigrid hierarchy (host)");
+  // the semi-Lagrangian tables' host half, beside everything up to the SL uploads below
+  SlPrep slp;
+  ThreadGroup slg;
+  if (stokes) slg.spawn([&c, &slp, &prm] { sl_prep(c, prm.scheme == PUCFEM_STOKES_FOOD, slp); });
   // A_visc on P (StokesColor.py:471-475)
   std::vector<uint8_t> isdir(N, 0);
   for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
@@ -3117,19 +3191,13 @@ void build(Ctx& c) {
     for (int q = 0; q < 9; ++q) c.litw[q] = c.dalloc<double>(c.nloc);
   }
   clk.mark("device: per-row data, BCs, halo, workspace");
-  // full-mesh replica in internal numbering
+  // full-mesh replica in internal numbering (the host half: sl_prep, on its thread since the hierarchy)
+  if (!stokes) sl_prep(c, false, slp);
+  slg.join();
+  clk.mark("SL: host tables (joined)");
   {
-    std::vector<double> X(N), Y(N);
-    parallel_for(N, [&](i64 g0, i64 g1) {
-      for (i64 g = g0; g < g1; ++g) {
-        X[g] = m.x[c.ord.new2old[g]];
-        Y[g] = m.y[c.ord.new2old[g]];
-      }
-    });
-    std::vector<i32> tri(3 * m.T);
-    parallel_for(3 * m.T, [&](i64 k0, i64 k1) {
-      for (i64 k = k0; k < k1; ++k) tri[k] = c.ord.old2new[m.tri[k]];
-    });
+    const std::vector<double>&X = slp.X, &Y = slp.Y;
+    const std::vector<i32>& tri = slp.tri;
     c.mx = c.upload(X);
     c.my = c.upload(Y);
     c.mtri = c.upload(tri);
@@ -3145,23 +3213,13 @@ void build(Ctx& c) {
       D.px = pts ? c.upload(G.px) : nullptr;
       D.py = pts ? c.upload(G.py) : nullptr;
     };
-    if (stokes) {  // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
-      std::vector<double> cx(m.T), cy(m.T);
-      parallel_for(m.T, [&](i64 t0, i64 t1) {
-        for (i64 t = t0; t < t1; ++t) {
-          const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
-          cx[t] = (m.x[a] + m.x[b] + m.x[d]) / 3;
-          cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
-        }
-      });
-      Grid G;
-      build_centroid_grid(cx, cy, 2.0, G);
+    if (stokes) {  // PointLocator centroids (StokesColor.py:321), their grid (sl_prep)
+      const std::vector<double>&cx = slp.cx, &cy = slp.cy;
+      const Grid& G = slp.G;
       dgrid(G, c.cgrid, true);
       c.has_cgrid = true;
       if (prm.scheme == PUCFEM_STOKES_FOOD) {  // tracer location (StokesFood only)
-        Grid TG;
-        build_tri_grid(X, Y, tri, 4.0, TG);
-        dgrid(TG, c.tgrid, false);
+        dgrid(slp.TG, c.tgrid, false);
         c.has_tgrid = true;
       }
       clk.mark("SL: centroid / triangle grids");
@@ -3192,42 +3250,16 @@ void build(Ctx& c) {
         drv2 = v2;
         clk.mark("SL: centroid 10-NN radii");
       }
-      std::vector<double> xy(2 * (size_t)N);
-      parallel_for(N, [&](i64 i0, i64 i1) {
-        for (i64 i = i0; i < i1; ++i) {
-          xy[2 * i] = X[i];
-          xy[2 * i + 1] = Y[i];
-        }
-      });
-      const double2* dxy = reinterpret_cast<const double2*>(c.upload(xy));
+      const double2* dxy = reinterpret_cast<const double2*>(c.upload(slp.xy));
       clk.mark("SL: vertex 11-NN radii");
       const int probe = std::getenv("PUCFEM_SL_PROBE") ? std::atoi(std::getenv("PUCFEM_SL_PROBE")) : 0;
-      // semi-Lagrangian point location: on a lattice hierarchy the lattice locator (no per-triangle
-      // records); PUCFEM_SL_RECORDS=1 forces the record locator (measurement / cross-check knob)
-      std::vector<lat::SlFace> sf;
-      std::vector<uint32_t> cells;
-      c.lat_sl = c.lattice && !c.mg.empty() && !(std::getenv("PUCFEM_SL_RECORDS") && std::atoi(std::getenv("PUCFEM_SL_RECORDS")));
+      c.lat_sl = slp.lat_sl;  // the lattice locator (sl_prep decided), else the record locator below
       if (c.lat_sl) {
-        try {
-          lattice_locator(c.macro, c.mg.back().latl, m, c.ord, sf, cells);
-        } catch (const std::exception&) {
-          c.lat_sl = false;  // a hierarchy not numbered face by face: the record locator below
-        }
-      }
-      clk.mark("SL: lattice locator tables");
-      if (c.lat_sl) {
-        Grid MG;
-        build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, MG, 1e-6);
         GridDev mg{};
-        dgrid(MG, mg, false);
-        // home faces: the macro face of every face-interior row (the first face tried)
-        const LatticeLevel& LL = c.mg.back().latl;
-        std::vector<i32> home(N, -1);
-        for (i64 f = 0; f < c.macro.nf; ++f)
-          for (i64 k = 0; k < LL.F; ++k) home[LL.face_start[f] + k] = (i32)f;
+        dgrid(slp.MG, mg, false);
         c.llgrid = LatLocDev{mg.nx, mg.ny, mg.x0, mg.y0, 1.0 / mg.hx, 1.0 / mg.hy, mg.start, mg.item,
-                             reinterpret_cast<const lat::SlFace*>(c.upload(sf)), c.upload(cells), dxy,
-                             drho2, drv2, c.upload(home), nullptr, LL.n, probe};
+                             reinterpret_cast<const lat::SlFace*>(c.upload(slp.sf)), c.upload(slp.cells), dxy,
+                             drho2, drv2, c.upload(slp.home), nullptr, c.mg.back().latl.n, probe};
         // zero-velocity rows (walls): the answer for the row's own node, once
         int32_t* dself = c.dalloc<int32_t>(N);
         hipLaunchKernelGGL(k_sl_self<LatLocDev>, dim3(2048), dim3(BS), 0, c.st, MeshDev{c.mx, c.my, c.mtri, m.T},
@@ -3283,9 +3315,7 @@ void build(Ctx& c) {
   if (stokes) {
     c.bc(c.ux, c.uy);
     c.halo(c.ux, c.uy);
-    std::vector<double> c0(N);
-    for (i64 g = 0; g < N; ++g) c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
-    HIPCHK(hipMemcpyAsync(c.c_full, c0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(c.c_full, slp.c0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
   }
   HIPCHK(hipStreamSynchronize(c.st));
   clk.mark("SL: locator / self table, initial state");
