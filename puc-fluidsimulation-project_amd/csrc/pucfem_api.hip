@@ -2241,10 +2241,10 @@ struct SetupClock {
 
 void assemble_device(Ctx& c, const HostMesh& m, const Ordering& ord, Csr& P, Assembly& A);
 
-void build_mg_host(Ctx& c, SetupClock& clk) {
+// the red refinements of the hierarchy (host only: levels' meshes and their midpoint parents); build()
+// runs it on a thread beside the finest level's assembly and pressure merge, which do not touch c.mg
+void mg_refine(Ctx& c) {
   const int Lv = c.mg_levels;
-  c.mg.clear();
-  c.mg.resize(Lv + 1);
   c.mg[0].mesh = c.coarse;
   for (int l = 1; l <= Lv; ++l) {
     HostMesh tmp;
@@ -2257,7 +2257,9 @@ void build_mg_host(Ctx& c, SetupClock& clk) {
               "the uploaded mesh is not the red refinement of the hierarchy's coarse mesh");
     }
   }
-  clk.mark("  mg: refinements");
+}
+void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
+  const int Lv = c.mg_levels;
   for (int l = 0; l < Lv; ++l) {
     MgLevel& L = c.mg[l];
     if (c.lattice) lattice_ordering(L.mesh, c.macro, l, L.ord, L.latl);
@@ -2598,6 +2600,13 @@ void build(Ctx& c) {
     make_ordering(m, prm.nstrips, c.ord);
   }
   clk.mark("ordering");
+  // the multigrid hierarchy's refinements on a thread beside the finest assembly and pressure merge
+  ThreadGroup refg;
+  if (stokes && prm.precond == 1 && c.mg_levels > 0) {
+    c.mg.clear();
+    c.mg.resize(c.mg_levels + 1);
+    refg.spawn([&c] { mg_refine(c); });
+  }
   if (c.dev_asm()) {
     assemble_device(c, m, c.ord, c.P, c.as);
     clk.mark("pattern + assembly (device)");
@@ -2630,6 +2639,8 @@ void build(Ctx& c) {
   }
   c.use_mg = stokes && prm.precond == 1 && c.mg_levels > 0;
   clk.mark("assembly + pressure merge");
+  refg.join();
+  clk.mark("  mg: refinements (joined)");
   if (c.use_mg) build_mg_host(c, clk);
   if (literal) {
     assemble_literal(m, c.ord, c.g_tri, c.op_pairs, c.dir_nodes, c.dir_vals,
