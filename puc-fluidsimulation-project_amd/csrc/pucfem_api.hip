@@ -1872,7 +1872,7 @@ struct Ctx {
         ~SmallRed() { f = false; }
       } small_red(red_small);
       const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
-      div(ux, uy, final_div, false, part_fd, rf);
+      div(ux, uy, nullptr, false, part_fd, rf);  // (the final div field is computed when read)
       if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
       const int nb = nb_sl(lp.n_own);
       const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
@@ -1896,7 +1896,9 @@ struct Ctx {
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
-    const bool f1 = div_rhs(usx, usy, div_star, vals);  // max |div u*| -> vals[0]
+    // max |div u*| -> vals[0]; the div u* field itself is computed when read (pucfem_get_field): nothing in the
+    // step reads it, and its 8 B/row store is a quarter of the kernel's bytes
+    const bool f1 = div_rhs(usx, usy, nullptr, vals);
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
     const int itp = pressure(yp, p, 1, f1);
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
@@ -1914,7 +1916,7 @@ struct Ctx {
     const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && !dist();
     if (!ovl) {
       const RedOut r = ro(vals + 1, CNT_DIV, 1, MAXB, 1u);
-      div(ux, uy, final_div, false, nullptr, r);
+      div(ux, uy, dye_impl ? final_div : nullptr, false, nullptr, r);  // (the implicit dye reads it)
       if (r.out) red_done(vals + 1, 1, true);
       else reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     }
@@ -3622,9 +3624,16 @@ int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count) {
       case PUCFEM_F_USTAR: get2(c.usx, c.usy); break;
       case PUCFEM_F_P: get1(c.p); break;
       case PUCFEM_F_P2: get1(c.p2); break;
-      case PUCFEM_F_DIV_STAR: get1(c.div_star); break;
+      case PUCFEM_F_DIV_STAR:  // computed from u* when read (the step records only its max)
+        if (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD) c.div(c.usx, c.usy, c.div_star, false);
+        get1(c.div_star);
+        break;
       case PUCFEM_F_DIV_U: get1(c.div_u); break;
-      case PUCFEM_F_FINAL_DIV: get1(c.final_div); break;
+      case PUCFEM_F_FINAL_DIV:  // likewise from u (the implicit dye variant keeps its own copy)
+        if ((c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD) && !c.dye_impl)
+          c.div(c.ux, c.uy, c.final_div, false);
+        get1(c.final_div);
+        break;
       case PUCFEM_F_SCALAR: get1(c.scalar); break;
       case PUCFEM_F_C: {
         require(count == N, "c is (N,)");

@@ -1276,7 +1276,9 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const dbl2* 
 }
 
 // ----------------------------------------------------------------------------- div / grad
-// calculate_divergence (StokesColor.py:130-165) in operator form: div = (Gx ux + Gy uy) / (area_sum + 1e-12).
+// calculate_divergence (StokesColor.py:130-165) in operator form: div = (Gx ux + Gy uy) / (area_sum + 1e-12)
+// into div (null: only its max |div| partials -- the step's div(u*) and final div fields are computed when
+// read, pucfem_get_field).
 // Optionally the pressure RHS of the row-scaled system: braw = (M + 1e-12) * (-(1/DT) * div)
 // (StokesColor.py:554 with A_pressure = K / (M + 1e-12)).  Partials: [0] max|div|, [1] sum(braw).
 template <bool C16>
@@ -1316,7 +1318,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
         face_grad_v(c, vy[r], bx, by);
         const int64_t row = F.base + t[r];
         const double d = (ax + by) / as;
-        stnt(div + row, d);
+        if (div) stnt(div + row, d);
         mx = fmax(mx, fabs(d));
         if (braw) {
           const double b = as * (negidt * d);
@@ -1359,7 +1361,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
       });
       if (row >= 0) {
         const double d = acc / as1[row];
-        stnt(div + row, d);
+        if (div) stnt(div + row, d);
         mx = fmax(mx, fabs(d));
         if (braw) {
           const double b = mp[row] * (negidt * d);
