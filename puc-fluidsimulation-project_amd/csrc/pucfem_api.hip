@@ -2465,7 +2465,9 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
     // gathered columns)
     std::vector<double> dv(L.nloc);
     const i64 r0 = L.own0(c.rank);
-    for (i64 i = 0; i < n; ++i) dv[i] = 1.0 / diag_of(A, A.val, r0 + i);
+    parallel_for(n, [&](i64 i0, i64 i1) {
+      for (i64 i = i0; i < i1; ++i) dv[i] = 1.0 / diag_of(A, A.val, r0 + i);
+    });
     for (i64 k = 0; k < L.lp.n_ghost; ++k) dv[n + k] = 1.0 / diag_of(A, A.val, L.lp.ghost_global[k]);
     B.dinv = upload_as<T>(c, dv);
     if (l < Lv) {
@@ -2657,14 +2659,16 @@ void build(Ctx& c) {
   std::vector<uint8_t> isdir(N, 0);
   for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
   const double dtnu = prm.dt * prm.nu;
-  c.Kv.assign(c.P.nnz(), 0.0);
-  for (i64 r = 0; r < N; ++r)
-    for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) {
-      const i32 j = c.P.col[k];
-      if (isdir[r]) c.Kv[k] = (j == r) ? 1.0 : 0.0;
-      else if (isdir[j]) c.Kv[k] = 0.0;
-      else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
-    }
+  c.Kv.resize(c.P.nnz());
+  parallel_for(N, [&](i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1; ++r)
+      for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) {
+        const i32 j = c.P.col[k];
+        if (isdir[r]) c.Kv[k] = (j == r) ? 1.0 : 0.0;
+        else if (isdir[j]) c.Kv[k] = 0.0;
+        else c.Kv[k] = (j == r) ? 1.0 + dtnu * c.as.K[k] : dtnu * c.as.K[k];
+      }
+  });
   if (stokes) {  // spectral interval of the Jacobi-scaled A_visc (Ctx::visc_R, Ctx::visc_lo)
     std::vector<double> dg(N);
     parallel_for(N, [&](i64 r0, i64 r1) {
@@ -2896,18 +2900,13 @@ void build(Ctx& c) {
     c.dDyeB = c.dalloc<double>(c.nloc);
   }
   clk.mark("device: K, G, dye operator");
-  // Jacobi symmetric scaling S A S of A_visc
-  auto scaled = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
+  // Jacobi symmetric scaling S A S: s_g = 1 / sqrt(a_gg); the scaled values s_r a_rk s_col go straight into
+  // the SELL image (only the skeleton rows on lattice hierarchies)
+  auto scaling = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
     sg.resize(N);
     parallel_for(N, [&](i64 g0, i64 g1) {
       for (i64 g = g0; g < g1; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
     });
-    std::vector<double> out(val.size());
-    parallel_for(N, [&](i64 r0, i64 r1) {
-      for (i64 r = r0; r < r1; ++r)
-        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) out[k] = sg[r] * val[k] * sg[A.col[k]];
-    });
-    return out;
   };
   auto local_vec = [&](const std::vector<double>& g) {  // owned + ghost entries of a global vector
     std::vector<double> v(c.nloc);
@@ -2917,8 +2916,8 @@ void build(Ctx& c) {
   };
   {
     std::vector<double> sg;
-    auto kvh = scaled(c.P, c.Kv, sg);
-    sell_values(c.P, lp, c.sP, kvh, tmp);
+    scaling(c.P, c.Kv, sg);
+    sell_values_fn(c.P, lp.r0, c.sP, [&](i64 r, i64 k) { return sg[r] * c.Kv[k] * sg[c.P.col[k]]; }, tmp);
     c.dKv = c.upload(tmp);
     c.dsv = c.upload(local_vec(sg));
     std::vector<double> sq(N);
@@ -2935,11 +2934,14 @@ void build(Ctx& c) {
   }
   if (stokes) {
     dsell(c.sPp, c.Pp, c.dPp);
-    std::vector<double> sg;
-    auto kph = scaled(c.Pp, c.Pp.val, sg);
-    sell_values(c.Pp, lp, c.sPp, kph, tmp);
-    c.dKp = c.upload(tmp);
-    c.dsp = c.upload(local_vec(sg));
+    if (!c.lattice) {  // the Jacobi-scaled pressure operator (Jacobi-CG and the SELL unit op; a lattice hierarchy
+                       // always runs the multigrid PCG on the unscaled one)
+      std::vector<double> sg;
+      scaling(c.Pp, c.Pp.val, sg);
+      sell_values_fn(c.Pp, lp.r0, c.sPp, [&](i64 r, i64 k) { return sg[r] * c.Pp.val[k] * sg[c.Pp.col[k]]; }, tmp);
+      c.dKp = c.upload(tmp);
+      c.dsp = c.upload(local_vec(sg));
+    }
   }
   if (c.use_mg) {
     sell_values(c.Pp, lp, c.sPp, c.Pp.val, tmp);
@@ -3836,7 +3838,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
         break;
       }
       case PUCFEM_OP_PRES: {
-        require(c.dKp, "no pressure operator (scheme is not Stokes)");
+        require(c.dKp || c.dKp_raw, "no pressure operator (scheme is not Stokes)");
         if (c.lattice) {  // the unscaled merged operator (the multigrid path's)
           perm_in(x, 1, t0, nullptr);
           spmv_on(c.st, c.dPp, c.fP.full(), c.dKp_raw, t0, o0);

@@ -384,53 +384,52 @@ void assemble_literal(const HostMesh& m, const Ordering& ord, const std::vector<
 void build_pressure(const Csr& P, const std::vector<double>& K, const std::vector<i32>& dof,
                     const std::vector<i32>& slave_of, Csr& Pp) {
   const i64 N = P.nrows;
-  // rows are independent (chunks of rows merged in parallel, then concatenated in row order)
-  std::vector<std::vector<std::pair<i32, double>>> cent(PAR_CHUNKS);
-  std::vector<std::vector<i64>> clen(PAR_CHUNKS);
-  parallel_chunks(N, [&](int ch, i64 r0, i64 r1) {
-    std::vector<std::pair<i32, double>> tmp;
-    for (i64 r = r0; r < r1; ++r) {
-      tmp.clear();
-      if (dof[r] != r) {  // slave: identity row, decoupled
-        tmp.push_back({(i32)r, 1.0});
-      } else {
-        auto add_row = [&](i64 src) {
-          for (i64 k = P.rowptr[src]; k < P.rowptr[src + 1]; ++k) tmp.push_back({dof[P.col[k]], K[k]});
-        };
-        add_row(r);
-        if (slave_of[r] >= 0) add_row(slave_of[r]);
-        // combine duplicates in insertion order (stable by column)
-        std::stable_sort(tmp.begin(), tmp.end(),
-                         [](const std::pair<i32, double>& a, const std::pair<i32, double>& b) { return a.first < b.first; });
-        size_t w = 0;
-        for (size_t k = 0; k < tmp.size(); ++k) {
-          if (w > 0 && tmp[w - 1].first == tmp[k].first) tmp[w - 1].second += tmp[k].second;
-          else tmp[w++] = tmp[k];
-        }
-        tmp.resize(w);
-      }
-      cent[ch].insert(cent[ch].end(), tmp.begin(), tmp.end());
-      clen[ch].push_back((i64)tmp.size());
+  // row r of the merged operator: a slave's identity row, or the master row plus its slave's row with the
+  // columns mapped to their dofs, stably sorted by column and duplicates combined in insertion order.
+  // Rows are independent: one pass counts them, the second writes them in place (parallel both).
+  auto merge_row = [&](i64 r, std::vector<std::pair<i32, double>>& tmp) {
+    tmp.clear();
+    if (dof[r] != r) {  // slave: identity row, decoupled
+      tmp.push_back({(i32)r, 1.0});
+      return;
     }
-  });
+    auto add_row = [&](i64 src) {
+      for (i64 k = P.rowptr[src]; k < P.rowptr[src + 1]; ++k) tmp.push_back({dof[P.col[k]], K[k]});
+    };
+    add_row(r);
+    if (slave_of[r] >= 0) add_row(slave_of[r]);
+    std::stable_sort(tmp.begin(), tmp.end(),
+                     [](const std::pair<i32, double>& a, const std::pair<i32, double>& b) { return a.first < b.first; });
+    size_t w = 0;
+    for (size_t k = 0; k < tmp.size(); ++k) {
+      if (w > 0 && tmp[w - 1].first == tmp[k].first) tmp[w - 1].second += tmp[k].second;
+      else tmp[w++] = tmp[k];
+    }
+    tmp.resize(w);
+  };
   Pp.nrows = N;
   Pp.rowptr.assign(N + 1, 0);
-  i64 r = 0;
-  for (int ch = 0; ch < PAR_CHUNKS; ++ch)
-    for (i64 l : clen[ch]) {
-      Pp.rowptr[r + 1] = Pp.rowptr[r] + l;
-      ++r;
+  parallel_for(N, [&](i64 r0, i64 r1) {
+    std::vector<std::pair<i32, double>> tmp;
+    for (i64 r = r0; r < r1; ++r) {
+      merge_row(r, tmp);
+      Pp.rowptr[r + 1] = (i64)tmp.size();
     }
+  });
+  for (i64 r = 0; r < N; ++r) Pp.rowptr[r + 1] += Pp.rowptr[r];
   Pp.col.resize(Pp.rowptr[N]);
   Pp.val.resize(Pp.rowptr[N]);
-  std::vector<i64> cstart(PAR_CHUNKS + 1, 0);
-  for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)cent[ch].size();
-  parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
-    for (i64 ch = c0; ch < c1; ++ch)
-      for (size_t q = 0; q < cent[ch].size(); ++q) {
-        Pp.col[cstart[ch] + q] = cent[ch][q].first;
-        Pp.val[cstart[ch] + q] = cent[ch][q].second;
+  parallel_for(N, [&](i64 r0, i64 r1) {
+    std::vector<std::pair<i32, double>> tmp;
+    for (i64 r = r0; r < r1; ++r) {
+      merge_row(r, tmp);
+      i64 o = Pp.rowptr[r];
+      for (const auto& e : tmp) {
+        Pp.col[o] = e.first;
+        Pp.val[o] = e.second;
+        ++o;
       }
+    }
   });
 }
 

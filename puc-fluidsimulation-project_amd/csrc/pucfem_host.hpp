@@ -208,6 +208,23 @@ struct Sell {
 // columns resolved in `cols`; int32 columns only (rows are not contiguous)
 void build_sell_rows(const Csr& A, i64 r0, const std::vector<i32>& rows, const LocalPlan& cols, Sell& S);
 void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
+// the SELL image of A's rows in S (rows r0 + k, or r0 + S.rows[k]) with entry values f(r, e) computed in
+// place (r: the row's global index, e: its CSR entry) -- no full-length value array for a SELL that
+// holds only the lattice skeleton's rows
+template <class F>
+void sell_values_fn(const Csr& A, i64 r0, const Sell& S, F&& f, std::vector<double>& out) {
+  out.assign(S.padded, 0.0);
+  parallel_for(S.nslices, [&](i64 s0, i64 s1) {
+    for (i64 s = s0; s < s1; ++s)
+      for (i64 l = 0; l < 64; ++l) {
+        const i64 k = s * 64 + l;
+        if (k >= S.nrows) continue;
+        const i64 r = r0 + (S.rows.empty() ? k : (i64)S.rows[k]);
+        const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
+        for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = f(r, b + e);
+      }
+  });
+}
 
 // ----------------------------------------------------------------------------- lattice layout
 // Macro primitives (the coarse mesh of a red-refinement hierarchy: faces, edges, vertices), their

@@ -129,7 +129,10 @@ def filter_wall_pairs(nodes_coords, pairs, tol=TOL, H=1.0):
 def boundary_sets(nodes_coords, markers, tol=TOL, H=1.0):
     """StokesColor.py:461-464: (wall, inner, dirichlet, interior) index arrays."""
     X = np.asarray(nodes_coords)
-    wall = np.where(np.isclose(X[:, 1], 0.0, atol=tol) | np.isclose(X[:, 1], H, atol=tol))[0]
+    y = X[:, 1]
+    # np.isclose(y, v, atol=tol) on finite values is |y - v| <= atol + rtol |v| (rtol 1e-5), written out:
+    # the same test, without isclose's inf / nan bookkeeping over every node (0.3 s at L7)
+    wall = np.where((np.abs(y - 0.0) <= tol + 1e-5 * 0.0) | (np.abs(y - H) <= tol + 1e-5 * abs(H)))[0]
     inner = np.where(markers == INNER_BOUNDARY_MARKER)[0]
     mask = np.zeros(X.shape[0], dtype=bool)
     mask[wall] = True
