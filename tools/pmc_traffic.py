@@ -111,16 +111,26 @@ def main():
         return [k for k in ks if int(k.rsplit("grid=", 1)[1]) == g]
 
     fine = widest(fine)
+    def pick(prefix, exclude=()):
+        return [k for k in res["kernels"] if k.startswith(prefix) and not any(k.startswith(x) for x in exclude)
+                and "hbm_bytes_per_launch" in res["kernels"][k]]
+
+    # keys: the bench's kernel classes (bench.py `kernels`, roofline.kernel); k_vcheb: the whole-grid steps
+    # only (the step pairs' SELL-only launches have smaller grids); k_mdot2 / k_pcomb: every basis size
     for key, ks in (("k_cheb", fine),
-                    ("k_cg_dir", [k for k in res["kernels"] if k.startswith("k_cg_dir<1,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_cg_dir<2>", [k for k in res["kernels"] if k.startswith("k_cg_dir<2,") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_sl", [k for k in res["kernels"] if k.startswith("k_sl") and not k.startswith("k_sl_") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_sl_slow", [k for k in res["kernels"] if k.startswith("k_sl_slow") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_vcheb<2>", widest([k for k in res["kernels"] if k.startswith("k_vcheb<2,") and "hbm_bytes_per_launch" in res["kernels"][k]])),
-                    ("k_div", [k for k in res["kernels"] if k.startswith("k_div<") and "hbm_bytes_per_launch" in res["kernels"][k]]),
+                    ("k_cg_dir", pick("k_cg_dir<1,")),
+                    ("k_cg_upd", pick("k_cg_upd<1>")),
+                    ("k_sl", pick("k_sl", ("k_sl_",))),
+                    ("k_sl_slow", pick("k_sl_slow")),
+                    ("k_vcheb", widest(pick("k_vcheb<"))),
+                    ("k_div", pick("k_div<")),
+                    ("k_grad_proj", pick("k_grad_proj<")),
+                    ("k_visc_prep", pick("k_visc_prep")),
+                    ("k_mdot2", pick("k_mdot2<")),
+                    ("k_pcomb", pick("k_pcomb<")),
                     # step pairs (both modes of the multigrid pair: the bench's class 10 averages them too)
-                    ("k_cheb_pair", [k for k in res["kernels"] if k.startswith("k_cheb_pair<") and "hbm_bytes_per_launch" in res["kernels"][k]]),
-                    ("k_vcheb_pair", [k for k in res["kernels"] if k.startswith("k_vcheb_pair") and "hbm_bytes_per_launch" in res["kernels"][k]])):
+                    ("k_cheb_pair", pick("k_cheb_pair<")),
+                    ("k_vcheb_pair", pick("k_vcheb_pair"))):
         if ks:
             n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
