@@ -995,6 +995,7 @@ struct Ctx {
     // adaptive test it replaces needed one extra step per solve to see the passing residual.)
     const int nb0 = nb;  // the first step's partial count
     step(0, 0.0, 1.0 / theta);
+    if (sl_gate == 1) dye_flush();
     Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
     if (ro(redbuf, CNT_VCHEB, 2 * NR).out) {
       red_done(redbuf, 2 * NR, false);
@@ -1861,6 +1862,17 @@ struct Ctx {
   // tail enqueued after the next step's viscous solve instead, beside the pressure solve: the time moved
   // between the streams, the step rate stayed, r8j.)
   hipEvent_t ev_gate = nullptr;
+  // where the main stream releases a step's dye tail (PUCFEM_SL_GATE, a measurement knob): 0 (default) at
+  // the end of the step; 1 after the next step's first viscous Chebyshev step (which then runs alone);
+  // 2 after the next step's viscous solve (round 3's r8j placement)
+  int sl_gate = std::getenv("PUCFEM_SL_GATE") ? std::atoi(std::getenv("PUCFEM_SL_GATE")) : 0;
+  double* sl_deferred = nullptr;  // the record of a tail waiting for its gate
+  void dye_flush() {
+    if (!sl_deferred) return;
+    double* r = sl_deferred;
+    sl_deferred = nullptr;
+    dye_tail(r);
+  }
   void dye_tail(double* rec) {
     HIPCHK(hipEventRecord(ev_gate, st));
     HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
@@ -1896,6 +1908,7 @@ struct Ctx {
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
+    dye_flush();  // (a deferred tail whose gate the viscous solve did not release)
     // max |div u*| -> vals[0]; the div u* field itself is computed when read (pucfem_get_field): nothing in the
     // step reads it, and its 8 B/row store is a quarter of the kernel's bytes
     const bool f1 = div_rhs(usx, usy, nullptr, vals);
@@ -1931,7 +1944,8 @@ struct Ctx {
       }
       hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);  // max |div u*|
       KCHK();
-      dye_tail(rec);
+      if (sl_gate > 0) sl_deferred = rec;  // released by the next step (dye_flush)
+      else dye_tail(rec);
     } else if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       if (dye_impl) {
@@ -3712,9 +3726,11 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
+          c.dye_flush();  // the last step's tail, when a gate deferred it
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
+          c.sl_deferred = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
           throw;
