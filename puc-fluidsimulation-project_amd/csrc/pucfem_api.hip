@@ -555,7 +555,11 @@ struct Ctx {
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
   // semi-Lagrangian grid: latency-bound gathers want more waves in flight than MAXB blocks give
-  static int nb_sl(i64 n) { return (int)std::max<i64>(1, std::min<i64>(SLB, (n + 4 * 64 - 1) / (4 * 64))); }
+  // (PUCFEM_SL_BLOCKS, a measurement knob: a smaller cap leaves the overlapped main stream more wave slots)
+  static int nb_sl(i64 n) {
+    static const int cap = std::getenv("PUCFEM_SL_BLOCKS") ? std::max(64, std::min(SLB, std::atoi(std::getenv("PUCFEM_SL_BLOCKS")))) : SLB;
+    return (int)std::max<i64>(1, std::min<i64>(cap, (n + 4 * 64 - 1) / (4 * 64)));
+  }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
   // ------------------------------------------------------------------ timing helpers
@@ -1633,7 +1637,10 @@ struct Ctx {
   void div(const double* ax, const double* ay, double* out, bool rhs, double* part = nullptr, RedOut r = RedOut{}) {
     const FaceDev fc = fK.part();
     with_c16(dP, [&](auto c16) {
-      klaunch(11, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 32.0 * (double)lp.n_own,
+      // ux, uy gathered once; div (when stored) and braw (the pressure rhs) written
+      klaunch(11,
+              (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows +
+                  (16.0 + (out ? 8.0 : 0.0) + (rhs ? 8.0 : 0.0)) * (double)lp.n_own,
               k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
               rhs ? braw : (double*)nullptr, part ? part : part_d, r);
