@@ -379,6 +379,9 @@ struct Ctx {
   // 1 / 2 the two pressure solves of a step, 3 / 4 standalone viscous / pressure solves (pucfem_solve)
   int last_it[6] = {0, 0, 0, 0, 0, 0};
   bool solved_before[6] = {false, false, false, false, false, false};  // last_it[which] holds a real count
+  // per slot: whether each of the last 8 solves that followed a solve of <= 1 iteration passed at its
+  // initial guess (bit 0 the latest) -- pcg_mg's pre-check policy
+  unsigned zero_hist[6] = {0u, 0u, 0u, 0u, 0u, 0u};
   bool lds_attr[3] = {false, false, false};  // k_cg_block<NR>: dynamic-LDS attribute set on this device
   double* solve_tmp = nullptr;  // pucfem_solve scratch (4 x nloc): standalone solves never touch the step state
   int* dits = nullptr;  // per-step iteration counts written by single-workgroup solves (no host sync)
@@ -1452,13 +1455,16 @@ struct Ctx {
     // check comes one iteration before the last solve's count (a no-op iteration costs more than a
     // check's round trip), then every iteration while the solve is short.  Past the start-up transient
     // the projected guess often passes the test itself (0 iterations): when the last solve took at most
-    // one iteration, the host reads the initial test before launching any (one round trip, where an
-    // iteration of early-exiting launches -- the V-cycle's ~70 -- costs ~0.3 ms of GPU time).
+    // one iteration and, of the last 8 such solves, at least 2 passed at their guess, the host reads the
+    // initial test before launching any (one round trip, where an iteration of early-exiting launches --
+    // the V-cycle's ~70 -- costs ~0.3 ms of GPU time; in the start-up transient, where no solve passes at
+    // its guess, the round trip would only idle the GPU: +0.25 ms per step in the driver window, r10b)
     const bool seen = solved_before[which];
     solved_before[which] = true;
     int chunk = std::max(1, std::min(maxit + 1, !seen ? 4 : (last_it[which] > 1 ? last_it[which] - 1 : 1)));
     bool done0 = false;
-    if (seen && last_it[which] <= 1) {
+    const bool eligible = seen && last_it[which] <= 1;
+    if (eligible && __builtin_popcount(zero_hist[which] & 0xffu) >= 2) {
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       done0 = h_ctl[0] != 0;
@@ -1529,6 +1535,7 @@ struct Ctx {
       chunk = it < 8 ? 1 : std::min(16, it / 4);
     }
     last_it[which] = h_ctl[1];
+    if (eligible) zero_hist[which] = (zero_hist[which] << 1) | (h_ctl[1] == 0 ? 1u : 0u);
     if (h_ctl[0] == 3) throw Error(PUCFEM_ENOCONV, "MG-PCG residual is not finite (iteration " + std::to_string(h_ctl[1]) + ")");
     if (h_ctl[0] != 1) throw Error(PUCFEM_ENOCONV, "MG-PCG did not converge within maxit=" + std::to_string(maxit));
     return h_ctl[1];
