@@ -59,6 +59,9 @@ def parse():
                     help="per-launch events on every kernel class (default: the roofline kernel only)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="time the steps without per-launch kernel events (no roofline block)")
+    ap.add_argument("--kernel-timing-steps", type=int, default=5,
+                    help="per-launch kernel events on the last N of the timed steps (each timed launch costs a few "
+                         "us of dispatch: events on all 20 steps slowed the step by ~2 %%, r10i)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--fine-steps", type=int, default=200)
     ap.add_argument("--steady-after", type=int, default=100,
@@ -139,12 +142,16 @@ def main():
         log(f"[bench] warmup step {k}: CG visc/p/p2 = {st.it_visc}/{st.it_p}/{st.it_p2}")
     # per-launch events on the roofline kernel only (each timed launch costs a few us of dispatch);
     # --kernel-table times every kernel class of the table below
-    sim.ctx.timing(0 if a.no_kernel_timing else (1 if a.kernel_table or a.precond != "mg" else 2))
+    kt_mode = 0 if a.no_kernel_timing else (1 if a.kernel_table or a.precond != "mg" else 2)
+    kt_steps = min(a.steps, max(1, a.kernel_timing_steps)) if kt_mode else 0
     barrier()
     sim.ctx.sync()
     n0, b0 = sim.ctx.counters()
     t0 = time.perf_counter()
-    stats = sim.step(a.steps)
+    stats = list(sim.step(a.steps - kt_steps)) if a.steps > kt_steps else []
+    if kt_steps:  # the last kt_steps timed steps carry the per-launch events (pucfem_timing_enable syncs)
+        sim.ctx.timing(kt_mode)
+        stats += list(sim.step(kt_steps))
     sim.ctx.sync()
     barrier()
     dt_local = time.perf_counter() - t0
@@ -240,7 +247,7 @@ def main():
     dom = max(ktab, key=lambda k: ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"]) if ktab else None
     ms_step = 1e3 * elapsed / a.steps
     for k in ktab:  # share of the timed region (the dye stream's kernels overlap the main stream's)
-        ktab[k]["ms_per_step"] = ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"] / a.steps
+        ktab[k]["ms_per_step"] = ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"] / kt_steps
         ktab[k]["share"] = ktab[k]["ms_per_step"] / ms_step
     if dom in ktab:
         kd = ktab[dom]
@@ -264,6 +271,7 @@ def main():
         "frac": step_gbs / HBM_PEAK_GBS / world, "floor_ms_per_step": bytes_per_step / (HBM_PEAK_GBS * 1e9 * world) * 1e3,
         "counted": "every kernel's algorithmic bytes (vectors once per row read or written, stored operators per entry)"}
     rec["kernels"] = ktab
+    rec["kernels_timed_steps"] = f"the last {kt_steps} of the {a.steps} timed steps" if kt_steps else None
     rec["kernel_batch"] = batch
     if a.steady_after > 0:
         rec["steady"] = steady_leg(sim, a.warmup + a.steps, a.steady_after, a.steady_steps, barrier, allmax, allsum,
