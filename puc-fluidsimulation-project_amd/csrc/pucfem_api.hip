@@ -940,7 +940,9 @@ struct Ctx {
     const int nbs = nb_for(A.nslices);
     const double bytes_sk = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                             32.0 * NR * (double)(A.own() - hf.rows);
-    auto pair_step = [&](double c1a, double c2a, double c1b, double c2b, bool check, bool fin) {
+    // first: the pair is the solve's steps 0 and 1: step 0 reads no d and both halves write the |r_0|^2 /
+    // |b|^2 partials (part_a / part_b: the SELL blocks at their block indices, the face items after them)
+    auto pair_step = [&](double c1a, double c2a, double c1b, double c2b, bool check, bool fin, bool first = false) {
       FaceDev fs = fc;
       fs.nb = 0;
       ChebVecs2 v1{}, v2{};
@@ -975,11 +977,13 @@ struct Ctx {
       const double fin_sk = fin ? 12.0 * NR * (double)(A.own() - hf.rows) : 0.0;
       double* pc = check ? part_c : nullptr;
       with_c16(A, [&](auto c16) {
-        klaunch(-1, bytes_sk, k_vcheb<decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a, c2a, 0,
-                (const int*)ctl, (double*)nullptr, (double*)nullptr, RedOut{});
+        klaunch(-1, bytes_sk - (first ? 4.0 * NR * (double)(A.own() - hf.rows) : 0.0), k_vcheb<decltype(c16)::value>,
+                dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a, c2a, first ? 1 : 0, (const int*)ctl,
+                first ? part_a : (double*)nullptr, first ? part_b : (double*)nullptr, RedOut{});
         KCHK();
-        klaunch(12, bytes_f, k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p, c1a, c2a, c1b, c2b, (const int*)ctl, pc,
-                (int32_t)nbs);
+        klaunch(12, bytes_f - (first ? 4.0 * NR * (double)hf.rows : 0.0), k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p,
+                c1a, c2a, c1b, c2b, (const int*)ctl, pc, (int32_t)nbs, first ? 1 : 0,
+                first ? part_a : (double*)nullptr, first ? part_b : (double*)nullptr);
         KCHK();
         klaunch(-1, bytes_sk + fin_sk, k_vcheb<decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
                 c1b, c2b, 0, (const int*)ctl, pc, (double*)nullptr, RedOut{});
@@ -1000,11 +1004,25 @@ struct Ctx {
     // no residual checks, no reductions and no host round trip.  (The bound is rigorous for the interval
     // [visc_lo, 1 + visc_R], which tests/test_host_assembly.py checks against the spectrum; the
     // adaptive test it replaces needed one extra step per solve to see the passing residual.)
-    const int nb0 = nb;  // the first step's partial count
-    step(0, 0.0, 1.0 / theta);
+    // With step pairs the solve starts with the pair (0, 1) -- one face pass where step 0 and a single step
+    // 1 took two -- and the step count K decides the rest: K <= 2 is done (the finish runs as k_visc_fin),
+    // K = 3 / 4 add a single step / a pair with the finish.  Without pairs: step 0 alone.
+    double rho_old = 1.0 / sigma;
+    int done = 1;
+    int nb0 = nb;  // the first step's partial count
+    const bool pair0 = pairs && !ro(redbuf, CNT_VCHEB, 2 * NR).out;
+    if (pair0) {
+      const double rho = 1.0 / (2.0 * sigma - rho_old);
+      pair_step(0.0, 1.0 / theta, rho * rho_old, 2.0 * rho / delta, true, false, true);
+      rho_old = rho;
+      done = 2;
+      nb0 = nbs + (int)hf.items;
+    } else {
+      step(0, 0.0, 1.0 / theta);
+    }
     if (sl_gate == 1) dye_flush();
     Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
-    if (ro(redbuf, CNT_VCHEB, 2 * NR).out) {
+    if (!pair0 && ro(redbuf, CNT_VCHEB, 2 * NR).out) {
       red_done(redbuf, 2 * NR, false);
     } else {
       rr = reduce_global(part_a, nb0, NR, false, 0);
@@ -1016,8 +1034,6 @@ struct Ctx {
     HIPCHK(hipEventRecord(have_r0, st));
     // while the host waits for |r_0|, the GPU already runs the steps the last solve certainly needed
     // (one fewer than its count): the round trip hides behind them
-    double rho_old = 1.0 / sigma;
-    int done = 1;
     // (step pairs: two steps per pass while at least two are due)
     auto pair_coefs = [&](double& c1a, double& c2a, double& c1b, double& c2b) {
       const double ra = 1.0 / (2.0 * sigma - rho_old), rb = 1.0 / (2.0 * sigma - ra);
@@ -1044,7 +1060,8 @@ struct Ctx {
     };
     // with step pairs only whole pairs go ahead of the round trip, and at least the last two steps
     // wait for it (so that they can run as one pair with the finish)
-    advance(pairs ? 1 + 2 * std::max(0, (last_it[which] - 3) / 2) : std::max(1, last_it[which] - 1));
+    advance(pair0 ? 2 + 2 * std::max(0, (last_it[which] - 4) / 2)
+                  : (pairs ? 1 + 2 * std::max(0, (last_it[which] - 3) / 2) : std::max(1, last_it[which] - 1)));
     HIPCHK(hipEventSynchronize(have_r0));
     timer.pool.push_back(have_r0);
     if (vcc.pending) {  // the previous solve's post-check (its copy preceded step 0 on the stream)
@@ -1080,6 +1097,32 @@ struct Ctx {
       last_it[which] = 0;
       return 0;
     }
+    // the a-posteriori check of the next solve: |r_kc|^2 (kc = K - 1, reduced from part_c) against
+    // |r_0| / T_kc(sigma)
+    auto post_check = [&](int kc, int nck) {
+      hipLaunchKernelGGL(k_reduce, dim3(NR), dim3(RB), 0, st, (const double*)part_c, nck, MAXB, NR, 0, redbuf + 48);
+      KCHK();
+      if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
+      HIPCHK(hipMemcpyAsync(h_pinned + 32, redbuf + 48, NR * sizeof(double), hipMemcpyDeviceToHost, st));
+      double tm = 1.0, tk = sigma;  // T_kc(sigma)
+      for (int k = 1; k < kc; ++k) {
+        const double tn = 2.0 * sigma * tk - tm;
+        tm = tk;
+        tk = tn;
+      }
+      vcc.pending = true;
+      vcc.nr = NR;
+      for (int c = 0; c < NR; ++c) {
+        vcc.bound2[c] = h_pinned[c] / (tk * tk);
+        vcc.floor2[c] = 1e-28 * h_pinned[8 + c];  // rounding: |r| ~ 1e-14 |b| is as far as it resolves
+      }
+    };
+    if (pair0 && done >= K) {  // the first pair did it (x_2, or more steps already launched)
+      if (K >= 2) post_check(1, nbs + (int)hf.items);  // |r_1|^2: the first pair's check partials
+      *out = xa;
+      last_it[which] = std::max(K, 1);
+      return done;
+    }
     if (done < K) {
       // the last step also reduces |r_{K-1}|^2 (its input's residual) for the a-posteriori check; with
       // step pairs it is the second step of a pair when an even number of steps is left
@@ -1103,22 +1146,7 @@ struct Ctx {
         nck = nb;
       }
       if (fuse) *fin_done = true;
-      hipLaunchKernelGGL(k_reduce, dim3(NR), dim3(RB), 0, st, (const double*)part_c, nck, MAXB, NR, 0, redbuf + 48);
-      KCHK();
-      if (dist()) comm->allreduce(redbuf + 48, NR, false, st);
-      HIPCHK(hipMemcpyAsync(h_pinned + 32, redbuf + 48, NR * sizeof(double), hipMemcpyDeviceToHost, st));
-      double tm = 1.0, tk = sigma;  // T_kc(sigma)
-      for (int k = 1; k < kc; ++k) {
-        const double tn = 2.0 * sigma * tk - tm;
-        tm = tk;
-        tk = tn;
-      }
-      vcc.pending = true;
-      vcc.nr = NR;
-      for (int c = 0; c < NR; ++c) {
-        vcc.bound2[c] = h_pinned[c] / (tk * tk);
-        vcc.floor2[c] = 1e-28 * h_pinned[8 + c];  // rounding: |r| ~ 1e-14 |b| is as far as it resolves
-      }
+      post_check(kc, nck);
     }
     advance(K);  // (steps beyond K, already launched, only reduce the residual further)
     *out = xa;  // x_done, done >= K

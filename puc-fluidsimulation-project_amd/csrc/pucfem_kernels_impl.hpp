@@ -1006,8 +1006,13 @@ constexpr int VP_WK = (VP_W + BS - 1) / BS;
 #endif
 constexpr int VP_G = PUCFEM_VP_G;  // rows of a thread loaded together (compile-time: an A/B knob)
 static_assert(VP_WK % VP_G == 0, "the window rows of a thread go in groups");
+// first: step a is the solve's step 0 (d_a is not read: c1a = 0) and the block also writes the partials of
+// |r_0|^2 and |b|^2 over its own rows into part_r0 / part_b0 (values c at c * MAXB + part_off + block, as
+// k_vcheb's first step does for the skeleton rows at their own block indices)
 __global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
-                                                   double c2b, const int* ctl, double* part_rr, int32_t part_off) {
+                                                   double c2b, const int* ctl, double* part_rr, int32_t part_off,
+                                                   int first = 0, double* part_r0 = nullptr,
+                                                   double* part_b0 = nullptr) {
   __shared__ dbl2 lx[VP_W];
   __shared__ double sh[4];
   if (ctl[0]) return;
@@ -1028,6 +1033,7 @@ __global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, doub
   // window is clamped to the window's first row (a valid address; not stored)
   dbl2 bt[VP_WK];
   flt2 dt[VP_WK];
+  double r00 = 0.0, r01 = 0.0, b00 = 0.0, b01 = 0.0;  // (first) |r_0|^2, |b|^2 over the block's own rows
 #pragma unroll
   for (int k0 = 0; k0 < VP_WK; k0 += VP_G) {
     if (k0 * BS >= nw) break;
@@ -1049,7 +1055,7 @@ __global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, doub
 #pragma unroll
       for (int q = 0; q < 6; ++q) xv[r][q] = v.xa[nb[r][q]];
       br[r] = v.b[row[r]];
-      dr[r] = v.da[row[r]];
+      dr[r] = first ? flt2{0.0f, 0.0f} : v.da[row[r]];
     }
 #pragma unroll
     for (int r = 0; r < VP_G; ++r) {
@@ -1062,9 +1068,17 @@ __global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, doub
         ax0 += a[1 + q] * xv[r][q].x;
         ax1 += a[1 + q] * xv[r][q].y;
       }
-      const double dn0 = c1a * (double)dr[r].x + c2a * (br[r].x - ax0);
-      const double dn1 = c1a * (double)dr[r].y + c2a * (br[r].y - ax1);
+      const double ra0 = br[r].x - ax0, ra1 = br[r].y - ax1;
+      // (k_vcheb's first step: dn = c2 r; the general form with c1a = 0 and d = 0 is the same value)
+      const double dn0 = first ? c2a * ra0 : c1a * (double)dr[r].x + c2a * ra0;
+      const double dn1 = first ? c2a * ra1 : c1a * (double)dr[r].y + c2a * ra1;
       if (ok[r]) lx[w] = dbl2{xv[r][6].x + dn0, xv[r][6].y + dn1};
+      if (first && ok[r] && w0 + w >= t0 && w0 + w < t1) {
+        r00 += ra0 * ra0;
+        r01 += ra1 * ra1;
+        b00 += br[r].x * br[r].x;
+        b01 += br[r].y * br[r].y;
+      }
       bt[k0 + r] = br[r];
       dt[k0 + r] = flt2{(float)dn0, (float)dn1};
     }
@@ -1129,7 +1143,17 @@ __global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, doub
       rr1 += rs1 * rs1;
     }
   }
-  if (!part_rr) return;  // the solve's last step: |r_{a+1}|^2 partials for the a-posteriori check
+  if (first && part_r0) {  // |r_0|^2 and |b|^2 partials of the solve's step 0
+    const double p0 = block_sum(r00, sh), p1 = block_sum(r01, sh);
+    const double q0 = block_sum(b00, sh), q1 = block_sum(b01, sh);
+    if (threadIdx.x == 0) {
+      part_r0[part_off + blockIdx.x] = p0;
+      part_r0[(int64_t)MAXB + part_off + blockIdx.x] = p1;
+      part_b0[part_off + blockIdx.x] = q0;
+      part_b0[(int64_t)MAXB + part_off + blockIdx.x] = q1;
+    }
+  }
+  if (!part_rr) return;  // |r_{a+1}|^2 partials for the a-posteriori check
   const double ta = block_sum(rr0, sh);
   const double tb = block_sum(rr1, sh);
   if (threadIdx.x == 0) {
