@@ -1092,7 +1092,7 @@ struct Ctx {
       if (tk < need) throw Error(PUCFEM_ENOCONV, "Chebyshev iteration would not converge within maxit=" + std::to_string(maxit));
       K = std::max(K, k);
     }
-    if (pass0 && done == 1) {
+    if (pass0 && (done == 1 || (pair0 && done == 2))) {  // y itself passes (the first pair left it intact)
       *out = y;
       last_it[which] = 0;
       return 0;
