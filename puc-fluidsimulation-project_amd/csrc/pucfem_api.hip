@@ -1704,16 +1704,19 @@ struct Ctx {
       it = 0;
     } else if (use_mg) {
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
-      if (proj) project_update(proj_slot(which), yst, bh, cg_r[0]);
+      // (the projection update and the finish in one pass: sc is null on the multigrid path)
+      if (proj) project_update(proj_slot(which), yst, bh, cg_r[0], pout);
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
       it = cg<1>(dPp, HFace{}, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
     }
-    algo_bytes += (20.0 + (sc ? 8.0 : 0.0)) * (double)n;  // master_of, y (, s) read; p written
-    hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
-                       (double*)nullptr, dmaster_of);
-    KCHK();
+    if (!(use_mg && proj)) {
+      algo_bytes += (20.0 + (sc ? 8.0 : 0.0)) * (double)n;  // master_of, y (, s) read; p written
+      hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
+                         (double*)nullptr, dmaster_of);
+      KCHK();
+    }
     halo(pout);
     return it;
   }
@@ -1840,15 +1843,25 @@ struct Ctx {
   // in pav[which]: then A v = r0 - r_final (A y = b - r_final for the first direction, whose solve
   // started from the warm start with x0 = 0) instead of an SpMV -- exact up to the CG recurrence's
   // rounding drift.
-  void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr) {
+  // pfin (with r_final): also the pressure solve's finish p = y with the slaves copied from their masters
+  // (k_cg_fin's work, unscaled), in the same pass
+  void project_update(int which, const double* y, const double* b = nullptr, const double* r_final = nullptr,
+                      double* pfin = nullptr) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     double *v = pv[which], *av = pav[which];
     if (r_final) {  // v = y - x0 and A v = r0 - r_final in one pass
       const bool whole = proj_m[which] == 0;
-      algo_bytes += 48.0 * (double)n;
-      hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], v,
-                         whole ? b : (const double*)av, r_final, av);
+      if (pfin) {
+        algo_bytes += 68.0 * (double)n;  // + master_of read, p written
+        hipLaunchKernelGGL(k_diff2_fin, dim3(grid_ew(n)), dim3(BS), 0, st, (int64_t)n, y,
+                           (const double*)proj_x0[which], v, whole ? b : (const double*)av, r_final, av,
+                           (const int32_t*)dmaster_of, pfin);
+      } else {
+        algo_bytes += 48.0 * (double)n;
+        hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], v,
+                           whole ? b : (const double*)av, r_final, av);
+      }
       KCHK();
     } else {
       hipLaunchKernelGGL(k_diff, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, proj_x0[which], v);

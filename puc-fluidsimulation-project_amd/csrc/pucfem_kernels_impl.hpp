@@ -658,6 +658,21 @@ __global__ void k_diff2(int64_t n, const double* __restrict__ a, const double* _
   }
 }
 
+// k_diff2 and the pressure solve's finish (k_cg_fin with master_of, unscaled) in one pass: the projection's
+// v = y - x0 and A v = a2 - r_final, and p = y with every periodic slave row copied from its master
+__global__ void k_diff2_fin(int64_t n, const double* __restrict__ y, const double* __restrict__ x0,
+                            double* __restrict__ v, const double* a2, const double* __restrict__ rf, double* av,
+                            const int32_t* __restrict__ master_of, double* __restrict__ p) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    const double yr = y[r], x = x0[r], a = a2[r], f = rf[r];
+    const int32_t m = master_of[r];
+    const double pr = m >= 0 ? y[m] : yr;
+    stnt(v + r, yr - x);
+    stnt(av + r, a - f);
+    p[r] = pr;
+  }
+}
+
 // ----------------------------------------------------------------------------- CG, direction updated in place
 // Jacobi-scaled CG (no preconditioner: the viscous solve, the Jacobi pressure path) with the direction
 // formed in the update kernel instead of at the direction kernel's gathered columns: the SpMV then
