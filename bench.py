@@ -255,7 +255,11 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(f"L{a.level}_n{world}", {}).get(dom.split()[0])
+                pj = json.load(open(pmc))
+                traffic = pj.get(f"L{a.level}_n{world}", {}).get(dom.split()[0])
+                ratio = pj.get(f"L{a.level}_n{world}_ratio", {}).get(dom.split()[0])
+                if ratio is not None:  # basis-size dependent passes: PMC / algorithmic ratio x these launches' bytes
+                    traffic = ratio * kd["bytes_per_launch"]
             except Exception:
                 traffic = None
         rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "kernel_share": kd["share"],

@@ -135,6 +135,21 @@ def main():
             n = sum(res["kernels"][k]["dispatches_fetch"] for k in ks)
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
                                for k in ks) / n
+    # the projection passes' bytes depend on the basis size M (their template argument): the ratio of PMC to
+    # algorithmic bytes over the instances with M >= 16 ((4 M + 24) n for k_mdot2, (4 M + 32) n for k_pcomb),
+    # which bench.py applies to the algorithmic bytes of the launches it timed
+    ratios = {}
+    if nrows:
+        for key, extra in (("k_mdot2", 24.0), ("k_pcomb", 32.0)):
+            pmc = alg = 0.0
+            for k, e in res["kernels"].items():
+                mm = re.match(r"^" + key + r"<(\d+)>", k)
+                if mm and int(mm.group(1)) >= 16 and "hbm_bytes_per_launch" in e:
+                    pmc += e["hbm_bytes_per_launch"] * e["dispatches_fetch"]
+                    alg += (4.0 * int(mm.group(1)) + extra) * nrows * e["dispatches_fetch"]
+            if alg > 0:
+                ratios[key] = pmc / alg
+    res[f"L{level}_n{world}_ratio"] = ratios
     res[f"L{level}_n{world}"] = summary
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({"calibration": res["calibration"], f"L{level}_n{world}": summary}))
