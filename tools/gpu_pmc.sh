@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/prof_$TAG
 for c in FETCH_SIZE WRITE_SIZE; do
   d=/tmp/prof_$TAG/$( [ $c = FETCH_SIZE ] && echo fetch || echo write )
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c -d $d -o run --output-format csv -- \
-    python "$ROOT/bench.py" "$@" --steps 1 --warmup 1 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.out" 2> "$OUT/pmc_$c.err" \
+    python "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-secondary "$@" > "$OUT/pmc_$c.out" 2> "$OUT/pmc_$c.err" \
     || { echo "pmc $c failed" >&2; tail -5 "$OUT/pmc_$c.err" >&2; exit 1; }
 done
 cp "$OUT/pmc_FETCH_SIZE.out" "$OUT/bench.out"

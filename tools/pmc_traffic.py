@@ -78,12 +78,18 @@ def main():
     res = {"counters": "FETCH_SIZE, WRITE_SIZE (separate passes, --kernel-trace only)", "kernels": {}}
     fr, fw = 2.0 * 1024.0, 1.0 * 1024.0
     check = None
-    cal = [k for k in kern if short(k[0]).endswith("k_diff2")]
-    if cal and nrows and fetch.get(cal[0]) and write.get(cal[0]):
-        f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
-        w_avg = sum(write[cal[0]]) / len(write[cal[0]])
-        check = {"kernel": "k_diff2", "nrows": nrows, "algorithmic_read": 32.0 * nrows,
-                 "corrected_read": f_avg * fr, "algorithmic_write": 16.0 * nrows, "corrected_write": w_avg * fw}
+    # calibration kernel: k_diff2_fin (round 4: the projection update fused with the pressure finish), a pure
+    # elementwise pass: 36 B/row read (y, x0, A v or b, r_final fp64; master_of int32; the slave rows' master
+    # values are 0.05 % of the rows) and 24 B/row written (v, A v, p); k_diff2 (32 / 16 B/row) before it
+    check = None
+    for name, rd, wr in (("k_diff2_fin", 36.0, 24.0), ("k_diff2", 32.0, 16.0)):
+        cal = [k for k in kern if short(k[0]).endswith(name)]
+        if cal and nrows and fetch.get(cal[0]) and write.get(cal[0]):
+            f_avg = sum(fetch[cal[0]]) / len(fetch[cal[0]])
+            w_avg = sum(write[cal[0]]) / len(write[cal[0]])
+            check = {"kernel": name, "nrows": nrows, "algorithmic_read": rd * nrows, "corrected_read": f_avg * fr,
+                     "algorithmic_write": wr * nrows, "corrected_write": w_avg * fw}
+            break
     res["calibration"] = {"read_bytes_per_unit": fr, "write_bytes_per_unit": fw,
                           "note": "FETCH_SIZE x2 KiB, WRITE_SIZE x1 KiB (guide's gfx950 corrections)",
                           "check": check}
@@ -152,7 +158,8 @@ def main():
     res[f"L{level}_n{world}_ratio"] = ratios
     res[f"L{level}_n{world}"] = summary
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps({"calibration": res["calibration"], f"L{level}_n{world}": summary}))
+    print(json.dumps({"calibration": res["calibration"], f"L{level}_n{world}": summary,
+                      f"L{level}_n{world}_ratio": res[f"L{level}_n{world}_ratio"]}))
 
 
 if __name__ == "__main__":
