@@ -181,7 +181,9 @@ def main():
         for kid, nm in ((0, "k_cheb"), (1, "k_resid"), (2, "k_cg_dir"), (16 * 8, "k_cheb+8 coarse launches"),
                         (256, "k_cheb, idle GPU at each launch"), (3, "k_cheb face rows only"),
                         (4, "k_cheb skeleton (SELL) rows only"), (5, "k_cg_dir face rows only"),
-                        (6, "k_cg_dir skeleton (SELL) rows only")):
+                        (6, "k_cg_dir skeleton (SELL) rows only"), (7, "k_div (SoA u, as in the step)"),
+                        (8, "k_div face rows only"), (9, "k_div skeleton (SELL) rows only"),
+                        (10, "k_div on interleaved (x, y) u"), (11, "k_div interleaved, face rows only")):
             mb, me, by = ct.c_double(), ct.c_double(), ct.c_double()
             L.check(L.lib().pucfem_bench_kernel(sim.ctx.h, kid, 20, ct.byref(mb), ct.byref(me), ct.byref(by)),
                     sim.ctx.h)

@@ -587,7 +587,11 @@ struct Ctx {
                  const double* w, int32_t* nf, RedOut ro = RedOut{}) {
     const MeshDev M{mx, my, mtri, mesh.T};
     if (lat_sl) {
-      klaunch(4, 8.0 * 6 * (double)n, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
+      // per row: coordinates 16, u 16, c 8 (the departure triangle's vertices lie near the row: their
+      // coordinate and c lines are the rows' own), home face 4, lattice cell entries 8 and fast-accept
+      // radii 8 (two triangles per node), the mixing weight 8, c_new written 8
+      const double sl_bytes = (16.0 + 16.0 + 8.0 + 4.0 + 8.0 + 8.0 + (w ? 8.0 : 0.0) + 8.0) * (double)n;
+      klaunch(4, sl_bytes, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
       klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
@@ -922,14 +926,13 @@ struct Ctx {
       // check: the post-check's |r_it|^2 partials (part_c)
       double* pr = it == 0 ? part_a : (check ? part_c : (double*)nullptr);
       with_c16(A, [&](auto c16) {
-        klaunch(9, it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes, k_vcheb<decltype(c16)::value>, dim3(nb),
+        // fin: + s, u read and u*, the increment written - d, x_out
+        klaunch(9, (it == 0 ? bytes - 4.0 * NR * (double)A.own() : bytes) + (fin ? 12.0 * NR * (double)A.own() : 0.0),
+                k_vcheb<decltype(c16)::value>, dim3(nb),
                 dim3(BS), A.view(), fc, val, v, c1, c2, it == 0 ? 1 : 0, (const int*)ctl, pr, pb, r0);
       });
       KCHK();
-      if (fin) {  // the solve's output is u* (haloed by viscous()), x_out was not written
-        algo_bytes += 12.0 * NR * (double)A.own();  // + s, u read and u*, the increment written - d, x_out
-        return;
-      }
+      if (fin) return;  // the solve's output is u* (haloed by viscous()), x_out was not written
       halo2(xb);
       std::swap(xa, xb);
     };
@@ -4777,6 +4780,31 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
                                   ff, (const float*)B.Aval, (const float*)c.r32, (const float*)B.x, B.res,
                                   (const int*)nullptr);
             break;
+          case 7:   // k_div as in the step (SoA u, the pressure rhs, partials)
+          case 8:   // its face part alone
+          case 9:   // its SELL (skeleton) part alone
+          case 10:  // k_div on interleaved (x, y) pairs
+          case 11:  // the same, face part alone
+            with_c16(c.dP, [&](auto d16) {
+              constexpr bool D16 = decltype(d16)::value;
+              const FaceDev fd = c.fK.part();
+              SellDev dv = c.dP.view();
+              if (kernel == 8 || kernel == 11) dv.nslices = 0;
+              const int g = kernel == 8 || kernel == 11 ? fd.nb + 8 : kernel == 9 ? c.div_grid() - fd.nb : c.div_grid();
+              const FaceDev fk = kernel == 9 ? FaceDev{} : fd;
+              const bool aos = kernel >= 10;
+              const double* xa = aos ? reinterpret_cast<const double*>(c.vx2[0]) : (const double*)c.ux;
+              if (aos)
+                hipExtLaunchKernelGGL(k_div<D16, true>, dim3(g), dim3(BS), 0, c.st, a, e, 0, dv, fk, (const double*)c.dGx,
+                                      (const double*)c.dGy, xa, (const double*)nullptr, (const double*)c.das1,
+                                      (double*)nullptr, (const double*)c.dmp, -1.0, c.braw, c.part_d, RedOut{});
+              else
+                hipExtLaunchKernelGGL(k_div<D16, false>, dim3(g), dim3(BS), 0, c.st, a, e, 0, dv, fk,
+                                      (const double*)c.dGx, (const double*)c.dGy, xa, (const double*)c.uy,
+                                      (const double*)c.das1, (double*)nullptr, (const double*)c.dmp, -1.0, c.braw,
+                                      c.part_d, RedOut{});
+            });
+            break;
           default:
             hipExtLaunchKernelGGL(k_cg_dir<1, 8, true, C16>, dim3(nb), dim3(BS), 0, c.st, a, e, 0, A.view(), fpt,
                                   (const double*)c.dKp_raw, v, c.lp.n_ghost, (const double*)one, 1, 1,
@@ -4795,6 +4823,13 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
       case 5: by = 32.0 * fr; break;
       case 6: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk; break;
       case 1: by = (4.0 + A.idx_bytes()) * (double)A.nnz + (12.0 + rb) * sk + 12.0 * fr; break;
+      case 7:
+      case 10:
+        by = (16.0 + c.dP.idx_bytes()) * (double)c.dP.nnz + c.dP.row_bytes() * (double)c.dP.nrows + 24.0 * (double)c.lp.n_own;
+        break;
+      case 8:
+      case 11: by = 24.0 * (double)c.fK.rows; break;
+      case 9: by = (16.0 + c.dP.idx_bytes()) * (double)c.dP.nnz + (c.dP.row_bytes() + 24.0) * (double)c.dP.nrows; break;
       default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk + 32.0 * fr;
     }
     MgLevel& Lc = c.mg[c.mg.size() >= 3 ? c.mg.size() - 3 : 0];

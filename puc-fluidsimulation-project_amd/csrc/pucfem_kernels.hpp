@@ -243,6 +243,35 @@ __device__ __forceinline__ void block_slices_n(int64_t nslices, int64_t nb, int6
   s0 = (nslices * b) / nb;
   s1 = (nslices * (b + 1)) / nb;
 }
+// Roles in a launch of face blocks (nbf of them: lattice face rows, face_rows / face_rows_k) and skeleton
+// blocks (the other nsk = gridDim.x - nbf: SELL slices, block_slices_n).  The skeleton blocks are
+// latency-bound (index -> value -> gather chains over few rows) and the face blocks stream, so with
+// PUCFEM_SKEL_SPREAD = p > 0 the skeleton blocks are dealt in units of 8 consecutive blocks evenly over
+// the first p % of the grid instead of all first; units of 8 keep a face block's index congruent to its
+// hardware block index mod 8 (the face kernels' XCD-grouped item order) and a skeleton unit's blocks on
+// the 8 XCDs.  p = 0: the skeleton blocks first (nsk a multiple of 8 either way: Ctx::sell_blocks).
+#ifndef PUCFEM_SKEL_SPREAD
+#define PUCFEM_SKEL_SPREAD 0
+#endif
+struct BlockRole {
+  bool face;
+  int32_t idx;  // face item / skeleton block index
+  int32_t nsk;  // skeleton blocks
+};
+__device__ __forceinline__ BlockRole block_role(int32_t nbf) {
+  const int32_t G = (int32_t)gridDim.x, b = (int32_t)blockIdx.x, nsk = G - nbf;
+  if (nbf <= 0) return BlockRole{false, b, G};
+  if (nsk <= 0) return BlockRole{true, b, 0};
+  if (PUCFEM_SKEL_SPREAD > 0 && (nsk & 7) == 0) {
+    const int32_t s8 = nsk >> 3, u = b >> 3;
+    const int32_t span = (int32_t)(((int64_t)(G >> 3) * PUCFEM_SKEL_SPREAD) / 100);
+    const int32_t P = span / s8 > 1 ? span / s8 : 1;
+    const int32_t k = u / P;
+    if (u - k * P == 0 && k < s8) return BlockRole{false, (k << 3) | (b & 7), nsk};
+    return BlockRole{true, b - 8 * (k + 1 < s8 ? k + 1 : s8), nsk};
+  }
+  return b >= nsk ? BlockRole{true, b - nsk, nsk} : BlockRole{false, b, nsk};
+}
 // row range of this block for row-wise (non-SpMV) kernels, aligned to the same slices
 __device__ __forceinline__ void block_rows(int64_t nrows, int64_t& r0, int64_t& r1) {
   int64_t s0, s1;

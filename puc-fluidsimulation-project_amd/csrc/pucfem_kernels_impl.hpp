@@ -19,9 +19,24 @@ namespace dev {
 #ifndef PUCFEM_DIV_K
 #define PUCFEM_DIV_K 2
 #endif
+// launch bounds of the gather kernels (k_cg_dir, k_vcheb, k_vcheb_pair, k_div, k_grad_proj, k_sl):
+// PUCFEM_GATHER_WAVES = w > 0 asks for >= w waves per SIMD (a register cap), 0: the compiler's choice
+#ifndef PUCFEM_GATHER_WAVES
+#define PUCFEM_GATHER_WAVES 0
+#endif
+#if PUCFEM_GATHER_WAVES > 0
+#define LB_GATHER __launch_bounds__(BS, PUCFEM_GATHER_WAVES)
+#else
+#define LB_GATHER __launch_bounds__(BS)
+#endif
 #ifndef PUCFEM_GRADP_K
 #define PUCFEM_GRADP_K 4
 #endif
+
+// SELL row dot product (defined with the multigrid kernels below)
+template <bool C16, typename T, typename VT, typename G>
+__device__ __forceinline__ T sell_row_dot_g(const SellDev& A, const VT* __restrict__ val, const G& gx, int64_t s,
+                                            int lane);
 
 // ----------------------------------------------------------------------------- lattice face rows
 // fn(F, lf, t, i, j) for the interior rows of the face part that block b of nbf runs (work items: chunks
@@ -137,8 +152,9 @@ __device__ __forceinline__ void face_grad_v(const double* c, const double (&v)[6
 template <bool C16>
 __global__ __launch_bounds__(BS) void k_spmv(SellDev A, FaceDev fc, const double* __restrict__ val,
                                              const double* __restrict__ x, double* __restrict__ y) {
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
+    face_rows(fc, role.idx, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
@@ -152,7 +168,7 @@ __global__ __launch_bounds__(BS) void k_spmv(SellDev A, FaceDev fc, const double
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+  block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -217,10 +233,11 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
       bb[c] += b * b;
     }
   };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     // groups of K rows per thread, every gathered value of a group loaded first (face_rows_k)
     constexpr int K = face_k(NR == 1 ? PUCFEM_INIT_K : 2);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -255,7 +272,7 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t off = A.off[s];
@@ -357,7 +374,7 @@ __device__ __forceinline__ void dir_slice(const SellDev& A, const double* __rest
 #define PUCFEM_DIR_K2 1
 #endif
 template <int NR, int WMAX, bool NT, bool C16, bool ZF = false>
-__global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
+__global__ LB_GATHER void k_cg_dir(SellDev A, FaceDev fc, const double* __restrict__ val, CgVecs<NR> v,
                                                int64_t n_ghost, const double* part_rr, int nb_rr, int stride_rr,
                                                const double* part_bb, int nb_bb, int stride_bb, double* scal,
                                                int* ctl, int it, int maxit, double tol2, double* part_pq,
@@ -400,10 +417,11 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
   // the first iteration's direction is r itself: p_old is neither read nor needed (k_cg_init does not
   // clear it; a uniform branch skips its loads)
   const bool first = it == 0;
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     // groups of K rows per thread, every load of the group first (face_rows_k)
     constexpr int K = face_k(NR == 1 ? PUCFEM_DIR_K1 : PUCFEM_DIR_K2);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -449,7 +467,7 @@ __global__ __launch_bounds__(BS) void k_cg_dir(SellDev A, FaceDev fc, const doub
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) dir_slice<NR, WMAX, NT, C16, ZF>(A, val, v, beta, first, s, lane, pq);
   }
@@ -696,9 +714,10 @@ __global__ __launch_bounds__(BS) void k_cgr_dir(SellDev A, FaceDev fc, const dou
     rq[c] += r * q;
     qq[c] += q * q;
   };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     constexpr int K = face_k(NR == 1 ? 4 : 2);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -734,7 +753,7 @@ __global__ __launch_bounds__(BS) void k_cgr_dir(SellDev A, FaceDev fc, const dou
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t row = sell_row(A, s, lane);
@@ -866,7 +885,7 @@ struct ChebVecs2 {
   float* inc[2];
 };
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs2 v,
+__global__ LB_GATHER void k_vcheb(SellDev A, FaceDev fc, const double* __restrict__ val, ChebVecs2 v,
                                               double c1, double c2, int first, const int* ctl, double* part_rr,
                                               double* part_bb, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
@@ -897,9 +916,10 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
     bb[0] += br.x * br.x;
     bb[1] += br.y * br.y;
   };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     constexpr int K = face_k(PUCFEM_VCHEB_K);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -934,7 +954,7 @@ __global__ __launch_bounds__(BS) void k_vcheb(SellDev A, FaceDev fc, const doubl
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t row = sell_row(A, s, lane);
@@ -1024,7 +1044,7 @@ static_assert(VP_WK % VP_G == 0, "the window rows of a thread go in groups");
 // first: step a is the solve's step 0 (d_a is not read: c1a = 0) and the block also writes the partials of
 // |r_0|^2 and |b|^2 over its own rows into part_r0 / part_b0 (values c at c * MAXB + part_off + block, as
 // k_vcheb's first step does for the skeleton rows at their own block indices)
-__global__ __launch_bounds__(BS) void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
+__global__ LB_GATHER void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, double c2a, double c1b,
                                                    double c2b, const int* ctl, double* part_rr, int32_t part_off,
                                                    int first = 0, double* part_r0 = nullptr,
                                                    double* part_b0 = nullptr) {
@@ -1320,19 +1340,21 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const dbl2* 
 // read, pucfem_get_field).
 // Optionally the pressure RHS of the row-scaled system: braw = (M + 1e-12) * (-(1/DT) * div)
 // (StokesColor.py:554 with A_pressure = K / (M + 1e-12)).  Partials: [0] max|div|, [1] sum(braw).
-template <bool C16>
-__global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double* __restrict__ gx,
+// AOS: ux points at interleaved (x, y) pairs (uy unused): one 16-B gather per neighbour
+template <bool C16, bool AOS = false>
+__global__ LB_GATHER void k_div(SellDev A, FaceDev fc, const double* __restrict__ gx,
                                             const double* __restrict__ gy, const double* __restrict__ ux,
                                             const double* __restrict__ uy, const double* __restrict__ as1,
                                             double* __restrict__ div, const double* __restrict__ mp, double negidt,
                                             double* __restrict__ braw, double* part, RedOut ro = RedOut{}) {
   __shared__ double sh[4];
   double mx = 0.0, sb = 0.0;
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     // interior rows: the lumped divergence of the face's stencil; area_sum = lumped mass there
     // groups of 2 rows per thread, the 24 gathered values of a group loaded first
     constexpr int K = face_k(PUCFEM_DIV_K);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       const double* c = fc.coef + lf * lat::NCOEF;
@@ -1344,8 +1366,14 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
         lat::neighbours(F, fc.n, t[r], i[r], j[r], nb, in);
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-          vx[r][k] = ux[nb[k]];
-          vy[r][k] = uy[nb[k]];
+          if constexpr (AOS) {
+            const dbl2 q = reinterpret_cast<const dbl2*>(ux)[nb[k]];
+            vx[r][k] = q.x;
+            vy[r][k] = q.y;
+          } else {
+            vx[r][k] = ux[nb[k]];
+            vy[r][k] = uy[nb[k]];
+          }
         }
       }
       const double as = c[lat::C_AS1];
@@ -1368,7 +1396,7 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t off = A.off[s];
@@ -1389,12 +1417,24 @@ __global__ __launch_bounds__(BS) void k_div(SellDev A, FaceDev fc, const double*
             ay[k] = ldnt(gy + e);
           }
 #pragma unroll
-          for (int k = 0; k < WN; ++k) acc += ax[k] * ux[cj[k]] + ay[k] * uy[cj[k]];
+          for (int k = 0; k < WN; ++k) {
+            if constexpr (AOS) {
+              const dbl2 q = reinterpret_cast<const dbl2*>(ux)[cj[k]];
+              acc += ax[k] * q.x + ay[k] * q.y;
+            } else {
+              acc += ax[k] * ux[cj[k]] + ay[k] * uy[cj[k]];
+            }
+          }
         } else {
           for (int k = 0; k < w; ++k) {
             const int64_t e = off + (int64_t)k * 64 + lane;
             const int32_t j = sell_col<C16>(A, e, base);
-            acc += ldnt(gx + e) * ux[j] + ldnt(gy + e) * uy[j];
+            if constexpr (AOS) {
+              const dbl2 q = reinterpret_cast<const dbl2*>(ux)[j];
+              acc += ldnt(gx + e) * q.x + ldnt(gy + e) * q.y;
+            } else {
+              acc += ldnt(gx + e) * ux[j] + ldnt(gy + e) * uy[j];
+            }
           }
         }
       });
@@ -1449,10 +1489,11 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
                                                const double* usy, double* ux, double* uy) {
   const double* bx = MODE == 0 ? usx : ux;
   const double* by = MODE == 0 ? usy : uy;
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     // interior rows are never Dirichlet nodes
     constexpr int K = face_k(PUCFEM_GRADP_K);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       const double* c = fc.coef + lf * lat::NCOEF;
@@ -1481,7 +1522,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+  block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -1529,7 +1570,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
 // projection u = u* - DT grad p (mode 0, all rows, StokesColor.py:561-562) or the masked second
 // projection u[interior] -= DT grad p2 (mode 1, StokesColor.py:572-573).
 template <bool C16>
-__global__ __launch_bounds__(BS) void k_grad_proj(SellDev A, FaceDev fc, const double* __restrict__ gx,
+__global__ LB_GATHER void k_grad_proj(SellDev A, FaceDev fc, const double* __restrict__ gx,
                                                   const double* __restrict__ gy, const double* __restrict__ p,
                                                   const double* __restrict__ as1, double dt, int mode,
                                                   const uint8_t* __restrict__ dirflag, const double* usx,
@@ -1543,8 +1584,9 @@ template <bool C16>
 __global__ __launch_bounds__(BS) void k_grad(SellDev A, FaceDev fc, const double* __restrict__ gx,
                                              const double* __restrict__ gy, const double* __restrict__ p,
                                              const double* __restrict__ as1, double* outx, double* outy) {
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
-    face_rows(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
+    face_rows(fc, role.idx, fc.nb, [&](const lat::FaceTab& F, int32_t lf, int32_t t, int32_t i, int32_t j) {
       int32_t nb[6];
       bool in[6];
       lat::neighbours(F, fc.n, t, i, j, nb, in);
@@ -1557,7 +1599,7 @@ __global__ __launch_bounds__(BS) void k_grad(SellDev A, FaceDev fc, const double
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+  block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = A.off[s];
@@ -1948,16 +1990,16 @@ __device__ __forceinline__ double sl_value(const SlTri& r, double xb, double yb,
   return w1 * c[r.a] + w2 * c[r.b] + w3 * c[r.d];
 }
 
-// lattice fast path: q strictly inside a cell of its row's home face, every load of the point issued
-// together (coordinates, field values, radii), the rank settled by a fast accept (sl_fast's tests);
-// -> true with the interpolated value, false: the general locate of k_sl_slow decides.  Scalars
-// only (a struct here ends in scratch memory).
-__device__ __forceinline__ bool sl_lattice_fast(const LatLocDev& L, int64_t g, double qx, double qy,
-                                                const double* __restrict__ c, double& cn) {
-  // the face: the row's home face, else the faces of q's macro-grid cell (first one holding q
-  // strictly inside a cell)
+// Lattice fast path, in two stages so that k_sl can overlap one row's second stage with the next row's
+// first.  Stage 1 (sl_lat_cell): q strictly inside a cell of its row's home face, else of the first face
+// of q's macro-grid cell holding q so -> the cell triangle's vertices and id (false: the general
+// locate of k_sl_slow decides).  Stage 2 (sl_lat_value): with the triangle's coordinates, field values
+// and radii loaded (all issued together), the det guard, the rank settled by a fast accept (sl_fast's
+// tests) and the interpolated value (false: k_sl_slow decides).  Scalars only (a struct here ends in
+// scratch memory).
+__device__ __forceinline__ bool sl_lat_cell(const LatLocDev& L, int32_t home, double qx, double qy, int32_t& v0,
+                                            int32_t& v1, int32_t& v2, int32_t& id) {
   const int32_t n = L.n;
-  const int32_t home = L.home[g];
   int32_t f = -1;
   double fu = 0.0, fv = 0.0;
   int32_t s = 0;
@@ -1999,20 +2041,24 @@ __device__ __forceinline__ bool sl_lattice_fast(const LatLocDev& L, int64_t g, d
   const int32_t c0 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[0], pj[0]);
   const int32_t c1 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[1], pj[1]);
   const int32_t c2 = lat::vertex(S.tab, S.va, S.vb, S.vc, n, pi[2], pj[2]);
-  const int32_t v0 = rot == 0 ? c0 : (rot == 1 ? c1 : c2);
-  const int32_t v1 = rot == 0 ? c1 : (rot == 1 ? c2 : c0);
-  const int32_t v2 = rot == 0 ? c2 : (rot == 1 ? c0 : c1);
-  const int32_t id = (int32_t)(S.t0 + (int64_t)(ent >> 2));
-  const double2 P1 = L.xy[v0], P2 = L.xy[v1], P3 = L.xy[v2];
-  const double f1 = c[v0], f2 = c[v1], f3 = c[v2];
-  const float rho2 = L.rho2[id], rv1 = L.rv2[v0], rv2 = L.rv2[v1], rv3 = L.rv2[v2];
+  v0 = rot == 0 ? c0 : (rot == 1 ? c1 : c2);
+  v1 = rot == 0 ? c1 : (rot == 1 ? c2 : c0);
+  v2 = rot == 0 ? c2 : (rot == 1 ? c0 : c1);
+  id = (int32_t)(S.t0 + (int64_t)(ent >> 2));
+  return true;
+}
+// stage 2 on the loaded values: P1..P3 the vertex coordinates, f1..f3 the field values, rho2 the
+// triangle's fast-accept radius, rv1..rv3 the vertices' radii
+__device__ __forceinline__ bool sl_lat_value(int32_t probe, double qx, double qy, double2 P1, double2 P2, double2 P3,
+                                             double f1, double f2, double f3, float rho2, float rv1, float rv2,
+                                             float rv3, double& cn) {
   const double x1 = P1.x, y1 = P1.y, x2 = P2.x, y2 = P2.y, x3 = P3.x, y3 = P3.y;
   // the weights are >= SL_LDEL up to rounding: the weight test passes; only its det guard remains
   const double det0 = (x2 - x1) * (y3 - y1) - (x3 - x1) * (y2 - y1);
   if (!(fabs(det0) >= 1e-14)) return false;
   const double ex = (x1 + x2 + x3) / 3.0 - qx, ey = (y1 + y2 + y3) / 3.0 - qy;
   const double bestd = ex * ex + ey * ey;
-  if (!(4.0 * bestd * (1.0 + 1e-9) < (double)rho2 || (L.probe & 1))) {
+  if (!(4.0 * bestd * (1.0 + 1e-9) < (double)rho2 || (probe & 1))) {
     const double d1 = (x1 - qx) * (x1 - qx) + (y1 - qy) * (y1 - qy);
     const double d2 = (x2 - qx) * (x2 - qx) + (y2 - qy) * (y2 - qy);
     const double d3 = (x3 - qx) * (x3 - qx) + (y3 - qy) * (y3 - qy);
@@ -2058,7 +2104,7 @@ __device__ __forceinline__ bool sl_fast(const LOC& L, const SlTri& r, double qx,
 // k_sl_slow block b runs the same waves' queues and adds its partial sums to block b's, so the
 // reductions keep a fixed order.
 template <class LOC>
-__global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, int64_t row0, int64_t n,
+__global__ LB_GATHER void k_sl(MeshDev M, LOC L, int64_t row0, int64_t n,
                                            const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                            const double* __restrict__ c, double* __restrict__ cout,
                                            const double* __restrict__ wmix, int32_t* notfound, double* part,
@@ -2070,47 +2116,98 @@ __global__ __launch_bounds__(BS) void k_sl(MeshDev M, LOC L, int64_t row0, int64
   block_rows(n, r0, r1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int32_t qn = 0;
-  // the row inputs of the next iteration are loaded one iteration ahead
   int64_t i = r0 + threadIdx.x;
-  double nx_ = 0.0, ny_ = 0.0, nvx = 0.0, nvy = 0.0;
-  if (LAT && i < r1) {
-    nx_ = M.x[row0 + i];
-    ny_ = M.y[row0 + i];
-    nvx = ux[i];
-    nvy = uy[i];
+  // LAT: a software pipeline over the thread's rows i, i + BS, ...: stage A (the row's coordinates,
+  // velocity and home face) loaded two rows ahead, stage B (departure point, face, cell -> the cell
+  // triangle: sl_lat_cell) one row ahead, stage C (the triangle's coordinates, field values and radii
+  // -> the value: sl_lat_value) on the current row, its loads issued before the next row's stage B so
+  // that the two dependent chains overlap.  Row i's operations are those of one pass, in one pass's order.
+  // (the row's own coordinates from the locator's interleaved table, whose lines the vertex loads of
+  // the departure triangles, near the row, then find in L2: 16 B/row less than M.x, M.y beside it)
+  double ax_ = 0.0, ay_ = 0.0, avx = 0.0, avy = 0.0;  // stage A of row i + BS
+  int32_t ah = -1;
+  int32_t bm = 0, b0 = 0, b1 = 0, b2 = 0, bid = 0;  // stage B of row i: mode 0 queue, 1 cell, 2 self
+  double bqx = 0.0, bqy = 0.0;
+  // (generic lambdas: instantiated for the lattice locator only)
+  auto stage_a = [&](const auto& LL, int64_t r) {
+    const double2 P = LL.xy[row0 + r];
+    ax_ = P.x;
+    ay_ = P.y;
+    avx = ux[r];
+    avy = uy[r];
+    ah = LL.home[row0 + r];
+  };
+  auto stage_b = [&](const auto& LL, int64_t r) {  // from the stage A values
+    double xb = py_mod1(ax_ - dt * avx * 1.0);
+    double yb = ay_ - dt * avy * 1.0;
+    if (yb < 0.0) yb = 1e-12;
+    if (yb > 1.0) yb = 1.0 - 1e-12;
+    bqx = xb;
+    bqy = yb;
+    // (the stage's outputs assigned from locals: through references the mode and id end in scratch)
+    int32_t m = 2, t0 = 0, t1 = 0, t2 = 0, tid = 0;
+    if (avx == 0.0 && avy == 0.0 && LL.self) {
+      // q is the row's own node (no-slip walls): on lattice lines, where several triangles pass the
+      // weight test; the answer for this q was settled once at build
+      tid = LL.self[row0 + r];
+    } else {
+      m = sl_lat_cell(LL, ah, xb, yb, t0, t1, t2, tid) ? 1 : 0;
+    }
+    bm = m;
+    b0 = t0;
+    b1 = t1;
+    b2 = t2;
+    bid = tid;
+  };
+  if constexpr (LAT) {
+    if (i < r1) {
+      stage_a(L, i);
+      stage_b(L, i);
+      if (i + BS < r1) stage_a(L, i + BS);
+    }
   }
   for (; i < r1; i += BS) {
     const int64_t g = row0 + i;
     bool done = false;
     double cn = 0.0;
     if constexpr (LAT) {
-      const double xg = nx_, yg = ny_, vx = nvx, vy = nvy;
-      if (i + BS < r1) {
-        nx_ = M.x[g + BS];
-        ny_ = M.y[g + BS];
-        nvx = ux[i + BS];
-        nvy = uy[i + BS];
+      const int32_t cm = bm, cid = bid;
+      const double qx = bqx, qy = bqy;
+      // stage C loads of row i
+      double2 P1{0.0, 0.0}, P2{0.0, 0.0}, P3{0.0, 0.0};
+      double f1 = 0.0, f2 = 0.0, f3 = 0.0;
+      float rho2 = 0.0f, rv1 = 0.0f, rv2 = 0.0f, rv3 = 0.0f;
+      if (cm == 1) {
+        P1 = L.xy[b0];
+        P2 = L.xy[b1];
+        P3 = L.xy[b2];
+        f1 = c[b0];
+        f2 = c[b1];
+        f3 = c[b2];
+        rho2 = L.rho2[cid];
+        rv1 = L.rv2[b0];
+        rv2 = L.rv2[b1];
+        rv3 = L.rv2[b2];
       }
-      double xb = py_mod1(xg - dt * vx * 1.0);
-      double yb = yg - dt * vy * 1.0;
-      if (yb < 0.0) yb = 1e-12;
-      if (yb > 1.0) yb = 1.0 - 1e-12;
-      if (vx == 0.0 && vy == 0.0 && L.self) {
-        // q is the row's own node (no-slip walls): on lattice lines, where several triangles pass the
-        // weight test; the answer for this q was settled once at build
-        const int32_t t = L.self[g];
+      // stage B of row i + BS, stage A of row i + 2 BS
+      if (i + BS < r1) {
+        stage_b(L, i + BS);
+        if (i + 2 * BS < r1) stage_a(L, i + 2 * BS);
+      }
+      if (cm == 2) {
+        const int32_t t = cid;
         if (t >= 0) {
           const int32_t va = M.tri[3 * (int64_t)t], vb = M.tri[3 * (int64_t)t + 1], vc = M.tri[3 * (int64_t)t + 2];
           const SlTri r{M.x[va], M.y[va], M.x[vb], M.y[vb], M.x[vc], M.y[vc], va, vb, vc, t};
-          cn = sl_value(r, xb, yb, c);
+          cn = sl_value(r, qx, qy, c);
         } else {
           cn = c[g];
           nnf += 1.0;
         }
         if (notfound) notfound[i] = t >= 0 ? 0 : 1;
         done = true;
-      } else {
-        done = sl_lattice_fast(L, g, xb, yb, c, cn);
+      } else if (cm == 1) {
+        done = sl_lat_value(L.probe, qx, qy, P1, P2, P3, f1, f2, f3, rho2, rv1, rv2, rv3, cn);
         if (done && notfound) notfound[i] = 0;
       }
     }
@@ -2870,9 +2967,10 @@ __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, c
     stnt(xout + row, (TO)xo);
     if constexpr (RD) acc_rz += rrow * (double)xo;
   };
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     constexpr int K = face_k(4);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -2922,7 +3020,7 @@ __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, c
     });
   } else {
     int64_t s0, s1;
-    block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
     const int lane = threadIdx.x & 63, wv = wave_id();
     for (int64_t s = s0 + wv; s < s1; s += 4) {
       const int64_t row = sell_row(A, s, lane);
@@ -3080,9 +3178,10 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
                                               const TB* __restrict__ b, const T* __restrict__ x,
                                               T* __restrict__ res, const int* ctl) {
   if (ctl && ctl[0]) return;
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     constexpr int K = face_k(4);  // groups of K rows per thread, every load first (face_rows_k)
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       int32_t nb[K][6];
@@ -3112,7 +3211,7 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
     return;
   }
   int64_t s0, s1;
-  block_slices_n(A.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+  block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t row = sell_row(A, s, lane);
@@ -3128,10 +3227,11 @@ __global__ __launch_bounds__(BS) void k_resid(SellDev A, FaceDev fc, const VT* _
 template <bool ADD, typename T>
 __device__ __forceinline__ void transfer_body(const SellDev& M, const FaceDev& fc, const T* __restrict__ val,
                                               const T* __restrict__ x, T* __restrict__ y) {
-  if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - fc.nb) {
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
     const int32_t n2 = fc.n2;
     constexpr int K = face_k(4);
-    face_rows_k<K>(fc, blockIdx.x - (gridDim.x - fc.nb), fc.nb,
+    face_rows_k<K>(fc, role.idx, fc.nb,
                    [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
                        const int32_t (&j)[K], const bool (&ok)[K]) {
       const lat::FaceTab G = fc.tab2[lf];
@@ -3175,7 +3275,7 @@ __device__ __forceinline__ void transfer_body(const SellDev& M, const FaceDev& f
     return;
   }
   int64_t s0, s1;
-  block_slices_n(M.nslices, gridDim.x - fc.nb, blockIdx.x, s0, s1);
+  block_slices_n(M.nslices, role.nsk, role.idx, s0, s1);
   const int lane = threadIdx.x & 63, wv = wave_id();
   for (int64_t s = s0 + wv; s < s1; s += 4) {
     const int64_t off = M.off[s];
