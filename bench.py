@@ -183,7 +183,9 @@ def main():
                         (4, "k_cheb skeleton (SELL) rows only"), (5, "k_cg_dir face rows only"),
                         (6, "k_cg_dir skeleton (SELL) rows only"), (7, "k_div (SoA u, as in the step)"),
                         (8, "k_div face rows only"), (9, "k_div skeleton (SELL) rows only"),
-                        (10, "k_div on interleaved (x, y) u"), (11, "k_div interleaved, face rows only")):
+                        (10, "k_div on interleaved (x, y) u"), (11, "k_div interleaved, face rows only"),
+                        (12, "k_cheb_pair<1> (face rows)"), (13, "k_cheb_pair<2> (face rows)"),
+                        (14, "k_vcheb_pair (face rows)")):
             mb, me, by = ct.c_double(), ct.c_double(), ct.c_double()
             L.check(L.lib().pucfem_bench_kernel(sim.ctx.h, kid, 20, ct.byref(mb), ct.byref(me), ct.byref(by)),
                     sim.ctx.h)

@@ -4780,6 +4780,34 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
                                   ff, (const float*)B.Aval, (const float*)c.r32, (const float*)B.x, B.res,
                                   (const int*)nullptr);
             break;
+          case 12:  // k_cheb_pair<1> (two smoothing steps on the face rows, general start)
+          case 13:  // k_cheb_pair<2> (the fused first two steps from x = 0, then the third)
+            if (c.mgp_x && c.fP.items > 0) {
+              const HFace& hf = c.fP;
+              MgPairVecs pv{(const float*)c.r32, (const float*)B.dinv, (const float*)B.x, B.x2, c.mgp_x,
+                            (const float*)B.d, c.mgp_d};
+              if (kernel == 12)
+                hipExtLaunchKernelGGL(k_cheb_pair<1>, dim3(hf.items), dim3(BS), 0, c.st, a, e, 0, hf.full(), pv, 0.3f,
+                                      0.7f, 0.0f, 0.3f, 0.7f, (const int*)nullptr);
+              else
+                hipExtLaunchKernelGGL(k_cheb_pair<2>, dim3(hf.items), dim3(BS), 0, c.st, a, e, 0, hf.full(), pv, 0.3f,
+                                      0.7f, 0.5f, 0.3f, 0.7f, (const int*)nullptr);
+            }
+            break;
+          case 14:  // k_vcheb_pair (two viscous Chebyshev steps on the face rows, general start)
+            if (c.vx2[2] && c.fVisc.items > 0) {
+              VPairVecs p{};
+              p.xa = c.vx2[0];
+              p.xb = c.vx2[1];
+              p.xc = c.vx2[2];
+              p.b = c.vb2;
+              p.da = c.vd2[0];
+              p.dc = c.vd2[1];
+              hipExtLaunchKernelGGL(k_vcheb_pair, dim3(c.fVisc.items), dim3(BS), 0, c.st, a, e, 0, c.fVisc.part(), p,
+                                    0.3, 0.7, 0.3, 0.7, (const int*)ctl0, (double*)nullptr, 0, 0, (double*)nullptr,
+                                    (double*)nullptr);
+            }
+            break;
           case 7:   // k_div as in the step (SoA u, the pressure rhs, partials)
           case 8:   // its face part alone
           case 9:   // its SELL (skeleton) part alone
@@ -4829,6 +4857,9 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
         break;
       case 8:
       case 11: by = 24.0 * (double)c.fK.rows; break;
+      case 12: by = 20.0 * (double)c.fP.rows; break;  // x_a, d_a, b read; x_{a+2}, d_{a+2} written (fp32)
+      case 13: by = 12.0 * (double)c.fP.rows; break;  // b read; x_{a+2}, d_{a+2} written
+      case 14: by = 64.0 * (double)c.fVisc.rows; break;  // x_a, b, d_a read; x_{a+2}, d_{a+2} written
       case 9: by = (16.0 + c.dP.idx_bytes()) * (double)c.dP.nnz + (c.dP.row_bytes() + 24.0) * (double)c.dP.nrows; break;
       default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk + 32.0 * fr;
     }
