@@ -428,6 +428,8 @@ struct Ctx {
   // PUCFEM_MG_PAIR=0 runs every step as its own k_cheb (a measurement knob); a third x buffer and a second
   // d buffer of the finest level are allocated on first use
   bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
+  // the finest mg_pair_levels levels smooth in step pairs (measurement knob PUCFEM_MG_PAIR_LEVELS)
+  int mg_pair_levels = std::getenv("PUCFEM_MG_PAIR_LEVELS") ? std::max(1, std::atoi(std::getenv("PUCFEM_MG_PAIR_LEVELS"))) : 1;
   int64_t mg_pairs = 0;
   float* mgp_x = nullptr;
   float* mgp_d = nullptr;
@@ -1207,10 +1209,10 @@ struct Ctx {
     // face interiors; not the step that writes z / the <r, z> partials
     bool pairs = false;
     if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
-      pairs = mg_pair && finest && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
-    if (pairs && !mgp_x) {
-      mgp_x = dalloc<float>(L.nloc);
-      mgp_d = dalloc<float>(L.nloc);
+      pairs = mg_pair && (int)(&mg.back() - &L) < mg_pair_levels && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
+    if (pairs && !mgp_x) {  // (sized for the finest level: every pair level uses them in turn)
+      mgp_x = dalloc<float>(mg.back().nloc);
+      mgp_d = dalloc<float>(mg.back().nloc);
     }
     T* dcur = B.d;  // the current d (a pair writes its d to the other buffer)
     double c20 = 0.0;
@@ -1259,10 +1261,10 @@ struct Ctx {
                       (const int*)ctl, (const double*)nullptr, (double*)nullptr, RedOut{}, (T*)nullptr);
               KCHK();
               if (mode == 1)
-                klaunch(10, bytes_f, k_cheb_pair<1>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
+                klaunch(finest ? 10 : -1, bytes_f, k_cheb_pair<1>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
                         (float)c20, (float)c1s[k + 1], (float)c2s[k + 1], (const int*)ctl);
               else
-                klaunch(10, bytes_f, k_cheb_pair<2>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
+                klaunch(finest ? 10 : -1, bytes_f, k_cheb_pair<2>, dim3(hf.items), dim3(BS), hf.full(), pv, (float)c1, (float)c2,
                         (float)c20, (float)c1s[k + 1], (float)c2s[k + 1], (const int*)ctl);
               KCHK();
               klaunch(-1, bytes_sk1, k_cheb<T, TB, T, VT, C, 1>, dim3(nbs), dim3(BS), A.view(), fs, val,

@@ -671,7 +671,7 @@ std::vector<float> knn_radius2(const Grid& G, const std::vector<double>& cx, con
       out[t] = f;
     }
   };
-  const int nt = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  const int nt = host_threads();
   ThreadGroup g;
   for (int w = 0; w < nt; ++w) g.spawn([&work, w, nt, T] { work(T * w / nt, T * (w + 1) / nt); });
   g.join();

@@ -3,6 +3,9 @@
 // exercised by the CPU test-suite through a host-only context.
 #pragma once
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <exception>
 #include <memory>
 #include <string>
@@ -48,10 +51,38 @@ struct ThreadGroup {
   }
   ~ThreadGroup() { wait(); }
 };
-// f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to 64)
+// host threads for the setup's parallel loops: PUCFEM_HOST_THREADS, else OMP_NUM_THREADS, else the cgroup's
+// CPU quota (cgroup v2 cpu.max), else the hardware threads; at most 64.  (A GPU box shows hundreds of
+// hardware threads to a process whose quota is 16 CPUs: 64 threads per loop there only add spawns and
+// throttling.)
+inline int host_threads() {
+  static const int n = [] {
+    auto env = [](const char* k) {
+      const char* e = std::getenv(k);
+      return e ? std::atoi(e) : 0;
+    };
+    int t = env("PUCFEM_HOST_THREADS");
+    if (t <= 0) t = env("OMP_NUM_THREADS");
+    if (t <= 0) {
+      if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long period = 0;
+        if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+          t = (int)std::max(1LL, std::atoll(q) / period);
+        std::fclose(f);
+      }
+    }
+    const int hw = (int)std::thread::hardware_concurrency();
+    if (t <= 0) t = hw > 0 ? hw : 1;
+    if (hw > 0) t = std::min(t, hw);
+    return std::max(1, std::min(t, 64));
+  }();
+  return n;
+}
+// f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to host_threads())
 template <class F>
 void parallel_for(i64 n, F&& f) {
-  const int nt = (int)std::max<i64>(1, std::min<i64>({64, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
+  const int nt = (int)std::max<i64>(1, std::min<i64>({(i64)host_threads(), n / 4096 + 1}));
   if (nt == 1) {
     f((i64)0, n);
     return;
@@ -65,7 +96,7 @@ void parallel_for(i64 n, F&& f) {
 constexpr int PAR_CHUNKS = 64;
 template <class F>
 void parallel_chunks(i64 n, F&& f) {
-  const int nt = (int)std::max<i64>(1, std::min<i64>({PAR_CHUNKS, (i64)std::thread::hardware_concurrency(), n / 4096 + 1}));
+  const int nt = (int)std::max<i64>(1, std::min<i64>({PAR_CHUNKS, (i64)host_threads(), n / 4096 + 1}));
   auto run = [&](int w) {
     for (int ch = w; ch < PAR_CHUNKS; ch += nt) f(ch, n * ch / PAR_CHUNKS, n * (ch + 1) / PAR_CHUNKS);
   };
