@@ -428,8 +428,6 @@ struct Ctx {
   // PUCFEM_MG_PAIR=0 runs every step as its own k_cheb (a measurement knob); a third x buffer and a second
   // d buffer of the finest level are allocated on first use
   bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
-  // the finest mg_pair_levels levels smooth in step pairs (measurement knob PUCFEM_MG_PAIR_LEVELS)
-  int mg_pair_levels = std::getenv("PUCFEM_MG_PAIR_LEVELS") ? std::max(1, std::atoi(std::getenv("PUCFEM_MG_PAIR_LEVELS"))) : 1;
   int64_t mg_pairs = 0;
   float* mgp_x = nullptr;
   float* mgp_d = nullptr;
@@ -560,10 +558,8 @@ struct Ctx {
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
   // semi-Lagrangian grid: latency-bound gathers want more waves in flight than MAXB blocks give
-  // (PUCFEM_SL_BLOCKS, a measurement knob: a smaller cap leaves the overlapped main stream more wave slots)
   static int nb_sl(i64 n) {
-    static const int cap = std::getenv("PUCFEM_SL_BLOCKS") ? std::max(64, std::min(SLB, std::atoi(std::getenv("PUCFEM_SL_BLOCKS")))) : SLB;
-    return (int)std::max<i64>(1, std::min<i64>(cap, (n + 4 * 64 - 1) / (4 * 64)));
+    return (int)std::max<i64>(1, std::min<i64>(SLB, (n + 4 * 64 - 1) / (4 * 64)));
   }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
@@ -1025,7 +1021,6 @@ struct Ctx {
     } else {
       step(0, 0.0, 1.0 / theta);
     }
-    if (sl_gate == 1) dye_flush();
     Red rr{redbuf, 1, 1}, bb{redbuf + NR, 1, 1};
     if (!pair0 && ro(redbuf, CNT_VCHEB, 2 * NR).out) {
       red_done(redbuf, 2 * NR, false);
@@ -1209,7 +1204,8 @@ struct Ctx {
     // face interiors; not the step that writes z / the <r, z> partials
     bool pairs = false;
     if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
-      pairs = mg_pair && (int)(&mg.back() - &L) < mg_pair_levels && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
+      // (finest level only: pairs on L6 / L5 too measured neutral to -0.7 %, r10m)
+      pairs = mg_pair && finest && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
     if (pairs && !mgp_x) {  // (sized for the finest level: every pair level uses them in turn)
       mgp_x = dalloc<float>(mg.back().nloc);
       mgp_d = dalloc<float>(mg.back().nloc);
@@ -1921,18 +1917,9 @@ struct Ctx {
   // the step record) on the side stream, after the main stream's event `gate`.  (Round 3 measured the
   // tail enqueued after the next step's viscous solve instead, beside the pressure solve: the time moved
   // between the streams, the step rate stayed, r8j.)
+  // (round 4 measured the tail released after the next step's first viscous step and after its viscous
+  // solve: neutral, r10f; it is released at the end of the step)
   hipEvent_t ev_gate = nullptr;
-  // where the main stream releases a step's dye tail (PUCFEM_SL_GATE, a measurement knob): 0 (default) at
-  // the end of the step; 1 after the next step's first viscous Chebyshev step (which then runs alone);
-  // 2 after the next step's viscous solve (round 3's r8j placement)
-  int sl_gate = std::getenv("PUCFEM_SL_GATE") ? std::atoi(std::getenv("PUCFEM_SL_GATE")) : 0;
-  double* sl_deferred = nullptr;  // the record of a tail waiting for its gate
-  void dye_flush() {
-    if (!sl_deferred) return;
-    double* r = sl_deferred;
-    sl_deferred = nullptr;
-    dye_tail(r);
-  }
   void dye_tail(double* rec) {
     HIPCHK(hipEventRecord(ev_gate, st));
     HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
@@ -1968,7 +1955,6 @@ struct Ctx {
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
-    dye_flush();  // (a deferred tail whose gate the viscous solve did not release)
     // max |div u*| -> vals[0]; the div u* field itself is computed when read (pucfem_get_field): nothing in the
     // step reads it, and its 8 B/row store is a quarter of the kernel's bytes
     const bool f1 = div_rhs(usx, usy, nullptr, vals);
@@ -2004,8 +1990,7 @@ struct Ctx {
       }
       hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 1);  // max |div u*|
       KCHK();
-      if (sl_gate > 0) sl_deferred = rec;  // released by the next step (dye_flush)
-      else dye_tail(rec);
+      dye_tail(rec);
     } else if (scheme == PUCFEM_STOKES_COLOR) {
       const int nb = nb_sl(lp.n_own);
       if (dye_impl) {
@@ -3786,11 +3771,9 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
-          c.dye_flush();  // the last step's tail, when a gate deferred it
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
-          c.sl_deferred = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
           throw;
