@@ -30,4 +30,9 @@ if [ -n "$PROF" ]; then
   find /tmp/prof_$TAG/stats -name "*stats*.csv" -exec cp {} "$OUT/" \;
   TR=$(find /tmp/prof_$TAG/stats -name "*kernel_trace.csv" | head -1)
   [ -n "$TR" ] && python tools/trace_window.py "$TR" --warmup 5 --steps 20 --top 90 > "$OUT/step_window.txt"
+  # the roofline kernel over the launches the bench's events time (the last 5 timed steps), against the
+  # profiled run's own bench line (rocprof.out)
+  RK=$(python -c "import json,sys; print(json.loads(open('$OUT/rocprof.out').read().strip().splitlines()[-1])['roofline']['kernel'])")
+  [ -n "$TR" ] && python tools/trace_window.py "$TR" --warmup 5 --steps 20 --last 5 --kernel "$RK" --top 30 > "$OUT/step_window_last5.txt"
+  [ -n "$TR" ] && gzip -c "$TR" > "$OUT/kernel_trace.csv.gz"
 fi

@@ -7,10 +7,10 @@ Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--level 7 --world 1]
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's memory-side request
 counters, FETCH_SIZE under-reports wide streaming reads by exactly 2x on gfx950, and other access
 widths must be calibrated on a known byte count in one's own access pattern.  The guide's
-corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_diff2 (the projection update of
-the pressure solves), a pure 8-B/lane elementwise kernel whose algorithmic traffic is exactly 32 B/row
-read (y, x0, A v or b, r_final) and 16 B/row written (v, A v), nrows from the bench line.  (Rounds 1-2
-checked k_visc_fin, which round 3 folded into the viscous solve's last step.)  Raw counter values are kept next
+corrections (FETCH_SIZE x2, WRITE_SIZE x1, KiB units) are checked on k_diff2_fin (the projection update
+of the pressure solves fused with the finish), a pure elementwise kernel whose algorithmic traffic is
+36 B/row read (y, x0, A v or b, r_final; master_of) and 24 B/row written (v, A v, p), nrows from the bench
+line.  (Round 3 checked k_diff2, rounds 1-2 k_visc_fin.)  Raw counter values are kept next
 to the corrected bytes.  Caveat: the L2 is write-back, so up to ~32 MiB of one kernel's dirty lines
 are evicted (and counted) during the next kernel.
 """
@@ -129,7 +129,9 @@ def main():
                     ("k_sl", pick("k_sl", ("k_sl_",))),
                     ("k_sl_slow", pick("k_sl_slow")),
                     ("k_vcheb", widest(pick("k_vcheb<"))),
-                    ("k_div", pick("k_div<")),
+                    # the step's divergence kernel only (SoA u, the full grid): the bench's kernel_batch
+                    # also launches its face / skeleton parts and the interleaved-u variant
+                    ("k_div", widest(pick("k_div<", ("k_div<false,true>", "k_div<true,true>")))),
                     ("k_grad_proj", pick("k_grad_proj<")),
                     ("k_visc_prep", pick("k_visc_prep")),
                     ("k_mdot2", pick("k_mdot2<")),

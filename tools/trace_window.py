@@ -10,6 +10,7 @@ grid size kept so multigrid levels stay apart), the window's span, busy time and
 """
 import argparse
 import csv
+import gzip
 import re
 from collections import defaultdict
 
@@ -26,8 +27,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--top", type=int, default=40)
+    # only the last N timed steps (the bench's per-launch events cover the last 5 of the 20 timed steps)
+    ap.add_argument("--last", type=int, default=0)
+    # a kernel name prefix: also print its launches' average over the window (every template instance)
+    ap.add_argument("--kernel", default="")
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    op = gzip.open if a.trace.endswith(".gz") else open
+    rows = list(csv.DictReader(op(a.trace, "rt")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # a step ends with its last k_stats: with the dye advection on a side stream (one k_stats per
     # stream per step) that is the side stream's, the stream k_sl runs on
@@ -37,6 +43,8 @@ def main():
     two = sl and len(nst) > 0 and len(set(nst)) > 1
     stats_idx = [i for i, r in enumerate(rows)
                  if "k_stats" in r["Kernel_Name"] and (not two or r[col] == sl[0])]
+    if a.last:
+        a.warmup, a.steps = a.warmup + a.steps - a.last, a.last
     i0 = stats_idx[a.warmup - 1] + 1
     i1 = stats_idx[a.warmup + a.steps - 1] + 1
     win = rows[i0:i1]
@@ -55,6 +63,11 @@ def main():
     span = t1 - t0
     print(f"window: {len(win)} kernels, span {span / 1e6:.2f} ms ({span / 1e6 / a.steps:.3f} ms/step), "
           f"busy {busy / 1e6:.2f} ms, gaps {(span - busy) / 1e6:.2f} ms")
+    if a.kernel:
+        ks = [(t, n) for k, (t, n) in agg.items() if k.startswith(a.kernel)]
+        if ks:
+            tt, nn = sum(t for t, _ in ks), sum(n for _, n in ks)
+            print(f"{a.kernel}*: {nn} launches, average {tt / nn / 1e3:.1f} us")
     for k, (tot, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: a.top]:
         print(f"{tot / 1e6:9.3f} ms {n:6d} {tot / n / 1e3:9.1f} us  {tot / span * 100:5.1f}%  {k}")
 
