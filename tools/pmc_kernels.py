@@ -12,7 +12,7 @@ d = sys.argv[1]
 pats = sys.argv[2:] or ["k_div<", "k_grad_proj<", "k_cheb<float, float, float, float, false, 1>", "k_vcheb<2",
                         "k_cg_init<1", "k_cg_upd<1>", "k_diff2", "k_cg_dir<1"]
 acc = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True) + glob.glob(os.path.join(d, "pass*.csv")):
     for row in csv.DictReader(open(f, newline="")):
         name = re.sub(r"\(.*", "", row["Kernel_Name"]).replace("void ", "").replace("pucfem::dev::", "")
         g = row.get("Grid_Size") or row.get("Grid_Size_X") or ""
