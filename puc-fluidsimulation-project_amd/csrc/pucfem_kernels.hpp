@@ -214,11 +214,16 @@ struct Wn {
   static constexpr int value = N;
 };
 // f(Wn<w>{}) for the common SELL slice widths -- straight-line code in which every index / value
-// load of the slice issues before the dependent gathers (widths 6-14: merged periodic-master
-// rows are wider than the 7-entry stencil rows) -- and f(Wn<0>{}) (a runtime-width loop) otherwise.  w must be wave-uniform.
+// load of the slice issues before the dependent gathers (widths 1-14: transfer rows are 1-9 wide,
+// merged periodic-master stencil rows wider than the 7-entry ones) -- and f(Wn<0>{}) (a runtime-width loop) otherwise.  w must be wave-uniform.
 template <class F>
 __device__ __forceinline__ void by_width(int w, F&& f) {
   switch (w) {
+    case 1: f(Wn<1>{}); break;
+    case 2: f(Wn<2>{}); break;
+    case 3: f(Wn<3>{}); break;
+    case 4: f(Wn<4>{}); break;
+    case 5: f(Wn<5>{}); break;
     case 6: f(Wn<6>{}); break;
     case 7: f(Wn<7>{}); break;
     case 8: f(Wn<8>{}); break;

@@ -282,13 +282,33 @@ __global__ __launch_bounds__(BS) void k_cg_init(SellDev A, FaceDev fc, const dou
       double acc[NR];
 #pragma unroll
       for (int c = 0; c < NR; ++c) acc[c] = 0.0;
-      for (int k = 0; k < w; ++k) {
-        const int64_t e = off + (int64_t)k * 64 + lane;
-        const double a = val[e];
-        const int32_t j = sell_col<C16, false>(A, e, base);
+      // every column / value load of the slice before the gathers (k_cg_dir's form), summed in k order
+      by_width(w, [&](auto wc) {
+        constexpr int WN = decltype(wc)::value;
+        if constexpr (WN > 0) {
+          int32_t cj[WN];
+          double av[WN];
 #pragma unroll
-        for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
-      }
+          for (int k = 0; k < WN; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            av[k] = val[e];
+            cj[k] = sell_col<C16, false>(A, e, base);
+          }
+#pragma unroll
+          for (int k = 0; k < WN; ++k) {
+#pragma unroll
+            for (int c = 0; c < NR; ++c) acc[c] += av[k] * v.y[c][cj[k]];
+          }
+        } else {
+          for (int k = 0; k < w; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            const double a = val[e];
+            const int32_t j = sell_col<C16, false>(A, e, base);
+#pragma unroll
+            for (int c = 0; c < NR; ++c) acc[c] += a * v.y[c][j];
+          }
+        }
+      });
       if (row >= 0) finish(row, acc);
     }
   }
@@ -3283,10 +3303,30 @@ __device__ __forceinline__ void transfer_body(const SellDev& M, const FaceDev& f
     const int64_t row = sell_row(M, s, lane);
     const T yr = ADD && row >= 0 ? y[row] : (T)0;
     T acc = 0;
-    for (int k = 0; k < w; ++k) {
-      const int64_t e = off + (int64_t)k * 64 + lane;
-      acc += val[e] * x[M.col[e]];
-    }
+    // every column / value load of the slice before the gathers (widths 1-14 unrolled), summed in k order
+    by_width(w, [&](auto wc) {
+      constexpr int WN = decltype(wc)::value;
+      if constexpr (WN > 0) {
+        int32_t cj[WN];
+        T av[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          cj[k] = M.col[e];
+          av[k] = val[e];
+        }
+        T xv[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) xv[k] = x[cj[k]];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) acc += av[k] * xv[k];
+      } else {
+        for (int k = 0; k < w; ++k) {
+          const int64_t e = off + (int64_t)k * 64 + lane;
+          acc += val[e] * x[M.col[e]];
+        }
+      }
+    });
     if (row >= 0) stnt(y + row, ADD ? yr + acc : acc);
   }
 }
