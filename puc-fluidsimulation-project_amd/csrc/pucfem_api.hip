@@ -20,6 +20,7 @@
 #include <tuple>
 #include <utility>
 #include <vector>
+#include <map>
 
 #include "pucfem.h"
 #include "pucfem_comm.hpp"
@@ -2890,6 +2891,16 @@ void build(Ctx& c) {
       std::vector<double> v;
       sell_values(c.Pp, c.lp, c.sPp, c.Pp.val, v);
       dump_sell(path, c.sPp, v);
+    }
+  }
+  if (clk.on) {  // slice widths of the skeleton SELLs (PUCFEM_SETUP_TIMING): > 14 runs the generic entry loop
+    for (const auto* S : {&c.sP, &c.sPp}) {
+      std::map<int, i64> h;
+      for (i32 w : S->slice_w) ++h[w];
+      std::fprintf(stderr, "[setup] SELL %s: %lld slices, widths", S == &c.sP ? "P (K, G)" : "Pp (pressure)",
+                   (long long)S->nslices);
+      for (auto& kv : h) std::fprintf(stderr, " %d:%lld", kv.first, (long long)kv.second);
+      std::fprintf(stderr, "\n");
     }
   }
   clk.mark("SELL images");
