@@ -475,6 +475,29 @@ struct Ctx {
   double* dqm = nullptr;  // re-seed coefficients (QMat) on the device
   bool proj_pend[5] = {false, false, false, false, false};  // v / A v wait for the next guess
   double *pv[5] = {}, *pav[5] = {};
+  // Pressure directions left pending (one rank, lattice, multigrid, shared-basis-free or shared): after a solve
+  // the projection update's v = y - x0 and A v = r0 - r_final are not stored; the next solve's k_mdot2 /
+  // k_pcomb form them from y, x0, pav (r0) and cg_r[0] (r_final) -- the same values, 60 B/row of k_diff2_fin
+  // saved for 24 B/row more in those passes -- and the gradient projection gathers the solution y through
+  // the merged (slave -> master) face tables and SELL columns instead of a separate p = y with the slaves
+  // copied (p_s = p_m exactly, so the same values).  proj_materialize() stores a pending direction
+  // (k_diff2) before anything could overwrite its inputs.
+  bool p_from_y = false;
+  DevSell dPm;  // dP with merged columns (the gradient's gathers of y)
+  bool pend_otf[5] = {};
+  const double* pend_y[5] = {};
+  // keep: a slot whose pending direction stays (its r_final is the one cg_r[0] still holds)
+  void proj_materialize(int keep = 0) {
+    for (int w = 1; w <= 2; ++w) {
+      if (!pend_otf[w] || w == keep) continue;
+      const i64 n = lp.n_own;
+      algo_bytes += 48.0 * (double)n;
+      hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, pend_y[w], (const double*)proj_x0[w], pv[w],
+                         (const double*)pav[w], (const double*)cg_r[0], pav[w]);
+      KCHK();
+      pend_otf[w] = false;
+    }
+  }
   // viscous warm start u^n + a polynomial extrapolation of the increments u* - u of the last steps:
   // dvinc[0..1] the last (x, y), [2..3] the one before, [4..5] the one before that, ...;
   // PUCFEM_VISC_EXTRAP (measurement knob): the order, 0 (off) .. VINC_MAX, default 5 (round 2, L7 driver
@@ -1635,6 +1658,7 @@ struct Ctx {
                            ext ? dvinc[last] : (float*)nullptr, ext ? dvinc[last + 1] : (float*)nullptr);
       }
     } else {
+      proj_materialize();  // (the CG's vectors include cg_r[0], a pending pressure direction's input)
       double* y[2] = {yvx, yvy};
       const double* b[2] = {bvx, bvy};
       if (proj) {  // the warm start u^n is replaced by the projection onto earlier solutions
@@ -1705,9 +1729,20 @@ struct Ctx {
       KCHK();
       it = 0;
     } else if (use_mg) {
+      // separate bases: the other slot's pending direction reads the r_final this solve overwrites
+      proj_materialize(proj ? proj_slot(which) : 0);
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
       // (the projection update and the finish in one pass: sc is null on the multigrid path)
-      if (proj) project_update(proj_slot(which), yst, bh, cg_r[0], pout);
+      if (proj) {
+        const int slot = proj_slot(which);
+        if (p_from_y && proj_m[slot] > 0) {  // the direction stays pending (the next solve forms it)
+          pend_otf[slot] = true;
+          pend_y[slot] = yst;
+          proj_pend[slot] = true;
+        } else {
+          project_update(slot, yst, bh, cg_r[0], pout);
+        }
+      }
     } else {
       double* y[1] = {yst};
       const double* b[1] = {bh};
@@ -1746,9 +1781,12 @@ struct Ctx {
     const int nb = grid_ew(n);
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
     // k_mdot2: X (fp32), b, A v, v read
-    klaunch(14, (4.0 * m + 24.0) * (double)n, mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
+    const bool otf = pend_otf[which];
+    const PendDir pd = otf ? PendDir{pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0]}
+                           : PendDir{nullptr, nullptr, nullptr};
+    klaunch(14, (4.0 * m + 24.0 + (otf ? 16.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)nloc, b, (const double*)pav[which], (const double*)pv[which],
-            op.null_free, proj_part, rmd);
+            op.null_free, proj_part, rmd, pd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
@@ -1761,10 +1799,11 @@ struct Ctx {
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
     // k_pcomb: X, v read; the new direction, x0, y written
-    klaunch(15, (4.0 * kq + 32.0) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
+    klaunch(15, (4.0 * kq + 32.0 + (otf ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)nloc, (const double*)proj_coef, (const double*)pv[which], op.null_free,
-            projX[which] + (i64)kq * nloc, y, proj_x0[which]);
+            projX[which] + (i64)kq * nloc, y, proj_x0[which], otf ? pend_y[which] : (const double*)nullptr);
     KCHK();
+    pend_otf[which] = false;
     H.coef_m = kq;
     proj_m[which] = kq + 1;
     proj_pend[which] = false;
@@ -1883,11 +1922,13 @@ struct Ctx {
     red_done(redbuf + 24, 1, false);
     return true;
   }
+  // pp: p, or with p_from_y the pressure solve's y (gathered through the merged tables and columns)
   void grad_proj(const double* pp, int mode) {
-    const FaceDev fc = fK.full();
-    with_c16(dP, [&](auto c16) {
-      klaunch(3, (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows + 40.0 * (double)lp.n_own,
-              k_grad_proj<decltype(c16)::value>, dim3(grid_full(fc, dP)), dim3(BS), dP.view(), fc, (const double*)dGx,
+    const FaceDev fc = p_from_y ? fP.full() : fK.full();
+    const DevSell& A = p_from_y ? dPm : dP;
+    with_c16(A, [&](auto c16) {
+      klaunch(3, (16.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 40.0 * (double)lp.n_own,
+              k_grad_proj<decltype(c16)::value>, dim3(grid_full(fc, A)), dim3(BS), A.view(), fc, (const double*)dGx,
               (const double*)dGy, pp, (const double*)das1, prm.dt, mode, (const uint8_t*)ddir, (const double*)usx,
               (const double*)usy, ux, uy);
     });
@@ -1962,12 +2003,12 @@ struct Ctx {
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
     const int itp = pressure(yp, p, 1, f1);
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
-    grad_proj(p, 0);
+    grad_proj(p_from_y ? yp : p, 0);
     bc(ux, uy);
     halo(ux, uy);
     const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
     const int itp2 = pressure(yp2, p2, 2, f2);
-    grad_proj(p2, 1);
+    grad_proj(p_from_y ? yp2 : p2, 1);
     halo(ux, uy);
     // single-rank explicit dye: the final-divergence record and the advection of this step (they read
     // the final u and c, write final_div, c_new and their own partials) run on a side stream,
@@ -3099,6 +3140,20 @@ void build(Ctx& c) {
   c.proj_k = c.use_mg && !c.dense ? proj_size(c.prm.proj_k) : 0;
   c.proj_shared = c.prm.proj_shared != 0;
   if (const char* e = std::getenv("PUCFEM_PROJ_SHARED")) c.proj_shared = std::atoi(e) != 0;
+  // pending pressure directions and the gradient on y (Ctx::p_from_y): one rank, lattice operators, the
+  // multigrid PCG with the projection, the explicit dye; PUCFEM_P_FROM_Y=0 keeps the stored form (a
+  // measurement knob: the same values either way)
+  c.p_from_y = stokes && c.lattice && !c.dist() && c.use_mg && c.proj_k > 0 && !c.dye_impl && c.dP.c16 == nullptr &&
+               !(std::getenv("PUCFEM_P_FROM_Y") && std::atoi(std::getenv("PUCFEM_P_FROM_Y")) == 0);
+  if (c.p_from_y) {  // dP with every column mapped to its periodic master (the dof map)
+    std::vector<i32> colm(c.sP.col.size());
+    for (size_t e = 0; e < colm.size(); ++e) {
+      const i32 j = c.sP.col[e];
+      colm[e] = j >= 0 && j < (i32)c.dof.size() ? c.dof[j] : j;
+    }
+    c.dPm = c.dP;
+    c.dPm.col = c.upload(colm);
+  }
   const bool block_visc = !c.dist() && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
   c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
   for (int w = 1; w <= 4; ++w) {
@@ -3694,8 +3749,19 @@ int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count) {
     switch (field) {
       case PUCFEM_F_U: get2(c.ux, c.uy); break;
       case PUCFEM_F_USTAR: get2(c.usx, c.usy); break;
-      case PUCFEM_F_P: get1(c.p); break;
-      case PUCFEM_F_P2: get1(c.p2); break;
+      case PUCFEM_F_P:  // with p_from_y the step keeps p in y (slaves not copied): p formed when read
+      case PUCFEM_F_P2: {
+        double* pf = field == PUCFEM_F_P ? c.p : c.p2;
+        if (c.p_from_y) {
+          const i64 n = c.lp.n_own;
+          hipLaunchKernelGGL(k_cg_fin, dim3(Ctx::grid_ew(n)), dim3(BS), 0, c.st, n, 1, (const double*)nullptr,
+                             (const double*)(field == PUCFEM_F_P ? c.yp : c.yp2), (const double*)nullptr, pf,
+                             (double*)nullptr, (const int32_t*)c.dmaster_of);
+          KCHK();
+        }
+        get1(pf);
+        break;
+      }
       case PUCFEM_F_DIV_STAR:  // computed from u* when read (the step records only its max)
         if (c.scheme == PUCFEM_STOKES_COLOR || c.scheme == PUCFEM_STOKES_FOOD) c.div(c.usx, c.usy, c.div_star, false);
         get1(c.div_star);
@@ -3782,6 +3848,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.cur_step = s;
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
+          c.proj_materialize();  // (no direction stays pending between API calls)
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
@@ -4333,7 +4400,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
-           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0);
+           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.p_from_y ? 64 : 0);
   });
 }
 

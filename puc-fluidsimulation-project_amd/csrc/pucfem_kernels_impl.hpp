@@ -577,11 +577,19 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
 // [<X_i, b> (M), <X_i, A v> (M), <v, b>, <v, A v>, sum_free v, sum_free b].  One instance per M:
 // the M loads of a row are unconditional (all in flight together); grid-stride rows keep the
 // resident waves on one compact window of every vector.
+// The last solve's direction may still be pending (D.y non-null): then v = y - x0 and A v = r0 - r_final are
+// formed here from the last solve's solution, guess, initial and final residuals (av holds r0) -- the
+// operations k_diff2_fin would have stored, so the same values -- instead of being read.
+struct PendDir {
+  const double* y;   // the last solve's solution (null: v and A v were stored)
+  const double* x0;  // its guess
+  const double* rf;  // its final residual
+};
 template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
                                               const double* __restrict__ v, const int32_t* __restrict__ master_of,
-                                              double* part, RedOut ro) {
+                                              double* part, RedOut ro, PendDir D) {
   constexpr int NA = 2 * M + 4;
   __shared__ double sh[NA][4];
   double acc[NA];
@@ -589,7 +597,15 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
   for (int i = 0; i < NA; ++i) acc[i] = 0.0;
   const int64_t step = (int64_t)gridDim.x * BS;
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
-    const double br = b[r], ar = av[r], vr = v[r];
+    const double br = b[r];
+    double ar, vr;
+    if (D.y) {
+      vr = D.y[r] - D.x0[r];
+      ar = av[r] - D.rf[r];
+    } else {
+      ar = av[r];
+      vr = v[r];
+    }
     double x[M > 0 ? M : 1];
 #pragma unroll
     for (int i = 0; i < M; ++i) x[i] = (double)X[i * ld + r];
@@ -651,12 +667,14 @@ __global__ void k_pcoef(const double* __restrict__ D, int m, const double* __res
 }
 
 // pass 2: the new direction X_M = s (v - mu 1_free - sum_i c_i X_i) and the guess
-// x0 = sum_i a_i X_i + alpha X_M (written to y and x0), one pass over the M basis vectors
+// x0 = sum_i a_i X_i + alpha X_M (written to y and x0), one pass over the M basis vectors.
+// yp non-null: v = yp - x0 (the pending direction, k_mdot2's PendDir) from the last solve's solution and the
+// old x0, each row read before this row's new x0 (and y, which may be yp's buffer) is written
 template <int M>
 __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ K, const double* __restrict__ v,
                                               const int32_t* __restrict__ master_of, ProjT* __restrict__ xm_out,
-                                              double* __restrict__ y, double* __restrict__ x0) {
+                                              double* y, double* x0, const double* yp) {
   double ka[M > 0 ? M : 1], kc[M > 0 ? M : 1];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
@@ -674,7 +692,8 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
       sa += ka[i] * x[i];
       sc += kc[i] * x[i];
     }
-    const double xm = s * (v[r] - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
+    const double vr = yp ? yp[r] - x0[r] : v[r];
+    const double xm = s * (vr - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
     const double g = sa + alpha * xm;
     stnt(xm_out + r, (ProjT)xm);
     stnt(y + r, g);

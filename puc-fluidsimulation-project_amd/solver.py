@@ -237,7 +237,8 @@ class Context:
                     viscous_iteration="chebyshev" if o[7] & 4 else "cg",
                     visc_check_failed=bool(o[7] & 8),
                     visc_step_pairs=bool(o[7] & 16),
-                    mg_step_pairs=bool(o[7] & 32))
+                    mg_step_pairs=bool(o[7] & 32),
+                    pending_pressure_directions=bool(o[7] & 64))
 
     def visc_interval(self):
         """[lo, hi] of the viscous Chebyshev iteration (pucfem_visc_interval)."""

@@ -384,6 +384,31 @@ def test_step_pairs_equal_single_steps(monkeypatch, refine, knob, key):
     b.close()
 
 
+@pytest.mark.parametrize("refine,shared", [(3, True), (3, False), (5, True)])
+def test_pending_pressure_directions_equal_stored(monkeypatch, refine, shared):
+    """The projection's new direction left pending after a pressure solve (v = y - x0 and A v = r0 - r_final
+    formed by the next solve's k_mdot2 / k_pcomb instead of stored by k_diff2_fin) and the gradient projection
+    gathering the solution y through the merged slave -> master tables (instead of p = y with the slaves
+    copied) compute the same values: the production run is bit-identical to the stored form, over step()
+    calls of several sizes (a pending direction is stored at the end of every call), including the
+    pressure fields read back."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    a = stokes(mesh, tol=S.Tolerances.production(proj_shared=shared))
+    monkeypatch.setenv("PUCFEM_P_FROM_Y", "0")
+    b = stokes(mesh, tol=S.Tolerances.production(proj_shared=shared))
+    assert a.ctx.path_info()["pending_pressure_directions"] and not b.ctx.path_info()["pending_pressure_directions"]
+    sa, sb = [], []
+    for k in (1, 3, 5):
+        sa += a.step(k)
+        sb += b.step(k)
+    assert [(s.it_visc, s.it_p, s.it_p2) for s in sa] == [(s.it_visc, s.it_p, s.it_p2) for s in sb]
+    assert np.array_equal(a.u, b.u) and np.array_equal(a.c, b.c)
+    assert np.array_equal(a.field(L.F_P), b.field(L.F_P))
+    assert np.array_equal(a.field(L.F_P2), b.field(L.F_P2))
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("records", ["0", "1"])
 def test_knn_radii_device_equals_host(monkeypatch, records):
     """The semi-Lagrangian fast-accept radii (k-NN distances of every centroid and vertex) are built on
