@@ -532,6 +532,10 @@ struct Ctx {
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_coef) (void)hipHostFree(h_coef);
       if (h_pinned) (void)hipHostFree(h_pinned);
+      for (int k = 0; k < 2; ++k) {
+        if (stage[k]) (void)hipHostFree(stage[k]);
+        if (stage_ev[k]) (void)hipEventDestroy(stage_ev[k]);
+      }
       comm.reset();
       if (st_sl) (void)hipStreamSynchronize(st_sl);
       if (ev_u) (void)hipEventDestroy(ev_u);
@@ -554,8 +558,69 @@ struct Ctx {
   template <class T>
   T* upload(const std::vector<T>& v) {
     T* p = dalloc<T>((i64)v.size());
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
+    if (!v.empty()) h2d(p, v.data(), sizeof(T) * v.size());
     return p;
+  }
+  // Setup copies of large pageable arrays through two pinned staging buffers (double-buffered; the host
+  // side of every chunk copied by the host threads): a pageable hipMemcpy moved 3 GB of device-assembly
+  // results in 0.66 s at L7.  h2d is ordered on st like hipMemcpyAsync; d2h returns with the data in dst.
+  static constexpr size_t STAGE_BYTES = size_t(64) << 20;
+  char* stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  bool stage_busy[2] = {false, false};
+  void stage_wait(int k) {
+    if (!stage[k]) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&stage[k]), STAGE_BYTES));
+      HIPCHK(hipEventCreateWithFlags(&stage_ev[k], hipEventDisableTiming));
+    }
+    if (stage_busy[k]) HIPCHK(hipEventSynchronize(stage_ev[k]));
+    stage_busy[k] = false;
+  }
+  static void host_copy(char* dst, const char* src, size_t len) {
+    parallel_for((i64)len, [&](i64 a, i64 b) { std::memcpy(dst + a, src + a, (size_t)(b - a)); });
+  }
+  void h2d(void* dst, const void* src, size_t bytes) {
+    if (bytes < (size_t(8) << 20)) {
+      HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+      return;
+    }
+    for (size_t off = 0, i = 0; off < bytes; off += STAGE_BYTES, ++i) {
+      const size_t len = std::min(STAGE_BYTES, bytes - off);
+      const int k = (int)(i & 1);
+      stage_wait(k);
+      host_copy(stage[k], static_cast<const char*>(src) + off, len);
+      HIPCHK(hipMemcpyAsync(static_cast<char*>(dst) + off, stage[k], len, hipMemcpyHostToDevice, st));
+      HIPCHK(hipEventRecord(stage_ev[k], st));
+      stage_busy[k] = true;
+    }
+  }
+  void d2h(void* dst, const void* src, size_t bytes) {
+    if (bytes < (size_t(8) << 20)) {
+      HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      return;
+    }
+    size_t prev_off = 0, prev_len = 0;
+    int prev_k = -1;
+    for (size_t off = 0, i = 0; off < bytes; off += STAGE_BYTES, ++i) {
+      const size_t len = std::min(STAGE_BYTES, bytes - off);
+      const int k = (int)(i & 1);
+      stage_wait(k);
+      HIPCHK(hipMemcpyAsync(stage[k], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipEventRecord(stage_ev[k], st));
+      stage_busy[k] = true;
+      if (prev_k >= 0) {  // the previous chunk, while this one is in flight
+        stage_wait(prev_k);
+        host_copy(static_cast<char*>(dst) + prev_off, stage[prev_k], prev_len);
+      }
+      prev_off = off;
+      prev_len = len;
+      prev_k = k;
+    }
+    if (prev_k >= 0) {
+      stage_wait(prev_k);
+      host_copy(static_cast<char*>(dst) + prev_off, stage[prev_k], prev_len);
+    }
   }
   // int16 column deltas for a square operator's SELL (prm.idx32 = 0 and the band fits); nloc: the
   // local vector length (owned + ghost), the wrap modulus
@@ -2487,6 +2552,11 @@ struct DevTmp {
     v.resize((size_t)n);
     if (n > 0) HIPCHK(hipMemcpyAsync(v.data(), p, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost, st));
   }
+  // through the context's pinned staging buffers (returns with the data on the host)
+  void get(std::vector<T>& v, i64 n, Ctx& c) const {
+    host_resize(v, (size_t)n);
+    if (n > 0) c.d2h(v.data(), p, sizeof(T) * (size_t)n);
+  }
 };
 
 // The stiffness pattern P and the K / Gx / Gy / lumped-mass / area-sum values of a mesh assembled on the
@@ -2496,10 +2566,15 @@ struct DevTmp {
 void assemble_device(Ctx& c, const HostMesh& m, const Ordering& ord, Csr& P, Assembly& A) {
   hipStream_t st = c.st;
   const i64 N = m.N, T = m.T;
+  SetupClock ck;  // (PUCFEM_SETUP_TIMING: the phases inside)
   const int nb = (int)std::min<i64>(16384, std::max<i64>(1, (3 * T + BS - 1) / BS));
   const int nbr = (int)std::min<i64>(16384, std::max<i64>(1, (N + BS - 1) / BS));
   DevTmp<i32> dtri(m.tri, st), dold2new(ord.old2new, st);
   DevTmp<double> dx(m.x, st), dy(m.y, st);
+  if (ck.on) {
+    HIPCHK(hipStreamSynchronize(st));
+    ck.mark("  asm: mesh upload");
+  }
   // incidence
   DevTmp<i32> cnt(N, st);
   hipLaunchKernelGGL(k_inc_count, dim3(nb), dim3(BS), 0, st, 3 * T, (const i32*)dtri.p, (const i32*)dold2new.p, cnt.p);
@@ -2540,14 +2615,19 @@ void assemble_device(Ctx& c, const HostMesh& m, const Ordering& ord, Csr& P, Ass
                      (const i32*)dold2new.p, (const double*)dx.p, (const double*)dy.p, (const i64*)drow.p,
                      (const i32*)dcol.p, K.p, Gx.p, Gy.p, M.p, as.p);
   KCHK();
-  dcol.get(P.col, nnz, st);
+  if (ck.on) {
+    HIPCHK(hipStreamSynchronize(st));
+    ck.mark("  asm: incidence, pattern, values (device)");
+  }
+  dcol.get(P.col, nnz, c);
   P.val.clear();
-  K.get(A.K, nnz, st);
-  Gx.get(A.Gx, nnz, st);
-  Gy.get(A.Gy, nnz, st);
-  M.get(A.M, N, st);
-  as.get(A.asum, N, st);
+  K.get(A.K, nnz, c);
+  Gx.get(A.Gx, nnz, c);
+  Gy.get(A.Gy, nnz, c);
+  M.get(A.M, N, c);
+  as.get(A.asum, N, c);
   HIPCHK(hipStreamSynchronize(st));
+  ck.mark("  asm: downloads");
 }
 
 // device values and work vectors of every multigrid level in the V-cycle's type T.
@@ -3014,14 +3094,15 @@ void build(Ctx& c) {
   // Jacobi symmetric scaling S A S: s_g = 1 / sqrt(a_gg); the scaled values s_r a_rk s_col go straight into
   // the SELL image (only the skeleton rows on lattice hierarchies)
   auto scaling = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
-    sg.resize(N);
+    host_resize(sg, N);
     parallel_for(N, [&](i64 g0, i64 g1) {
       for (i64 g = g0; g < g1; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
     });
   };
   auto local_vec = [&](const std::vector<double>& g) {  // owned + ghost entries of a global vector
-    std::vector<double> v(c.nloc);
-    for (i64 i = 0; i < no; ++i) v[i] = g[lp.r0 + i];
+    std::vector<double> v;
+    host_resize(v, c.nloc);
+    parallel_for(no, [&](i64 i0, i64 i1) { std::memcpy(v.data() + i0, g.data() + lp.r0 + i0, sizeof(double) * (i1 - i0)); });
     for (i64 k = 0; k < lp.n_ghost; ++k) v[no + k] = g[lp.ghost_global[k]];
     return v;
   };
@@ -3031,8 +3112,11 @@ void build(Ctx& c) {
     sell_values_fn(c.P, lp.r0, c.sP, [&](i64 r, i64 k) { return sg[r] * c.Kv[k] * sg[c.P.col[k]]; }, tmp);
     c.dKv = c.upload(tmp);
     c.dsv = c.upload(local_vec(sg));
-    std::vector<double> sq(N);
-    for (i64 g = 0; g < N; ++g) sq[g] = 1.0 / sg[g];
+    std::vector<double> sq;
+    host_resize(sq, N);
+    parallel_for(N, [&](i64 g0, i64 g1) {
+      for (i64 g = g0; g < g1; ++g) sq[g] = 1.0 / sg[g];
+    });
     c.dsqv = c.upload(local_vec(sq));
     if (c.lattice) {  // scaled A_visc, skeleton columns: s_j, 0 for Dirichlet columns (StokesColor.py:473-475)
       std::vector<double> w = local_vec(sg);
@@ -3043,6 +3127,7 @@ void build(Ctx& c) {
       c.dwsk = c.upload(w);
     }
   }
+  clk.mark("  dev: scaled A_visc");
   if (stokes) {
     dsell(c.sPp, c.Pp, c.dPp);
     if (!c.lattice) {  // the Jacobi-scaled pressure operator (Jacobi-CG and the SELL unit op; a lattice hierarchy
@@ -3064,6 +3149,7 @@ void build(Ctx& c) {
     c.mg_single = c.prm.mg_single != 0;
     if (c.mg_single) mg_alloc<float>(c, tmp);
     else mg_alloc<double>(c, tmp);
+    clk.mark("  dev: pressure SELL, level values");
     if (c.lattice) {  // the face parts of every lattice operator (pucfem_lattice.hpp)
       auto mkface = [&](const std::vector<lat::FaceTab>& tab, const std::vector<lat::FaceTab>* tab2, const double* coef,
                         const float* coef32, int l, int l2, int op) {
@@ -3105,6 +3191,7 @@ void build(Ctx& c) {
         }
       }
     }
+    clk.mark("  dev: lattice face tables");
     // coarsest: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
     {
       MgLevel& L0 = c.mg[0];
@@ -3216,19 +3303,27 @@ void build(Ctx& c) {
   clk.mark("device: projections, dense");
   // per-row data
   {
-    std::vector<double> as1(no), mp(no), wm(no);
-    std::vector<uint8_t> df(no);
-    std::vector<i32> so(no, -1), mo(no, -1);
-    for (i64 i = 0; i < no; ++i) {
-      const i64 g = lp.r0 + i;
-      as1[i] = c.as.asum[g] + 1e-12;
-      mp[i] = c.as.M[g] + 1e-12;
-      wm[i] = m.mk[c.ord.new2old[g]] == 0 ? c.as.M[g] : 0.0;
-      df[i] = isdir[g];
-      if (c.slave_of[g] >= 0) so[i] = to_local(lp, c.slave_of[g]);
-      if (c.master_of[g] >= 0) mo[i] = to_local(lp, c.master_of[g]);
-      require(so[i] < (i32)no && mo[i] < (i32)no, "periodic partner on another rank");
-    }
+    std::vector<double> as1, mp, wm;
+    std::vector<uint8_t> df;
+    std::vector<i32> so, mo;
+    host_resize(as1, no);
+    host_resize(mp, no);
+    host_resize(wm, no);
+    host_resize(df, no);
+    host_resize(so, no);
+    host_resize(mo, no);
+    parallel_for(no, [&](i64 i0, i64 i1) {
+      for (i64 i = i0; i < i1; ++i) {
+        const i64 g = lp.r0 + i;
+        as1[i] = c.as.asum[g] + 1e-12;
+        mp[i] = c.as.M[g] + 1e-12;
+        wm[i] = m.mk[c.ord.new2old[g]] == 0 ? c.as.M[g] : 0.0;
+        df[i] = isdir[g];
+        so[i] = c.slave_of[g] >= 0 ? to_local(lp, c.slave_of[g]) : -1;
+        mo[i] = c.master_of[g] >= 0 ? to_local(lp, c.master_of[g]) : -1;
+        require(so[i] < (i32)no && mo[i] < (i32)no, "periodic partner on another rank");
+      }
+    });
     c.das1 = c.upload(as1);
     c.dmp = c.upload(mp);
     c.dwmix = c.upload(wm);
@@ -3236,6 +3331,7 @@ void build(Ctx& c) {
     c.dslave_of = c.upload(so);
     c.dmaster_of = c.upload(mo);
   }
+  clk.mark("  dev: per-row data");
   // BC lists: sequential copy semantics resolved symbolically (caller numbering), then local
   {
     std::vector<i64> src(N);
@@ -3288,6 +3384,7 @@ void build(Ctx& c) {
     c.ddval = c.upload(dv);
     c.dbctmp = c.dalloc<double>(2 * std::max(1, c.ncopy));
   }
+  clk.mark("  dev: BC lists");
   // halo plan
   c.nsend = (i64)lp.send_local.size();
   c.dsend = c.upload(lp.send_local);

@@ -852,25 +852,71 @@ bool lu_inverse(std::vector<double>& A, i64 n) {
 }
 
 bool spd_inverse(std::vector<double>& A, i64 n) {
-  // Cholesky A = L L^T (lower, in place), then inv = L^-T L^-1
-  for (i64 j = 0; j < n; ++j) {
-    double d = A[j * n + j];
-    for (i64 k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
-    if (!(d > 0)) return false;
-    d = std::sqrt(d);
-    A[j * n + j] = d;
-    for (i64 i = j + 1; i < n; ++i) {
-      double s = A[i * n + j];
-      for (i64 k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
-      A[i * n + j] = s / d;
+  // Cholesky A = L L^T (lower, in place), then inv = L^-T L^-1.
+  // Left-looking by rows, rows dealt cyclically to the threads: row i's entry in column j needs only row i
+  // (its own thread's) and row j up to its diagonal, so the owner of row j publishes its diagonal (`ready`)
+  // and the other threads go on with column j without a barrier.  Same operations in the same order as
+  // the serial loop: bit-identical factor.
+  const int nt = (int)std::max<i64>(1, std::min<i64>((i64)host_threads(), n / 64));
+  {
+    std::atomic<i64> ready{0};  // rows [0, ready) final up to and including their diagonal
+    std::atomic<bool> bad{false};
+    auto work = [&](int t) {
+      for (i64 j = 0; j < n; ++j) {
+        if (j % nt == t) {
+          double d = A[j * n + j];
+          for (i64 k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+          if (!(d > 0)) {
+            bad.store(true, std::memory_order_release);
+            ready.store(n, std::memory_order_release);
+            return;
+          }
+          A[j * n + j] = std::sqrt(d);
+          ready.store(j + 1, std::memory_order_release);
+        } else {
+          for (int spin = 0; ready.load(std::memory_order_acquire) <= j; ++spin)
+            if (spin > 64) std::this_thread::yield();
+        }
+        if (bad.load(std::memory_order_acquire)) return;
+        const double d = A[j * n + j];
+        const double* aj = A.data() + j * n;
+        i64 i = j + 1 + ((t - (j + 1) % nt) % nt + nt) % nt;  // first row > j of thread t
+        for (; i < n; i += nt) {
+          double* ai = A.data() + i * n;
+          double s = ai[j];
+          for (i64 k = 0; k < j; ++k) s -= ai[k] * aj[k];
+          ai[j] = s / d;
+        }
+      }
+    };
+    if (nt == 1) {
+      work(0);
+    } else {
+      ThreadGroup g;
+      for (int t = 0; t < nt; ++t) g.spawn([&work, t] { work(t); });
+      g.join();
     }
+    if (bad.load()) return false;
   }
   // Linv (lower): column j of W = L^-1 by forward substitution, columns independent -> threads; stored
   // transposed (Wt[j][i] = W[i][j]) so both loops below read contiguous rows.  Same operations in the
   // same order as the column-by-column loop: the inverse is bit-identical to the serial one.
+  // (triangular work per row: rows dealt cyclically to the threads, not parallel_for's contiguous ranges)
+  auto cyclic = [nt](i64 n_, auto&& f) {
+    if (nt == 1) {
+      for (i64 i = 0; i < n_; ++i) f(i);
+      return;
+    }
+    ThreadGroup g;
+    for (int t = 0; t < nt; ++t)
+      g.spawn([&f, t, nt, n_] {
+        for (i64 i = t; i < n_; i += nt) f(i);
+      });
+    g.join();
+  };
   std::vector<double> Wt(n * n, 0.0);
-  parallel_for(n, [&](i64 j0, i64 j1) {
-    for (i64 j = j0; j < j1; ++j) {
+  cyclic(n, [&](i64 j) {
+    {
       double* w = Wt.data() + j * n;
       w[j] = 1.0 / A[j * n + j];
       for (i64 i = j + 1; i < n; ++i) {
@@ -881,8 +927,8 @@ bool spd_inverse(std::vector<double>& A, i64 n) {
     }
   });
   // inv = W^T W: inv[i][j] = sum_{k >= i} W[k][i] W[k][j] (j <= i), rows independent -> threads
-  parallel_for(n, [&](i64 i0, i64 i1) {
-    for (i64 i = i0; i < i1; ++i) {
+  cyclic(n, [&](i64 i) {
+    {
       const double* wi = Wt.data() + i * n;
       for (i64 j = 0; j <= i; ++j) {
         const double* wj = Wt.data() + j * n;

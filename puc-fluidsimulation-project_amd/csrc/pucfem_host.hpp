@@ -14,6 +14,8 @@
 #include <utility>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "pucfem_lattice.hpp"
 
 namespace pucfem {
@@ -90,6 +92,20 @@ void parallel_for(i64 n, F&& f) {
   ThreadGroup g;
   for (int w = 0; w < nt; ++w) g.spawn([&, w] { f(n * w / nt, n * (w + 1) / nt); });
   g.join();
+}
+// v.resize(n) for a large array the setup fills next: the fresh allocation is advised onto transparent
+// huge pages first (first-touch zero-fill of 4 KiB pages ran at ~1.6 GB/s, half the rate on 2 MiB pages)
+template <class T>
+void host_resize(std::vector<T>& v, size_t n) {
+  if (n * sizeof(T) >= (size_t(32) << 20) && v.capacity() < n) {
+    std::vector<T>().swap(v);
+    v.reserve(n);
+    const uintptr_t HP = uintptr_t(1) << 21;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(v.data()) + HP - 1) & ~(HP - 1);
+    const uintptr_t e = reinterpret_cast<uintptr_t>(v.data()) + n * sizeof(T);
+    if (e > a) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+  }
+  v.resize(n);
 }
 // f(chunk, r0, r1) over PAR_CHUNKS fixed chunks of [0, n) (independent of the machine's thread
 // count: per-chunk partial sums combined in chunk order are reproducible everywhere)
