@@ -2145,19 +2145,21 @@ struct Ctx {
     const i64 n = lp.n_own;
     double* x = dalloc<double>(nloc);
     double* y = dalloc<double>(nloc);
-    std::vector<double> x0(n);
-    for (i64 i = 0; i < n; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)i);
-    const double* dinv = upload(lmax_dinv);
+    std::vector<double> x0(n);  // (global row index: a partitioned run iterates the single-rank vector)
+    for (i64 i = 0; i < n; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)(lp.r0 + i));
+    const double* dinv = upload(std::vector<double>(lmax_dinv.begin() + lp.r0, lmax_dinv.begin() + lp.r0 + n));
     HIPCHK(hipMemcpyAsync(x, x0.data(), sizeof(double) * n, hipMemcpyHostToDevice, st));
     const int nb = nb_rows(n), ge = grid_ew(n);
     double lam = 0.0;
     for (int it = 0; it < 30; ++it) {
+      halo(x);
       spmv_on(st, dPp, fP.full(), dKp_raw, x, y);
       hipLaunchKernelGGL(k_vmul, dim3(ge), dim3(BS), 0, st, n, (const double*)y, dinv, y);
       hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(BS), 0, st, n, (const double*)x, (const double*)x, (const double*)y,
                          (const double*)y, part_a);
       hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, redbuf);
       KCHK();
+      if (dist()) comm->allreduce(redbuf, 2, false, st);
       HIPCHK(hipMemcpyAsync(h_pinned, redbuf, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       const double nx = h_pinned[0], ny = h_pinned[1];
@@ -2465,8 +2467,9 @@ void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
   F.master_of = c.master_of;
   // the transfers of every level (serial builders, one thread per level) and the lmax estimates (each
   // parallel inside) read only what the level operators above produced: they run concurrently
-  // the finest level's power iteration runs on the device at the end of build() (single rank)
-  c.lmax_dev = c.world == 1 && !c.host_only;
+  // the finest level's power iteration runs on the device at the end of build() (every rank its strip:
+  // halos before the products, the two norms all-reduced)
+  c.lmax_dev = !c.host_only;
   {
     ThreadGroup g;  // joined on every exit path; a level's exception reaches the caller from join()
     for (int l = 1; l <= Lv; ++l)
