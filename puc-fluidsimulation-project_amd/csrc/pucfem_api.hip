@@ -1813,6 +1813,10 @@ struct Ctx {
       const double* b[1] = {bh};
       it = cg<1>(dPp, HFace{}, dKp, y, b, prm.rtol_pres, prm.maxit_pres, which);
     }
+    if (use_mg && proj && p_from_y) {  // p stays in y: the gradient gathers y's ghosts
+      halo(yst);
+      return it;
+    }
     if (!(use_mg && proj)) {
       algo_bytes += (20.0 + (sc ? 8.0 : 0.0)) * (double)n;  // master_of, y (, s) read; p written
       hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
@@ -3230,19 +3234,35 @@ void build(Ctx& c) {
   c.proj_k = c.use_mg && !c.dense ? proj_size(c.prm.proj_k) : 0;
   c.proj_shared = c.prm.proj_shared != 0;
   if (const char* e = std::getenv("PUCFEM_PROJ_SHARED")) c.proj_shared = std::atoi(e) != 0;
-  // pending pressure directions and the gradient on y (Ctx::p_from_y): one rank, lattice operators, the
-  // multigrid PCG with the projection, the explicit dye; PUCFEM_P_FROM_Y=0 keeps the stored form (a
-  // measurement knob: the same values either way)
-  c.p_from_y = stokes && c.lattice && !c.dist() && c.use_mg && c.proj_k > 0 && !c.dye_impl && c.dP.c16 == nullptr &&
+  // pending pressure directions and the gradient on y (Ctx::p_from_y): lattice operators, the multigrid PCG
+  // with the projection, the explicit dye; PUCFEM_P_FROM_Y=0 keeps the stored form (a measurement knob: the
+  // same values either way).  Partitioned runs exchange y's halo instead of p's.
+  c.p_from_y = stokes && c.lattice && c.use_mg && c.proj_k > 0 && !c.dye_impl && c.dP.c16 == nullptr &&
                !(std::getenv("PUCFEM_P_FROM_Y") && std::atoi(std::getenv("PUCFEM_P_FROM_Y")) == 0);
-  if (c.p_from_y) {  // dP with every column mapped to its periodic master (the dof map)
+  if (c.p_from_y) {  // dP with every column mapped to its periodic master (the dof map), in local ids
     std::vector<i32> colm(c.sP.col.size());
-    for (size_t e = 0; e < colm.size(); ++e) {
+    const i64 nl = (i64)c.nloc;
+    bool ok = true;
+    for (size_t e = 0; e < colm.size() && ok; ++e) {
       const i32 j = c.sP.col[e];
-      colm[e] = j >= 0 && j < (i32)c.dof.size() ? c.dof[j] : j;
+      colm[e] = j;
+      if (j < 0 || j >= nl) continue;
+      const i32 g = j < no ? (i32)(lp.r0 + j) : lp.ghost_global[j - no];
+      const i32 mg = c.dof[g];
+      if (mg == g) continue;
+      if (mg >= lp.r0 && mg < lp.r1) {
+        colm[e] = (i32)(mg - lp.r0);
+      } else {
+        auto it = std::lower_bound(lp.ghost_global.begin(), lp.ghost_global.end(), mg);
+        if (it == lp.ghost_global.end() || *it != mg) ok = false;  // a master outside the local columns
+        else colm[e] = (i32)(no + (it - lp.ghost_global.begin()));
+      }
     }
-    c.dPm = c.dP;
-    c.dPm.col = c.upload(colm);
+    c.p_from_y = ok;
+    if (ok) {
+      c.dPm = c.dP;
+      c.dPm.col = c.upload(colm);
+    }
   }
   const bool block_visc = !c.dist() && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
   c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
