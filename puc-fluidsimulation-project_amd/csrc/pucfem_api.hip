@@ -2149,10 +2149,14 @@ struct Ctx {
     const i64 n = lp.n_own;
     double* x = dalloc<double>(nloc);
     double* y = dalloc<double>(nloc);
-    std::vector<double> x0(n);  // (global row index: a partitioned run iterates the single-rank vector)
-    for (i64 i = 0; i < n; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)(lp.r0 + i));
-    const double* dinv = upload(std::vector<double>(lmax_dinv.begin() + lp.r0, lmax_dinv.begin() + lp.r0 + n));
-    HIPCHK(hipMemcpyAsync(x, x0.data(), sizeof(double) * n, hipMemcpyHostToDevice, st));
+    std::vector<double> x0;  // (global row index: a partitioned run iterates the single-rank vector)
+    host_resize(x0, n);
+    parallel_for(n, [&](i64 i0, i64 i1) {
+      for (i64 i = i0; i < i1; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)(lp.r0 + i));
+    });
+    double* dinv = dalloc<double>(n);
+    h2d(dinv, lmax_dinv.data() + lp.r0, sizeof(double) * n);
+    h2d(x, x0.data(), sizeof(double) * n);
     const int nb = nb_rows(n), ge = grid_ew(n);
     double lam = 0.0;
     for (int it = 0; it < 30; ++it) {
@@ -2713,23 +2717,24 @@ struct SlPrep {
   bool lat_sl = false;
 };
 void sl_prep(const Ctx& c, bool food, SlPrep& P) {
+  SetupClock ck;  // (its own thread: the marks interleave with build()'s)
   const HostMesh& m = c.mesh;
   const i64 N = m.N;
-  P.X.resize(N);
-  P.Y.resize(N);
+  host_resize(P.X, N);
+  host_resize(P.Y, N);
   parallel_for(N, [&](i64 g0, i64 g1) {
     for (i64 g = g0; g < g1; ++g) {
       P.X[g] = m.x[c.ord.new2old[g]];
       P.Y[g] = m.y[c.ord.new2old[g]];
     }
   });
-  P.tri.resize(3 * m.T);
+  host_resize(P.tri, 3 * m.T);
   parallel_for(3 * m.T, [&](i64 k0, i64 k1) {
     for (i64 k = k0; k < k1; ++k) P.tri[k] = c.ord.old2new[m.tri[k]];
   });
   // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
-  P.cx.resize(m.T);
-  P.cy.resize(m.T);
+  host_resize(P.cx, m.T);
+  host_resize(P.cy, m.T);
   parallel_for(m.T, [&](i64 t0, i64 t1) {
     for (i64 t = t0; t < t1; ++t) {
       const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
@@ -2737,9 +2742,11 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
       P.cy[t] = (m.y[a] + m.y[b] + m.y[d]) / 3;
     }
   });
+  ck.mark("  sl: node / triangle tables, centroids");
   build_centroid_grid(P.cx, P.cy, 2.0, P.G);
+  ck.mark("  sl: centroid grid");
   if (food) build_tri_grid(P.X, P.Y, P.tri, 4.0, P.TG);  // tracer location (StokesFood only)
-  P.xy.resize(2 * (size_t)N);
+  host_resize(P.xy, 2 * (size_t)N);
   parallel_for(N, [&](i64 i0, i64 i1) {
     for (i64 i = i0; i < i1; ++i) {
       P.xy[2 * i] = P.X[i];
@@ -2756,17 +2763,24 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
       P.lat_sl = false;  // a hierarchy not numbered face by face: the record locator
     }
   }
+  ck.mark("  sl: xy, lattice locator");
   if (P.lat_sl) {
     build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, P.MG, 1e-6);
     // home faces: the macro face of every face-interior row (the first face tried)
     const LatticeLevel& LL = c.mg.back().latl;
-    P.home.assign(N, -1);
-    for (i64 f = 0; f < c.macro.nf; ++f)
-      for (i64 k = 0; k < LL.F; ++k) P.home[LL.face_start[f] + k] = (i32)f;
+    host_resize(P.home, N);
+    std::fill(P.home.begin(), P.home.end(), -1);
+    parallel_for(c.macro.nf, [&](i64 f0, i64 f1) {
+      for (i64 f = f0; f < f1; ++f)
+        for (i64 k = 0; k < LL.F; ++k) P.home[LL.face_start[f] + k] = (i32)f;
+    }, 1);
   }
   // initial dye c = 1[x < 0.5] (StokesColor.py:493-495)
-  P.c0.resize(N);
-  for (i64 g = 0; g < N; ++g) P.c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
+  host_resize(P.c0, N);
+  parallel_for(N, [&](i64 g0, i64 g1) {
+    for (i64 g = g0; g < g1; ++g) P.c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
+  });
+  ck.mark("  sl: home faces, initial dye");
 }
 
 void build(Ctx& c) {

@@ -226,7 +226,7 @@ void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P, const Inciden
   for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)ccol[ch].size();
   parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
     for (i64 ch = c0; ch < c1; ++ch) std::copy(ccol[ch].begin(), ccol[ch].end(), P.col.begin() + cstart[ch]);
-  });
+  }, 1);
 }
 
 // ----------------------------------------------------------------------------- assembly
@@ -573,7 +573,7 @@ void sell_values(const Csr& A, const LocalPlan& lp, const Sell& S, const std::ve
         i64 b = A.rowptr[lp.r0 + r], len = A.rowptr[lp.r0 + r + 1] - b;
         for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
       }
-  });
+  }, 64);
 }
 
 // ----------------------------------------------------------------------------- grids
@@ -601,23 +601,54 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
   grid_dims(*std::min_element(cx.begin(), cx.end()), *std::max_element(cx.begin(), cx.end()),
             *std::min_element(cy.begin(), cy.end()), *std::max_element(cy.begin(), cy.end()), T, per_cell, G);
   const i64 nc = (i64)G.nx * G.ny;
-  std::vector<i32> cell(T);
-  G.cell_start.assign(nc + 1, 0);
+  std::vector<i32> cell;
+  host_resize(cell, T);
   parallel_for(T, [&](i64 t0, i64 t1) {
     for (i64 t = t0; t < t1; ++t) cell[t] = cell_of(cy[t], G.y0, G.hy, G.ny) * G.nx + cell_of(cx[t], G.x0, G.hx, G.nx);
   });
-  for (i64 t = 0; t < T; ++t) G.cell_start[cell[t] + 1]++;
+  // counting sort by cell, ascending triangle id inside each cell.  Each thread owns a contiguous range of
+  // cells and scans every triangle (two passes over the 4 B cell ids) for those in its range: the same
+  // order as one sequential pass, no per-thread histograms of all cells.
+  G.cell_start.assign(nc + 1, 0);
+  host_resize(G.item, T);
+  host_resize(G.px, T);
+  host_resize(G.py, T);
+  const int nt = (int)std::max<i64>(1, std::min<i64>((i64)host_threads(), T / 65536 + 1));
+  auto range = [&](int w, i64& c0, i64& c1) {
+    c0 = nc * w / nt;
+    c1 = nc * (w + 1) / nt;
+  };
+  auto run = [&](auto&& f) {
+    if (nt == 1) {
+      f(0);
+      return;
+    }
+    ThreadGroup g;
+    for (int w = 0; w < nt; ++w) g.spawn([&f, w] { f(w); });
+    g.join();
+  };
+  run([&](int w) {  // counts
+    i64 c0, c1;
+    range(w, c0, c1);
+    for (i64 t = 0; t < T; ++t) {
+      const i64 c = cell[t];
+      if (c >= c0 && c < c1) G.cell_start[c + 1]++;
+    }
+  });
   for (i64 c = 0; c < nc; ++c) G.cell_start[c + 1] += G.cell_start[c];
-  G.item.assign(T, 0);
-  G.px.assign(T, 0);
-  G.py.assign(T, 0);
-  std::vector<i32> fill(G.cell_start.begin(), G.cell_start.end() - 1);
-  for (i64 t = 0; t < T; ++t) {  // ascending triangle id inside each cell
-    i32 k = fill[cell[t]]++;
-    G.item[k] = (i32)t;
-    G.px[k] = cx[t];
-    G.py[k] = cy[t];
-  }
+  run([&](int w) {  // the fill
+    i64 c0, c1;
+    range(w, c0, c1);
+    std::vector<i32> fill(G.cell_start.begin() + c0, G.cell_start.begin() + c1);
+    for (i64 t = 0; t < T; ++t) {
+      const i64 c = cell[t];
+      if (c < c0 || c >= c1) continue;
+      const i32 k = fill[c - c0]++;
+      G.item[k] = (i32)t;
+      G.px[k] = cx[t];
+      G.py[k] = cy[t];
+    }
+  });
 }
 
 std::vector<float> centroid_knn_radius2(const Grid& G, const std::vector<double>& cx, const std::vector<double>& cy,
@@ -1036,7 +1067,7 @@ void sell_values_x(const Csr& A, i64 r0, const Sell& S, const std::vector<double
         const i64 b = A.rowptr[r0 + r], len = A.rowptr[r0 + r + 1] - b;
         for (i64 k = 0; k < len; ++k) out[S.slice_off[s] + k * 64 + l] = val[b + k];
       }
-  });
+  }, 64);
 }
 
 }  // namespace pucfem
@@ -1558,7 +1589,7 @@ void lattice_locator(const Macro& M, const LatticeLevel& LL, const HostMesh& m, 
         }
       }
     }
-  });
+  }, 1);
   if (bad[0]) throw std::runtime_error("lattice locator: a face's fine triangles do not follow face 0's numbering");
 }
 

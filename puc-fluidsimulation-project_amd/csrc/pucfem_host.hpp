@@ -81,10 +81,11 @@ inline int host_threads() {
   }();
   return n;
 }
-// f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to host_threads())
+// f(r0, r1) over a split of [0, n) into contiguous ranges, one thread each (up to host_threads(), and one
+// per `grain` items: loops over heavy items -- faces, SELL slices, chunks -- pass a small grain)
 template <class F>
-void parallel_for(i64 n, F&& f) {
-  const int nt = (int)std::max<i64>(1, std::min<i64>({(i64)host_threads(), n / 4096 + 1}));
+void parallel_for(i64 n, F&& f, i64 grain = 4096) {
+  const int nt = (int)std::max<i64>(1, std::min<i64>({(i64)host_threads(), n / std::max<i64>(1, grain) + 1}));
   if (nt == 1) {
     f((i64)0, n);
     return;
@@ -270,7 +271,7 @@ void sell_values_fn(const Csr& A, i64 r0, const Sell& S, F&& f, std::vector<doub
         const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
         for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = f(r, b + e);
       }
-  });
+  }, 64);
 }
 
 // ----------------------------------------------------------------------------- lattice layout
