@@ -2376,7 +2376,9 @@ double lmax_estimate(const Csr& A, bool power = true, std::vector<double>* dinv_
     if (dinv_out) dinv_out->swap(dinv);
     return gersh;
   }
-  for (i64 i = 0; i < n; ++i) x[i] = 1.0 + 0.5 * std::sin((double)i);
+  parallel_for(n, [&](i64 i0, i64 i1) {
+    for (i64 i = i0; i < i1; ++i) x[i] = 1.0 + 0.5 * std::sin((double)i);
+  });
   double lam = 0.0;
   for (int it = 0; it < 30; ++it) {
     parallel_chunks(n, [&](int ch, i64 r0, i64 r1) {
@@ -2495,10 +2497,11 @@ void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
     } catch (...) {
       e0 = std::current_exception();
     }
+    clk.mark("  mg: lmax estimates (host)");
     g.join();
     if (e0) std::rethrow_exception(e0);
   }
-  clk.mark("  mg: transfers + lmax estimates");
+  clk.mark("  mg: transfers (joined)");
 }
 
 // ------------------------------------------------------------------ operator build

@@ -1,0 +1,44 @@
+"""The host runtime's threaded setup pieces give the same bits for any thread count: the dense coarse
+inverse (`spd_inverse`: pipelined Cholesky, cyclic triangular stages) equals the serial column-by-column
+inverse, and the centroid grid's range-split counting sort equals a sequential one.  A small C++
+driver (tests/cpp/host_threads_check.cpp) is compiled against pucfem_host.cpp and run under several
+PUCFEM_HOST_THREADS values (the count is read once per process)."""
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "puc-fluidsimulation-project_amd" / "csrc"
+
+
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    exe = tmp_path_factory.mktemp("hostthreads") / "host_threads_check"
+    subprocess.run([cxx, "-O2", "-std=c++17", "-pthread", f"-I{CSRC}", str(ROOT / "tests" / "cpp" / "host_threads_check.cpp"),
+                    str(CSRC / "pucfem_host.cpp"), "-o", str(exe)], check=True, timeout=600)
+    return exe
+
+
+def run(exe, threads):
+    env = dict(os.environ, PUCFEM_HOST_THREADS=str(threads))
+    out = subprocess.run([str(exe)], env=env, check=True, capture_output=True, text=True, timeout=300).stdout
+    return out.strip().splitlines()
+
+
+def test_threaded_setup_pieces_are_thread_count_independent(driver):
+    ref = run(driver, 1)
+    assert len(ref) == 8
+    for line in ref:
+        if line.startswith("spd n="):
+            assert "ok=1 serial_equal=1" in line, line
+        elif line.startswith("grid"):
+            assert "sequential_equal=1" in line, line
+    assert "spd indefinite ok=0" in ref
+    for t in (2, 3, 8):
+        assert run(driver, t) == ref
