@@ -452,6 +452,7 @@ struct Ctx {
   // (which = 3, 4: the viscous solve's x and y components, proj_k_visc directions each)
   int proj_k = 0, proj_k_visc = 0;
   ProjT* projX[5] = {};
+  i64 ldx = 0;  // the basis vectors' stride: nloc rounded up to even (8-B aligned pairs of rows)
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
   // Deferred update (project_guess): after a solve only v = y - x0 and A v are formed; the next
@@ -1854,7 +1855,7 @@ struct Ctx {
     const PendDir pd = otf ? PendDir{pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0]}
                            : PendDir{nullptr, nullptr, nullptr};
     klaunch(14, (4.0 * m + 24.0 + (otf ? 16.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)nloc, b, (const double*)pav[which], (const double*)pv[which],
+            (const ProjT*)projX[which], (int64_t)ldx, b, (const double*)pav[which], (const double*)pv[which],
             op.null_free, proj_part, rmd, pd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
@@ -1869,8 +1870,8 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
     // k_pcomb: X, v read; the new direction, x0, y written
     klaunch(15, (4.0 * kq + 32.0 + (otf ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)nloc, (const double*)proj_coef, (const double*)pv[which], op.null_free,
-            projX[which] + (i64)kq * nloc, y, proj_x0[which], otf ? pend_y[which] : (const double*)nullptr);
+            (const ProjT*)projX[which], (int64_t)ldx, (const double*)proj_coef, (const double*)pv[which], op.null_free,
+            projX[which] + (i64)kq * ldx, y, proj_x0[which], otf ? pend_y[which] : (const double*)nullptr);
     KCHK();
     pend_otf[which] = false;
     H.coef_m = kq;
@@ -1938,7 +1939,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(dqm, &qm, sizeof(QMat), hipMemcpyHostToDevice, st));
     const i64 n = lp.n_own;
     algo_bytes += 4.0 * (double)(m + kq) * (double)n;
-    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], nloc, m,
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], ldx, m,
                        (const double*)dqm, kq,
                        projXalt[which]);
     KCHK();
@@ -3283,12 +3284,13 @@ void build(Ctx& c) {
   }
   const bool block_visc = !c.dist() && c.block_cg && no <= (i64)CGB_THREADS * CGB_MAXR;
   c.proj_k_visc = stokes && !c.dense && !block_visc ? proj_size(c.prm.proj_k_visc) : 0;
+  c.ldx = (c.nloc + 1) & ~(i64)1;
   for (int w = 1; w <= 4; ++w) {
     const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
     if (k > 0) {
-      c.projX[w] = c.dalloc<ProjT>((i64)k * c.nloc);
+      c.projX[w] = c.dalloc<ProjT>((i64)k * c.ldx);
       c.proj_x0[w] = c.dalloc<double>(c.nloc);
-      c.projXalt[w] = c.dalloc<ProjT>((i64)k * c.nloc);  // re-seeding target
+      c.projXalt[w] = c.dalloc<ProjT>((i64)k * c.ldx);  // re-seeding target
     }
   }
   if (stokes && !c.dense && !block_visc && c.proj_k_visc == 0 && c.visc_extrap > 0)

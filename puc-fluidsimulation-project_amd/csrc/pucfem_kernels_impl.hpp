@@ -547,6 +547,8 @@ constexpr int PROJ_MAX = 32;
 // directions to fp32 perturbs their A-inner products by ~1e-7, below that; the dots and the
 // combinations are formed in fp64.  Halves the two passes over the basis (2 m vector reads per solve).
 using ProjT = float;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef float flt2 __attribute__((ext_vector_type(2)));
 
 // basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X.
 // Q: the re-seed coefficients in device memory, row-major [PROJ_KEEP_MAX][PROJ_MAX] (block-uniform loads)
@@ -585,6 +587,13 @@ struct PendDir {
   const double* x0;  // its guess
   const double* rf;  // its final residual
 };
+// PUCFEM_PROJ_R (compile-time A/B knob, 1 or 2): rows per thread and iteration of k_mdot2 / k_pcomb; with 2
+// every basis vector is read as 8-B pairs (the basis stride ldx is even) and the fp64 vectors as 16-B pairs
+#ifndef PUCFEM_PROJ_R
+#define PUCFEM_PROJ_R 1
+#endif
+constexpr int PROJ_R = PUCFEM_PROJ_R;
+static_assert(PROJ_R == 1 || PROJ_R == 2, "PUCFEM_PROJ_R must be 1 or 2");
 template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
@@ -596,7 +605,21 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
 #pragma unroll
   for (int i = 0; i < NA; ++i) acc[i] = 0.0;
   const int64_t step = (int64_t)gridDim.x * BS;
-  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+  // one row's contribution, in the order of the single-row loop
+  auto row = [&](const float* x, double br, double ar, double vr, bool free_row) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      acc[i] += (double)x[i] * br;
+      acc[M + i] += (double)x[i] * ar;
+    }
+    acc[2 * M] += vr * br;
+    acc[2 * M + 1] += vr * ar;
+    if (free_row) {
+      acc[2 * M + 2] += vr;
+      acc[2 * M + 3] += br;
+    }
+  };
+  auto one = [&](int64_t r) {
     const double br = b[r];
     double ar, vr;
     if (D.y) {
@@ -606,20 +629,41 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
       ar = av[r];
       vr = v[r];
     }
-    double x[M > 0 ? M : 1];
+    float x[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = (double)X[i * ld + r];
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    row(x, br, ar, vr, master_of && master_of[r] < 0);
+  };
+  if constexpr (PROJ_R == 1) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) one(r);
+  } else {
+    const int64_t np = n / 2;
+    for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += step) {
+      const int64_t r = 2 * q;
+      const dbl2 bb = *reinterpret_cast<const dbl2*>(b + r);
+      dbl2 aa, vv;
+      if (D.y) {
+        const dbl2 y2 = *reinterpret_cast<const dbl2*>(D.y + r), x2 = *reinterpret_cast<const dbl2*>(D.x0 + r);
+        const dbl2 a2 = *reinterpret_cast<const dbl2*>(av + r), f2 = *reinterpret_cast<const dbl2*>(D.rf + r);
+        vv = dbl2{y2.x - x2.x, y2.y - x2.y};
+        aa = dbl2{a2.x - f2.x, a2.y - f2.y};
+      } else {
+        aa = *reinterpret_cast<const dbl2*>(av + r);
+        vv = *reinterpret_cast<const dbl2*>(v + r);
+      }
+      float x0[M > 0 ? M : 1], x1[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-      acc[i] += x[i] * br;
-      acc[M + i] += x[i] * ar;
+      for (int i = 0; i < M; ++i) {
+        const flt2 t = *reinterpret_cast<const flt2*>(X + i * ld + r);
+        x0[i] = t.x;
+        x1[i] = t.y;
+      }
+      int2 mo = make_int2(0, 0);
+      if (master_of) mo = *reinterpret_cast<const int2*>(master_of + r);
+      row(x0, bb.x, aa.x, vv.x, master_of && mo.x < 0);
+      row(x1, bb.y, aa.y, vv.y, master_of && mo.y < 0);
     }
-    acc[2 * M] += vr * br;
-    acc[2 * M + 1] += vr * ar;
-    if (master_of && master_of[r] < 0) {
-      acc[2 * M + 2] += vr;
-      acc[2 * M + 3] += br;
-    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(n - 1);
   }
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -682,22 +726,58 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
     kc[i] = K[M + i];
   }
   const double s = K[2 * M], mu = K[2 * M + 1], alpha = K[2 * M + 2];
-  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
-    double x[M > 0 ? M : 1];
-#pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = (double)X[i * ld + r];
+  // x: the row's basis values; vr its v; returns (x_M, g)
+  auto comb = [&](const float* x, double vr, bool free_row, double& xm, double& g) {
     double sa = 0.0, sc = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      sa += ka[i] * x[i];
-      sc += kc[i] * x[i];
+      sa += ka[i] * (double)x[i];
+      sc += kc[i] * (double)x[i];
     }
+    xm = s * (vr - (free_row ? mu : 0.0) - sc);
+    g = sa + alpha * xm;
+  };
+  auto one = [&](int64_t r) {
+    float x[M > 0 ? M : 1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
     const double vr = yp ? yp[r] - x0[r] : v[r];
-    const double xm = s * (vr - (master_of && master_of[r] < 0 ? mu : 0.0) - sc);
-    const double g = sa + alpha * xm;
+    double xm, g;
+    comb(x, vr, master_of && master_of[r] < 0, xm, g);
     stnt(xm_out + r, (ProjT)xm);
     stnt(y + r, g);
     stnt(x0 + r, g);
+  };
+  if constexpr (PROJ_R == 1) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) one(r);
+  } else {
+    const int64_t np = n / 2;
+    for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += (int64_t)gridDim.x * BS) {
+      const int64_t r = 2 * q;
+      float xa[M > 0 ? M : 1], xb[M > 0 ? M : 1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const flt2 t = *reinterpret_cast<const flt2*>(X + i * ld + r);
+        xa[i] = t.x;
+        xb[i] = t.y;
+      }
+      dbl2 vv;
+      if (yp) {
+        const dbl2 y2 = *reinterpret_cast<const dbl2*>(yp + r), o2 = *reinterpret_cast<const dbl2*>(x0 + r);
+        vv = dbl2{y2.x - o2.x, y2.y - o2.y};
+      } else {
+        vv = *reinterpret_cast<const dbl2*>(v + r);
+      }
+      int2 mo = make_int2(0, 0);
+      if (master_of) mo = *reinterpret_cast<const int2*>(master_of + r);
+      double ma, ga, mb, gb;
+      comb(xa, vv.x, master_of && mo.x < 0, ma, ga);
+      comb(xb, vv.y, master_of && mo.y < 0, mb, gb);
+      stnt(reinterpret_cast<flt2*>(xm_out + r), flt2{(ProjT)ma, (ProjT)mb});
+      stnt(reinterpret_cast<dbl2*>(y + r), dbl2{ga, gb});
+      stnt(reinterpret_cast<dbl2*>(x0 + r), dbl2{ga, gb});
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(n - 1);
   }
 }
 
@@ -907,8 +987,7 @@ __global__ __launch_bounds__(BS) void k_cgr_upd(CgVecs<NR> v, int64_t nrows, con
 // The solver's vectors interleave the x and y components of u (dbl2: one 16-B gather per neighbour where
 // the two components were two 8-B gathers; round 4 lab, tools/vlayout_lab.hip: the face-row step 215 ->
 // 170 us warm, 252 -> 221 us cold at L7 size); u and u* themselves stay SoA.
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-typedef float flt2 __attribute__((ext_vector_type(2)));
+// (dbl2 / flt2: the 16-B / 8-B vector types defined with ProjT above)
 struct ChebVecs2 {
   const dbl2* xin;
   dbl2* xout;
