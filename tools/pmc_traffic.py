@@ -144,11 +144,14 @@ def main():
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
                                for k in ks) / n
     # the projection passes' bytes depend on the basis size M (their template argument): the ratio of PMC to
-    # algorithmic bytes over the instances with M >= 16 ((4 M + 24) n for k_mdot2, (4 M + 32) n for k_pcomb),
-    # which bench.py applies to the algorithmic bytes of the launches it timed
+    # algorithmic bytes over the instances with M >= 16 ((4 M + 40) n for k_mdot2, (4 M + 40) n for k_pcomb with
+    # the production path's pending directions -- v = y - x0 and A v = r0 - r_final formed in the passes, +16 /
+    # +8 B per row; PUCFEM_P_FROM_Y=0 runs: 24 / 32), which bench.py applies to the algorithmic bytes of the
+    # launches it timed
     ratios = {}
+    pend = os.environ.get("PUCFEM_P_FROM_Y", "1") != "0"
     if nrows:
-        for key, extra in (("k_mdot2", 24.0), ("k_pcomb", 32.0)):
+        for key, extra in (("k_mdot2", 40.0 if pend else 24.0), ("k_pcomb", 40.0 if pend else 32.0)):
             pmc = alg = 0.0
             for k, e in res["kernels"].items():
                 mm = re.match(r"^" + key + r"<(\d+)>", k)
