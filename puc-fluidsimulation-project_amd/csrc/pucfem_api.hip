@@ -2184,6 +2184,51 @@ struct Ctx {
     return std::min(gersh, 1.1 * lam);
   }
 
+  // a coarse multigrid level's lmax: lmax_estimate's 30-step power iteration on the level's device operator
+  // (its V-cycle values: fp32 in the fp32 cycle) instead of on the host, min(Gershgorin bound gersh, 1.1 lam);
+  // a partitioned level exchanges its halo before each product and all-reduces the norms
+  template <typename T>
+  double lmax_level_device(MgLevel& L, double gersh) {
+    MgBufs<T>& B = bufs<T>(L);
+    const i64 n = L.lp.n_own, r0 = L.own0(rank);
+    std::vector<T> x0;
+    host_resize(x0, n);
+    parallel_for(n, [&](i64 i0, i64 i1) {
+      for (i64 i = i0; i < i1; ++i) x0[i] = (T)(1.0 + 0.5 * std::sin((double)(r0 + i)));
+    });
+    h2d(B.x, x0.data(), sizeof(T) * n);
+    HIPCHK(hipMemsetAsync(B.b, 0, sizeof(T) * L.nloc, st));
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
+    const FaceDev fr = L.hA.full();
+    const DevSell& A = L.dA;
+    const int nb = nb_rows(n), ge = grid_ew(n);
+    double lam = 0.0;
+    for (int it = 0; it < 30; ++it) {
+      mg_halo(L, B.x);
+      B.with_vals([&](auto* val) {
+        using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
+        with_c16(A, [&](auto c16) {
+          hipLaunchKernelGGL((k_resid<T, T, VT, decltype(c16)::value, 0>), dim3(grid_full(fr, A)), dim3(BS), 0, st,
+                             A.view(), fr, val, (const T*)B.b, (const T*)B.x, B.res, (const int*)ctl);
+        });
+      });
+      hipLaunchKernelGGL(k_pow_step<T>, dim3(nb), dim3(BS), 0, st, (int64_t)n, (const T*)B.x, (const T*)B.res,
+                         (const T*)B.dinv, B.x2, part_a);
+      hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_a, nb, MAXB, 2, 0, redbuf);
+      KCHK();
+      if (dist() && !L.rep) comm->allreduce(redbuf, 2, false, st);
+      HIPCHK(hipMemcpyAsync(h_pinned, redbuf, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const double nx = h_pinned[0], ny = h_pinned[1];
+      lam = std::sqrt(ny / nx);
+      hipLaunchKernelGGL(k_pow_scale<T>, dim3(ge), dim3(BS), 0, st, (int64_t)n, (const T*)B.x2, 1.0 / std::sqrt(ny),
+                         B.x);
+      KCHK();
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return std::min(gersh, 1.1 * lam);
+  }
+
   // implicit dye step (good_visualization.py:700-718) from cin with velocity (vx, vy) and its lumped
   // divergence dv into cout: assemble the merged operator, rhs = M c, BiCGStab from c, periodic copies
   int dye_step(const double* vx, const double* vy, const double* dv, const double* cin, double* cout) {
@@ -2492,9 +2537,9 @@ void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
       });
     std::exception_ptr e0;
     try {
-      for (int l = 0; l <= Lv; ++l)
+      for (int l = 0; l <= Lv; ++l)  // (device power iterations: the Gershgorin bound here, the rest in build())
         c.mg[l].lmax = l == Lv && c.lmax_dev ? lmax_estimate(c.Pp, false, &c.lmax_dinv)
-                                             : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp);
+                                             : lmax_estimate(l == Lv ? c.Pp : c.mg[l].Pp, !(c.lmax_dev && l >= 1));
     } catch (...) {
       e0 = std::current_exception();
     }
@@ -3602,6 +3647,10 @@ void build(Ctx& c) {
     MgLevel& F = c.mg[c.mg_levels];
     F.lmax = c.lmax_device(F.lmax);
     clk.mark("finest lmax (device power iteration)");
+    for (int l = 1; l < c.mg_levels; ++l)
+      c.mg[l].lmax = c.mg_single ? c.lmax_level_device<float>(c.mg[l], c.mg[l].lmax)
+                                 : c.lmax_level_device<double>(c.mg[l], c.mg[l].lmax);
+    clk.mark("coarse lmax (device power iterations)");
   }
 }
 

@@ -2884,6 +2884,31 @@ __global__ void k_stats(const double* vals, double* out, int parts) {
 }
 
 // ----------------------------------------------------------------------------- BiCGStab pieces (literal operators)
+// a multigrid level's power iteration (Ctx::lmax_level_device): y = D^-1 A x from res = 0 - A x (k_resid with
+// b = 0), partial sums of x.x and y.y (stride MAXB, the k_dot2 layout)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_pow_step(int64_t n, const T* __restrict__ x, const T* __restrict__ res,
+                                                 const T* __restrict__ dinv, T* __restrict__ y, double* part) {
+  __shared__ double sh[4];
+  double sx = 0.0, sy = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    const T yi = dinv[i] * -res[i];
+    y[i] = yi;
+    sx += (double)x[i] * (double)x[i];
+    sy += (double)yi * (double)yi;
+  }
+  const double t1 = block_sum(sx, sh), t2 = block_sum(sy, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = t1;
+    part[MAXB + blockIdx.x] = t2;
+  }
+}
+template <typename T>
+__global__ void k_pow_scale(int64_t n, const T* __restrict__ y, double s, T* __restrict__ x) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) x[i] = (T)(s * (double)y[i]);
+}
 __global__ __launch_bounds__(BS) void k_dot2(int64_t n, const double* a, const double* b, const double* c,
                                              const double* d, double* part) {
   __shared__ double sh[4];
