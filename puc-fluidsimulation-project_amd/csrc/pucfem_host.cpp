@@ -785,47 +785,82 @@ void build_prolongation(i64 Nc, const std::vector<i32>& ea, const std::vector<i3
                         Csr& P) {
   const i64 Nf = (i64)of.new2old.size();
   P.nrows = Nf;
-  P.rowptr.assign(Nf + 1, 0);
-  P.col.clear();
-  P.val.clear();
-  for (i64 g = 0; g < Nf; ++g) {
-    if (master_of_f[g] < 0) {
-      const i64 o = of.new2old[g];
-      if (o < Nc) {
-        P.col.push_back(dof_c[oc.old2new[o]]);
-        P.val.push_back(1.0);
-      } else {
-        i32 a = dof_c[oc.old2new[ea[o - Nc]]], b = dof_c[oc.old2new[eb[o - Nc]]];
-        if (a == b) {
-          P.col.push_back(a);
-          P.val.push_back(1.0);
-        } else {
-          if (b < a) std::swap(a, b);
-          P.col.push_back(a);
-          P.val.push_back(0.5);
-          P.col.push_back(b);
-          P.val.push_back(0.5);
-        }
-      }
+  // row g: nothing (a periodic slave), its coarse node, or the two coarse ends of its midpoint edge
+  // (one entry when both ends merge); two threaded passes, lengths then entries
+  auto row = [&](i64 g, i32* col, double* val) -> int {
+    if (master_of_f[g] >= 0) return 0;
+    const i64 o = of.new2old[g];
+    if (o < Nc) {
+      col[0] = dof_c[oc.old2new[o]];
+      val[0] = 1.0;
+      return 1;
     }
-    P.rowptr[g + 1] = (i64)P.col.size();
-  }
+    i32 a = dof_c[oc.old2new[ea[o - Nc]]], b = dof_c[oc.old2new[eb[o - Nc]]];
+    if (a == b) {
+      col[0] = a;
+      val[0] = 1.0;
+      return 1;
+    }
+    if (b < a) std::swap(a, b);
+    col[0] = a;
+    val[0] = 0.5;
+    col[1] = b;
+    val[1] = 0.5;
+    return 2;
+  };
+  host_resize(P.rowptr, Nf + 1);
+  P.rowptr[0] = 0;
+  parallel_for(Nf, [&](i64 g0, i64 g1) {
+    i32 c[2];
+    double v[2];
+    for (i64 g = g0; g < g1; ++g) P.rowptr[g + 1] = row(g, c, v);
+  });
+  for (i64 g = 0; g < Nf; ++g) P.rowptr[g + 1] += P.rowptr[g];
+  host_resize(P.col, P.rowptr[Nf]);
+  host_resize(P.val, P.rowptr[Nf]);
+  parallel_for(Nf, [&](i64 g0, i64 g1) {
+    for (i64 g = g0; g < g1; ++g) row(g, P.col.data() + P.rowptr[g], P.val.data() + P.rowptr[g]);
+  });
 }
 
+// counting sort by column; each thread owns a contiguous range of columns and scans every entry (rows in
+// ascending order inside every column, as one sequential pass)
 void transpose(const Csr& A, i64 ncols, Csr& At) {
   At.nrows = ncols;
   At.rowptr.assign(ncols + 1, 0);
-  for (i64 k = 0; k < A.nnz(); ++k) At.rowptr[A.col[k] + 1]++;
-  for (i64 c = 0; c < ncols; ++c) At.rowptr[c + 1] += At.rowptr[c];
-  At.col.assign(A.nnz(), 0);
-  At.val.assign(A.nnz(), 0.0);
-  std::vector<i64> fill(At.rowptr.begin(), At.rowptr.end() - 1);
-  for (i64 r = 0; r < A.nrows; ++r)
-    for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
-      const i64 d = fill[A.col[k]]++;
-      At.col[d] = (i32)r;
-      At.val[d] = A.val[k];
+  const i64 nnz = A.nnz();
+  const int nt = (int)std::max<i64>(1, std::min<i64>((i64)host_threads(), nnz / 65536 + 1));
+  auto run = [&](auto&& f) {
+    if (nt == 1) {
+      f(0);
+      return;
     }
+    ThreadGroup g;
+    for (int w = 0; w < nt; ++w) g.spawn([&f, w] { f(w); });
+    g.join();
+  };
+  run([&](int w) {
+    const i64 c0 = ncols * w / nt, c1 = ncols * (w + 1) / nt;
+    for (i64 k = 0; k < nnz; ++k) {
+      const i64 c = A.col[k];
+      if (c >= c0 && c < c1) At.rowptr[c + 1]++;
+    }
+  });
+  for (i64 c = 0; c < ncols; ++c) At.rowptr[c + 1] += At.rowptr[c];
+  host_resize(At.col, nnz);
+  host_resize(At.val, nnz);
+  run([&](int w) {
+    const i64 c0 = ncols * w / nt, c1 = ncols * (w + 1) / nt;
+    std::vector<i64> fill(At.rowptr.begin() + c0, At.rowptr.begin() + c1);
+    for (i64 r = 0; r < A.nrows; ++r)
+      for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+        const i64 c = A.col[k];
+        if (c < c0 || c >= c1) continue;
+        const i64 d = fill[c - c0]++;
+        At.col[d] = (i32)r;
+        At.val[d] = A.val[k];
+      }
+  });
 }
 
 bool lu_inverse(std::vector<double>& A, i64 n) {

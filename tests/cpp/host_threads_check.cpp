@@ -107,5 +107,36 @@ int main() {
     std::printf("grid T=%ld cells=%ld sequential_equal=%d hash=%016llx\n", (long)T, (long)nc, same ? 1 : 0,
                 (unsigned long long)fnv(G.item.data(), sizeof(i32) * T, fnv(G.cell_start.data(), sizeof(i32) * (nc + 1))));
   }
+  for (i64 nr : {50, 200000}) {  // transpose (the restriction of every level): against a sequential counting sort
+    std::mt19937_64 r(nr);
+    const i64 nc = nr / 3 + 1;
+    Csr A;
+    A.nrows = nr;
+    A.rowptr.assign(nr + 1, 0);
+    for (i64 i = 0; i < nr; ++i) {
+      const int len = (int)(r() % 3);
+      for (int k = 0; k < len; ++k) {
+        A.col.push_back((i32)(r() % nc));
+        A.val.push_back((double)(r() % 1000) / 7.0);
+      }
+      A.rowptr[i + 1] = (i64)A.col.size();
+    }
+    Csr T;
+    transpose(A, nc, T);
+    std::vector<i64> rp(nc + 1, 0);
+    for (i32 c : A.col) rp[c + 1]++;
+    for (i64 c = 0; c < nc; ++c) rp[c + 1] += rp[c];
+    std::vector<i32> col(A.col.size());
+    std::vector<double> val(A.col.size());
+    std::vector<i64> fill(rp.begin(), rp.end() - 1);
+    for (i64 i = 0; i < nr; ++i)
+      for (i64 k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) {
+        const i64 d = fill[A.col[k]]++;
+        col[d] = (i32)i;
+        val[d] = A.val[k];
+      }
+    const bool same = T.nrows == nc && T.rowptr == rp && T.col == col && T.val == val;
+    std::printf("transpose rows=%ld nnz=%ld sequential_equal=%d\n", (long)nr, (long)A.col.size(), same ? 1 : 0);
+  }
   return 0;
 }

@@ -1,6 +1,6 @@
 """The host runtime's threaded setup pieces give the same bits for any thread count: the dense coarse
 inverse (`spd_inverse`: pipelined Cholesky, cyclic triangular stages) equals the serial column-by-column
-inverse, and the centroid grid's range-split counting sort equals a sequential one.  A small C++
+inverse, and the centroid grid's and the transpose's range-split counting sorts equal sequential ones.  A small C++
 driver (tests/cpp/host_threads_check.cpp) is compiled against pucfem_host.cpp and run under several
 PUCFEM_HOST_THREADS values (the count is read once per process)."""
 import os
@@ -33,11 +33,11 @@ def run(exe, threads):
 
 def test_threaded_setup_pieces_are_thread_count_independent(driver):
     ref = run(driver, 1)
-    assert len(ref) == 8
+    assert len(ref) == 10
     for line in ref:
         if line.startswith("spd n="):
             assert "ok=1 serial_equal=1" in line, line
-        elif line.startswith("grid"):
+        elif line.startswith(("grid", "transpose")):
             assert "sequential_equal=1" in line, line
     assert "spd indefinite ok=0" in ref
     for t in (2, 3, 8):
