@@ -2910,7 +2910,7 @@ void build(Ctx& c) {
   std::vector<uint8_t> isdir(N, 0);
   for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
   const double dtnu = prm.dt * prm.nu;
-  c.Kv.resize(c.P.nnz());
+  host_resize(c.Kv, c.P.nnz());
   parallel_for(N, [&](i64 r0, i64 r1) {
     for (i64 r = r0; r < r1; ++r)
       for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) {
@@ -2921,7 +2921,8 @@ void build(Ctx& c) {
       }
   });
   if (stokes) {  // spectral interval of the Jacobi-scaled A_visc (Ctx::visc_R, Ctx::visc_lo)
-    std::vector<double> dg(N);
+    std::vector<double> dg;
+    host_resize(dg, N);
     parallel_for(N, [&](i64 r0, i64 r1) {
       for (i64 r = r0; r < r1; ++r) dg[r] = diag_of(c.P, c.Kv, r);
     });

@@ -221,7 +221,7 @@ void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P, const Inciden
       P.rowptr[r + 1] = P.rowptr[r] + l;
       ++r;
     }
-  P.col.resize(P.rowptr[N]);
+  host_resize(P.col, P.rowptr[N]);
   std::vector<i64> cstart(PAR_CHUNKS + 1, 0);
   for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)ccol[ch].size();
   parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
@@ -417,8 +417,8 @@ void build_pressure(const Csr& P, const std::vector<double>& K, const std::vecto
     }
   });
   for (i64 r = 0; r < N; ++r) Pp.rowptr[r + 1] += Pp.rowptr[r];
-  Pp.col.resize(Pp.rowptr[N]);
-  Pp.val.resize(Pp.rowptr[N]);
+  host_resize(Pp.col, Pp.rowptr[N]);
+  host_resize(Pp.val, Pp.rowptr[N]);
   parallel_for(N, [&](i64 r0, i64 r1) {
     std::vector<std::pair<i32, double>> tmp;
     for (i64 r = r0; r < r1; ++r) {
