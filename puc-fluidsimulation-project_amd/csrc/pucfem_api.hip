@@ -138,36 +138,55 @@ struct Timer {
   double bytes[NCLS] = {};
   int64_t n[NCLS] = {};
   hipEvent_t get() {
-    if (pool.empty()) {
-      hipEvent_t e;
-      HIPCHK(hipEventCreate(&e));
-      return e;
-    }
+    if (pool.empty())  // in batches: the samples stay pending until their solve's test is read
+      for (int k = 0; k < 256; ++k) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        pool.push_back(e);
+      }
     hipEvent_t e = pool.back();
     pool.pop_back();
     return e;
   }
+  size_t done = 0;  // samples accounted so far (the absolute index of pend[0])
+  size_t mark() const { return done + pend.size(); }
+  void account(const Pend& p) {
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
+    ms[p.cls] += t;
+    bytes[p.cls] += p.bytes;
+    n[p.cls]++;
+    pool.push_back(p.a);
+    pool.push_back(p.b);
+  }
   void flush() {
     for (auto& p : pend) {
-      float t = 0;
       HIPCHK(hipEventSynchronize(p.b));
-      HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
-      ms[p.cls] += t;
-      bytes[p.cls] += p.bytes;
-      n[p.cls]++;
-      pool.push_back(p.a);
-      pool.push_back(p.b);
+      account(p);
     }
+    done += pend.size();
     pend.clear();
   }
-  // drop the pending samples from index k on (launches that found the solve converged and returned
+  // account the finished samples before absolute index `limit` without waiting: called while the GPU runs the
+  // work just enqueued, so the host's event reads overlap it (a blocking flush after a solve's convergence
+  // read idled the GPU ~0.12 ms per pressure solve, r10x trace)
+  void flush_ready(size_t limit) {
+    size_t i = 0;
+    for (; i < pend.size() && done + i < limit; ++i)
+      if (hipEventQuery(pend[i].b) != hipSuccess) break;
+    for (size_t k = 0; k < i; ++k) account(pend[k]);
+    pend.erase(pend.begin(), pend.begin() + (std::ptrdiff_t)i);
+    done += i;
+  }
+  // drop the pending samples from absolute index k on (launches that found the solve converged and returned
   // without work: counting them would credit their bytes to a near-zero duration)
   void drop_from(size_t k) {
-    for (size_t i = k; i < pend.size(); ++i) {
+    const size_t r = k > done ? k - done : 0;
+    for (size_t i = r; i < pend.size(); ++i) {
       pool.push_back(pend[i].a);
       pool.push_back(pend[i].b);
     }
-    if (k < pend.size()) pend.resize(k);
+    if (r < pend.size()) pend.resize(r);
   }
   ~Timer() {
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -542,6 +561,7 @@ struct Ctx {
       if (ev_u) (void)hipEventDestroy(ev_u);
       if (ev_sl) (void)hipEventDestroy(ev_sl);
       if (ev_gate) (void)hipEventDestroy(ev_gate);
+      if (ev_wait) (void)hipEventDestroy(ev_wait);
       if (st_sl) (void)hipStreamDestroy(st_sl);
       if (st) (void)hipStreamDestroy(st);
     }
@@ -670,6 +690,34 @@ struct Ctx {
       hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
     }
   }
+  // The solvers' host reads (convergence tests, |r_0|) wait by polling the event instead of a blocking
+  // synchronize: a blocking wait that outlasts the runtime's short active spin sleeps on an interrupt, and
+  // its wake-up left the GPU idle ~0.1 ms after every pressure solve (r10x trace: 124 us before each
+  // k_grad_proj).  PUCFEM_SPIN_WAIT=0 keeps the blocking calls (measurement knob).
+  bool spin_wait = !(std::getenv("PUCFEM_SPIN_WAIT") && std::atoi(std::getenv("PUCFEM_SPIN_WAIT")) == 0);
+  hipEvent_t ev_wait = nullptr;
+  void wait_event(hipEvent_t e) {
+    if (!spin_wait) {
+      HIPCHK(hipEventSynchronize(e));
+      return;
+    }
+    for (;;) {
+      const hipError_t q = hipEventQuery(e);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) HIPCHK(q);
+      __builtin_ia32_pause();
+    }
+  }
+  void sync_st() {  // hipStreamSynchronize(st) for the solvers' reads
+    if (!spin_wait) {
+      HIPCHK(hipStreamSynchronize(st));
+      return;
+    }
+    if (!ev_wait) HIPCHK(hipEventCreateWithFlags(&ev_wait, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev_wait, st));
+    wait_event(ev_wait);
+  }
+
   // k_sl over rows [row0, row0 + n) of the full replica c (cout: the new values), either locator
   void sl_launch(int nb, i64 row0, i64 n, const double* vx, const double* vy, double dt, const double* cf, double* cn,
                  const double* w, int32_t* nf, RedOut ro = RedOut{}) {
@@ -1152,7 +1200,7 @@ struct Ctx {
     // wait for it (so that they can run as one pair with the finish)
     advance(pair0 ? 2 + 2 * std::max(0, (last_it[which] - 4) / 2)
                   : (pairs ? 1 + 2 * std::max(0, (last_it[which] - 3) / 2) : std::max(1, last_it[which] - 1)));
-    HIPCHK(hipEventSynchronize(have_r0));
+    wait_event(have_r0);
     timer.pool.push_back(have_r0);
     if (vcc.pending) {  // the previous solve's post-check (its copy preceded step 0 on the stream)
       vcc.pending = false;
@@ -1585,14 +1633,14 @@ struct Ctx {
     const bool eligible = seen && last_it[which] <= 1;
     if (eligible && __builtin_popcount(zero_hist[which] & 0xffu) >= 2) {
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      sync_st();
       done0 = h_ctl[0] != 0;
     }
     for (bool first = true; !done0; first = false) {
       if (!first) marks.clear();  // the previous chunk's samples are flushed
       bmarks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
-        marks.push_back({it, timer.pend.size()});  // this iteration's V-cycle works iff not converged at it
+        marks.push_back({it, timer.mark()});  // this iteration's V-cycle works iff not converged at it
         bmarks.push_back({it, algo_bytes});
         ro_rz = ro(redbuf + 32, CNT_RZ, 1);
         precondition();
@@ -1634,16 +1682,15 @@ struct Ctx {
         std::swap(v.po[0], v.pn[0]);
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (timer.on) {
-        if (h_ctl[0])  // iterations from the converged one on launched kernels that did no work
-          for (auto& mk : marks)
-            if (mk.first >= h_ctl[1]) {
-              timer.drop_from(mk.second);
-              break;
-            }
-        timer.flush();
-      }
+      // the samples before this chunk, while the GPU runs it (this chunk's stay pending until its test is read)
+      if (timer.on && !marks.empty()) timer.flush_ready(marks.front().second);
+      sync_st();
+      if (timer.on && h_ctl[0])  // iterations from the converged one on launched kernels that did no work
+        for (auto& mk : marks)
+          if (mk.first >= h_ctl[1]) {
+            timer.drop_from(mk.second);
+            break;
+          }
       if (h_ctl[0])  // the bytes of the iterations that found the solve converged did not move
         for (auto& bm : bmarks)
           if (bm.first >= h_ctl[1]) {
