@@ -147,6 +147,7 @@ def main():
     barrier()
     sim.ctx.sync()
     n0, b0 = sim.ctx.counters()
+    cls0 = [sim.ctx.class_counters(k) for k in range(16)]
     t0 = time.perf_counter()
     stats = list(sim.step(a.steps - kt_steps)) if a.steps > kt_steps else []
     if kt_steps:  # the last kt_steps timed steps carry the per-launch events (pucfem_timing_enable syncs)
@@ -156,6 +157,7 @@ def main():
     barrier()
     dt_local = time.perf_counter() - t0
     n1, b1 = sim.ctx.counters()
+    cls1 = [sim.ctx.class_counters(k) for k in range(16)]
     elapsed = allmax(dt_local)
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
     names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_grad_proj", "k_sl",
@@ -169,8 +171,13 @@ def main():
     for k, nm in enumerate(names):
         ms, n, b = sim.ctx.timing_get(k)
         if n:
+            gbs = b / (ms / n * 1e-3) / 1e9
+            # the class over the WHOLE timed window: its launches and algorithmic bytes there (every launch,
+            # pucfem_class_counters) at the rate its timed launches ran
+            wn, wb = cls1[k][0] - cls0[k][0], cls1[k][1] - cls0[k][1]
             ktab[nm] = {"launches_timed": n, "avg_launch_ms": ms / n, "bytes_per_launch": b,
-                        "achieved_GBps": b / (ms / n * 1e-3) / 1e9}
+                        "achieved_GBps": gbs, "window_launches": wn,
+                        "window_ms_est": wb / (gbs * 1e9) * 1e3 if gbs > 0 else 0.0}
     sim.ctx.timing(False)
     # the same kernels launched back to back outside the step (pucfem_bench_kernel): per-launch time
     # of a batch between two events, and the average of per-launch dispatch events
@@ -248,11 +255,14 @@ def main():
     # bytes per launch are the library's own counts: vectors once per row read or
     # written, stored operators per entry; timed with HIP events taken by each launch's dispatch on the
     # stream it runs on.
-    dom = max(ktab, key=lambda k: ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"]) if ktab else None
+    # The dominant class is chosen over the whole timed window: each class's window bytes at its timed rate
+    # (the per-launch events cover only the last steps, which past the transient under-weigh the solves)
+    dom = max(ktab, key=lambda k: ktab[k]["window_ms_est"]) if ktab else None
     ms_step = 1e3 * elapsed / a.steps
     for k in ktab:  # share of the timed region (the dye stream's kernels overlap the main stream's)
         ktab[k]["ms_per_step"] = ktab[k]["launches_timed"] * ktab[k]["avg_launch_ms"] / kt_steps
         ktab[k]["share"] = ktab[k]["ms_per_step"] / ms_step
+        ktab[k]["share_window"] = ktab[k]["window_ms_est"] / (1e3 * elapsed)
     if dom in ktab:
         kd = ktab[dom]
         traffic = None
@@ -266,7 +276,9 @@ def main():
                     traffic = ratio * kd["bytes_per_launch"]
             except Exception:
                 traffic = None
-        rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "kernel_share": kd["share"],
+        rec["roofline"] = {"bound": "hbm", "kernel": dom.split()[0], "kernel_share": kd["share_window"],
+                           "kernel_choice": "the class with the largest estimated time over the whole timed window "
+                                            "(its window bytes at its timed rate)",
                            "achieved": kd["achieved_GBps"],
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kd["achieved_GBps"] / HBM_PEAK_GBS,
                            "traffic": traffic, "bytes_per_launch": kd["bytes_per_launch"],
@@ -294,6 +306,16 @@ def main():
     if rank == 0 and world == 1 and not a.no_secondary:
         rec["mesh_fine"] = secondary_fine(pf, a.fine_steps)
         rec["heat_fine"] = heat_fine(pf)
+    if rank == 0 and world == 1:
+        # the GPU / CPU ratios measured on this host on BOTH sides (north_star's target: >= 50x the CPU numpy
+        # path on mesh_fine)
+        cb, fine = rec.get("cpu_baseline"), rec.get("mesh_fine")
+        rec["vs_cpu_measured"] = {
+            "same_config_L5": cb["same_config"]["ratio"] if cb and "same_config" in cb else None,
+            "mesh_fine_vs_cpu_port": fine["ratio_vs_oracle"] if fine else None,
+            "mesh_fine_target": 50.0,
+            "note": "mesh_fine (1,067 nodes) is launch-latency bound on the GPU; the literal reference's 5.8 steps/s "
+                    "(BASELINE.md) was measured on another host and is not used for these ratios"}
     if rank == 0:
         print(json.dumps(rec))
     if world > 1:
@@ -427,14 +449,19 @@ def cpu_baseline(pf, level, stats, l5=None):
     sps = n / (time.perf_counter() - t)
     n_full = stats_nodes(pf, level)
     scale = m.N / n_full
-    rec = {"value": sps * scale, "unit": "timesteps/s", "cores": cores, "kind": "port",
-           "label": "CPU sparse restatement", "nproc": os.cpu_count(),
+    # value: the rate MEASURED on this host at L5 (the largest mesh the sparse factorisations fit); the
+    # benchmarked mesh's CPU rate is only extrapolated (linear in the node count), reported apart
+    rec = {"value": sps, "unit": "timesteps/s", "cores": cores, "kind": "port",
+           "label": "CPU sparse restatement", "nproc": os.cpu_count(), "mesh": f"mesh_fine x{lv} ({m.N} nodes)",
            "measured": {"mesh": f"mesh_fine x{lv}", "nodes": m.N, "steps_per_s": sps, "setup_s": t_setup},
+           "extrapolated_to_benchmark_mesh": {"mesh": f"mesh_fine x{level}", "steps_per_s": sps * scale,
+                                              "method": f"x{scale:.5f}, the node ratio (a lower bound on the CPU "
+                                                        f"cost: the sparse LU solves grow faster than linearly)"},
            "sample": (f"CPU sparse restatement (oracle StokesRef: scipy SuperLU solves, numpy element loops, "
                       f"KDTree SL; element loops / SL / viscous solves on up to {cores} threads, pressure "
                       f"SuperLU single-threaded; nproc={os.cpu_count()}) timed directly on mesh_fine x{lv} "
                       f"({m.N} nodes): {n} steps at {sps:.4f} steps/s after one untimed step, factorisation "
-                      f"setup {t_setup:.1f}s excluded; value scaled x{scale:.5f} (node ratio) to x{level}")}
+                      f"setup {t_setup:.1f}s excluded")}
     if l5 is not None and lv == 5:
         rec["same_config"] = {"mesh": "mesh_fine x5", "gpu_steps_per_s": l5["steps_per_s"], "cpu_steps_per_s": sps,
                               "ratio": l5["steps_per_s"] / sps}

@@ -240,6 +240,11 @@ int pucfem_timing_enable(void* ctx, int32_t on);
 int pucfem_timing_get(void* ctx, int32_t kclass, double* total_ms, int64_t* launches,
                       double* bytes_per_launch);
 int pucfem_sync(void* ctx);
+/* cumulative launches and algorithmic bytes of one kernel class (the classes of pucfem_timing_get) over EVERY
+   launch since the context's creation, timed or not (launches of a solve after its convergence, which do no
+   work, are taken back): with the timed launches' rate, bench.py weighs the classes over the whole timed
+   window.  Measurement only. */
+int pucfem_class_counters(void* ctx, int32_t kclass, int64_t* launches, double* bytes);
 /* cumulative counters of the calling thread / context since its creation (bench.py's step roofline):
    launches = kernel launches issued by this thread through the library; bytes = the algorithmic bytes of
    the context's launched kernels (each vector counted once per row it is read or written, stored operators
@@ -289,6 +294,12 @@ int pucfem_comm_counters(void* ctx, int64_t* out6);
    out2 = [lo, hi], lo = max(1 - R, 1 / max_i a_ii), hi = 1 + R, R the Gershgorin radius.  Every
    eigenvalue lies inside (tests/test_host_assembly.py checks it against scipy's eigensolver). */
 int pucfem_visc_interval(void* ctx, double* out2);
+/* The pressure multigrid's smoothing interval on one level (0 = coarsest .. levels) of a single-rank context:
+   the Chebyshev smoother of D^-1 A runs on [lmax / mg_ratio, lmax] (the np.linalg.solve sites
+   StokesColor.py:555,569 it preconditions).  out4 = [lmax in use, the device power iteration's Rayleigh
+   quotient (0: estimated on the host), the host 30-step power iteration's quotient on the level's fp64
+   operator (computed by this call), the host Gershgorin bound]; lmax = min(Gershgorin, 1.1 x quotient). */
+int pucfem_mg_lmax(void* ctx, int32_t level, double* out4);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

@@ -82,6 +82,7 @@ SIGNATURES = {
     "pucfem_dye_step": ([_P, _D, _D, _D, _I32], ct.c_int),
     "pucfem_comm_info": ([_P, ct.POINTER(ct.c_int64)], ct.c_int),
     "pucfem_visc_interval": ([_P, ct.POINTER(ct.c_double)], ct.c_int),
+    "pucfem_mg_lmax": ([_P, ct.c_int32, _D], ct.c_int),
     "pucfem_tracer_step": ([_P, _D, ct.c_double, ct.c_int32], ct.c_int),
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
     "pucfem_mixing_index_w": ([_P, _D, _D, _D], ct.c_int),
@@ -89,6 +90,7 @@ SIGNATURES = {
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),
     "pucfem_timing_get": ([_P, ct.c_int32, _D, _I64, _D], ct.c_int),
     "pucfem_counters": ([_P, _I64, _D], ct.c_int),
+    "pucfem_class_counters": ([_P, ct.c_int32, _I64, _D], ct.c_int),
     "pucfem_comm_counters": ([_P, _I64], ct.c_int),
     "pucfem_sync": ([_P], ct.c_int),
     "pucfem_bench_dir": ([_P, ct.c_int32, ct.c_int32, ct.c_int32, _D], ct.c_int),

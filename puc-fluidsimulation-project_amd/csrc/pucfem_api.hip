@@ -229,6 +229,7 @@ struct MgLevel {
   std::vector<i64> rs;      // partition of this level's internal ids
   LocalPlan lp;
   double lmax = 2.0;
+  double lam_dev = 0.0;  // the device power iteration's last Rayleigh quotient (0: not run; pucfem_mg_lmax)
   // device
   Sell sA, sPr, sR;         // host SELL images (built with the plans, also on host-only contexts)
   DevSell dA, dPr, dR;
@@ -298,6 +299,30 @@ struct Ctx {
   // counted once per row it is read or written, stored operators per entry; launches that find their
   // solve already converged (no work) are taken back once the host learns the iteration count
   double algo_bytes = 0.0;
+  // per kernel class (Timer's classes), every launch timed or not: launches and algorithmic bytes
+  // (pucfem_class_counters: bench.py weighs the classes over the whole timed window with them)
+  double cls_bytes[Timer::NCLS] = {};
+  int64_t cls_n[Timer::NCLS] = {};
+  struct ByteMark {  // the counters at one point (launches after a solve's convergence are taken back)
+    double total;
+    double cb[Timer::NCLS];
+    int64_t cn[Timer::NCLS];
+  };
+  ByteMark bmark_now() const {
+    ByteMark m{algo_bytes, {}, {}};
+    for (int k = 0; k < Timer::NCLS; ++k) {
+      m.cb[k] = cls_bytes[k];
+      m.cn[k] = cls_n[k];
+    }
+    return m;
+  }
+  void bmark_restore(const ByteMark& m) {
+    algo_bytes = m.total;
+    for (int k = 0; k < Timer::NCLS; ++k) {
+      cls_bytes[k] = m.cb[k];
+      cls_n[k] = m.cn[k];
+    }
+  }
 
   // ---- inputs
   HostMesh mesh;
@@ -506,13 +531,18 @@ struct Ctx {
   DevSell dPm;  // dP with merged columns (the gradient's gathers of y)
   bool pend_otf[5] = {};
   const double* pend_y[5] = {};
+  // the solve after a projected guess accumulates its correction v = sum alpha_k p_k in pv[slot] (k_cg_upd's
+  // vacc; k_pcomb clears it with the guess): pend_acc -- the pending / stored v is that accumulator, not y - x0
+  bool pend_acc[5] = {};
+  double* cg_vacc = nullptr;  // pcg_mg's accumulator of the current solve (null: none)
   // keep: a slot whose pending direction stays (its r_final is the one cg_r[0] still holds)
   void proj_materialize(int keep = 0) {
     for (int w = 1; w <= 2; ++w) {
       if (!pend_otf[w] || w == keep) continue;
       const i64 n = lp.n_own;
       algo_bytes += 48.0 * (double)n;
-      hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, pend_y[w], (const double*)proj_x0[w], pv[w],
+      hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, pend_y[w], (const double*)proj_x0[w],
+                         pend_acc[w] ? (double*)nullptr : pv[w],
                          (const double*)pav[w], (const double*)cg_r[0], pav[w]);
       KCHK();
       pend_otf[w] = false;
@@ -680,6 +710,10 @@ struct Ctx {
   template <typename... KArgs, typename... Args>
   void klaunch(int cls, double bytes, void (*kernel)(KArgs...), dim3 g, dim3 b, Args... args) {
     algo_bytes += bytes;
+    if (cls >= 0) {
+      cls_bytes[cls] += bytes;
+      ++cls_n[cls];
+    }
     if (timer.on && cls >= 0 && ((timer.mask >> cls) & 1u)) {
       hipEvent_t a = timer.get(), e = timer.get();
       ++g_nlaunch;
@@ -695,17 +729,27 @@ struct Ctx {
   // its wake-up left the GPU idle ~0.1 ms after every pressure solve (r10x trace: 124 us before each
   // k_grad_proj).  PUCFEM_SPIN_WAIT=0 keeps the blocking calls (measurement knob).
   bool spin_wait = !(std::getenv("PUCFEM_SPIN_WAIT") && std::atoi(std::getenv("PUCFEM_SPIN_WAIT")) == 0);
+  int spin_us = std::getenv("PUCFEM_SPIN_US") ? std::max(0, std::atoi(std::getenv("PUCFEM_SPIN_US"))) : 500;
   hipEvent_t ev_wait = nullptr;
   void wait_event(hipEvent_t e) {
     if (!spin_wait) {
       HIPCHK(hipEventSynchronize(e));
       return;
     }
-    for (;;) {
+    // a bounded spin (the solvers' reads wait tens of microseconds): a longer wait blocks, so no host core
+    // stays pinned beside other ranks' and the setup's threads
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; ++k) {
       const hipError_t q = hipEventQuery(e);
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) HIPCHK(q);
+      if ((k & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) {
+        HIPCHK(hipEventSynchronize(e));
+        return;
+      }
+#if defined(__x86_64__)
       __builtin_ia32_pause();
+#endif
     }
   }
   void sync_st() {  // hipStreamSynchronize(st) for the solvers' reads
@@ -949,12 +993,12 @@ struct Ctx {
     // host convergence checks: the first after as many iterations as the last solve took (the control
     // test after each update lets the check see convergence without a further launch)
     int chunk = std::max(1, std::min(maxit + 1, last_it[which] > 0 ? last_it[which] : 4));
-    std::vector<double> bmark;  // algo_bytes at the start of each iteration of the current chunk
+    std::vector<ByteMark> bmark;  // the byte counters at the start of each iteration of the current chunk
     for (;;) {
       const int it0 = it;
       bmark.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
-        bmark.push_back(algo_bytes);
+        bmark.push_back(bmark_now());
         // HIP-event timing samples every 8th iteration (bounded event count for long solves)
         const bool samp = (it & 7) == 0;
         with_c16(A, [&](auto c16) {
@@ -975,7 +1019,7 @@ struct Ctx {
       HIPCHK(hipStreamSynchronize(st));
       if (timer.on) timer.flush();
       // iterations from the converged one on were launched but did no work
-      if (h_ctl[0] && h_ctl[1] >= it0 && h_ctl[1] < it) algo_bytes = bmark[h_ctl[1] - it0];
+      if (h_ctl[0] && h_ctl[1] >= it0 && h_ctl[1] < it) bmark_restore(bmark[h_ctl[1] - it0]);
       if (h_ctl[0]) break;
       chunk = std::max(1, std::min(64, it / 8));
     }
@@ -1552,6 +1596,26 @@ struct Ctx {
   // one A-orthonormal basis serves both) that collects the solutions of both -- slot 1 for both; else a
   // basis per solve.  Separate bases stop improving at 16 directions; a shared one keeps improving up to
   // PROJ_MAX = 32 (r8l: 72 -> 63 pressure iterations over the driver window, +2 % steps/s)
+  // PUCFEM_PCG_TRACE=1 (diagnostic): the relative residual of every pressure PCG iteration on stderr (a host
+  // round trip per iteration)
+  bool pcg_trace = false;  // (read at every solve)
+  long n_pcg_traced = 0;
+  void trace_pcg(int which, int it) {
+    double h[5];
+    HIPCHK(hipMemcpyAsync(h, redbuf, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h + 1, redbuf + 8, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h + 2, redbuf + 32, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h + 3, ctl, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int cc[2];
+    std::memcpy(cc, h + 3, sizeof(cc));
+    if (it == 0) ++n_pcg_traced;
+    std::fprintf(stderr, "[pcg] solve %ld (slot %d) it %d |r|/|b| %.3e <r,z> %.3e ctl %d/%d\n", n_pcg_traced, which, it,
+                 std::sqrt(h[0] / h[1]), h[2], cc[0], cc[1]);
+  }
+  // PUCFEM_PROJ_SPMV=1 (diagnostic knob): the projection update's A v by an SpMV of v = y - x0 instead of the
+  // CG's residuals r0 - r_final (no pending directions)
+  bool proj_spmv = std::getenv("PUCFEM_PROJ_SPMV") && std::atoi(std::getenv("PUCFEM_PROJ_SPMV")) != 0;
   bool proj_shared = false;  // prm.proj_shared (PUCFEM_PROJ_SHARED=0/1 overrides it: a measurement knob)
   int proj_slot(int which) const { return proj_shared && which == 2 ? 1 : which; }
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
@@ -1607,7 +1671,7 @@ struct Ctx {
     const RedOut rdir = ro(redbuf + 16, CNT_DIR, 1), rupd = ro(redbuf, CNT_UPD, 1);
     // (iteration, first timing sample): samples from the converged iteration on are dropped
     std::vector<std::pair<int, size_t>> marks;
-    std::vector<std::pair<int, double>> bmarks;  // (iteration, algo_bytes at its start) of the current chunk
+    std::vector<std::pair<int, ByteMark>> bmarks;  // (iteration, the byte counters at its start) of the current chunk
     if (!merged_conv) {
       hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
       KCHK();
@@ -1626,6 +1690,8 @@ struct Ctx {
     // initial test before launching any (one round trip, where an iteration of early-exiting launches --
     // the V-cycle's ~70 -- costs ~0.3 ms of GPU time; in the start-up transient, where no solve passes at
     // its guess, the round trip would only idle the GPU: +0.25 ms per step in the driver window, r10b)
+    pcg_trace = std::getenv("PUCFEM_PCG_TRACE") && std::atoi(std::getenv("PUCFEM_PCG_TRACE")) != 0;
+    if (pcg_trace) trace_pcg(which, 0);
     const bool seen = solved_before[which];
     solved_before[which] = true;
     int chunk = std::max(1, std::min(maxit + 1, !seen ? 4 : (last_it[which] > 1 ? last_it[which] - 1 : 1)));
@@ -1641,7 +1707,7 @@ struct Ctx {
       bmarks.clear();
       for (int k = 0; k < chunk; ++k, ++it) {
         marks.push_back({it, timer.mark()});  // this iteration's V-cycle works iff not converged at it
-        bmarks.push_back({it, algo_bytes});
+        bmarks.push_back({it, bmark_now()});
         ro_rz = ro(redbuf + 32, CNT_RZ, 1);
         precondition();
         ro_rz = RedOut{};
@@ -1666,8 +1732,8 @@ struct Ctx {
         else pq = reduce_global(part_c, nb, 1, false, 2);
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
-        klaunch(2, bytes_upd, k_cg_upd<1>, dim3(nbu), dim3(BS), vu, n, pq.p, pq.nb, pq.stride,
-                (const double*)scal, (const int*)ctl, part_a, r32o, rupd);
+        klaunch(2, bytes_upd + (cg_vacc ? 16.0 * (double)n : 0.0), k_cg_upd<1>, dim3(nbu), dim3(BS), vu, n, pq.p,
+                pq.nb, pq.stride, (const double*)scal, (const int*)ctl, part_a, r32o, rupd, cg_vacc);
         KCHK();
         if (rupd.out) rr = Red{redbuf, 1, 1}, red_done(redbuf, 1, false);
         else if (!merged_conv) rr = reduce_global(part_a, nbu, 1, false, 0);
@@ -1680,6 +1746,7 @@ struct Ctx {
         }
         KCHK();
         std::swap(v.po[0], v.pn[0]);
+        if (pcg_trace) trace_pcg(which, it + 1);
       }
       HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       // the samples before this chunk, while the GPU runs it (this chunk's stay pending until its test is read)
@@ -1694,7 +1761,7 @@ struct Ctx {
       if (h_ctl[0])  // the bytes of the iterations that found the solve converged did not move
         for (auto& bm : bmarks)
           if (bm.first >= h_ctl[1]) {
-            algo_bytes = bm.second;
+            bmark_restore(bm.second);
             break;
           }
       if (h_ctl[0]) break;
@@ -1834,7 +1901,8 @@ struct Ctx {
     KCHK();
     if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
-    if (proj) project_guess(proj_slot(which), bh, yst);
+    const bool projected = proj && project_guess(proj_slot(which), bh, yst);
+    const bool acc = projected && !proj_spmv;  // the CG accumulates v (k_pcomb cleared pv)
     int it;
     if (dense) {
       hipLaunchKernelGGL(k_dense_mv<double>, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dPinv, bh, yst,
@@ -1844,11 +1912,16 @@ struct Ctx {
     } else if (use_mg) {
       // separate bases: the other slot's pending direction reads the r_final this solve overwrites
       proj_materialize(proj ? proj_slot(which) : 0);
+      cg_vacc = acc ? pv[proj_slot(which)] : nullptr;
       it = pcg_mg(yst, bh, prm.rtol_pres, prm.maxit_pres, which);
+      cg_vacc = nullptr;
       // (the projection update and the finish in one pass: sc is null on the multigrid path)
       if (proj) {
         const int slot = proj_slot(which);
-        if (p_from_y && proj_m[slot] > 0) {  // the direction stays pending (the next solve forms it)
+        pend_acc[slot] = acc;
+        if (proj_spmv) {
+          project_update(slot, yst);  // A v by an SpMV of the stored v
+        } else if (p_from_y && proj_m[slot] > 0) {  // the direction stays pending (the next solve forms it)
           pend_otf[slot] = true;
           pend_y[slot] = yst;
           proj_pend[slot] = true;
@@ -1865,7 +1938,7 @@ struct Ctx {
       halo(yst);
       return it;
     }
-    if (!(use_mg && proj)) {
+    if (!(use_mg && proj) || proj_spmv) {
       algo_bytes += (20.0 + (sc ? 8.0 : 0.0)) * (double)n;  // master_of, y (, s) read; p written
       hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 1, sc, yst, (const double*)nullptr, pout,
                          (double*)nullptr, dmaster_of);
@@ -1884,7 +1957,8 @@ struct Ctx {
   // x0 together, k_pcomb) do both: 2m + 9 vector passes per solve where a separate update took
   // 4m + 15.  A full basis is re-seeded first (proj_reseed).  With an empty basis the solve keeps
   // its warm start (x0 = 0).
-  void project_guess(int which, const double* b, double* y) {
+  // returns whether a guess was projected (false: the first solve of the basis keeps its warm start)
+  bool project_guess(int which, const double* b, double* y) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     ProjHist& H = proj_hist[which];
@@ -1893,15 +1967,19 @@ struct Ctx {
     if (!proj_pend[which]) {  // first solve: no direction yet
       HIPCHK(hipMemsetAsync(proj_x0[which], 0, sizeof(double) * n, st));
       H.gamma.clear();
-      return;
+      return false;
     }
     const int nb = grid_ew(n);
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
     // k_mdot2: X (fp32), b, A v, v read
     const bool otf = pend_otf[which];
-    const PendDir pd = otf ? PendDir{pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0]}
-                           : PendDir{nullptr, nullptr, nullptr};
-    klaunch(14, (4.0 * m + 24.0 + (otf ? 16.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
+    // a pending direction: A v from the residuals; v accumulated (pend_acc) or y - x0 (the first direction)
+    const bool vdiff = otf && !pend_acc[which];
+    const PendDir pd = otf ? PendDir{pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0],
+                                     pend_acc[which] ? (const double*)pv[which] : nullptr}
+                           : PendDir{nullptr, nullptr, nullptr, nullptr};
+    klaunch(14, (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb),
+            dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)ldx, b, (const double*)pav[which], (const double*)pv[which],
             op.null_free, proj_part, rmd, pd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
@@ -1915,15 +1993,18 @@ struct Ctx {
                        1.0 / (double)n_free, proj_coef);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
-    // k_pcomb: X, v read; the new direction, x0, y written
-    klaunch(15, (4.0 * kq + 32.0 + (otf ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
+    // k_pcomb: X, v read; the new direction, y and x0 (or the cleared accumulator of the coming solve) written
+    const bool acc_next = which <= 2 && !proj_spmv;
+    klaunch(15, (4.0 * kq + 32.0 + (vdiff ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)ldx, (const double*)proj_coef, (const double*)pv[which], op.null_free,
-            projX[which] + (i64)kq * ldx, y, proj_x0[which], otf ? pend_y[which] : (const double*)nullptr);
+            projX[which] + (i64)kq * ldx, y, acc_next ? (double*)nullptr : proj_x0[which],
+            vdiff ? pend_y[which] : (const double*)nullptr, acc_next ? pv[which] : (double*)nullptr);
     KCHK();
     pend_otf[which] = false;
     H.coef_m = kq;
     proj_m[which] = kq + 1;
     proj_pend[which] = false;
+    return true;
   }
   // coordinates bookkeeping: the last guess's coefficients (h_coef, copied with it; read after the
   // solve's host synchronisation) give the last solution y = x0 + v in the basis,
@@ -2008,16 +2089,17 @@ struct Ctx {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     double *v = pv[which], *av = pav[which];
-    if (r_final) {  // v = y - x0 and A v = r0 - r_final in one pass
+    if (r_final) {  // v = y - x0 (unless the solve accumulated it) and A v = r0 - r_final in one pass
       const bool whole = proj_m[which] == 0;
+      double* vout = pend_acc[which] ? nullptr : v;
       if (pfin) {
-        algo_bytes += 68.0 * (double)n;  // + master_of read, p written
+        algo_bytes += (vout ? 68.0 : 52.0) * (double)n;  // + master_of read, p written
         hipLaunchKernelGGL(k_diff2_fin, dim3(grid_ew(n)), dim3(BS), 0, st, (int64_t)n, y,
-                           (const double*)proj_x0[which], v, whole ? b : (const double*)av, r_final, av,
+                           (const double*)proj_x0[which], vout, whole ? b : (const double*)av, r_final, av,
                            (const int32_t*)dmaster_of, pfin);
       } else {
-        algo_bytes += 48.0 * (double)n;
-        hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], v,
+        algo_bytes += (vout ? 48.0 : 24.0) * (double)n;
+        hipLaunchKernelGGL(k_diff2, dim3(grid_ew(n)), dim3(BS), 0, st, n, y, (const double*)proj_x0[which], vout,
                            whole ? b : (const double*)av, r_final, av);
       }
       KCHK();
@@ -2193,16 +2275,19 @@ struct Ctx {
 
   // the finest multigrid level's lmax (lmax_estimate's power iteration, on the device operator):
   // min(Gershgorin bound gersh, 1.1 x 30 steps of x <- D^-1 A x / |D^-1 A x|)
-  double lmax_device(double gersh) {
+  double lmax_device(double gersh, double* lam_out) {
     const i64 n = lp.n_own;
-    double* x = dalloc<double>(nloc);
-    double* y = dalloc<double>(nloc);
+    struct Scratch {  // setup scratch: freed on return, not kept with the context
+      double* p = nullptr;
+      Scratch(i64 m) { HIPCHK(hipMalloc(&p, sizeof(double) * (size_t)std::max<i64>(1, m))); }
+      ~Scratch() { (void)hipFree(p); }
+    } xt(nloc), yt(nloc), dt(n);
+    double *x = xt.p, *y = yt.p, *dinv = dt.p;
     std::vector<double> x0;  // (global row index: a partitioned run iterates the single-rank vector)
-    host_resize(x0, n);
+    host_alloc_fresh(x0, n);
     parallel_for(n, [&](i64 i0, i64 i1) {
       for (i64 i = i0; i < i1; ++i) x0[i] = 1.0 + 0.5 * std::sin((double)(lp.r0 + i));
     });
-    double* dinv = dalloc<double>(n);
     h2d(dinv, lmax_dinv.data() + lp.r0, sizeof(double) * n);
     h2d(x, x0.data(), sizeof(double) * n);
     const int nb = nb_rows(n), ge = grid_ew(n);
@@ -2228,6 +2313,7 @@ struct Ctx {
     HIPCHK(hipStreamSynchronize(st));
     lmax_dinv.clear();
     lmax_dinv.shrink_to_fit();
+    *lam_out = lam;
     return std::min(gersh, 1.1 * lam);
   }
 
@@ -2239,7 +2325,7 @@ struct Ctx {
     MgBufs<T>& B = bufs<T>(L);
     const i64 n = L.lp.n_own, r0 = L.own0(rank);
     std::vector<T> x0;
-    host_resize(x0, n);
+    host_alloc_fresh(x0, n);
     parallel_for(n, [&](i64 i0, i64 i1) {
       for (i64 i = i0; i < i1; ++i) x0[i] = (T)(1.0 + 0.5 * std::sin((double)(r0 + i)));
     });
@@ -2273,6 +2359,7 @@ struct Ctx {
       KCHK();
     }
     HIPCHK(hipStreamSynchronize(st));
+    L.lam_dev = lam;
     return std::min(gersh, 1.1 * lam);
   }
 
@@ -2448,7 +2535,8 @@ inline void require(bool ok, const std::string& msg) {
 // the norms summed per chunk and then in chunk order: the same value on every machine.  power = false:
 // the Gershgorin bound only, with D^-1 in *dinv_out (the finest level's power iteration then runs on
 // the device, Ctx::lmax_device)
-double lmax_estimate(const Csr& A, bool power = true, std::vector<double>* dinv_out = nullptr) {
+double lmax_estimate(const Csr& A, bool power = true, std::vector<double>* dinv_out = nullptr,
+                     double* lam_out = nullptr) {
   const i64 n = A.nrows;
   std::vector<double> dinv(n), x(power ? n : 0), y(power ? n : 0);
   std::vector<double> cg(PAR_CHUNKS, 0.0), cx(PAR_CHUNKS), cy(PAR_CHUNKS);
@@ -2497,6 +2585,7 @@ double lmax_estimate(const Csr& A, bool power = true, std::vector<double>* dinv_
       for (i64 r = r0; r < r1; ++r) x[r] = y[r] * inv;
     });
   }
+  if (lam_out) *lam_out = lam;
   return std::min(gersh, 1.1 * lam);
 }
 
@@ -2572,7 +2661,8 @@ void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
   // parallel inside) read only what the level operators above produced: they run concurrently
   // the finest level's power iteration runs on the device at the end of build() (every rank its strip:
   // halos before the products, the two norms all-reduced)
-  c.lmax_dev = !c.host_only;
+  // PUCFEM_LMAX_HOST=1 (measurement knob): every level's power iteration on the host's fp64 operator
+  c.lmax_dev = !c.host_only && !(std::getenv("PUCFEM_LMAX_HOST") && std::atoi(std::getenv("PUCFEM_LMAX_HOST")));
   {
     ThreadGroup g;  // joined on every exit path; a level's exception reaches the caller from join()
     for (int l = 1; l <= Lv; ++l)
@@ -2661,7 +2751,7 @@ struct DevTmp {
   }
   // through the context's pinned staging buffers (returns with the data on the host)
   void get(std::vector<T>& v, i64 n, Ctx& c) const {
-    host_resize(v, (size_t)n);
+    host_alloc_fresh(v, (size_t)n);
     if (n > 0) c.d2h(v.data(), p, sizeof(T) * (size_t)n);
   }
 };
@@ -2816,21 +2906,21 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
   SetupClock ck;  // (its own thread: the marks interleave with build()'s)
   const HostMesh& m = c.mesh;
   const i64 N = m.N;
-  host_resize(P.X, N);
-  host_resize(P.Y, N);
+  host_alloc_fresh(P.X, N);
+  host_alloc_fresh(P.Y, N);
   parallel_for(N, [&](i64 g0, i64 g1) {
     for (i64 g = g0; g < g1; ++g) {
       P.X[g] = m.x[c.ord.new2old[g]];
       P.Y[g] = m.y[c.ord.new2old[g]];
     }
   });
-  host_resize(P.tri, 3 * m.T);
+  host_alloc_fresh(P.tri, 3 * m.T);
   parallel_for(3 * m.T, [&](i64 k0, i64 k1) {
     for (i64 k = k0; k < k1; ++k) P.tri[k] = c.ord.old2new[m.tri[k]];
   });
   // PointLocator centroids (StokesColor.py:321): (x1 + x2 + x3) / 3
-  host_resize(P.cx, m.T);
-  host_resize(P.cy, m.T);
+  host_alloc_fresh(P.cx, m.T);
+  host_alloc_fresh(P.cy, m.T);
   parallel_for(m.T, [&](i64 t0, i64 t1) {
     for (i64 t = t0; t < t1; ++t) {
       const i32 a = m.tri[3 * t], b = m.tri[3 * t + 1], d = m.tri[3 * t + 2];
@@ -2842,7 +2932,7 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
   build_centroid_grid(P.cx, P.cy, 2.0, P.G);
   ck.mark("  sl: centroid grid");
   if (food) build_tri_grid(P.X, P.Y, P.tri, 4.0, P.TG);  // tracer location (StokesFood only)
-  host_resize(P.xy, 2 * (size_t)N);
+  host_alloc_fresh(P.xy, 2 * (size_t)N);
   parallel_for(N, [&](i64 i0, i64 i1) {
     for (i64 i = i0; i < i1; ++i) {
       P.xy[2 * i] = P.X[i];
@@ -2864,7 +2954,7 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
     build_tri_grid(c.macro.x, c.macro.y, c.macro.tri, 0.25, P.MG, 1e-6);
     // home faces: the macro face of every face-interior row (the first face tried)
     const LatticeLevel& LL = c.mg.back().latl;
-    host_resize(P.home, N);
+    host_alloc_fresh(P.home, N);
     std::fill(P.home.begin(), P.home.end(), -1);
     parallel_for(c.macro.nf, [&](i64 f0, i64 f1) {
       for (i64 f = f0; f < f1; ++f)
@@ -2872,7 +2962,7 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
     }, 1);
   }
   // initial dye c = 1[x < 0.5] (StokesColor.py:493-495)
-  host_resize(P.c0, N);
+  host_alloc_fresh(P.c0, N);
   parallel_for(N, [&](i64 g0, i64 g1) {
     for (i64 g = g0; g < g1; ++g) P.c0[g] = m.x[c.ord.new2old[g]] < 0.5 ? 1.0 : 0.0;
   });
@@ -2957,7 +3047,7 @@ void build(Ctx& c) {
   std::vector<uint8_t> isdir(N, 0);
   for (i32 d : c.dir_nodes) isdir[c.ord.old2new[d]] = 1;
   const double dtnu = prm.dt * prm.nu;
-  host_resize(c.Kv, c.P.nnz());
+  host_alloc_fresh(c.Kv, c.P.nnz());
   parallel_for(N, [&](i64 r0, i64 r1) {
     for (i64 r = r0; r < r1; ++r)
       for (i64 k = c.P.rowptr[r]; k < c.P.rowptr[r + 1]; ++k) {
@@ -2969,7 +3059,7 @@ void build(Ctx& c) {
   });
   if (stokes) {  // spectral interval of the Jacobi-scaled A_visc (Ctx::visc_R, Ctx::visc_lo)
     std::vector<double> dg;
-    host_resize(dg, N);
+    host_alloc_fresh(dg, N);
     parallel_for(N, [&](i64 r0, i64 r1) {
       for (i64 r = r0; r < r1; ++r) dg[r] = diag_of(c.P, c.Kv, r);
     });
@@ -3212,14 +3302,14 @@ void build(Ctx& c) {
   // Jacobi symmetric scaling S A S: s_g = 1 / sqrt(a_gg); the scaled values s_r a_rk s_col go straight into
   // the SELL image (only the skeleton rows on lattice hierarchies)
   auto scaling = [&](const Csr& A, const std::vector<double>& val, std::vector<double>& sg) {
-    host_resize(sg, N);
+    host_alloc_fresh(sg, N);
     parallel_for(N, [&](i64 g0, i64 g1) {
       for (i64 g = g0; g < g1; ++g) sg[g] = 1.0 / std::sqrt(diag_of(A, val, g));
     });
   };
   auto local_vec = [&](const std::vector<double>& g) {  // owned + ghost entries of a global vector
     std::vector<double> v;
-    host_resize(v, c.nloc);
+    host_alloc_fresh(v, c.nloc);
     parallel_for(no, [&](i64 i0, i64 i1) { std::memcpy(v.data() + i0, g.data() + lp.r0 + i0, sizeof(double) * (i1 - i0)); });
     for (i64 k = 0; k < lp.n_ghost; ++k) v[no + k] = g[lp.ghost_global[k]];
     return v;
@@ -3231,7 +3321,7 @@ void build(Ctx& c) {
     c.dKv = c.upload(tmp);
     c.dsv = c.upload(local_vec(sg));
     std::vector<double> sq;
-    host_resize(sq, N);
+    host_alloc_fresh(sq, N);
     parallel_for(N, [&](i64 g0, i64 g1) {
       for (i64 g = g0; g < g1; ++g) sq[g] = 1.0 / sg[g];
     });
@@ -3348,7 +3438,7 @@ void build(Ctx& c) {
   // pending pressure directions and the gradient on y (Ctx::p_from_y): lattice operators, the multigrid PCG
   // with the projection, the explicit dye; PUCFEM_P_FROM_Y=0 keeps the stored form (a measurement knob: the
   // same values either way).  Partitioned runs exchange y's halo instead of p's.
-  c.p_from_y = stokes && c.lattice && c.use_mg && c.proj_k > 0 && !c.dye_impl && c.dP.c16 == nullptr &&
+  c.p_from_y = stokes && c.lattice && c.use_mg && c.proj_k > 0 && !c.dye_impl && c.dP.c16 == nullptr && !c.proj_spmv &&
                !(std::getenv("PUCFEM_P_FROM_Y") && std::atoi(std::getenv("PUCFEM_P_FROM_Y")) == 0);
   if (c.p_from_y) {  // dP with every column mapped to its periodic master (the dof map), in local ids
     std::vector<i32> colm(c.sP.col.size());
@@ -3368,6 +3458,16 @@ void build(Ctx& c) {
         if (it == lp.ghost_global.end() || *it != mg) ok = false;  // a master outside the local columns
         else colm[e] = (i32)(no + (it - lp.ghost_global.begin()));
       }
+    }
+    // every rank takes the same path: a rank whose merged columns reach outside its local columns would
+    // halo p while its neighbours send y (whose slave entries are not copies of their masters)
+    if (c.dist()) {
+      std::vector<double> bad(1, ok ? 0.0 : 1.0);
+      DevTmp<double> t(bad, c.st);
+      c.comm->allreduce(t.p, 1, true, c.st);
+      t.get(bad, 1, c.st);
+      HIPCHK(hipStreamSynchronize(c.st));
+      ok = bad[0] == 0.0;
     }
     c.p_from_y = ok;
     if (ok) {
@@ -3441,12 +3541,12 @@ void build(Ctx& c) {
     std::vector<double> as1, mp, wm;
     std::vector<uint8_t> df;
     std::vector<i32> so, mo;
-    host_resize(as1, no);
-    host_resize(mp, no);
-    host_resize(wm, no);
-    host_resize(df, no);
-    host_resize(so, no);
-    host_resize(mo, no);
+    host_alloc_fresh(as1, no);
+    host_alloc_fresh(mp, no);
+    host_alloc_fresh(wm, no);
+    host_alloc_fresh(df, no);
+    host_alloc_fresh(so, no);
+    host_alloc_fresh(mo, no);
     parallel_for(no, [&](i64 i0, i64 i1) {
       for (i64 i = i0; i < i1; ++i) {
         const i64 g = lp.r0 + i;
@@ -3693,7 +3793,7 @@ void build(Ctx& c) {
   clk.mark("SL: locator / self table, initial state");
   if (c.use_mg && c.lmax_dev) {
     MgLevel& F = c.mg[c.mg_levels];
-    F.lmax = c.lmax_device(F.lmax);
+    F.lmax = c.lmax_device(F.lmax, &F.lam_dev);
     clk.mark("finest lmax (device power iteration)");
     for (int l = 1; l < c.mg_levels; ++l)
       c.mg[l].lmax = c.mg_single ? c.lmax_level_device<float>(c.mg[l], c.mg[l].lmax)
@@ -4591,6 +4691,15 @@ int pucfem_counters(void* ctx, int64_t* launches, double* bytes) {
   });
 }
 
+int pucfem_class_counters(void* ctx, int32_t kclass, int64_t* launches, double* bytes) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    require(kclass >= 0 && kclass < Timer::NCLS, "kernel class out of range");
+    *launches = c.cls_n[kclass];
+    *bytes = c.cls_bytes[kclass];
+  });
+}
+
 int pucfem_sync(void* ctx) {
   return guard(ctx, [&] {
     Ctx& c = *C(ctx);
@@ -4637,6 +4746,23 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
            (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.p_from_y ? 64 : 0);
+  });
+}
+
+int pucfem_mg_lmax(void* ctx, int32_t level, double* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    require(c.use_mg && level >= 0 && level <= c.mg_levels, "level of a multigrid hierarchy");
+    require(!c.dist(), "a single-rank context (the host estimate iterates the whole level)");
+    const MgLevel& L = c.mg[level];
+    const Csr& A = level == c.mg_levels ? c.Pp : L.Pp;
+    double lam = 0.0;
+    o[0] = L.lmax;
+    o[1] = L.lam_dev;
+    o[3] = lmax_estimate(A, false);
+    lmax_estimate(A, true, nullptr, &lam);
+    o[2] = lam;
   });
 }
 

@@ -221,7 +221,7 @@ void build_pattern(const HostMesh& m, const Ordering& ord, Csr& P, const Inciden
       P.rowptr[r + 1] = P.rowptr[r] + l;
       ++r;
     }
-  host_resize(P.col, P.rowptr[N]);
+  host_alloc_fresh(P.col, P.rowptr[N]);
   std::vector<i64> cstart(PAR_CHUNKS + 1, 0);
   for (int ch = 0; ch < PAR_CHUNKS; ++ch) cstart[ch + 1] = cstart[ch] + (i64)ccol[ch].size();
   parallel_for(PAR_CHUNKS, [&](i64 c0, i64 c1) {
@@ -417,8 +417,8 @@ void build_pressure(const Csr& P, const std::vector<double>& K, const std::vecto
     }
   });
   for (i64 r = 0; r < N; ++r) Pp.rowptr[r + 1] += Pp.rowptr[r];
-  host_resize(Pp.col, Pp.rowptr[N]);
-  host_resize(Pp.val, Pp.rowptr[N]);
+  host_alloc_fresh(Pp.col, Pp.rowptr[N]);
+  host_alloc_fresh(Pp.val, Pp.rowptr[N]);
   parallel_for(N, [&](i64 r0, i64 r1) {
     std::vector<std::pair<i32, double>> tmp;
     for (i64 r = r0; r < r1; ++r) {
@@ -602,7 +602,7 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
             *std::min_element(cy.begin(), cy.end()), *std::max_element(cy.begin(), cy.end()), T, per_cell, G);
   const i64 nc = (i64)G.nx * G.ny;
   std::vector<i32> cell;
-  host_resize(cell, T);
+  host_alloc_fresh(cell, T);
   parallel_for(T, [&](i64 t0, i64 t1) {
     for (i64 t = t0; t < t1; ++t) cell[t] = cell_of(cy[t], G.y0, G.hy, G.ny) * G.nx + cell_of(cx[t], G.x0, G.hx, G.nx);
   });
@@ -610,9 +610,9 @@ void build_centroid_grid(const std::vector<double>& cx, const std::vector<double
   // cells and scans every triangle (two passes over the 4 B cell ids) for those in its range: the same
   // order as one sequential pass, no per-thread histograms of all cells.
   G.cell_start.assign(nc + 1, 0);
-  host_resize(G.item, T);
-  host_resize(G.px, T);
-  host_resize(G.py, T);
+  host_alloc_fresh(G.item, T);
+  host_alloc_fresh(G.px, T);
+  host_alloc_fresh(G.py, T);
   const int nt = (int)std::max<i64>(1, std::min<i64>((i64)host_threads(), T / 65536 + 1));
   auto range = [&](int w, i64& c0, i64& c1) {
     c0 = nc * w / nt;
@@ -808,7 +808,7 @@ void build_prolongation(i64 Nc, const std::vector<i32>& ea, const std::vector<i3
     val[1] = 0.5;
     return 2;
   };
-  host_resize(P.rowptr, Nf + 1);
+  host_alloc_fresh(P.rowptr, Nf + 1);
   P.rowptr[0] = 0;
   parallel_for(Nf, [&](i64 g0, i64 g1) {
     i32 c[2];
@@ -816,8 +816,8 @@ void build_prolongation(i64 Nc, const std::vector<i32>& ea, const std::vector<i3
     for (i64 g = g0; g < g1; ++g) P.rowptr[g + 1] = row(g, c, v);
   });
   for (i64 g = 0; g < Nf; ++g) P.rowptr[g + 1] += P.rowptr[g];
-  host_resize(P.col, P.rowptr[Nf]);
-  host_resize(P.val, P.rowptr[Nf]);
+  host_alloc_fresh(P.col, P.rowptr[Nf]);
+  host_alloc_fresh(P.val, P.rowptr[Nf]);
   parallel_for(Nf, [&](i64 g0, i64 g1) {
     for (i64 g = g0; g < g1; ++g) row(g, P.col.data() + P.rowptr[g], P.val.data() + P.rowptr[g]);
   });
@@ -847,8 +847,8 @@ void transpose(const Csr& A, i64 ncols, Csr& At) {
     }
   });
   for (i64 c = 0; c < ncols; ++c) At.rowptr[c + 1] += At.rowptr[c];
-  host_resize(At.col, nnz);
-  host_resize(At.val, nnz);
+  host_alloc_fresh(At.col, nnz);
+  host_alloc_fresh(At.val, nnz);
   run([&](int w) {
     const i64 c0 = ncols * w / nt, c1 = ncols * (w + 1) / nt;
     std::vector<i64> fill(At.rowptr.begin() + c0, At.rowptr.begin() + c1);

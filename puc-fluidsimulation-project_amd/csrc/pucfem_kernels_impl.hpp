@@ -507,7 +507,9 @@ __global__ LB_GATHER void k_cg_dir(SellDev A, FaceDev fc, const double* __restri
 template <int NR>
 __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, const double* part_pq, int nb_pq,
                                                int stride_pq, const double* scal, const int* ctl, double* part_rr,
-                                               float* __restrict__ r32 = nullptr, RedOut ro = RedOut{}) {
+                                               float* __restrict__ r32 = nullptr, RedOut ro = RedOut{},
+                                               double* __restrict__ vacc = nullptr) {
+  // vacc (NR = 1, optional): the correction sum_k alpha_k p_k accumulated beside y (the projection's v)
   __shared__ double sh[4];
   if (ctl[0]) return;
   double alpha[NR], rr[NR];
@@ -522,7 +524,9 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
   for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
 #pragma unroll
     for (int c = 0; c < NR; ++c) {
-      stnt(v.y[c] + i, v.y[c][i] + alpha[c] * v.pn[c][i]);
+      const double pi = v.pn[c][i];
+      stnt(v.y[c] + i, v.y[c][i] + alpha[c] * pi);
+      if (NR == 1 && vacc) stnt(vacc + i, vacc[i] + alpha[c] * pi);
       const double r = v.r[c][i] - alpha[c] * v.q[c][i];
       stnt(v.r[c] + i, r);
       if (NR == 1 && r32) stnt(r32 + i, (float)r);
@@ -546,7 +550,11 @@ constexpr int PROJ_MAX = 32;
 // relative residual is 1e-6 .. 1e-5 against the solve's rtol 1e-8), and rounding the A-orthonormal
 // directions to fp32 perturbs their A-inner products by ~1e-7, below that; the dots and the
 // combinations are formed in fp64.  Halves the two passes over the basis (2 m vector reads per solve).
+#ifdef PUCFEM_PROJ_F64
+using ProjT = double;  // (A/B variant: the basis in fp64)
+#else
 using ProjT = float;
+#endif
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef float flt2 __attribute__((ext_vector_type(2)));
 
@@ -579,21 +587,21 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
 // [<X_i, b> (M), <X_i, A v> (M), <v, b>, <v, A v>, sum_free v, sum_free b].  One instance per M:
 // the M loads of a row are unconditional (all in flight together); grid-stride rows keep the
 // resident waves on one compact window of every vector.
-// The last solve's direction may still be pending (D.y non-null): then v = y - x0 and A v = r0 - r_final are
-// formed here from the last solve's solution, guess, initial and final residuals (av holds r0) -- the
-// operations k_diff2_fin would have stored, so the same values -- instead of being read.
+// The last solve's direction may still be pending: then A v = r0 - r_final is formed here from the solve's initial
+// and final residuals (av holds r0, D.rf the final one) -- the operations k_diff2_fin would have stored, so the
+// same values -- instead of being read.  v itself is the CG's accumulated correction sum_k alpha_k p_k
+// (k_cg_upd's vacc, D.v) after a projected guess: the same vector as y - x0 in exact arithmetic, but y - x0
+// formed from the two stored fp64 vectors carries their rounding, whose A-norm is not small against a
+// correction of ~1e-8 of y (at L7, A x of a rounded smooth field has a relative noise of ~1e-8 of b): A v
+// from the residuals then does not match that v, the new direction is mis-normalised and the basis decays
+// (driver-window rtol 5e-8 runs went from 0-1 to 6 iterations per solve, profiles/r11_projection.txt).
+// Without D.v (the first direction, whose guess was 0): v = D.y - D.x0.
 struct PendDir {
-  const double* y;   // the last solve's solution (null: v and A v were stored)
+  const double* y;   // the last solve's solution (with x0; used when v is null)
   const double* x0;  // its guess
-  const double* rf;  // its final residual
+  const double* rf;  // its final residual (null: A v was stored in av)
+  const double* v;   // its accumulated correction (null: y - x0, or the stored v)
 };
-// PUCFEM_PROJ_R (compile-time A/B knob, 1 or 2): rows per thread and iteration of k_mdot2 / k_pcomb; with 2
-// every basis vector is read as 8-B pairs (the basis stride ldx is even) and the fp64 vectors as 16-B pairs
-#ifndef PUCFEM_PROJ_R
-#define PUCFEM_PROJ_R 1
-#endif
-constexpr int PROJ_R = PUCFEM_PROJ_R;
-static_assert(PROJ_R == 1 || PROJ_R == 2, "PUCFEM_PROJ_R must be 1 or 2");
 template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
@@ -605,8 +613,13 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
 #pragma unroll
   for (int i = 0; i < NA; ++i) acc[i] = 0.0;
   const int64_t step = (int64_t)gridDim.x * BS;
-  // one row's contribution, in the order of the single-row loop
-  auto row = [&](const float* x, double br, double ar, double vr, bool free_row) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+    const double br = b[r];
+    const double ar = D.rf ? av[r] - D.rf[r] : av[r];
+    const double vr = D.v ? D.v[r] : (D.y ? D.y[r] - D.x0[r] : v[r]);
+    ProjT x[M > 0 ? M : 1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       acc[i] += (double)x[i] * br;
@@ -614,56 +627,10 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
     }
     acc[2 * M] += vr * br;
     acc[2 * M + 1] += vr * ar;
-    if (free_row) {
+    if (master_of && master_of[r] < 0) {
       acc[2 * M + 2] += vr;
       acc[2 * M + 3] += br;
     }
-  };
-  auto one = [&](int64_t r) {
-    const double br = b[r];
-    double ar, vr;
-    if (D.y) {
-      vr = D.y[r] - D.x0[r];
-      ar = av[r] - D.rf[r];
-    } else {
-      ar = av[r];
-      vr = v[r];
-    }
-    float x[M > 0 ? M : 1];
-#pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
-    row(x, br, ar, vr, master_of && master_of[r] < 0);
-  };
-  if constexpr (PROJ_R == 1) {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) one(r);
-  } else {
-    const int64_t np = n / 2;
-    for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += step) {
-      const int64_t r = 2 * q;
-      const dbl2 bb = *reinterpret_cast<const dbl2*>(b + r);
-      dbl2 aa, vv;
-      if (D.y) {
-        const dbl2 y2 = *reinterpret_cast<const dbl2*>(D.y + r), x2 = *reinterpret_cast<const dbl2*>(D.x0 + r);
-        const dbl2 a2 = *reinterpret_cast<const dbl2*>(av + r), f2 = *reinterpret_cast<const dbl2*>(D.rf + r);
-        vv = dbl2{y2.x - x2.x, y2.y - x2.y};
-        aa = dbl2{a2.x - f2.x, a2.y - f2.y};
-      } else {
-        aa = *reinterpret_cast<const dbl2*>(av + r);
-        vv = *reinterpret_cast<const dbl2*>(v + r);
-      }
-      float x0[M > 0 ? M : 1], x1[M > 0 ? M : 1];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const flt2 t = *reinterpret_cast<const flt2*>(X + i * ld + r);
-        x0[i] = t.x;
-        x1[i] = t.y;
-      }
-      int2 mo = make_int2(0, 0);
-      if (master_of) mo = *reinterpret_cast<const int2*>(master_of + r);
-      row(x0, bb.x, aa.x, vv.x, master_of && mo.x < 0);
-      row(x1, bb.y, aa.y, vv.y, master_of && mo.y < 0);
-    }
-    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(n - 1);
   }
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -711,14 +678,15 @@ __global__ void k_pcoef(const double* __restrict__ D, int m, const double* __res
 }
 
 // pass 2: the new direction X_M = s (v - mu 1_free - sum_i c_i X_i) and the guess
-// x0 = sum_i a_i X_i + alpha X_M (written to y and x0), one pass over the M basis vectors.
-// yp non-null: v = yp - x0 (the pending direction, k_mdot2's PendDir) from the last solve's solution and the
-// old x0, each row read before this row's new x0 (and y, which may be yp's buffer) is written
+// x0 = sum_i a_i X_i + alpha X_M (written to y, and to x0 when given), one pass over the M basis vectors.
+// v: the stored or accumulated direction, or with yp non-null v = yp - x0 (the first direction) from the last
+// solve's solution and its guess, each row read before this row's new values are written.  vz (optional): the
+// next solve's correction accumulator, cleared (it may be v's buffer: each row reads v first)
 template <int M>
 __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict__ X, int64_t ld,
-                                              const double* __restrict__ K, const double* __restrict__ v,
+                                              const double* __restrict__ K, const double* v,
                                               const int32_t* __restrict__ master_of, ProjT* __restrict__ xm_out,
-                                              double* y, double* x0, const double* yp) {
+                                              double* y, double* x0, const double* yp, double* vz) {
   double ka[M > 0 ? M : 1], kc[M > 0 ? M : 1];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
@@ -726,58 +694,23 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
     kc[i] = K[M + i];
   }
   const double s = K[2 * M], mu = K[2 * M + 1], alpha = K[2 * M + 2];
-  // x: the row's basis values; vr its v; returns (x_M, g)
-  auto comb = [&](const float* x, double vr, bool free_row, double& xm, double& g) {
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    ProjT x[M > 0 ? M : 1];
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    const double vr = yp ? yp[r] - x0[r] : v[r];
     double sa = 0.0, sc = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       sa += ka[i] * (double)x[i];
       sc += kc[i] * (double)x[i];
     }
-    xm = s * (vr - (free_row ? mu : 0.0) - sc);
-    g = sa + alpha * xm;
-  };
-  auto one = [&](int64_t r) {
-    float x[M > 0 ? M : 1];
-#pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
-    const double vr = yp ? yp[r] - x0[r] : v[r];
-    double xm, g;
-    comb(x, vr, master_of && master_of[r] < 0, xm, g);
+    const double xm = s * (vr - ((master_of && master_of[r] < 0) ? mu : 0.0) - sc);
+    const double g = sa + alpha * xm;
     stnt(xm_out + r, (ProjT)xm);
     stnt(y + r, g);
-    stnt(x0 + r, g);
-  };
-  if constexpr (PROJ_R == 1) {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) one(r);
-  } else {
-    const int64_t np = n / 2;
-    for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += (int64_t)gridDim.x * BS) {
-      const int64_t r = 2 * q;
-      float xa[M > 0 ? M : 1], xb[M > 0 ? M : 1];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        const flt2 t = *reinterpret_cast<const flt2*>(X + i * ld + r);
-        xa[i] = t.x;
-        xb[i] = t.y;
-      }
-      dbl2 vv;
-      if (yp) {
-        const dbl2 y2 = *reinterpret_cast<const dbl2*>(yp + r), o2 = *reinterpret_cast<const dbl2*>(x0 + r);
-        vv = dbl2{y2.x - o2.x, y2.y - o2.y};
-      } else {
-        vv = *reinterpret_cast<const dbl2*>(v + r);
-      }
-      int2 mo = make_int2(0, 0);
-      if (master_of) mo = *reinterpret_cast<const int2*>(master_of + r);
-      double ma, ga, mb, gb;
-      comb(xa, vv.x, master_of && mo.x < 0, ma, ga);
-      comb(xb, vv.y, master_of && mo.y < 0, mb, gb);
-      stnt(reinterpret_cast<flt2*>(xm_out + r), flt2{(ProjT)ma, (ProjT)mb});
-      stnt(reinterpret_cast<dbl2*>(y + r), dbl2{ga, gb});
-      stnt(reinterpret_cast<dbl2*>(x0 + r), dbl2{ga, gb});
-    }
-    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(n - 1);
+    if (x0) stnt(x0 + r, g);
+    if (vz) stnt(vz + r, 0.0);
   }
 }
 
@@ -785,26 +718,27 @@ __global__ void k_diff(int64_t n, const double* __restrict__ a, const double* __
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) stnt(out + r, a[r] - b[r]);
 }
 
-// out = a - b and out2 = a2 - b2 (out2 may alias a2: each row reads before it writes)
+// out = a - b (when out is given) and out2 = a2 - b2 (out2 may alias a2: each row reads before it writes)
 __global__ void k_diff2(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out,
                         const double* a2, const double* __restrict__ b2, double* out2) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
-    const double x = a[r], y = b[r], x2 = a2[r], y2 = b2[r];
-    stnt(out + r, x - y);
+    const double x2 = a2[r], y2 = b2[r];
+    if (out) stnt(out + r, a[r] - b[r]);
     stnt(out2 + r, x2 - y2);
   }
 }
 
 // k_diff2 and the pressure solve's finish (k_cg_fin with master_of, unscaled) in one pass: the projection's
-// v = y - x0 and A v = a2 - r_final, and p = y with every periodic slave row copied from its master
+// v = y - x0 (when v is given; else v is the CG's accumulated correction) and A v = a2 - r_final, and p = y with
+// every periodic slave row copied from its master
 __global__ void k_diff2_fin(int64_t n, const double* __restrict__ y, const double* __restrict__ x0,
                             double* __restrict__ v, const double* a2, const double* __restrict__ rf, double* av,
                             const int32_t* __restrict__ master_of, double* __restrict__ p) {
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
-    const double yr = y[r], x = x0[r], a = a2[r], f = rf[r];
+    const double yr = y[r], a = a2[r], f = rf[r];
     const int32_t m = master_of[r];
     const double pr = m >= 0 ? y[m] : yr;
-    stnt(v + r, yr - x);
+    if (v) stnt(v + r, yr - x0[r]);
     stnt(av + r, a - f);
     p[r] = pr;
   }

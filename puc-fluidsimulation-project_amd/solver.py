@@ -246,6 +246,13 @@ class Context:
         self._c(self.L.pucfem_visc_interval(self.h, o))
         return float(o[0]), float(o[1])
 
+    def mg_lmax(self, level):
+        """The multigrid smoothing interval's top on `level` (pucfem_mg_lmax): lmax in use, the device power
+        iteration's quotient (0: host), the host fp64 power iteration's quotient, the Gershgorin bound."""
+        o = (ct.c_double * 4)()
+        self._c(self.L.pucfem_mg_lmax(self.h, int(level), o))
+        return dict(lmax=o[0], lam_device=o[1], lam_host=o[2], gershgorin=o[3])
+
     def comm_info(self):
         """Multi-rank data flow of the last step (pucfem_comm_info)."""
         o = (ct.c_int64 * 4)()
@@ -279,6 +286,12 @@ class Context:
         (pucfem_counters): differences over a timed region give launches and the HBM floor per step."""
         n, b = ct.c_int64(), ct.c_double()
         self._c(self.L.pucfem_counters(self.h, ct.byref(n), ct.byref(b)))
+        return n.value, b.value
+
+    def class_counters(self, kclass):
+        """(launches, algorithmic bytes) of one kernel class over every launch so far (pucfem_class_counters)."""
+        n, b = ct.c_int64(), ct.c_double()
+        self._c(self.L.pucfem_class_counters(self.h, int(kclass), ct.byref(n), ct.byref(b)))
         return n.value, b.value
 
     def sync(self):

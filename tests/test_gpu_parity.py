@@ -456,3 +456,43 @@ def test_mg_and_jacobi_steps_agree(single):
     assert all(x.it_p < 40 for x in sa) and all(x.it_p > 200 for x in sb)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("refine", [3, 5])
+def test_mg_lmax_device_equals_host(refine):
+    """The multigrid smoothing interval [lmax / ratio, lmax] (the preconditioner of the pressure solves that
+    replace np.linalg.solve at StokesColor.py:555,569): every level's device power iteration (fp64 on the finest
+    level, the fp32 V-cycle values below it) gives the host fp64 power iteration's quotient on the same level
+    operator, and lmax = min(Gershgorin, 1.1 x quotient)."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    sim = stokes(mesh, tol=S.Tolerances.production())
+    levels = sim.ctx.info()["mg_levels"]
+    assert levels == refine + 1
+    for lv in range(levels):
+        d = sim.ctx.mg_lmax(lv)
+        if lv == 0:  # the coarsest level is solved densely; its interval comes from the host estimate
+            assert d["lam_device"] == 0.0
+            lam = d["lam_host"]
+        else:
+            lam = d["lam_device"]
+            assert abs(lam - d["lam_host"]) <= 1e-5 * d["lam_host"], (lv, d)
+        assert abs(d["lmax"] - min(d["gershgorin"], 1.1 * lam)) <= 1e-12 * d["lmax"], (lv, d)
+        assert 1.0 < d["lmax"] <= d["gershgorin"] + 1e-12
+    sim.close()
+
+
+@pytest.mark.timeout(300)
+def test_projection_basis_holds_below_the_guess_floor_L7():
+    """Regression (round 5): with the projection's new direction formed as y - x0 from the two stored fp64
+    vectors, A v from the CG's residuals did not match it once the guesses reached ~1e-7 of b on L7 (the rounding
+    of y and x0 has an A-norm comparable to the correction), the basis decayed and a solve at rtol 5e-8 went from
+    0-1 to 6 iterations from step ~110 on.  The CG now accumulates v itself: 20 steps past the transient at
+    rtol 5e-8 take at most 2 iterations per solve on average."""
+    mesh = pf.load_mesh("fine", refine=7)
+    sim = stokes(mesh, tol=S.Tolerances.production(rtol_pres=5e-8))
+    sim.step(100)
+    st = sim.step(20)
+    its = sum(s.it_p + s.it_p2 for s in st)
+    print(f"L7 steps 100-119 at rtol 5e-8: {its} pressure iterations over 40 solves")
+    assert its <= 80, [(s.it_p, s.it_p2) for s in st]
+    sim.close()

@@ -31,6 +31,9 @@ from importlib import import_module  # noqa: E402
 S = import_module("puc-fluidsimulation-project_amd.solver")
 
 TOL_STEP = 1e-6
+# the margin the docs claim for the production tolerance's per-step error past the transient:
+# at least 2x under the 1e-6 bar (r11f: worst |dc| 1.77e-7 over steps 100-149, 5.6x)
+TOL_MARGIN = TOL_STEP / 2
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -94,30 +97,35 @@ def test_production_rtol_L7_driver_window():
 def test_production_rtol_L7_per_step_past_transient():
     """Per-step error of the production tolerance on L7 past the start-up transient (the reference's run is
     6000 steps, StokesColor.py:44,537-586): a tight run (rtol_pres 1e-12) is the trajectory; at every step
-    100..149 the production run is put on the tight run's state (u, c), both take one step, and the
-    production step must land within 1e-6 of the tight one.  The production run keeps its own projection
-    basis and solve history from its first 100 steps (setting u restarts only its viscous extrapolation)."""
+    100..149, and again at 1000..1019, the production run is put on the tight run's state (u, c), both take one
+    step, and the production step must land within TOL_MARGIN (half the 1e-6 bar) of the tight one.  The
+    production run keeps its own projection basis and solve history from its own trajectory (setting u
+    restarts only its viscous extrapolation)."""
     mesh = pf.load_mesh("fine", refine=7)
     assert mesh.N == 14230528
     a = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, S.Tolerances.production())
     b = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, S.Tolerances.production(rtol_pres=1e-12))
-    a.step(100)
-    b.step(100)
-    worst_u = worst_c = 0.0
-    its_a = its_b = 0
-    for k in range(100, 150):
-        a.u = b.u
-        a.c = b.c
-        sa, sb = a.step(1)[0], b.step(1)[0]
-        its_a += sa.it_p + sa.it_p2
-        its_b += sb.it_p + sb.it_p2
-        du = float(np.abs(a.u - b.u).max())
-        dc = float(np.abs(a.c - b.c).max())
-        worst_u, worst_c = max(worst_u, du), max(worst_c, dc)
-        assert du < TOL_STEP and dc < TOL_STEP, (k, du, dc)
-    assert its_b > its_a
-    print(f"L7 steps 100-149 from a common state, rtol {S.PRODUCTION_RTOL_PRES:g} vs 1e-12: worst per-step "
-          f"|du| = {worst_u:.2e}, |dc| = {worst_c:.2e} (bar {TOL_STEP:g}); pressure iterations {its_a} vs {its_b}")
+    done = 0
+    for start, window in ((100, 50), (1000, 20)):
+        a.step(start - done)
+        b.step(start - done)
+        worst_u = worst_c = 0.0
+        its_a = its_b = 0
+        for k in range(start, start + window):
+            a.u = b.u
+            a.c = b.c
+            sa, sb = a.step(1)[0], b.step(1)[0]
+            its_a += sa.it_p + sa.it_p2
+            its_b += sb.it_p + sb.it_p2
+            du = float(np.abs(a.u - b.u).max())
+            dc = float(np.abs(a.c - b.c).max())
+            worst_u, worst_c = max(worst_u, du), max(worst_c, dc)
+            assert du < TOL_MARGIN and dc < TOL_MARGIN, (k, du, dc)
+        done = start + window
+        assert its_b > its_a
+        print(f"L7 steps {start}-{done - 1} from a common state, rtol {S.PRODUCTION_RTOL_PRES:g} vs 1e-12: worst "
+              f"per-step |du| = {worst_u:.2e}, |dc| = {worst_c:.2e} (bar {TOL_STEP:g}, margin "
+              f"{TOL_STEP / max(worst_u, worst_c):.1f}x); pressure iterations {its_a} vs {its_b}")
     a.close()
     b.close()
 
