@@ -290,6 +290,7 @@ def main():
         "bytes_per_step": bytes_per_step, "ms_per_step": rec["ms_per_step"], "achieved": step_gbs,
         "frac": step_gbs / HBM_PEAK_GBS / world, "floor_ms_per_step": bytes_per_step / (HBM_PEAK_GBS * 1e9 * world) * 1e3,
         "counted": "every kernel's algorithmic bytes (vectors once per row read or written, stored operators per entry)"}
+    rec["projection"] = sim.ctx.proj_info()  # re-seeds, guess-monitor restarts, last guess residuals
     rec["kernels"] = ktab
     rec["kernels_timed_steps"] = f"the last {kt_steps} of the {a.steps} timed steps" if kt_steps else None
     rec["kernel_batch"] = batch
@@ -361,6 +362,7 @@ def steady_leg(sim, done, after, steps, barrier, allmax, allsum, world):
     n1, b1 = sim.ctx.counters()
     ms = 1e3 * el / steps
     return {"after_steps": max(after, done), "steps": steps, "steps_per_s": steps / el, "ms_per_step": ms,
+            "projection": sim.ctx.proj_info(),
             "launches_per_step": (n1 - n0) / steps,
             "step_roofline_frac": allsum(b1 - b0) / steps / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9 * world),
             "cg_iters_per_step": {"visc": [s.it_visc for s in st], "p": [s.it_p for s in st],

@@ -300,6 +300,11 @@ int pucfem_visc_interval(void* ctx, double* out2);
    quotient (0: estimated on the host), the host 30-step power iteration's quotient on the level's fp64
    operator (computed by this call), the host Gershgorin bound]; lmax = min(Gershgorin, 1.1 x quotient). */
 int pucfem_mg_lmax(void* ctx, int32_t level, double* out4);
+/* The pressure solves' projected initial guesses (successive right-hand sides, pucfem_params.proj_k; the solves
+   replace np.linalg.solve at StokesColor.py:555,569): out4 = [bases re-seeded so far, bases restarted by the guess
+   monitor (a projected guess > 50x worse than the best of its basis' last 8), the last projected guess's relative residual
+   |b - A x0| / |b| of basis 1 and of basis 2 (0: none yet)]. */
+int pucfem_proj_info(void* ctx, double* out4);
 
 /* ---- host-only (no device needed) ---------------------------------------------------- */
 /* Red refinement, `levels` times.  Call with xy_out == NULL to get sizes. */

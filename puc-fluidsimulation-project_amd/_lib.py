@@ -83,6 +83,7 @@ SIGNATURES = {
     "pucfem_comm_info": ([_P, ct.POINTER(ct.c_int64)], ct.c_int),
     "pucfem_visc_interval": ([_P, ct.POINTER(ct.c_double)], ct.c_int),
     "pucfem_mg_lmax": ([_P, ct.c_int32, _D], ct.c_int),
+    "pucfem_proj_info": ([_P, _D], ct.c_int),
     "pucfem_tracer_step": ([_P, _D, ct.c_double, ct.c_int32], ct.c_int),
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
     "pucfem_mixing_index_w": ([_P, _D, _D, _D], ct.c_int),

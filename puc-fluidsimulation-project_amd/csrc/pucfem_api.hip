@@ -698,8 +698,12 @@ struct Ctx {
   int nb_mg(i64 nslices) const { return (int)std::max<i64>(1, std::min<i64>(mg_nb_max, (nslices + 3) / 4)); }
   int nb_rows(i64 n) const { return nb_for((n + 63) / 64); }
   // semi-Lagrangian grid: latency-bound gathers want more waves in flight than MAXB blocks give
-  static int nb_sl(i64 n) {
-    return (int)std::max<i64>(1, std::min<i64>(SLB, (n + 4 * 64 - 1) / (4 * 64)));
+  // PUCFEM_SL_BLOCKS (measurement knob): a cap on k_sl's grid below SLB (fewer resident waves beside the main
+  // stream's kernels; the rows per block grow, the per-wave queue follows them)
+  int sl_cap = std::getenv("PUCFEM_SL_BLOCKS") ? std::max(8, std::min(SLB, std::atoi(std::getenv("PUCFEM_SL_BLOCKS"))))
+                                               : SLB;
+  int nb_sl(i64 n) const {
+    return (int)std::max<i64>(1, std::min<i64>(sl_cap, (n + 4 * 64 - 1) / (4 * 64)));
   }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
@@ -1616,6 +1620,43 @@ struct Ctx {
   // PUCFEM_PROJ_SPMV=1 (diagnostic knob): the projection update's A v by an SpMV of v = y - x0 instead of the
   // CG's residuals r0 - r_final (no pending directions)
   bool proj_spmv = std::getenv("PUCFEM_PROJ_SPMV") && std::atoi(std::getenv("PUCFEM_PROJ_SPMV")) != 0;
+  // the PCG's initial <r, r> and <b, b> beside the control word (k_conv / k_reduce_conv write them at iteration
+  // 0; pcg_mg's control reads bring them along): the projected guess's quality, h_note() after a solve
+  double* ctl_note() const { return reinterpret_cast<double*>(ctl + 2); }
+  double guess_rel() const {
+    const double* h = reinterpret_cast<const double*>(h_ctl + 2);
+    return h[1] > 0.0 ? std::sqrt(h[0] / h[1]) : 0.0;
+  }
+  // Guess monitor (round 5).  A projection basis whose A-orthonormality has decayed (rounding of the fp32 basis
+  // through repeated re-seeds; with 12 directions, re-seeded every solve, steady L7 steps went from 0-1 to 5
+  // iterations per solve, r11g) gives guesses orders of magnitude worse than the last ones while the flow
+  // changes smoothly; the decay builds up over a few solves (r11h: 5e-8 -> 1e-4 of b in ~4 solves).  When a
+  // projected guess's relative residual exceeds 50x the best of the last 8 projected guesses of its basis (and
+  // 10x the tolerance), the basis restarts from the next solution (Fischer's restart).  Healthy steady guesses
+  // spread over ~10x (2.6e-8 .. 2.9e-7 at L7, r11e); in the start-up transient they fall step by step.
+  static constexpr int GUESS_HIST = 8;
+  double guess_last[5] = {0, 0, 0, 0, 0};
+  double guess_hist[5][GUESS_HIST] = {};
+  int guess_n[5] = {0, 0, 0, 0, 0};
+  int64_t n_restart = 0;
+  bool guess_decayed(int slot, double g) {
+    double best = 0.0;
+    const int k = std::min(guess_n[slot], GUESS_HIST);
+    for (int i = 0; i < k; ++i) best = i == 0 ? guess_hist[slot][i] : std::min(best, guess_hist[slot][i]);
+    guess_hist[slot][guess_n[slot] % GUESS_HIST] = g;
+    ++guess_n[slot];
+    guess_last[slot] = g;
+    return k > 0 && g > 50.0 * best && g > 10.0 * prm.rtol_pres;
+  }
+  void proj_restart(int slot) {
+    proj_m[slot] = 0;
+    proj_pend[slot] = false;
+    pend_otf[slot] = false;
+    pend_acc[slot] = false;
+    proj_hist[slot] = ProjHist{};
+    guess_n[slot] = 0;
+    ++n_restart;
+  }
   bool proj_shared = false;  // prm.proj_shared (PUCFEM_PROJ_SHARED=0/1 overrides it: a measurement knob)
   int proj_slot(int which) const { return proj_shared && which == 2 ? 1 : which; }
   int pcg_mg(double* y, const double* b, double tol, int maxit, int which) {
@@ -1662,7 +1703,7 @@ struct Ctx {
       rr = reduce_global(part_a, nb, 1, false, 0);
       if (merged_conv) {
         hipLaunchKernelGGL(k_reduce_conv, dim3(1), dim3(RB), 0, st, (const double*)part_b, nb, MAXB, redbuf + 8,
-                           (const double*)rr.p, (const double*)(redbuf + 8), tol2, ctl, 0);
+                           (const double*)rr.p, (const double*)(redbuf + 8), tol2, ctl, 0, ctl_note());
         KCHK();
       } else {
         bb = reduce_global(part_b, nb, 1, false, 1);
@@ -1673,7 +1714,7 @@ struct Ctx {
     std::vector<std::pair<int, size_t>> marks;
     std::vector<std::pair<int, ByteMark>> bmarks;  // (iteration, the byte counters at its start) of the current chunk
     if (!merged_conv) {
-      hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1);
+      hipLaunchKernelGGL(k_conv, dim3(1), dim3(64), 0, st, rr.p, bb.p, tol2, ctl, 0, 1, ctl_note());
       KCHK();
     }
     // direction: z (4 B in the fp32 cycle) and p_old gathered once, p and q written
@@ -1698,7 +1739,7 @@ struct Ctx {
     bool done0 = false;
     const bool eligible = seen && last_it[which] <= 1;
     if (eligible && __builtin_popcount(zero_hist[which] & 0xffu) >= 2) {
-      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
       sync_st();
       done0 = h_ctl[0] != 0;
     }
@@ -1748,7 +1789,7 @@ struct Ctx {
         std::swap(v.po[0], v.pn[0]);
         if (pcg_trace) trace_pcg(which, it + 1);
       }
-      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
       // the samples before this chunk, while the GPU runs it (this chunk's stay pending until its test is read)
       if (timer.on && !marks.empty()) timer.flush_ready(marks.front().second);
       sync_st();
@@ -1928,6 +1969,7 @@ struct Ctx {
         } else {
           project_update(slot, yst, bh, cg_r[0], pout);
         }
+        if (projected && guess_decayed(slot, guess_rel())) proj_restart(slot);
       }
     } else {
       double* y[1] = {yst};
@@ -3654,7 +3696,7 @@ void build(Ctx& c) {
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
   }
   c.scal = c.dalloc<double>(32);
-  c.ctl = c.dalloc<int>(4);
+  c.ctl = c.dalloc<int>(8);  // [0..1] the control word, bytes 8..23: the PCG's initial <r, r>, <b, b> (k_conv's note)
   c.redbuf = c.dalloc<double>(8 * 64);
   c.dcnt = c.dalloc<unsigned>(Ctx::CNT_N);
   c.vals = c.dalloc<double>(16);
@@ -3830,7 +3872,7 @@ int pucfem_ctx_create(int32_t device, void** out) {
     if (!c->host_only) {
       HIPCHK(hipSetDevice(device));
       HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-      HIPCHK(hipHostMalloc((void**)&c->h_ctl, 4 * sizeof(int), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_coef, 5 * Ctx::NCOEF * sizeof(double), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64 * sizeof(double), hipHostMallocDefault));
     }
@@ -4763,6 +4805,17 @@ int pucfem_mg_lmax(void* ctx, int32_t level, double* o) {
     o[3] = lmax_estimate(A, false);
     lmax_estimate(A, true, nullptr, &lam);
     o[2] = lam;
+  });
+}
+
+int pucfem_proj_info(void* ctx, double* o) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_built();
+    o[0] = (double)c.n_reseed;
+    o[1] = (double)c.n_restart;
+    o[2] = c.guess_last[1];
+    o[3] = c.guess_last[2];
   });
 }
 

@@ -1269,7 +1269,13 @@ __global__ void k_cgr_ctl(const double* rr, const double* bb, double tol2, int* 
 // for every right-hand side c < nr, so the host's check after an iteration sees it (and a V-cycle
 // or direction kernel launched after it returns at once).  k_cg_dir would find the same at
 // iteration it; a NaN is left to it.
-__global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl, int it, int nr) {
+// note (optional): rr[0] and bb[0] copied there (the PCG's initial residual, read with the control word)
+__global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl, int it, int nr,
+                       double* note = nullptr) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && note) {
+    note[0] = rr[0];
+    note[1] = bb[0];
+  }
   if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[0] == 0) {
     bool conv = true;
     for (int c = 0; c < nr; ++c) conv = conv && rr[c] <= tol2 * bb[c];
@@ -2756,7 +2762,7 @@ __global__ __launch_bounds__(RB) void k_reduce_t(const double* part, int nb, int
 // reduction of <r, r> and its convergence test in one launch (single rank: no all-reduce in between)
 __global__ __launch_bounds__(RB) void k_reduce_conv(const double* part, int nb, int stride, double* out,
                                                     const double* rr, const double* bb, double tol2, int* ctl,
-                                                    int it) {
+                                                    int it, double* note = nullptr) {
   __shared__ double sh[RB / 64];
   double a[RU];
 #pragma unroll
@@ -2778,6 +2784,10 @@ __global__ __launch_bounds__(RB) void k_reduce_conv(const double* part, int nb, 
     double y = sh[0];
     for (int w = 1; w < RB / 64; ++w) y += sh[w];
     out[0] = y;
+    if (note) {  // (k_conv's note)
+      note[0] = rr[0];
+      note[1] = bb[0];
+    }
     if (ctl[0] == 0 && rr[0] <= tol2 * bb[0]) {  // k_conv
       ctl[0] = 1;
       ctl[1] = it;

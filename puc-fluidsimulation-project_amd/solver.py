@@ -253,6 +253,12 @@ class Context:
         self._c(self.L.pucfem_mg_lmax(self.h, int(level), o))
         return dict(lmax=o[0], lam_device=o[1], lam_host=o[2], gershgorin=o[3])
 
+    def proj_info(self):
+        """Projected pressure guesses (pucfem_proj_info): re-seeds, monitor restarts, last guess residuals."""
+        o = (ct.c_double * 4)()
+        self._c(self.L.pucfem_proj_info(self.h, o))
+        return dict(reseeds=int(o[0]), restarts=int(o[1]), guess_rel=(o[2], o[3]))
+
     def comm_info(self):
         """Multi-rank data flow of the last step (pucfem_comm_info)."""
         o = (ct.c_int64 * 4)()
