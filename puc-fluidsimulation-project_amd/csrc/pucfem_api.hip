@@ -1587,14 +1587,23 @@ struct Ctx {
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
-  void precondition() {
+  void precondition(double* rz_part = nullptr) {
+    if (!rz_part) rz_part = part_d + 2 * MAXB;
     if (mg_single) {
-      vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], part_d + 2 * MAXB);
+      vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], rz_part);
     } else {
       halo(cg_r[0]);
-      vcycle<double, double>((int)mg.size() - 1, cg_r[0], cg_r[0], part_d + 2 * MAXB);
+      vcycle<double, double>((int)mg.size() - 1, cg_r[0], cg_r[0], rz_part);
     }
   }
+  // Chronopoulos-Gear PCG (k_cgcg_*): the multi-rank pressure solves, one all-reduce per iteration instead of three;
+  // PUCFEM_CGCG=1 / 0 forces it on / off (measurement and test knob: the single-rank path keeps the standard form,
+  // 24 B/row less per iteration)
+  int cgcg_env = std::getenv("PUCFEM_CGCG") ? std::atoi(std::getenv("PUCFEM_CGCG")) : -1;
+  bool use_cgcg() const { return cgcg_env >= 0 ? cgcg_env != 0 : dist(); }
+  double* part_cc = nullptr;  // CGCG_NV x MAXB partials
+  double* cgcg_sc = nullptr;  // k_cgcg_coef's scalars (8)
+  int64_t cgcg_iters = 0;     // iterations run in the single-reduction form (pucfem_comm_info)
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
   // prm.proj_shared: both pressure solves of a step project onto ONE basis (the same merged operator, so
   // one A-orthonormal basis serves both) that collects the solutions of both -- slot 1 for both; else a
@@ -1721,6 +1730,14 @@ struct Ctx {
     const double bytes_dir = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
                              (mg_single ? 28.0 : 32.0) * (double)n;
     const double bytes_upd = (48.0 + (mg_single ? 4.0 : 0.0)) * (double)n;  // + the fp32 r copy
+    // the single-reduction form: w = A z (z gathered once, r and s_old read, w written), the update (z, w, p, s,
+    // y, r read; p, s, y, r written; the fp32 r copy, the accumulated correction)
+    const bool cgcg = use_cgcg();
+    const double zb = mg_single ? 4.0 : 8.0;
+    const double bytes_w = (8.0 + dPp.idx_bytes()) * (double)dPp.nnz + dPp.row_bytes() * (double)dPp.nrows +
+                           (zb + 24.0) * (double)n;
+    const double bytes_cu = (zb + 72.0 + (mg_single ? 4.0 : 0.0) + (cg_vacc ? 16.0 : 0.0)) * (double)n;
+    const double* rho0 = rr.p;  // the initial <r, r> (k_cgcg_coef's rho at iteration 0)
     int it = 0;
     // an iteration = V-cycle, direction, update, convergence test (k_conv): the host checks right
     // after a test, so a solve that converges at a check launches no V-cycle after it.  The first
@@ -1749,6 +1766,40 @@ struct Ctx {
       for (int k = 0; k < chunk; ++k, ++it) {
         marks.push_back({it, timer.mark()});  // this iteration's V-cycle works iff not converged at it
         bmarks.push_back({it, bmark_now()});
+        if (cgcg) {  // single-reduction iteration (k_cgcg_*)
+          ++cgcg_iters;
+          precondition(part_cc + 3 * MAXB);
+          if (mg_single) mg_halo(mg.back(), z32);
+          else halo(z);
+          with_c16(dPp, [&](auto c16) {
+            if (mg_single)
+              klaunch(1, bytes_w, k_cgcg_w<decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
+                      (const double*)dKp_raw, (const double*)nullptr, (const float*)z32, (const double*)cg_r[0],
+                      it > 0 ? (const double*)cg_q[0] : (const double*)nullptr, cg_pb[0], part_cc, (const int*)ctl);
+            else
+              klaunch(1, bytes_w, k_cgcg_w<decltype(c16)::value, false>, dim3(nb), dim3(BS), dPp.view(), fc,
+                      (const double*)dKp_raw, (const double*)z, (const float*)nullptr, (const double*)cg_r[0],
+                      it > 0 ? (const double*)cg_q[0] : (const double*)nullptr, cg_pb[0], part_cc, (const int*)ctl);
+          });
+          KCHK();
+          launch_reduce(part_cc, nb, MAXB, CGCG_NV, false, redbuf + 64);
+          KCHK();
+          if (dist()) comm->allreduce(redbuf + 64, CGCG_NV, false, st);
+          hipLaunchKernelGGL(k_cgcg_coef, dim3(1), dim3(64), 0, st, (const double*)(redbuf + 64), (const double*)bb.p,
+                             cgcg_sc, tol2, ctl, it, maxit, (const double*)rho0);
+          KCHK();
+          if (mg_single)
+            klaunch(2, bytes_cu, k_cgcg_upd<true>, dim3(nb), dim3(BS), (int64_t)n, (const double*)nullptr,
+                    (const float*)z32, (const double*)cg_pb[0], cg_pa[0], cg_q[0], y, cg_r[0], r32o, cg_vacc,
+                    (const double*)cgcg_sc, (const int*)ctl, it, part_cc);
+          else
+            klaunch(2, bytes_cu, k_cgcg_upd<false>, dim3(nb), dim3(BS), (int64_t)n, (const double*)z,
+                    (const float*)nullptr, (const double*)cg_pb[0], cg_pa[0], cg_q[0], y, cg_r[0], r32o, cg_vacc,
+                    (const double*)cgcg_sc, (const int*)ctl, it, part_cc);
+          KCHK();
+          if (pcg_trace) trace_pcg(which, it + 1);
+          continue;
+        }
         ro_rz = ro(redbuf + 32, CNT_RZ, 1);
         precondition();
         ro_rz = RedOut{};
@@ -3696,6 +3747,8 @@ void build(Ctx& c) {
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
   }
   c.scal = c.dalloc<double>(32);
+  c.part_cc = c.dalloc<double>(CGCG_NV * MAXB);
+  c.cgcg_sc = c.dalloc<double>(8);
   c.ctl = c.dalloc<int>(8);  // [0..1] the control word, bytes 8..23: the PCG's initial <r, r>, <b, b> (k_conv's note)
   c.redbuf = c.dalloc<double>(8 * 64);
   c.dcnt = c.dalloc<unsigned>(Ctx::CNT_N);

@@ -541,6 +541,188 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
   red_finish(ro, part_rr, sh);
 }
 
+// ----------------------------------------------------------------------------- single-reduction PCG
+// Chronopoulos-Gear PCG (one all-reduce per iteration, the multi-rank pressure solves; PUCFEM_CGCG=1 forces it on
+// one rank).  Iteration i, from r_i, p_(i-1), s_(i-1) = A p_(i-1):
+//   z_i = M r_i (the V-cycle; its last smoothing step writes the <r_i, z_i> partials),  w_i = A z_i  (k_cgcg_w),
+//   ONE reduction of the 8 values [rho_i, <r_i, s_(i-1)>, <s_(i-1), s_(i-1)>  (k_cgcg_upd of iteration i-1, exact),
+//                                  gamma_i = <r_i, z_i>, delta_i = <w_i, z_i>, <r_i, w_i>, <w_i, w_i>, <w_i, s_(i-1)>]
+//   beta = gamma_i / gamma_(i-1), alpha = gamma_i / (delta_i - beta gamma_i / alpha_(i-1))      (k_cgcg_coef),
+//   p_i = z_i + beta p_(i-1), s_i = w_i + beta s_(i-1), y += alpha p_i, r_(i+1) = r_i - alpha s_i  (k_cgcg_upd).
+// The convergence test of r_(i+1) comes from the same reduction: rho_(i+1) = rho_i - 2 alpha <r_i, s_i> +
+// alpha^2 <s_i, s_i>, with <r_i, s_i> = <r_i, w_i> + beta <r_i, s_(i-1)> and <s_i, s_i> = <w_i, w_i> +
+// 2 beta <w_i, s_(i-1)> + beta^2 <s_(i-1), s_(i-1)> -- exact dots, one step of recurrence (relative error
+// ~eps rho_i / rho_(i+1)); rho_i itself is the exact lagged value.  Per iteration against the three reductions of
+// the standard form: one all-reduce instead of three, 24 B/row more (s, w).
+// Partial layout: value v at part[v * MAXB + block], one grid (nb blocks) for all producers.
+constexpr int CGCG_NV = 8;
+template <bool C16, bool ZF>
+__global__ LB_GATHER void k_cgcg_w(SellDev A, FaceDev fc, const double* __restrict__ val, const double* __restrict__ z,
+                                   const float* __restrict__ zf, const double* __restrict__ r,
+                                   const double* __restrict__ s_old, double* __restrict__ w, double* part,
+                                   const int* ctl) {
+  __shared__ double sh[4];
+  if (ctl[0]) return;
+  auto zg = [&](int64_t j) -> double {
+    if constexpr (ZF) return (double)zf[j];
+    else return z[j];
+  };
+  double d[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // delta, <r, w>, <w, w>, <w, s_old>
+  auto finish = [&](int64_t row, double q) {
+    stnt(w + row, q);
+    d[0] += zg(row) * q;
+    d[1] += r[row] * q;
+    d[2] += q * q;
+    if (s_old) d[3] += q * s_old[row];
+  };
+  const BlockRole role = block_role(fc.nb);
+  if (role.face) {
+    constexpr int K = face_k(PUCFEM_DIR_K1);
+    face_rows_k<K>(fc, role.idx, fc.nb,
+                   [&](const lat::FaceTab& F, int32_t lf, const int32_t (&t)[K], const int32_t (&i)[K],
+                       const int32_t (&j)[K], const bool (&ok)[K]) {
+      int32_t nb[K][6];
+      bool in[K][6];
+#pragma unroll
+      for (int q = 0; q < K; ++q) lat::neighbours(F, fc.n, t[q], i[q], j[q], nb[q], in[q]);
+      double a[K][7];
+#pragma unroll
+      for (int q = 0; q < K; ++q) face_kcoefs(fc, lf, nb[q], in[q], a[q]);
+      double zv[K][7];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        zv[q][6] = zg(F.base + t[q]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) zv[q][k] = zg(nb[q][k]);
+      }
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        if (!ok[q]) continue;
+        double acc = a[q][0] * zv[q][6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) acc += a[q][1 + k] * zv[q][k];
+        finish(F.base + t[q], acc);
+      }
+    });
+  } else {
+    int64_t s0, s1;
+    block_slices_n(A.nslices, role.nsk, role.idx, s0, s1);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    for (int64_t sl = s0 + wv; sl < s1; sl += 4) {
+      const int64_t off = A.off[sl];
+      const int wd = A.w[sl];
+      const int64_t row = sell_row(A, sl, lane);
+      const int32_t base = (int32_t)(sl * 64);
+      double acc = 0.0;
+      by_width(wd, [&](auto wc) {
+        constexpr int WN = decltype(wc)::value;
+        if constexpr (WN > 0) {
+          int32_t cj[WN];
+          double av[WN];
+#pragma unroll
+          for (int k = 0; k < WN; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            cj[k] = sell_col<C16, false>(A, e, base);
+            av[k] = val[e];
+          }
+#pragma unroll
+          for (int k = 0; k < WN; ++k) acc += av[k] * zg(cj[k]);
+        } else {
+          for (int k = 0; k < wd; ++k) {
+            const int64_t e = off + (int64_t)k * 64 + lane;
+            acc += val[e] * zg(sell_col<C16, false>(A, e, base));
+          }
+        }
+      });
+      if (row >= 0) finish(row, acc);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const double t = block_sum(d[v], sh);
+    if (threadIdx.x == 0) part[(4 + v) * MAXB + blockIdx.x] = t;
+  }
+}
+
+// the scalars of iteration `it` from the 8 reduced values (red8; bb: <b, b>); state sc: [0] alpha_it, [1] beta_it,
+// [2] gamma_it, [3] alpha_(it-1), [4] gamma_(it-1).  ctl: {1, it} when rho_it passes (no update), {1, it + 1} when
+// the recurrence rho_(it+1) passes (the update of `it` completes the solve), {3, it} not finite, {2, it} maxit
+__global__ void k_cgcg_coef(const double* __restrict__ red8, const double* __restrict__ bb, double* sc, double tol2,
+                            int* ctl, int it, int maxit, const double* rho0) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || ctl[0]) return;
+  const double rho = it == 0 ? rho0[0] : red8[0];
+  const double rs_old = it == 0 ? 0.0 : red8[1], ss_old = it == 0 ? 0.0 : red8[2];
+  const double gamma = red8[3], delta = red8[4], rw = red8[5], ww = red8[6], ws = it == 0 ? 0.0 : red8[7];
+  const double b2 = bb[0];
+  if (!isfinite(rho) || !isfinite(gamma) || !isfinite(delta)) {
+    ctl[0] = 3;
+    ctl[1] = it;
+    return;
+  }
+  if (rho <= tol2 * b2) {
+    ctl[0] = 1;
+    ctl[1] = it;
+    return;
+  }
+  if (it >= maxit) {
+    ctl[0] = 2;
+    ctl[1] = it;
+    return;
+  }
+  const double beta = it == 0 ? 0.0 : gamma / sc[4];
+  const double alpha = it == 0 ? gamma / delta : gamma / (delta - beta * gamma / sc[3]);
+  const double rs = rw + beta * rs_old, ss = ww + 2.0 * beta * ws + beta * beta * ss_old;
+  const double rho1 = rho - 2.0 * alpha * rs + alpha * alpha * ss;
+  sc[0] = alpha;
+  sc[1] = beta;
+  sc[3] = alpha;
+  sc[4] = gamma;
+  if (rho1 <= tol2 * b2) {
+    ctl[0] = 1;
+    ctl[1] = it + 1;
+  }
+}
+
+// the update of iteration `it` (skipped when the solve converged before it); partials of rho_(it+1),
+// <r_(it+1), s_it>, <s_it, s_it> into values 0..2 of part (the next iteration's exact lagged values)
+template <bool ZF>
+__global__ __launch_bounds__(BS) void k_cgcg_upd(int64_t n, const double* __restrict__ z, const float* __restrict__ zf,
+                                                 const double* __restrict__ w, double* __restrict__ p,
+                                                 double* __restrict__ s, double* __restrict__ y, double* __restrict__ r,
+                                                 float* __restrict__ r32, double* __restrict__ vacc,
+                                                 const double* __restrict__ sc, const int* ctl, int it, double* part) {
+  __shared__ double sh[4];
+  if (ctl[0] && ctl[1] <= it) return;
+  const double alpha = sc[0], beta = sc[1];
+  const bool first = it == 0;
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
+    double zi;
+    if constexpr (ZF) zi = (double)zf[i];
+    else zi = z[i];
+    const double pi = zi + (first ? 0.0 : beta * p[i]);
+    const double si = w[i] + (first ? 0.0 : beta * s[i]);
+    stnt(p + i, pi);
+    stnt(s + i, si);
+    stnt(y + i, y[i] + alpha * pi);
+    if (vacc) stnt(vacc + i, vacc[i] + alpha * pi);
+    const double rn = r[i] - alpha * si;
+    stnt(r + i, rn);
+    if (r32) stnt(r32 + i, (float)rn);
+    d0 += rn * rn;
+    d1 += rn * si;
+    d2 += si * si;
+  }
+  const double t0 = block_sum(d0, sh), t1 = block_sum(d1, sh), t2 = block_sum(d2, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = t0;
+    part[MAXB + blockIdx.x] = t1;
+    part[2 * MAXB + blockIdx.x] = t2;
+  }
+}
+
 // ----------------------------------------------------------------------------- solution projection
 // Successive right-hand sides (Fischer 1998): the pressure solves of consecutive steps keep an
 // A-orthonormal basis X of their recent solution directions; the initial guess is the A-orthogonal

@@ -496,3 +496,21 @@ def test_projection_basis_holds_below_the_guess_floor_L7():
     print(f"L7 steps 100-119 at rtol 5e-8: {its} pressure iterations over 40 solves")
     assert its <= 80, [(s.it_p, s.it_p2) for s in st]
     sim.close()
+
+
+@pytest.mark.parametrize("refine", [3, 5])
+def test_single_reduction_pcg_matches_standard(monkeypatch, refine):
+    """The Chronopoulos-Gear form of the pressure PCG (one all-reduce per iteration: the multi-rank solves of
+    StokesColor.py:555,569) forced on one rank solves the same systems as the standard form: 12 production steps
+    agree to the solves' tolerance and take the same iteration counts up to one per solve."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    a = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.setenv("PUCFEM_CGCG", "1")
+    b = stokes(mesh, tol=S.Tolerances.production())
+    sa, sb = a.step(12), b.step(12)
+    assert np.abs(a.u - b.u).max() < 1e-7
+    assert np.abs(a.c - b.c).max() < 1e-6
+    for x, y in zip(sa, sb):
+        assert abs(x.it_p - y.it_p) <= 1 and abs(x.it_p2 - y.it_p2) <= 1, (x.it_p, x.it_p2, y.it_p, y.it_p2)
+    a.close()
+    b.close()

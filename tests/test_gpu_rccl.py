@@ -40,16 +40,18 @@ def unique_id():
 
 
 @pytest.mark.timeout(300)
-def test_rccl_one_rank_selftest_and_steps():
+def test_rccl_one_rank_selftest_and_steps(monkeypatch):
     """RCCL communicator of one rank: the all-reduce / ring send-recv self-test on the library stream,
     then 6 StokesColor steps on L3 at the production settings through the multi-rank code path, equal
-    to the plain single-rank run."""
+    to the plain single-rank run in the same PCG form (the multi-rank pressure solves run the single-reduction
+    Chronopoulos-Gear PCG: PUCFEM_CGCG=1 puts the reference run on it)."""
     mesh = pf.load_mesh("fine", refine=3)
     tol = S.Tolerances.production()
     sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol, dist=(0, 1, unique_id()))
     assert sim.ctx.comm_info()["backend"] == "rccl"
     t = sim.ctx.comm_selftest()
     assert t["backend"] == "rccl" and t["sum_err"] == 0 and t["max_err"] == 0 and t["recv_err"] == 0, t
+    monkeypatch.setenv("PUCFEM_CGCG", "1")
     ref = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, tol)
     assert ref.ctx.comm_info()["backend"] is None
     for k in range(6):
@@ -63,12 +65,13 @@ def test_rccl_one_rank_selftest_and_steps():
 
 
 @pytest.mark.timeout(300)
-def test_rccl_one_rank_food_tracers():
+def test_rccl_one_rank_food_tracers(monkeypatch):
     """The StokesFood tracer exchange (one all-reduce of 3 x 488 values per step) through RCCL."""
     mesh = pf.load_mesh("fine", refine=2)
     tol = S.Tolerances.production()
     bc = S.SquirmerBC(B2=-5.0, nu=1.0)
     sim = S.StokesSimulation(mesh, bc, 0.01, "food", 0, tol, dist=(0, 1, unique_id()))
+    monkeypatch.setenv("PUCFEM_CGCG", "1")  # (the multi-rank PCG form)
     ref = S.StokesSimulation(mesh, bc, 0.01, "food", 0, tol)
     sa, sb = sim.step(5), ref.step(5)
     assert sim.ctx.comm_info()["tracer_allreduce_values"] == 3 * 488

@@ -45,6 +45,7 @@ for t in th:
     t.join()
 assert not errs, errs
 print(f"L{level} N={mesh.N} W={world} mg_rep_nodes={rep_nodes or 'default'}")
+pts = []
 for k in range(steps):
     h = [rows[r][k]["dye_halo_values"] for r in range(world)]
     a = [rows[r][k]["allgather_values"] for r in range(world)]
@@ -56,3 +57,14 @@ for k in range(steps):
           f"{mx['allreduce_calls']} all-reduces ({mx['allreduce_values']} values), {mx['sends']} sends "
           f"({mx['send_bytes'] / 1e6:.2f} MB), {mx['broadcasts']} broadcasts, {mx['groups']} groups, "
           f"{mx['launches']} kernel launches")
+    pts.append((rows[0][k]["its"][1] + rows[0][k]["its"][2], mx["allreduce_calls"], mx["groups"]))
+# per pressure PCG iteration: the slope over the steps (least squares of the counts against the iterations)
+import numpy as np  # noqa: E402
+
+it_, ar_, gr_ = (np.array(v, dtype=float) for v in zip(*pts))
+if len(pts) > 1 and np.ptp(it_) > 0:
+    A = np.stack([it_, np.ones_like(it_)], 1)
+    sa = np.linalg.lstsq(A, ar_, rcond=None)[0]
+    sg = np.linalg.lstsq(A, gr_, rcond=None)[0]
+    print(f"per pressure PCG iteration: {sa[0]:.2f} all-reduces, {sg[0]:.2f} grouped exchanges "
+          f"(per step outside the iterations: {sa[1]:.1f} all-reduces, {sg[1]:.1f} groups)")
