@@ -188,9 +188,9 @@ def main():
         for kid, nm in ((0, "k_cheb"), (1, "k_resid"), (2, "k_cg_dir"), (16 * 8, "k_cheb+8 coarse launches"),
                         (256, "k_cheb, idle GPU at each launch"), (3, "k_cheb face rows only"),
                         (4, "k_cheb skeleton (SELL) rows only"), (5, "k_cg_dir face rows only"),
-                        (6, "k_cg_dir skeleton (SELL) rows only"), (7, "k_div (SoA u, as in the step)"),
+                        (6, "k_cg_dir skeleton (SELL) rows only"), (7, "k_div (as in the step: interleaved u)"),
                         (8, "k_div face rows only"), (9, "k_div skeleton (SELL) rows only"),
-                        (10, "k_div on interleaved (x, y) u"), (11, "k_div interleaved, face rows only"),
+                        (10, "k_div on a viscous (x, y) buffer"), (11, "k_div interleaved, face rows only"),
                         (12, "k_cheb_pair<1> (face rows)"), (13, "k_cheb_pair<2> (face rows)"),
                         (14, "k_vcheb_pair (face rows)")):
             mb, me, by = ct.c_double(), ct.c_double(), ct.c_double()

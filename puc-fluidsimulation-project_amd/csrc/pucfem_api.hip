@@ -1867,18 +1867,23 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ building blocks of the step
-  void bc(double* a, double* b) {  // makePerBCU + makeDirBCU on owned rows
+  // makePerBCU + makeDirBCU on owned rows: the interleaved velocity (a = its x components, b = a + 1), or with
+  // b null one plain vector (the heat / Poisson scalar)
+  void bc(double* a, double* b) {
+    const int vs = b ? VS : 1;
     if (ncopy == 0 && ndir == 0) return;
     const int nb = (int)std::min<i64>(1024, std::max<i64>(1, (ncopy + ndir + BS - 1) / BS));
     if (bc_gather && ncopy > 0) {
       hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcsrc,
-                         dbctmp, dir_ncomp, a, b);
+                         dbctmp, dir_ncomp, a, b, vs);
       KCHK();
     }
     hipLaunchKernelGGL(k_bc_apply, dim3(nb), dim3(BS), 0, st, ncopy, dcdst, dcsrc,
-                       bc_gather ? (const double*)dbctmp : nullptr, ndir, ddnode, ddval, dir_ncomp, a, b);
+                       bc_gather ? (const double*)dbctmp : nullptr, ndir, ddnode, ddval, dir_ncomp, a, b, vs);
     KCHK();
   }
+  // halo of the interleaved velocity u / u* (component pointers)
+  void halo_v(double* vx) { halo2(reinterpret_cast<dbl2*>(vx)); }
   // PUCFEM_VISC_FUSE_FIN=0 (measurement knob): k_visc_fin as its own launch after the solve
   bool visc_fuse_fin = !(std::getenv("PUCFEM_VISC_FUSE_FIN") && std::atoi(std::getenv("PUCFEM_VISC_FUSE_FIN")) == 0);
   int viscous(int& iters) {  // StokesColor.py:540-547
@@ -1950,7 +1955,7 @@ struct Ctx {
       } else {
         algo_bytes += 40.0 * (double)n;
         hipLaunchKernelGGL(k_cg_fin, dim3(grid_ew(n)), dim3(BS), 0, st, n, 2, dsv, yvx, yvy, usx, usy,
-                           (const int32_t*)nullptr);
+                           (const int32_t*)nullptr, VS);
       }
     }
     if (ext) {  // the new increment replaces the oldest: (d1, d2, d3) <- (new, d1, d2)
@@ -1962,7 +1967,7 @@ struct Ctx {
     }
     KCHK();
     bc(usx, usy);
-    halo(usx, usy);
+    halo_v(usx);
     return 0;
   }
   // grid of k_div (its partials: max |div|, sum braw)
@@ -1974,7 +1979,7 @@ struct Ctx {
       klaunch(11,
               (16.0 + dP.idx_bytes()) * (double)dP.nnz + dP.row_bytes() * (double)dP.nrows +
                   (16.0 + (out ? 8.0 : 0.0) + (rhs ? 8.0 : 0.0)) * (double)lp.n_own,
-              k_div<decltype(c16)::value>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
+              k_div<decltype(c16)::value, true>, dim3(div_grid()), dim3(BS), dP.view(), fc, (const double*)dGx,
               (const double*)dGy, ax, ay, (const double*)das1, out, (const double*)dmp, -(1.0 / prm.dt),
               rhs ? braw : (double*)nullptr, part ? part : part_d, r);
     });
@@ -2297,11 +2302,11 @@ struct Ctx {
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
     grad_proj(p_from_y ? yp : p, 0);
     bc(ux, uy);
-    halo(ux, uy);
+    halo_v(ux);
     const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
     const int itp2 = pressure(yp2, p2, 2, f2);
     grad_proj(p_from_y ? yp2 : p2, 1);
-    halo(ux, uy);
+    halo_v(ux);
     // single-rank explicit dye: the final-divergence record and the advection of this step (they read
     // the final u and c, write final_div, c_new and their own partials) run on a side stream,
     // overlapped with the next step's viscous solve and first pressure solve; the main stream waits
@@ -2482,11 +2487,11 @@ struct Ctx {
     if (ncopy > 0) {  // c[slave] = c[master] (good_visualization.py:715-716)
       if (bc_gather) {
         hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcsrc,
-                           dbctmp, 1, cout, cout);
+                           dbctmp, 1, cout, cout, 1);
         KCHK();
       }
       hipLaunchKernelGGL(k_bc_apply, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, st, ncopy, dcdst, dcsrc,
-                         bc_gather ? (const double*)dbctmp : nullptr, 0, ddnode, ddval, 1, cout, cout);
+                         bc_gather ? (const double*)dbctmp : nullptr, 0, ddnode, ddval, 1, cout, cout, 1);
       KCHK();
     }
     return it;
@@ -2503,13 +2508,15 @@ struct Ctx {
       // no replica of u: each rank interpolates the tracers in its own triangles from its owned and
       // ghost values (placed at their global ids), then one all-reduce of 3 x ntr values hands every
       // rank all the velocities (StokesFood's 488 tracers: ~12 KB per step instead of the whole u)
-      HIPCHK(hipMemcpyAsync(ufx + lp.r0, ux, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-      HIPCHK(hipMemcpyAsync(ufy + lp.r0, uy, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(k_unstride, dim3(grid_ew(lp.n_own)), dim3(BS), 0, st, lp.n_own, (const double*)ux, VS,
+                         ufx + lp.r0);
+      hipLaunchKernelGGL(k_unstride, dim3(grid_ew(lp.n_own)), dim3(BS), 0, st, lp.n_own, (const double*)uy, VS,
+                         ufy + lp.r0);
       if (lp.n_ghost > 0) {
         hipLaunchKernelGGL(k_scatter_ghosts, dim3(grid_ew(lp.n_ghost)), dim3(BS), 0, st, lp.n_ghost,
-                           (const int32_t*)dghost_global, (const double*)(ux + lp.n_own), ufx);
+                           (const int32_t*)dghost_global, (const double*)(ux + VS * lp.n_own), ufx, VS);
         hipLaunchKernelGGL(k_scatter_ghosts, dim3(grid_ew(lp.n_ghost)), dim3(BS), 0, st, lp.n_ghost,
-                           (const int32_t*)dghost_global, (const double*)(uy + lp.n_own), ufy);
+                           (const int32_t*)dghost_global, (const double*)(uy + VS * lp.n_own), ufy, VS);
       }
       hipLaunchKernelGGL(k_tracer_vel, dim3((ntr + BS - 1) / BS), dim3(BS), 0, st, MeshDev{mx, my, mtri, mesh.T},
                          tgrid, (const double*)ufx, (const double*)ufy, ntr, (const double*)trx, (const double*)try_,
@@ -3718,9 +3725,14 @@ void build(Ctx& c) {
   c.dsend = c.upload(lp.send_local);
   c.dsendbuf = c.dalloc<double>(2 * std::max<i64>(1, c.nsend));
   // fields + workspace
-  for (double** f : {&c.ux, &c.uy, &c.usx, &c.usy, &c.p, &c.p2, &c.yp, &c.yp2, &c.yvx, &c.yvy, &c.div_star,
-                     &c.div_u, &c.final_div, &c.braw, &c.bh, &c.bvx, &c.bvy, &c.scalar})
+  for (double** f : {&c.p, &c.p2, &c.yp, &c.yp2, &c.yvx, &c.yvy, &c.div_star, &c.div_u, &c.final_div, &c.braw,
+                     &c.bh, &c.bvx, &c.bvy, &c.scalar})
     *f = c.dalloc<double>(c.nloc);
+  // u and u*: interleaved (x, y) pairs (VS); ux / usx point at the pairs, uy / usy at their y components
+  c.ux = c.dalloc<double>(2 * c.nloc);
+  c.uy = c.ux + 1;
+  c.usx = c.dalloc<double>(2 * c.nloc);
+  c.usy = c.usx + 1;
   for (int q = 0; q < 2; ++q) {
     c.cg_r[q] = c.dalloc<double>(c.nloc);
     c.cg_pa[q] = c.dalloc<double>(c.nloc);
@@ -3881,7 +3893,7 @@ void build(Ctx& c) {
   // initial state: u = 0 then makeDirBCU (StokesColor.py:482-483); c = 1[x < 0.5] (:493-495)
   if (stokes) {
     c.bc(c.ux, c.uy);
-    c.halo(c.ux, c.uy);
+    c.halo_v(c.ux);
     HIPCHK(hipMemcpyAsync(c.c_full, slp.c0.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
   }
   HIPCHK(hipStreamSynchronize(c.st));
@@ -4089,17 +4101,17 @@ int pucfem_set_field(void* ctx, int32_t field, const double* buf, int64_t count)
     c.need_dev();
     c.need_built();
     const i64 N = c.mesh.N, no = c.lp.n_own;
-    auto own2 = [&](double* a, double* b) {
+    auto own2 = [&](double* a, double*) {  // (the interleaved velocity: a = its pairs)
       require(count == 2 * N, "field must be (N, 2)");
-      std::vector<double> x(no), y(no);
+      std::vector<double> xy(2 * no);
       for (i64 i = 0; i < no; ++i) {
         const i64 o = c.ord.new2old[c.lp.r0 + i];
-        x[i] = buf[2 * o];
-        y[i] = buf[2 * o + 1];
+        xy[2 * i] = buf[2 * o];
+        xy[2 * i + 1] = buf[2 * o + 1];
       }
-      HIPCHK(hipMemcpyAsync(a, x.data(), sizeof(double) * no, hipMemcpyHostToDevice, c.st));
-      HIPCHK(hipMemcpyAsync(b, y.data(), sizeof(double) * no, hipMemcpyHostToDevice, c.st));
-      c.halo(a, b);
+      HIPCHK(hipMemcpyAsync(a, xy.data(), sizeof(double) * 2 * no, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      c.halo_v(a);
     };
     auto own1 = [&](double* a) {
       require(count == N, "field must be (N,)");
@@ -4158,16 +4170,15 @@ int pucfem_get_field(void* ctx, int32_t field, double* buf, int64_t count) {
     c.need_dev();
     c.need_built();
     const i64 N = c.mesh.N, no = c.lp.n_own;
-    auto get2 = [&](const double* a, const double* b) {
+    auto get2 = [&](const double* a, const double*) {  // (the interleaved velocity)
       require(count == 2 * N, "field is (N, 2)");
-      std::vector<double> x(no), y(no);
-      HIPCHK(hipMemcpyAsync(x.data(), a, sizeof(double) * no, hipMemcpyDeviceToHost, c.st));
-      HIPCHK(hipMemcpyAsync(y.data(), b, sizeof(double) * no, hipMemcpyDeviceToHost, c.st));
+      std::vector<double> xy(2 * no);
+      HIPCHK(hipMemcpyAsync(xy.data(), a, sizeof(double) * 2 * no, hipMemcpyDeviceToHost, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
       for (i64 i = 0; i < no; ++i) {
         const i64 o = c.ord.new2old[c.lp.r0 + i];
-        buf[2 * o] = x[i];
-        buf[2 * o + 1] = y[i];
+        buf[2 * o] = xy[2 * i];
+        buf[2 * o + 1] = xy[2 * i + 1];
       }
     };
     auto get1 = [&](const double* a) {
@@ -4440,7 +4451,7 @@ int pucfem_apply(void* ctx, int32_t op, const double* x, double* y) {
       case PUCFEM_OP_DIV: {
         perm_in(x, 2, t0, t1);
         with_c16(c.dP, [&](auto c16) {
-          hipLaunchKernelGGL(k_div<decltype(c16)::value>, dim3(c.div_grid()), dim3(BS), 0, c.st, c.dP.view(),
+          hipLaunchKernelGGL((k_div<decltype(c16)::value, false>), dim3(c.div_grid()), dim3(BS), 0, c.st, c.dP.view(),
                              c.fK.part(), c.dGx, c.dGy, t0, t1, c.das1, o0, c.dmp, -1.0, (double*)nullptr, c.part_d, RedOut{});
         });
         KCHK();
@@ -4490,14 +4501,14 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
     double *s0 = c.solve_tmp, *s1 = s0 + c.nloc, *s2 = s1 + c.nloc, *s3 = s2 + c.nloc;
     if (op == PUCFEM_OP_VISC) {
       // rhs = b (as u^n, initial guess b): the viscous CG without BCs
-      std::vector<double> bx(N), by(N);
+      std::vector<double> bxy(2 * N);  // (k_visc_prep reads u interleaved: s0 / s0 + 1 over 2 N of scratch)
       for (i64 g = 0; g < N; ++g) {
-        bx[g] = b[2 * c.ord.new2old[g]];
-        by[g] = b[2 * c.ord.new2old[g] + 1];
+        bxy[2 * g] = b[2 * c.ord.new2old[g]];
+        bxy[2 * g + 1] = b[2 * c.ord.new2old[g] + 1];
       }
-      HIPCHK(hipMemcpyAsync(s0, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-      HIPCHK(hipMemcpyAsync(s1, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-      hipLaunchKernelGGL(k_visc_prep<false>, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s1,
+      HIPCHK(hipMemcpyAsync(s0, bxy.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice, c.st));
+      HIPCHK(hipStreamSynchronize(c.st));
+      hipLaunchKernelGGL(k_visc_prep<false>, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s0 + 1,
                          c.bvx, c.bvy, c.yvx, c.yvy, VincDev{});
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
@@ -4573,17 +4584,18 @@ int pucfem_sl_advect(void* ctx, const double* cin, const double* u, double dt, d
     c.need_built();
     require(!c.dist() && c.has_cgrid, "sl_advect needs a single-rank Stokes context");
     const i64 N = c.mesh.N;
-    std::vector<double> a(N), bx(N), by(N);
+    std::vector<double> a(N), bxy(2 * N);
     for (i64 g = 0; g < N; ++g) {
       const i64 o = c.ord.new2old[g];
       a[g] = cin[o];
-      bx[g] = u[2 * o];
-      by[g] = u[2 * o + 1];
+      bxy[2 * g] = u[2 * o];
+      bxy[2 * g + 1] = u[2 * o + 1];
     }
-    double *cf = c.litw[0] ? c.litw[0] : c.cg_pa[0], *cn = c.cg_pb[0], *tx = c.cg_q[0], *ty = c.cg_q[1];
+    // u as the step stores it (interleaved pairs) in scratch: the step's state stays untouched
+    if (!c.solve_tmp) c.solve_tmp = c.dalloc<double>(4 * c.nloc);
+    double *cf = c.litw[0] ? c.litw[0] : c.cg_pa[0], *cn = c.cg_pb[0], *tx = c.solve_tmp, *ty = tx + 1;
     HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(tx, bxy.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice, c.st));
     const int nb = c.nb_sl(N);
     c.sl_launch(nb, 0, N, tx, ty, dt, cf, cn, c.dwmix, c.dnotfound);
     KCHK();
@@ -4620,12 +4632,13 @@ int pucfem_apply_bc(void* ctx, int32_t which, double* u) {
     if (ncopy + ndir > 0) {
       if (c.bc_gather && ncopy > 0) {
         hipLaunchKernelGGL(k_bc_gather, dim3(std::min(1024, (ncopy + BS - 1) / BS)), dim3(BS), 0, c.st, ncopy,
-                           c.dcsrc, c.dbctmp, c.dir_ncomp, tx, ty);
+                           c.dcsrc, c.dbctmp, c.dir_ncomp, tx, ty, 1);
         KCHK();
       }
       const int nb = (int)std::min<i64>(1024, std::max<i64>(1, (ncopy + ndir + BS - 1) / BS));
       hipLaunchKernelGGL(k_bc_apply, dim3(nb), dim3(BS), 0, c.st, ncopy, c.dcdst, c.dcsrc,
-                         c.bc_gather ? (const double*)c.dbctmp : nullptr, ndir, c.ddnode, c.ddval, c.dir_ncomp, tx, ty);
+                         c.bc_gather ? (const double*)c.dbctmp : nullptr, ndir, c.ddnode, c.ddval, c.dir_ncomp, tx, ty,
+                         1);
       KCHK();
     }
     HIPCHK(hipMemcpyAsync(bx.data(), tx, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
@@ -4645,17 +4658,18 @@ int pucfem_dye_step(void* ctx, const double* cin, const double* u, double* cout,
     c.need_built();
     require(c.dye_impl, "dye_step needs a context built with dye_scheme = 1 (implicit)");
     const i64 N = c.mesh.N;
-    std::vector<double> a(N), bx(N), by(N);
+    std::vector<double> a(N), bxy(2 * N);
     for (i64 g = 0; g < N; ++g) {
       const i64 o = c.ord.new2old[g];
       a[g] = cin[o];
-      bx[g] = u[2 * o];
-      by[g] = u[2 * o + 1];
+      bxy[2 * g] = u[2 * o];
+      bxy[2 * g + 1] = u[2 * o + 1];
     }
-    double *tx = c.cg_q[0], *ty = c.cg_q[1], *cf = c.cg_pa[0], *cn = c.cg_pb[0], *dv = c.litw[8];
+    // u as the step stores it (interleaved pairs) in scratch: the step's state stays untouched
+    if (!c.solve_tmp) c.solve_tmp = c.dalloc<double>(4 * c.nloc);
+    double *tx = c.solve_tmp, *ty = tx + 1, *cf = c.cg_pa[0], *cn = c.cg_pb[0], *dv = c.litw[8];
     HIPCHK(hipMemcpyAsync(cf, a.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(tx, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(ty, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(tx, bxy.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice, c.st));
     c.div(tx, ty, dv, false);
     const int it = c.dye_step(tx, ty, dv, cf, cn);
     HIPCHK(hipMemcpyAsync(a.data(), cn, sizeof(double) * N, hipMemcpyDeviceToHost, c.st));
@@ -4673,13 +4687,12 @@ int pucfem_tracer_step(void* ctx, const double* u, double dt, int32_t nsteps) {
     require(!c.dist(), "tracer_step unit op is single-rank");
     require(c.has_tgrid, "tracer_step needs a STOKES_FOOD context (the tracer grid)");
     const i64 N = c.mesh.N;
-    std::vector<double> bx(N), by(N);
+    std::vector<double> bxy(2 * N);  // (u interleaved, as the step stores it)
     for (i64 g = 0; g < N; ++g) {
-      bx[g] = u[2 * c.ord.new2old[g]];
-      by[g] = u[2 * c.ord.new2old[g] + 1];
+      bxy[2 * g] = u[2 * c.ord.new2old[g]];
+      bxy[2 * g + 1] = u[2 * c.ord.new2old[g] + 1];
     }
-    HIPCHK(hipMemcpyAsync(c.ux, bx.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(c.uy, by.data(), sizeof(double) * N, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(c.ux, bxy.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice, c.st));
     for (int s = 0; s < nsteps; ++s) c.tracer_advance(dt);
     HIPCHK(hipStreamSynchronize(c.st));
   });
@@ -5339,7 +5352,7 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
                                     (double*)nullptr);
             }
             break;
-          case 7:   // k_div as in the step (SoA u, the pressure rhs, partials)
+          case 7:   // k_div as in the step (interleaved u, the pressure rhs, partials)
           case 8:   // its face part alone
           case 9:   // its SELL (skeleton) part alone
           case 10:  // k_div on interleaved (x, y) pairs
@@ -5351,8 +5364,8 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
               if (kernel == 8 || kernel == 11) dv.nslices = 0;
               const int g = kernel == 8 || kernel == 11 ? fd.nb + 8 : kernel == 9 ? c.div_grid() - fd.nb : c.div_grid();
               const FaceDev fk = kernel == 9 ? FaceDev{} : fd;
-              const bool aos = kernel >= 10;
-              const double* xa = aos ? reinterpret_cast<const double*>(c.vx2[0]) : (const double*)c.ux;
+              const bool aos = true;  // (the step's u is interleaved: 7-9 on u itself, 10-11 on a viscous buffer)
+              const double* xa = kernel >= 10 ? reinterpret_cast<const double*>(c.vx2[0]) : (const double*)c.ux;
               if (aos)
                 hipExtLaunchKernelGGL(k_div<D16, true>, dim3(g), dim3(BS), 0, c.st, a, e, 0, dv, fk, (const double*)c.dGx,
                                       (const double*)c.dGy, xa, (const double*)nullptr, (const double*)c.das1,

@@ -25,7 +25,10 @@ constexpr int BS = 256;     // threads per block
 constexpr int MAXB = 32768;
 constexpr int EWB = 8192;   // max blocks of a row-wise (SELL / elementwise) grid
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
-constexpr int SLB = 4096;   // max blocks (= partial stride) of the semi-Lagrangian kernel
+constexpr int SLB = 4096;
+// Velocity storage: u and u* are interleaved (x, y) pairs (one 16-B gather per neighbour in k_div, the tracers and
+// the dye weights); kernels take the component pointers ux = u2, uy = u2 + 1 and index them at VS * i
+constexpr int VS = 2;   // max blocks (= partial stride) of the semi-Lagrangian kernel
 #ifndef PUCFEM_FACE_RPT
 #define PUCFEM_FACE_RPT 4
 #endif

@@ -1153,10 +1153,9 @@ __global__ LB_GATHER void k_vcheb(SellDev A, FaceDev fc, const double* __restric
     if (fin) {
       const double s = v.s[row];
       const double a0 = s * (x0.x + dn0), a1 = s * (x0.y + dn1);
-      stnt(v.us[0] + row, a0);
-      stnt(v.us[1] + row, a1);
-      stnt(v.inc[0] + row, (float)(a0 - v.u[0][row]));
-      stnt(v.inc[1] + row, (float)(a1 - v.u[1][row]));
+      stnt(reinterpret_cast<dbl2*>(v.us[0]) + row, dbl2{a0, a1});  // (interleaved u*)
+      stnt(v.inc[0] + row, (float)(a0 - v.u[0][VS * row]));
+      stnt(v.inc[1] + row, (float)(a1 - v.u[1][VS * row]));
     } else {
       const flt2 dn = {(float)dn0, (float)dn1};
       const dbl2 xo = {x0.x + dn0, x0.y + dn1};
@@ -1418,10 +1417,9 @@ __global__ LB_GATHER void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, doub
       if (fin) {
         const double s = v.s[row];
         const double au0 = s * (xv[r][6].x + dn0), au1 = s * (xv[r][6].y + dn1);
-        stnt(v.us[0] + row, au0);
-        stnt(v.us[1] + row, au1);
-        stnt(v.inc[0] + row, (float)(au0 - v.u[0][row]));
-        stnt(v.inc[1] + row, (float)(au1 - v.u[1][row]));
+        stnt(reinterpret_cast<dbl2*>(v.us[0]) + row, dbl2{au0, au1});  // (interleaved u*)
+        stnt(v.inc[0] + row, (float)(au0 - v.u[0][VS * row]));
+        stnt(v.inc[1] + row, (float)(au1 - v.u[1][VS * row]));
       } else {
         stnt(v.dc + row, flt2{(float)dn0, (float)dn1});
         stnt(v.xc + row, dbl2{xv[r][6].x + dn0, xv[r][6].y + dn1});
@@ -1487,14 +1485,15 @@ __global__ void k_conv(const double* rr, const double* bb, double tol2, int* ctl
 }
 
 // x = S y; slaves (master_of >= 0) take their master's value (p_s = p_m).
+// (xs: the element stride of x0 / x1 -- VS when they are the interleaved velocity's components)
 __global__ void k_cg_fin(int64_t n, int nr, const double* __restrict__ s, const double* y0, const double* y1,
-                         double* x0, double* x1, const int32_t* __restrict__ master_of) {
+                         double* x0, double* x1, const int32_t* __restrict__ master_of, int xs = 1) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     int64_t j = i;
     if (master_of && master_of[i] >= 0) j = master_of[i];
     const double sj = s ? s[j] : 1.0;
-    x0[i] = sj * y0[j];
-    if (nr > 1) x1[i] = sj * y1[j];
+    x0[xs * i] = sj * y0[j];
+    if (nr > 1) x1[xs * i] = sj * y1[j];
   }
 }
 
@@ -1548,7 +1547,7 @@ __global__ void k_visc_prep(int64_t n, const double* __restrict__ s, const doubl
                             const double* ux, const double* uy, double* bx, double* by, double* yx, double* yy,
                             VincDev D) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-    const double a = ux[i] + 0.0, b = uy[i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
+    const double a = ux[VS * i] + 0.0, b = uy[VS * i] + 0.0;  // rhs = u + DT * b_force, b_force = 0
     double ga, gb;
     visc_start(D, i, a, b, ga, gb);
     if constexpr (AOS) {
@@ -1569,10 +1568,9 @@ __global__ void k_visc_fin_soa(int64_t n, const double* __restrict__ s, const do
                                float* __restrict__ dx, float* __restrict__ dy) {
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const double a = s[i] * yx[i], b = s[i] * yy[i];
-    stnt(usx + i, a);
-    stnt(usy + i, b);
-    stnt(dx + i, (float)(a - ux[i]));
-    stnt(dy + i, (float)(b - uy[i]));
+    stnt(reinterpret_cast<dbl2*>(usx) + i, dbl2{a, b});  // (usy = usx + 1: interleaved)
+    stnt(dx + i, (float)(a - ux[VS * i]));
+    stnt(dy + i, (float)(b - uy[VS * i]));
   }
 }
 // u* = S y (both components, y interleaved) and, with dx non-null, the increment u* - u for the next
@@ -1583,11 +1581,10 @@ __global__ void k_visc_fin(int64_t n, const double* __restrict__ s, const dbl2* 
   for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
     const dbl2 yi = y[i];
     const double a = s[i] * yi.x, b = s[i] * yi.y;
-    stnt(usx + i, a);
-    stnt(usy + i, b);
+    stnt(reinterpret_cast<dbl2*>(usx) + i, dbl2{a, b});  // (usy = usx + 1: interleaved)
     if (dx) {
-      stnt(dx + i, (float)(a - ux[i]));
-      stnt(dy + i, (float)(b - uy[i]));
+      stnt(dx + i, (float)(a - ux[VS * i]));
+      stnt(dy + i, (float)(b - uy[VS * i]));
     }
   }
 }
@@ -1745,8 +1742,8 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
                                                const double* __restrict__ as1, double dt,
                                                const uint8_t* __restrict__ dirflag, const double* usx,
                                                const double* usy, double* ux, double* uy) {
+  // (u, u* interleaved: bx / ux point at the pairs, by / uy are their y components)
   const double* bx = MODE == 0 ? usx : ux;
-  const double* by = MODE == 0 ? usy : uy;
   const BlockRole role = block_role(fc.nb);
   if (role.face) {
     // interior rows are never Dirichlet nodes
@@ -1763,8 +1760,9 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
         lat::neighbours(F, fc.n, t[r], i[r], j[r], nb, in);
 #pragma unroll
         for (int k = 0; k < 6; ++k) v[r][k] = p[nb[k]];
-        ox[r] = bx[F.base + t[r]];
-        oy[r] = by[F.base + t[r]];
+        const dbl2 o = reinterpret_cast<const dbl2*>(bx)[F.base + t[r]];
+        ox[r] = o.x;
+        oy[r] = o.y;
       }
       const double d = c[lat::C_AS1];
 #pragma unroll
@@ -1773,8 +1771,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
         double ax, ay;
         face_grad_v(c, v[r], ax, ay);
         const int64_t row = F.base + t[r];
-        stnt(ux + row, ox[r] - dt * (ax / d));
-        stnt(uy + row, oy[r] - dt * (ay / d));
+        stnt(reinterpret_cast<dbl2*>(ux) + row, dbl2{ox[r] - dt * (ax / d), oy[r] - dt * (ay / d)});
       }
     });
     return;
@@ -1788,7 +1785,8 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
     const int64_t row = sell_row(A, s, lane);
     const int32_t base = (int32_t)(s * 64);
     const int64_t rr = row >= 0 ? row : 0;
-    const double ox = bx[rr], oy = by[rr], d = as1[rr];
+    const dbl2 o = reinterpret_cast<const dbl2*>(bx)[rr];
+    const double ox = o.x, oy = o.y, d = as1[rr];
     const bool dirichlet = MODE == 1 && dirflag[rr] != 0;
     double ax = 0.0, ay = 0.0;
     by_width(w, [&](auto wc) {
@@ -1818,10 +1816,7 @@ __device__ __forceinline__ void grad_proj_body(const SellDev& A, const FaceDev& 
         }
       }
     });
-    if (row >= 0 && !dirichlet) {
-      stnt(ux + row, ox - dt * (ax / d));
-      stnt(uy + row, oy - dt * (ay / d));
-    }
+    if (row >= 0 && !dirichlet) stnt(reinterpret_cast<dbl2*>(ux) + row, dbl2{ox - dt * (ax / d), oy - dt * (ay / d)});
   }
 }
 
@@ -1886,25 +1881,27 @@ __global__ __launch_bounds__(BS) void k_grad(SellDev A, FaceDev fc, const double
 // copies whose destination is a Dirichlet node (the Dirichlet value wins), so the two write sets are
 // disjoint; when a source is also written, k_bc_gather first saves the sources in tmp (a separate
 // launch orders every read before any write), else tmp is null and k_bc_apply reads u directly.
+// (vs: the element stride of u0 / u1 -- VS for the interleaved velocity, 1 for a plain vector)
 __global__ void k_bc_gather(int ncopy, const int32_t* __restrict__ csrc, double* __restrict__ tmp, int ncomp,
-                            const double* __restrict__ u0, const double* __restrict__ u1) {
+                            const double* __restrict__ u0, const double* __restrict__ u1, int vs) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ncopy; k += gridDim.x * blockDim.x) {
-    tmp[2 * k] = u0[csrc[k]];
-    if (ncomp > 1) tmp[2 * k + 1] = u1[csrc[k]];
+    tmp[2 * k] = u0[(int64_t)vs * csrc[k]];
+    if (ncomp > 1) tmp[2 * k + 1] = u1[(int64_t)vs * csrc[k]];
   }
 }
 __global__ void k_bc_apply(int ncopy, const int32_t* __restrict__ cdst, const int32_t* __restrict__ csrc,
                            const double* tmp, int ndir, const int32_t* __restrict__ dnode,
-                           const double* __restrict__ dval, int ncomp, double* u0, double* u1) {
+                           const double* __restrict__ dval, int ncomp, double* u0, double* u1, int vs) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ncopy + ndir; k += gridDim.x * blockDim.x) {
     if (k < ncopy) {
-      const int d = cdst[k];
-      const double a = tmp ? tmp[2 * k] : u0[csrc[k]];
-      const double b = ncomp > 1 ? (tmp ? tmp[2 * k + 1] : u1[csrc[k]]) : 0.0;
+      const int64_t d = (int64_t)vs * cdst[k], sidx = (int64_t)vs * csrc[k];
+      const double a = tmp ? tmp[2 * k] : u0[sidx];
+      const double b = ncomp > 1 ? (tmp ? tmp[2 * k + 1] : u1[sidx]) : 0.0;
       u0[d] = a;
       if (ncomp > 1) u1[d] = b;
     } else {
-      const int j = k - ncopy, d = dnode[j];
+      const int j = k - ncopy;
+      const int64_t d = (int64_t)vs * dnode[j];
       u0[d] = dval[ncomp * j];
       if (ncomp > 1) u1[d] = dval[ncomp * j + 1];
     }
@@ -2391,8 +2388,8 @@ __global__ LB_GATHER void k_sl(MeshDev M, LOC L, int64_t row0, int64_t n,
     const double2 P = LL.xy[row0 + r];
     ax_ = P.x;
     ay_ = P.y;
-    avx = ux[r];
-    avy = uy[r];
+    avx = ux[VS * r];
+    avy = uy[VS * r];
     ah = LL.home[row0 + r];
   };
   auto stage_b = [&](const auto& LL, int64_t r) {  // from the stage A values
@@ -2508,7 +2505,7 @@ __global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int
   for (int32_t p = lane; p < cnt; p += 64) {
     const int64_t i = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)], g = row0 + i;
     double xb, yb;
-    sl_point(M, g, ux[i], uy[i], dt, xb, yb);
+    sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
     SlTri r;
     double bestd;
     float rho2;
@@ -2569,7 +2566,8 @@ __global__ __launch_bounds__(BS) void k_dye_w(MeshDev M, const double* __restric
     double w0 = 0.0, w1 = 0.0, w2 = 0.0;
     if (fabs(det) >= 1e-14) {
       const double area = 0.5 * fabs(det), den = 2 * fabs(det);
-      const double ucx = ((ux[a] + ux[b]) + ux[d]) / 3.0, ucy = ((uy[a] + uy[b]) + uy[d]) / 3.0;
+      const double ucx = ((ux[VS * a] + ux[VS * b]) + ux[VS * d]) / 3.0,
+                   ucy = ((uy[VS * a] + uy[VS * b]) + uy[VS * d]) / 3.0;
       w0 = (area / 3) * (ucx * ((y2 - y3) / den) + ucy * ((x3 - x2) / den));
       w1 = (area / 3) * (ucx * ((y3 - y1) / den) + ucy * ((x1 - x3) / den));
       w2 = (area / 3) * (ucx * ((y1 - y2) / den) + ucy * ((x2 - x1) / den));
@@ -2714,8 +2712,9 @@ __device__ __forceinline__ int32_t tracer_locate(const MeshDev& M, const GridDev
   }
   return -1;
 }
+// (vs: the element stride of ux / uy)
 __device__ __forceinline__ void tracer_interp(const MeshDev& M, int32_t t, const double* __restrict__ ux,
-                                              const double* __restrict__ uy, double px, double py, double& vx,
+                                              const double* __restrict__ uy, int vs, double px, double py, double& vx,
                                               double& vy) {
   const int32_t a = M.tri[3 * t], b = M.tri[3 * t + 1], d = M.tri[3 * t + 2];
   const double x0 = M.x[a], y0 = M.y[a];
@@ -2725,8 +2724,8 @@ __device__ __forceinline__ void tracer_interp(const MeshDev& M, int32_t t, const
   const double* uu[2] = {ux, uy};
 #pragma unroll
   for (int q = 0; q < 2; ++q) {  // Triangulation::calculate_plane_coefficients
-    const double z0 = uu[q][a];
-    const double s1z = uu[q][b] - z0, s2z = uu[q][d] - z0;
+    const double z0 = uu[q][(int64_t)vs * a];
+    const double s1z = uu[q][(int64_t)vs * b] - z0, s2z = uu[q][(int64_t)vs * d] - z0;
     const double nx = s1y * s2z - s1z * s2y;
     const double ny = s1z * s2x - s1x * s2z;
     const double pa = -nx / nz, pb = -ny / nz;
@@ -2759,7 +2758,7 @@ __global__ void k_tracer(MeshDev M, GridDev G, const double* __restrict__ ux, co
     const double px = tx[k], py = ty[k];
     double vx = NAN, vy = NAN;
     const int32_t found = tracer_locate(M, G, px, py);
-    if (found >= 0) tracer_interp(M, found, ux, uy, px, py, vx, vy);
+    if (found >= 0) tracer_interp(M, found, ux, uy, VS, px, py, vx, vy);
     eaten += tracer_move(tx, ty, status, k, vx, vy, dt, cx, cy, capture);
   }
   const double t = block_sum(eaten, sh);
@@ -2776,7 +2775,7 @@ __global__ void k_tracer_vel(MeshDev M, GridDev G, const double* __restrict__ fx
     double vx = 0.0, vy = 0.0, f = 0.0;
     const int32_t t = tracer_locate(M, G, px, py);
     if (t >= 0 && M.tri[3 * t] >= own0 && M.tri[3 * t] < own1) {
-      tracer_interp(M, t, fx, fy, px, py, vx, vy);
+      tracer_interp(M, t, fx, fy, 1, px, py, vx, vy);  // (plain full replicas)
       f = 1.0;
     }
     tv[3 * k] = vx;
@@ -2798,10 +2797,15 @@ __global__ void k_tracer_move(int32_t ntr, double* tx, double* ty, double* statu
   if (threadIdx.x == 0) *eaten_out = t;
 }
 // ghost values of a local vector into their global positions of a full-size array
+// (vs: the element stride of v)
 __global__ void k_scatter_ghosts(int64_t ng, const int32_t* __restrict__ ghost_global, const double* __restrict__ v,
-                                 double* __restrict__ full) {
+                                 double* __restrict__ full, int vs) {
   for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < ng; k += (int64_t)gridDim.x * BS)
-    full[ghost_global[k]] = v[k];
+    full[ghost_global[k]] = v[vs * k];
+}
+// out[i] = v[vs * i] (a strided component into a plain vector)
+__global__ void k_unstride(int64_t n, const double* __restrict__ v, int vs, double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = v[vs * i];
 }
 
 // ----------------------------------------------------------------------------- device assembly
@@ -3080,7 +3084,7 @@ __global__ __launch_bounds__(BS) void k_yrange(int64_t n, const double* __restri
   int64_t r0, r1;
   block_rows(n, r0, r1);
   for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
-    double yb = y[i] - dt * vy[i] * 1.0;
+    double yb = y[i] - dt * vy[VS * i] * 1.0;
     if (yb < 0.0) yb = 1e-12;
     if (yb > 1.0) yb = 1.0 - 1e-12;
     lo = fmax(lo, 1.0 - yb);
@@ -3810,6 +3814,7 @@ __global__ __launch_bounds__(CGB_THREADS) void k_cg_block(SellDev A, const doubl
 
 
 // dense 2-RHS matvec (small-mesh direct viscous solve): y0 = A x0, y1 = A x1; one wave per row
+// (x0 / x1 and y0 / y1: the interleaved velocity's components, stride VS)
 __global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x0,
                                                   const double* __restrict__ x1, double* __restrict__ y0,
                                                   double* __restrict__ y1) {
@@ -3819,14 +3824,14 @@ __global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __res
     double s0 = 0.0, s1 = 0.0;
     for (int64_t j = lane; j < n; j += 64) {
       const double v = a[j];
-      s0 += v * x0[j];
-      s1 += v * x1[j];
+      s0 += v * x0[VS * j];
+      s1 += v * x1[VS * j];
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
     if (lane == 0) {
-      y0[row] = s0;
-      y1[row] = s1;
+      y0[VS * row] = s0;
+      y1[VS * row] = s1;
     }
   }
 }
