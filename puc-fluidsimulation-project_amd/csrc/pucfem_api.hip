@@ -496,7 +496,10 @@ struct Ctx {
   // (which = 3, 4: the viscous solve's x and y components, proj_k_visc directions each)
   int proj_k = 0, proj_k_visc = 0;
   ProjT* projX[5] = {};
-  i64 ldx = 0;  // the basis vectors' stride: nloc rounded up to even (8-B aligned pairs of rows)
+  i64 ldx = 0;  // column-major basis (PUCFEM_PROJ_TILED=0): the vectors' stride, nloc rounded up to even
+  // the basis of slot w: its ld argument (tiled: the capacity) and the offset of its vector i
+  i64 pld(int w) const { return PUCFEM_PROJ_TILED ? (w <= 2 ? proj_k : proj_k_visc) : ldx; }
+  i64 pcol(int w, int i) const { return PUCFEM_PROJ_TILED ? 64 * (i64)i : (i64)i * ldx; }
   double* proj_x0[5] = {};
   int proj_m[5] = {0, 0, 0, 0, 0};
   // Deferred update (project_guess): after a solve only v = y - x0 and A v are formed; the next
@@ -2078,7 +2081,7 @@ struct Ctx {
                            : PendDir{nullptr, nullptr, nullptr, nullptr};
     klaunch(14, (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb),
             dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)ldx, b, (const double*)pav[which], (const double*)pv[which],
+            (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], (const double*)pv[which],
             op.null_free, proj_part, rmd, pd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
@@ -2094,8 +2097,8 @@ struct Ctx {
     // k_pcomb: X, v read; the new direction, y and x0 (or the cleared accumulator of the coming solve) written
     const bool acc_next = which <= 2 && !proj_spmv;
     klaunch(15, (4.0 * kq + 32.0 + (vdiff ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)ldx, (const double*)proj_coef, (const double*)pv[which], op.null_free,
-            projX[which] + (i64)kq * ldx, y, acc_next ? (double*)nullptr : proj_x0[which],
+            (const ProjT*)projX[which], (int64_t)pld(which), (const double*)proj_coef, (const double*)pv[which],
+            op.null_free, projX[which] + pcol(which, kq), y, acc_next ? (double*)nullptr : proj_x0[which],
             vdiff ? pend_y[which] : (const double*)nullptr, acc_next ? pv[which] : (double*)nullptr);
     KCHK();
     pend_otf[which] = false;
@@ -2165,7 +2168,7 @@ struct Ctx {
     HIPCHK(hipMemcpyAsync(dqm, &qm, sizeof(QMat), hipMemcpyHostToDevice, st));
     const i64 n = lp.n_own;
     algo_bytes += 4.0 * (double)(m + kq) * (double)n;
-    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], ldx, m,
+    hipLaunchKernelGGL(k_reseed, dim3(grid_ew(n)), dim3(BS), 0, st, n, (const ProjT*)projX[which], pld(which), m,
                        (const double*)dqm, kq,
                        projXalt[which]);
     KCHK();
@@ -3581,9 +3584,10 @@ void build(Ctx& c) {
   for (int w = 1; w <= 4; ++w) {
     const int k = w <= 2 ? c.proj_k : c.proj_k_visc;
     if (k > 0) {
-      c.projX[w] = c.dalloc<ProjT>((i64)k * c.ldx);
+      const i64 pn = PUCFEM_PROJ_TILED ? (c.nloc + 63) / 64 * 64 * k : (i64)k * c.ldx;
+      c.projX[w] = c.dalloc<ProjT>(pn);
       c.proj_x0[w] = c.dalloc<double>(c.nloc);
-      c.projXalt[w] = c.dalloc<ProjT>((i64)k * c.ldx);  // re-seeding target
+      c.projXalt[w] = c.dalloc<ProjT>(pn);  // re-seeding target
     }
   }
   if (stokes && !c.dense && !block_visc && c.proj_k_visc == 0 && c.visc_extrap > 0)

@@ -740,6 +740,20 @@ using ProjT = float;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef float flt2 __attribute__((ext_vector_type(2)));
 
+// Basis layout.  PUCFEM_PROJ_TILED (default): tiles of 64 rows, inside a tile each of the basis' kcap vectors holds
+// 64 consecutive values -- element (i, r) at ((r / 64) kcap + i) 64 + r % 64, ld = kcap: a wave's 64 rows of all
+// vectors are one contiguous block (one DRAM stream instead of one per vector), a new vector's 64 values one
+// 256-B segment.  0: column-major, (i, r) at i ld + r, ld = the vector stride
+#ifndef PUCFEM_PROJ_TILED
+#define PUCFEM_PROJ_TILED 1
+#endif
+__host__ __device__ __forceinline__ int64_t pxi(int i, int64_t r, int64_t ld) {
+#if PUCFEM_PROJ_TILED
+  return (((r >> 6) * ld + i) << 6) + (r & 63);
+#else
+  return (int64_t)i * ld + r;
+#endif
+}
 // basis re-seeding: out_i = sum_j q[i][j] X_j (i < kq <= PROJ_KEEP_MAX, j < m), one pass over X.
 // Q: the re-seed coefficients in device memory, row-major [PROJ_KEEP_MAX][PROJ_MAX] (block-uniform loads)
 constexpr int PROJ_KEEP_MAX = 16;
@@ -764,7 +778,7 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
     for (int j = 0; j < m; ++j) {
       double x[RESEED_R];
 #pragma unroll
-      for (int k = 0; k < RESEED_R; ++k) x[k] = rk[k] < n ? (double)X[j * ld + rk[k]] : 0.0;
+      for (int k = 0; k < RESEED_R; ++k) x[k] = rk[k] < n ? (double)X[pxi(j, rk[k], ld)] : 0.0;
 #pragma unroll
       for (int i = 0; i < PROJ_KEEP_MAX; ++i) {
         const double q = Q[i * PROJ_MAX + j];
@@ -777,7 +791,7 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
       if (i < kq)
 #pragma unroll
         for (int k = 0; k < RESEED_R; ++k)
-          if (rk[k] < n) out[i * ld + rk[k]] = (ProjT)acc[i][k];
+          if (rk[k] < n) out[pxi(i, rk[k], ld)] = (ProjT)acc[i][k];
   }
 }
 
@@ -819,7 +833,7 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
     const double vr = D.v ? D.v[r] : (D.y ? D.y[r] - D.x0[r] : v[r]);
     ProjT x[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    for (int i = 0; i < M; ++i) x[i] = X[pxi(i, r, ld)];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       acc[i] += (double)x[i] * br;
@@ -897,7 +911,7 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
     ProjT x[M > 0 ? M : 1];
 #pragma unroll
-    for (int i = 0; i < M; ++i) x[i] = X[i * ld + r];
+    for (int i = 0; i < M; ++i) x[i] = X[pxi(i, r, ld)];
     const double vr = yp ? yp[r] - x0[r] : v[r];
     double sa = 0.0, sc = 0.0;
 #pragma unroll
@@ -907,7 +921,7 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
     }
     const double xm = s * (vr - ((master_of && master_of[r] < 0) ? mu : 0.0) - sc);
     const double g = sa + alpha * xm;
-    stnt(xm_out + r, (ProjT)xm);
+    stnt(xm_out + pxi(0, r, ld), (ProjT)xm);  // (xm_out: the basis at the new vector's column)
     stnt(y + r, g);
     if (x0) stnt(x0 + r, g);
     if (vz) stnt(vz + r, 0.0);
