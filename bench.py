@@ -192,7 +192,7 @@ def main():
                         (8, "k_div face rows only"), (9, "k_div skeleton (SELL) rows only"),
                         (10, "k_div on a viscous (x, y) buffer"), (11, "k_div interleaved, face rows only"),
                         (12, "k_cheb_pair<1> (face rows)"), (13, "k_cheb_pair<2> (face rows)"),
-                        (14, "k_vcheb_pair (face rows)")):
+                        (14, "k_vcheb_pair (face rows)"), (15, "k_reseed (projection basis re-seed)")):
             mb, me, by = ct.c_double(), ct.c_double(), ct.c_double()
             L.check(L.lib().pucfem_bench_kernel(sim.ctx.h, kid, 20, ct.byref(mb), ct.byref(me), ct.byref(by)),
                     sim.ctx.h)

@@ -5342,6 +5342,14 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
                                       0.7f, 0.5f, 0.3f, 0.7f, (const int*)nullptr);
             }
             break;
+          case 15:  // k_reseed: the pressure basis (all proj_k vectors) into PROJ_KEEP_MAX new ones (scratch target)
+            if (c.proj_k > 0 && c.dqm) {
+              const i64 n = c.lp.n_own;
+              hipExtLaunchKernelGGL(k_reseed, dim3(Ctx::grid_ew(n)), dim3(BS), 0, c.st, a, e, 0, (int64_t)n,
+                                    (const ProjT*)c.projX[1], (int64_t)c.pld(1), c.proj_k, (const double*)c.dqm,
+                                    (int)PROJ_KEEP_MAX, c.projXalt[1]);
+            }
+            break;
           case 14:  // k_vcheb_pair (two viscous Chebyshev steps on the face rows, general start)
             if (c.vx2[2] && c.fVisc.items > 0) {
               VPairVecs p{};
@@ -5408,6 +5416,7 @@ int pucfem_bench_kernel(void* ctx, int32_t kernel, int32_t iters, double* ms_bat
       case 12: by = 20.0 * (double)c.fP.rows; break;  // x_a, d_a, b read; x_{a+2}, d_{a+2} written (fp32)
       case 13: by = 12.0 * (double)c.fP.rows; break;  // b read; x_{a+2}, d_{a+2} written
       case 14: by = 64.0 * (double)c.fVisc.rows; break;  // x_a, b, d_a read; x_{a+2}, d_{a+2} written
+      case 15: by = 4.0 * (c.proj_k + PROJ_KEEP_MAX) * (double)c.lp.n_own; break;  // the basis read, the new one written
       case 9: by = (16.0 + c.dP.idx_bytes()) * (double)c.dP.nnz + (c.dP.row_bytes() + 24.0) * (double)c.dP.nrows; break;
       default: by = (8.0 + A.idx_bytes()) * (double)A.nnz + (32.0 + rb) * sk + 32.0 * fr;
     }

@@ -760,38 +760,29 @@ constexpr int PROJ_KEEP_MAX = 16;
 struct QMat {
   double q[PROJ_KEEP_MAX][PROJ_MAX];
 };
-// RESEED_R rows per thread share each (uniform, scalar-loaded) coefficient: one row at a time reloaded all
-// 16 x 32 coefficients per row (1.18 ms per re-seed at L7, r10z); the per-row operations are unchanged
-constexpr int RESEED_R = 4;
+// The re-seed coefficients are staged in LDS once per block, and a row's m basis values are all loaded before the
+// sums (the j loop with one load per step waited one memory round trip per vector: 1.18 ms at L7, r10z); the per-row
+// operations and their order are unchanged (acc_i += q_ij x_j, j ascending)
+// The re-seed coefficients are staged in LDS once per block (uniform loads of all 16 x 32 of them per row from
+// device memory: 1.18 ms at L7 in-step, r10z; isolated 0.77 ms with LDS, r11q, where all 32 basis loads issued first
+// and then the sums took 1.93 ms); the per-row operations and their order are unchanged
 __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restrict__ X, int64_t ld, int m,
                                                const double* __restrict__ Q, int kq, ProjT* __restrict__ out) {
-  const int64_t chunk = (int64_t)BS * RESEED_R;
-  for (int64_t r0 = (int64_t)blockIdx.x * chunk; r0 < n; r0 += (int64_t)gridDim.x * chunk) {
-    double acc[PROJ_KEEP_MAX][RESEED_R];
+  __shared__ double q[PROJ_KEEP_MAX * PROJ_MAX];
+  for (int t = threadIdx.x; t < PROJ_KEEP_MAX * PROJ_MAX; t += BS) q[t] = Q[t];
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += (int64_t)gridDim.x * BS) {
+    double acc[PROJ_KEEP_MAX];
 #pragma unroll
-    for (int i = 0; i < PROJ_KEEP_MAX; ++i)
-#pragma unroll
-      for (int k = 0; k < RESEED_R; ++k) acc[i][k] = 0.0;
-    int64_t rk[RESEED_R];
-#pragma unroll
-    for (int k = 0; k < RESEED_R; ++k) rk[k] = r0 + (int64_t)k * BS + threadIdx.x;
+    for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] = 0.0;
     for (int j = 0; j < m; ++j) {
-      double x[RESEED_R];
+      const double x = (double)X[pxi(j, r, ld)];
 #pragma unroll
-      for (int k = 0; k < RESEED_R; ++k) x[k] = rk[k] < n ? (double)X[pxi(j, rk[k], ld)] : 0.0;
-#pragma unroll
-      for (int i = 0; i < PROJ_KEEP_MAX; ++i) {
-        const double q = Q[i * PROJ_MAX + j];
-#pragma unroll
-        for (int k = 0; k < RESEED_R; ++k) acc[i][k] += q * x[k];
-      }
+      for (int i = 0; i < PROJ_KEEP_MAX; ++i) acc[i] += q[i * PROJ_MAX + j] * x;
     }
 #pragma unroll
     for (int i = 0; i < PROJ_KEEP_MAX; ++i)
-      if (i < kq)
-#pragma unroll
-        for (int k = 0; k < RESEED_R; ++k)
-          if (rk[k] < n) out[pxi(i, rk[k], ld)] = (ProjT)acc[i][k];
+      if (i < kq) out[pxi(i, r, ld)] = (ProjT)acc[i];
   }
 }
 
