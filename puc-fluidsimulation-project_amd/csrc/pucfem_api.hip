@@ -1911,6 +1911,9 @@ struct Ctx {
                       !(!dist() && block_cg && !fVisc.items && dP.nrows <= (int64_t)CGB_THREADS * CGB_MAXR);
     // (k_visc_prep folded into the solve's first step was measured 9 % slower in round 3, r9i: the window
     // recomputes the start's 64 B/row of inputs on 25 % more rows, so the fusion saved no bytes)
+    // (folded into the previous step's second k_grad_proj, which holds the final u in registers: bit-identical,
+    // ~50 us less kernel time per step, yet 0.4-1.4 % slower in four A/B pairs with and without the dye
+    // overlap, r11s; not kept)
     // u, s, sq, the increments read; b, y written
     const double prep_bytes = (64.0 + 8.0 * vd.order) * (double)n;
     if (cheb)

@@ -14,7 +14,7 @@ for e in "$@"; do
 import json, sys
 r = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 it = r['cg_iters_per_step']
-print(f"  value {r['value']:.3f} steps/s  ms/step {r['ms_per_step']:.2f}  p {sum(it['p'])} p2 {sum(it['p2'])} visc {sum(it['visc_2rhs'])}")
+print(f"  value {r['value']:.3f} steps/s  ms/step {r['ms_per_step']:.2f}  p {sum(it['p'])} p2 {sum(it['p2'])} visc {sum(it.get('visc_cheb_steps', it.get('visc_2rhs', [])))}")
 for k, v in r.get("kernels", {}).items():
     print(f"    {k:40s} {v['avg_launch_ms']*1e3:8.1f} us")
 PY
