@@ -1290,6 +1290,25 @@ struct VPairVecs {
   float* inc[2];
 };
 constexpr int VP_HALO = 256;  // window rows on each side: n <= VP_HALO (lattice size of the face)
+// A step pair's second-step neighbour: from the LDS window (in-face neighbour; lw clamped into the window), else
+// the global x_{a+1} at a skeleton row.  The LDS value is read unconditionally and the global one under the
+// branch: written as `in ? lds[lw] : glob[g]`, the compiler merges the two loads into one generic (flat) load of
+// a selected address, which is slower than ds_read for every row although only the rows next to the skeleton
+// take the global path.
+// (the empty asm pins the LDS value in registers before the branch, so the loads cannot be merged)
+__device__ __forceinline__ void pin_reg(float& x) { asm("" : "+v"(x)); }
+__device__ __forceinline__ void pin_reg(dbl2& x) { asm("" : "+v"(x.x), "+v"(x.y)); }
+template <typename T>
+__device__ __forceinline__ T pair_nbr(const T* lds, int32_t lw, const T* glob, int64_t g, bool in) {
+#ifdef PUCFEM_PAIR_SELECT_LOAD  // (A/B: the merged form)
+  return in ? lds[lw] : glob[g];
+#else
+  T x = lds[lw];
+  pin_reg(x);
+  if (!in) x = glob[g];
+  return x;
+#endif
+}
 constexpr int VP_W = BS * FACE_RPT + 2 * VP_HALO;
 constexpr int VP_WK = (VP_W + BS - 1) / BS;
 #ifndef PUCFEM_VP_G
@@ -1397,7 +1416,7 @@ __global__ LB_GATHER void k_vcheb_pair(FaceDev fc, VPairVecs v, double c1a, doub
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
         const int32_t lw = min(max(nb[r][q] - F.base - w0, 0), nw - 1);
-        xv[r][q] = in[r][q] ? lx[lw] : v.xb[nb[r][q]];
+        xv[r][q] = pair_nbr(lx, lw, v.xb, nb[r][q], in[r][q]);
       }
     }
 #pragma unroll
@@ -3457,7 +3476,7 @@ __global__ __launch_bounds__(BS) void k_cheb_pair(FaceDev fc, MgPairVecs v, floa
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
         const int32_t lw = min(max(nb[q] - F.base - w0, 0), nw - 1);
-        ax += a[1 + q] * (in[q] ? lx[lw] : v.xb[nb[q]]);
+        ax += a[1 + q] * pair_nbr(lx, lw, v.xb, nb[q], in[q]);
         bnd = bnd || !in[q];
       }
       const float dn = c1b * dt[k] + c2b * di * (bt[k] - ax);
