@@ -129,9 +129,9 @@ def main():
                     ("k_sl", pick("k_sl", ("k_sl_",))),
                     ("k_sl_slow", pick("k_sl_slow")),
                     ("k_vcheb", widest(pick("k_vcheb<"))),
-                    # the step's divergence kernel only (SoA u, the full grid): the bench's kernel_batch
-                    # also launches its face / skeleton parts and the interleaved-u variant
-                    ("k_div", widest(pick("k_div<", ("k_div<false,true>", "k_div<true,true>")))),
+                    # the step's divergence kernel (interleaved u, the full grid): the bench's kernel_batch
+                    # also launches its face / skeleton parts (smaller grids)
+                    ("k_div", widest(pick("k_div<", ("k_div<false,false>", "k_div<true,false>")))),
                     ("k_grad_proj", pick("k_grad_proj<")),
                     ("k_visc_prep", pick("k_visc_prep")),
                     ("k_mdot2", pick("k_mdot2<")),
@@ -144,14 +144,13 @@ def main():
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
                                for k in ks) / n
     # the projection passes' bytes depend on the basis size M (their template argument): the ratio of PMC to
-    # algorithmic bytes over the instances with M >= 16 ((4 M + 40) n for k_mdot2, (4 M + 40) n for k_pcomb with
-    # the production path's pending directions -- v = y - x0 and A v = r0 - r_final formed in the passes, +16 /
-    # +8 B per row; PUCFEM_P_FROM_Y=0 runs: 24 / 32), which bench.py applies to the algorithmic bytes of the
-    # launches it timed
+    # algorithmic bytes over the instances with M >= 16 ((4 M + 32) n for both with the production path's pending
+    # directions -- the CG's accumulated v and A v = r0 - r_final formed in k_mdot2; PUCFEM_P_FROM_Y=0 runs:
+    # 24 / 32), which bench.py applies to the algorithmic bytes of the launches it timed
     ratios = {}
     pend = os.environ.get("PUCFEM_P_FROM_Y", "1") != "0"
     if nrows:
-        for key, extra in (("k_mdot2", 40.0 if pend else 24.0), ("k_pcomb", 40.0 if pend else 32.0)):
+        for key, extra in (("k_mdot2", 32.0 if pend else 24.0), ("k_pcomb", 32.0)):
             pmc = alg = 0.0
             for k, e in res["kernels"].items():
                 mm = re.match(r"^" + key + r"<(\d+)>", k)
