@@ -25,10 +25,16 @@ constexpr int BS = 256;     // threads per block
 constexpr int MAXB = 32768;
 constexpr int EWB = 8192;   // max blocks of a row-wise (SELL / elementwise) grid
 constexpr int KNN = 10;     // PointLocator k (StokesColor.py:324)
-constexpr int SLB = 4096;
+// max blocks (= partial stride) of the semi-Lagrangian kernel.  At L7 a block of 8192 runs ~1,700 rows: shorter-lived
+// blocks free wave slots sooner for the main stream's kernels beside the dye stream (4096 -> 8192: k_sl 600 -> 520 us
+// in-step, driver window +0.5-1 %, steps 100-119 +1.5-2 %; 6144 / 10240 / 16384 measured too, r11x / r11y)
+#ifndef PUCFEM_SLB
+#define PUCFEM_SLB 8192
+#endif
+constexpr int SLB = PUCFEM_SLB;
 // Velocity storage: u and u* are interleaved (x, y) pairs (one 16-B gather per neighbour in k_div, the tracers and
 // the dye weights); kernels take the component pointers ux = u2, uy = u2 + 1 and index them at VS * i
-constexpr int VS = 2;   // max blocks (= partial stride) of the semi-Lagrangian kernel
+constexpr int VS = 2;
 #ifndef PUCFEM_FACE_RPT
 #define PUCFEM_FACE_RPT 4
 #endif
