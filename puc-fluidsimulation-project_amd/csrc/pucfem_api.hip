@@ -705,6 +705,10 @@ struct Ctx {
   // stream's kernels; the rows per block grow, the per-wave queue follows them)
   int sl_cap = std::getenv("PUCFEM_SL_BLOCKS") ? std::max(8, std::min(SLB, std::atoi(std::getenv("PUCFEM_SL_BLOCKS"))))
                                                : SLB;
+  // PUCFEM_SL_LDS (measurement knob): dynamic LDS bytes requested by the k_sl launches (unused by the kernel): caps
+  // the k_sl blocks resident per CU (160 KB / bytes), leaving wave slots and registers to the main stream
+  size_t sl_lds = std::getenv("PUCFEM_SL_LDS") ? (size_t)std::max(0, std::min(65536, std::atoi(std::getenv("PUCFEM_SL_LDS"))))
+                                               : 0;
   int nb_sl(i64 n) const {
     return (int)std::max<i64>(1, std::min<i64>(sl_cap, (n + 4 * 64 - 1) / (4 * 64)));
   }
@@ -714,6 +718,7 @@ struct Ctx {
   // Launch on the library stream.  When timing (cls >= 0), the start / stop events are taken by the
   // kernel's dispatch itself (hipExtLaunchKernelGGL): the sample is the kernel's own duration, as
   // rocprofv3 reports it, without the command-processor gap a separately recorded event adds.
+  size_t kl_lds = 0;  // dynamic LDS of the launch (0 but around the k_sl launches with PUCFEM_SL_LDS)
   template <typename... KArgs, typename... Args>
   void klaunch(int cls, double bytes, void (*kernel)(KArgs...), dim3 g, dim3 b, Args... args) {
     algo_bytes += bytes;
@@ -724,11 +729,11 @@ struct Ctx {
     if (timer.on && cls >= 0 && ((timer.mask >> cls) & 1u)) {
       hipEvent_t a = timer.get(), e = timer.get();
       ++g_nlaunch;
-      hipExtLaunchKernelGGL(kernel, g, b, 0, st, a, e, 0, args...);
+      hipExtLaunchKernelGGL(kernel, g, b, kl_lds, st, a, e, 0, args...);
       timer.pend.push_back({cls, a, e, bytes});
       if (timer.pend.size() > 4096) timer.flush();  // bounded number of live events
     } else {
-      hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
+      hipLaunchKernelGGL(kernel, g, b, kl_lds, st, args...);
     }
   }
   // The solvers' host reads (convergence tests, |r_0|) wait by polling the event instead of a blocking
@@ -773,6 +778,11 @@ struct Ctx {
   void sl_launch(int nb, i64 row0, i64 n, const double* vx, const double* vy, double dt, const double* cf, double* cn,
                  const double* w, int32_t* nf, RedOut ro = RedOut{}) {
     const MeshDev M{mx, my, mtri, mesh.T};
+    struct LdsScope {  // (reset on unwind)
+      size_t& v;
+      LdsScope(size_t& x, size_t n) : v(x) { v = n; }
+      ~LdsScope() { v = 0; }
+    } lds_scope(kl_lds, sl_lds);
     if (lat_sl) {
       // per row: coordinates 16, u 16, c 8 (the departure triangle's vertices lie near the row: their
       // coordinate and c lines are the rows' own), home face 4, lattice cell entries 8 and fast-accept
