@@ -350,7 +350,7 @@ struct Ctx {
   // ---- device operators
   DevSell dP, dPp, dLit;
   double *dK = nullptr, *dGx = nullptr, *dGy = nullptr, *dKv = nullptr, *dKp = nullptr, *dLitv = nullptr;
-  double *dsv = nullptr, *dsqv = nullptr, *dsp = nullptr, *dsqp = nullptr, *dlit_dinv = nullptr;
+  double *dsv = nullptr, *dsp = nullptr, *dlit_dinv = nullptr;
   double *das1 = nullptr, *dmp = nullptr, *dwmix = nullptr;
   uint8_t* ddir = nullptr;
   int32_t *dslave_of = nullptr, *dmaster_of = nullptr;
@@ -1924,15 +1924,15 @@ struct Ctx {
     // (folded into the previous step's second k_grad_proj, which holds the final u in registers: bit-identical,
     // ~50 us less kernel time per step, yet 0.4-1.4 % slower in four A/B pairs with and without the dye
     // overlap, r11s; not kept)
-    // u, s, sq, the increments read; b, y written
-    const double prep_bytes = (64.0 + 8.0 * vd.order) * (double)n;
+    // u, s, the increments read; b, y written
+    const double prep_bytes = (56.0 + 8.0 * vd.order) * (double)n;
     if (cheb)
       klaunch(13, prep_bytes, k_visc_prep<true>, dim3(grid_ew(n)), dim3(BS), (int64_t)n, (const double*)dsv,
-              (const double*)dsqv, (const double*)ux, (const double*)uy, reinterpret_cast<double*>(vb2),
+              (const double*)ux, (const double*)uy, reinterpret_cast<double*>(vb2),
               (double*)nullptr, reinterpret_cast<double*>(vx2[0]), (double*)nullptr, vd);
     else
       klaunch(13, prep_bytes, k_visc_prep<false>, dim3(grid_ew(n)), dim3(BS), (int64_t)n, (const double*)dsv,
-              (const double*)dsqv, (const double*)ux, (const double*)uy, bvx, bvy, yvx, yvy, vd);
+              (const double*)ux, (const double*)uy, bvx, bvy, yvx, yvy, vd);
     KCHK();
     // with the extrapolated start the solve's last Chebyshev step also does k_visc_fin's work
     const int last = 2 * (visc_extrap - 1);
@@ -3435,13 +3435,7 @@ void build(Ctx& c) {
     scaling(c.P, c.Kv, sg);
     sell_values_fn(c.P, lp.r0, c.sP, [&](i64 r, i64 k) { return sg[r] * c.Kv[k] * sg[c.P.col[k]]; }, tmp);
     c.dKv = c.upload(tmp);
-    c.dsv = c.upload(local_vec(sg));
-    std::vector<double> sq;
-    host_alloc_fresh(sq, N);
-    parallel_for(N, [&](i64 g0, i64 g1) {
-      for (i64 g = g0; g < g1; ++g) sq[g] = 1.0 / sg[g];
-    });
-    c.dsqv = c.upload(local_vec(sq));
+    c.dsv = c.upload(local_vec(sg));  // (k_visc_prep forms 1 / s itself)
     if (c.lattice) {  // scaled A_visc, skeleton columns: s_j, 0 for Dirichlet columns (StokesColor.py:473-475)
       std::vector<double> w = local_vec(sg);
       for (i64 i = 0; i < no; ++i)
@@ -4525,7 +4519,7 @@ int pucfem_solve(void* ctx, int32_t op, const double* b, double* x, double rtol,
       }
       HIPCHK(hipMemcpyAsync(s0, bxy.data(), sizeof(double) * 2 * N, hipMemcpyHostToDevice, c.st));
       HIPCHK(hipStreamSynchronize(c.st));
-      hipLaunchKernelGGL(k_visc_prep<false>, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, c.dsqv, s0, s0 + 1,
+      hipLaunchKernelGGL(k_visc_prep<false>, dim3(Ctx::grid_ew(N)), dim3(BS), 0, c.st, N, c.dsv, s0, s0 + 1,
                          c.bvx, c.bvy, c.yvx, c.yvy, VincDev{});
       KCHK();
       double* y[2] = {c.yvx, c.yvy};
