@@ -537,6 +537,9 @@ struct Ctx {
   // the solve after a projected guess accumulates its correction v = sum alpha_k p_k in pv[slot] (k_cg_upd's
   // vacc; k_pcomb clears it with the guess): pend_acc -- the pending / stored v is that accumulator, not y - x0
   bool pend_acc[5] = {};
+  // the accumulated v of slot is zero (its solve passed at the guess: no update ran, so the accumulator, which the
+  // first update starts instead of a cleared buffer, was not written); k_mdot2 / k_pcomb then read no v
+  bool pend_vzero[5] = {};
   double* cg_vacc = nullptr;  // pcg_mg's accumulator of the current solve (null: none)
   // keep: a slot whose pending direction stays (its r_final is the one cg_r[0] still holds)
   void proj_materialize(int keep = 0) {
@@ -1675,6 +1678,7 @@ struct Ctx {
     proj_pend[slot] = false;
     pend_otf[slot] = false;
     pend_acc[slot] = false;
+    pend_vzero[slot] = false;
     proj_hist[slot] = ProjHist{};
     guess_n[slot] = 0;
     ++n_restart;
@@ -1802,11 +1806,13 @@ struct Ctx {
                              cgcg_sc, tol2, ctl, it, maxit, (const double*)rho0);
           KCHK();
           if (mg_single)
-            klaunch(2, bytes_cu, k_cgcg_upd<true>, dim3(nb), dim3(BS), (int64_t)n, (const double*)nullptr,
+            klaunch(2, bytes_cu - (cg_vacc && it == 0 ? 8.0 * (double)n : 0.0), k_cgcg_upd<true>, dim3(nb), dim3(BS),
+                    (int64_t)n, (const double*)nullptr,
                     (const float*)z32, (const double*)cg_pb[0], cg_pa[0], cg_q[0], y, cg_r[0], r32o, cg_vacc,
                     (const double*)cgcg_sc, (const int*)ctl, it, part_cc);
           else
-            klaunch(2, bytes_cu, k_cgcg_upd<false>, dim3(nb), dim3(BS), (int64_t)n, (const double*)z,
+            klaunch(2, bytes_cu - (cg_vacc && it == 0 ? 8.0 * (double)n : 0.0), k_cgcg_upd<false>, dim3(nb), dim3(BS),
+                    (int64_t)n, (const double*)z,
                     (const float*)nullptr, (const double*)cg_pb[0], cg_pa[0], cg_q[0], y, cg_r[0], r32o, cg_vacc,
                     (const double*)cgcg_sc, (const int*)ctl, it, part_cc);
           KCHK();
@@ -1837,8 +1843,9 @@ struct Ctx {
         else pq = reduce_global(part_c, nb, 1, false, 2);
         CgVecs<1> vu = v;
         vu.r[0] = cg_r[0];
-        klaunch(2, bytes_upd + (cg_vacc ? 16.0 * (double)n : 0.0), k_cg_upd<1>, dim3(nbu), dim3(BS), vu, n, pq.p,
-                pq.nb, pq.stride, (const double*)scal, (const int*)ctl, part_a, r32o, rupd, cg_vacc);
+        klaunch(2, bytes_upd + (cg_vacc ? (it == 0 ? 8.0 : 16.0) * (double)n : 0.0), k_cg_upd<1>, dim3(nbu), dim3(BS),
+                vu, n, pq.p, pq.nb, pq.stride, (const double*)scal, (const int*)ctl, part_a, r32o, rupd, cg_vacc,
+                it == 0 ? 1 : 0);
         KCHK();
         if (rupd.out) rr = Red{redbuf, 1, 1}, red_done(redbuf, 1, false);
         else if (!merged_conv) rr = reduce_global(part_a, nbu, 1, false, 0);
@@ -2032,6 +2039,7 @@ struct Ctx {
       if (proj) {
         const int slot = proj_slot(which);
         pend_acc[slot] = acc;
+        pend_vzero[slot] = acc && it == 0;
         if (proj_spmv) {
           project_update(slot, yst);  // A v by an SpMV of the stored v
         } else if (p_from_y && proj_m[slot] > 0) {  // the direction stays pending (the next solve forms it)
@@ -2089,12 +2097,14 @@ struct Ctx {
     const bool otf = pend_otf[which];
     // a pending direction: A v from the residuals; v accumulated (pend_acc) or y - x0 (the first direction)
     const bool vdiff = otf && !pend_acc[which];
-    const PendDir pd = otf ? PendDir{pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0],
-                                     pend_acc[which] ? (const double*)pv[which] : nullptr}
+    const bool vz0 = pend_vzero[which];  // (v = 0: neither v nor y - x0 is read)
+    const double* vp = vz0 ? nullptr : (const double*)pv[which];
+    const PendDir pd = otf ? PendDir{vz0 ? nullptr : pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0],
+                                     pend_acc[which] ? vp : nullptr}
                            : PendDir{nullptr, nullptr, nullptr, nullptr};
-    klaunch(14, (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0)) * (double)n, mdot2_kernel(m), dim3(nb),
-            dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], (const double*)pv[which],
+    klaunch(14, (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0)) * (double)n,
+            mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
+            (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], vp,
             op.null_free, proj_part, rmd, pd);
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
@@ -2107,12 +2117,15 @@ struct Ctx {
                        1.0 / (double)n_free, proj_coef);
     KCHK();
     HIPCHK(hipMemcpyAsync(h_coef + which * NCOEF, proj_coef, sizeof(double) * NCOEF, hipMemcpyDeviceToHost, st));
-    // k_pcomb: X, v read; the new direction, y and x0 (or the cleared accumulator of the coming solve) written
+    // k_pcomb: X, v read; the new direction, y and x0 written (not x0 when the coming solve accumulates its
+    // correction: the first update starts the accumulator, so it needs no clearing either)
     const bool acc_next = which <= 2 && !proj_spmv;
-    klaunch(15, (4.0 * kq + 32.0 + (vdiff ? 8.0 : 0.0)) * (double)n, pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
-            (const ProjT*)projX[which], (int64_t)pld(which), (const double*)proj_coef, (const double*)pv[which],
+    klaunch(15, (4.0 * kq + (acc_next ? 24.0 : 32.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0)) * (double)n,
+            pcomb_kernel(kq), dim3(nb), dim3(BS), (int64_t)n,
+            (const ProjT*)projX[which], (int64_t)pld(which), (const double*)proj_coef, vp,
             op.null_free, projX[which] + pcol(which, kq), y, acc_next ? (double*)nullptr : proj_x0[which],
-            vdiff ? pend_y[which] : (const double*)nullptr, acc_next ? pv[which] : (double*)nullptr);
+            vdiff ? pend_y[which] : (const double*)nullptr, (double*)nullptr);
+    pend_vzero[which] = false;
     KCHK();
     pend_otf[which] = false;
     H.coef_m = kq;

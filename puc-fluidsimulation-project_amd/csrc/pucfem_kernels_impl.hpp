@@ -508,8 +508,9 @@ template <int NR>
 __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, const double* part_pq, int nb_pq,
                                                int stride_pq, const double* scal, const int* ctl, double* part_rr,
                                                float* __restrict__ r32 = nullptr, RedOut ro = RedOut{},
-                                               double* __restrict__ vacc = nullptr) {
-  // vacc (NR = 1, optional): the correction sum_k alpha_k p_k accumulated beside y (the projection's v)
+                                               double* __restrict__ vacc = nullptr, int vfirst = 0) {
+  // vacc (NR = 1, optional): the correction sum_k alpha_k p_k accumulated beside y (the projection's v);
+  // vfirst: the solve's first update, which starts the sum (no read of the buffer)
   __shared__ double sh[4];
   if (ctl[0]) return;
   double alpha[NR], rr[NR];
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(BS) void k_cg_upd(CgVecs<NR> v, int64_t nrows, cons
     for (int c = 0; c < NR; ++c) {
       const double pi = v.pn[c][i];
       stnt(v.y[c] + i, v.y[c][i] + alpha[c] * pi);
-      if (NR == 1 && vacc) stnt(vacc + i, vacc[i] + alpha[c] * pi);
+      if (NR == 1 && vacc) stnt(vacc + i, vfirst ? alpha[c] * pi : vacc[i] + alpha[c] * pi);
       const double r = v.r[c][i] - alpha[c] * v.q[c][i];
       stnt(v.r[c] + i, r);
       if (NR == 1 && r32) stnt(r32 + i, (float)r);
@@ -707,7 +708,7 @@ __global__ __launch_bounds__(BS) void k_cgcg_upd(int64_t n, const double* __rest
     stnt(p + i, pi);
     stnt(s + i, si);
     stnt(y + i, y[i] + alpha * pi);
-    if (vacc) stnt(vacc + i, vacc[i] + alpha * pi);
+    if (vacc) stnt(vacc + i, first ? alpha * pi : vacc[i] + alpha * pi);
     const double rn = r[i] - alpha * si;
     stnt(r + i, rn);
     if (r32) stnt(r32 + i, (float)rn);
@@ -821,7 +822,7 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
     const double br = b[r];
     const double ar = D.rf ? av[r] - D.rf[r] : av[r];
-    const double vr = D.v ? D.v[r] : (D.y ? D.y[r] - D.x0[r] : v[r]);
+    const double vr = D.v ? D.v[r] : (D.y ? D.y[r] - D.x0[r] : (v ? v[r] : 0.0));  // (all null: v = 0)
     ProjT x[M > 0 ? M : 1];
 #pragma unroll
     for (int i = 0; i < M; ++i) x[i] = X[pxi(i, r, ld)];
@@ -903,7 +904,7 @@ __global__ __launch_bounds__(BS) void k_pcomb(int64_t n, const ProjT* __restrict
     ProjT x[M > 0 ? M : 1];
 #pragma unroll
     for (int i = 0; i < M; ++i) x[i] = X[pxi(i, r, ld)];
-    const double vr = yp ? yp[r] - x0[r] : v[r];
+    const double vr = yp ? yp[r] - x0[r] : (v ? v[r] : 0.0);  // (both null: v = 0)
     double sa = 0.0, sc = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
