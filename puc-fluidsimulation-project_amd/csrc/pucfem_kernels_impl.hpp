@@ -3449,7 +3449,12 @@ __global__ __launch_bounds__(BS) void k_cheb_pair(FaceDev fc, MgPairVecs v, floa
         ax = a[0] * x1;
       } else {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) g[q] = c20 * (in[q] ? di : v.dinv[nb[q]]) * v.b[nb[q]];
+        for (int q = 0; q < 6; ++q) {
+          // (a skeleton neighbour's 1 / diag; loaded for every neighbour at a clamped address -- the row's own
+          // entry when in-face -- instead of under a branch per neighbour: 92 -> 86 us isolated, r12d)
+          const float dv = v.dinv[in[q] ? row : nb[q]];
+          g[q] = c20 * (in[q] ? di : dv) * v.b[nb[q]];
+        }
         ax = a[0] * (c20 * di * brow);
         x1 = c20 * di * brow;
         d1 = x1;
