@@ -124,6 +124,7 @@ __device__ __forceinline__ void face_kcoefs(const FaceDev& fc, int32_t lf, const
       const double vs = c[lat::C_VS], g = vs * c[lat::C_DTNU];
       a[0] = vs * c[lat::C_VD] * vs;
 #pragma unroll
+      // (under a branch: loading wsk at every neighbour cost the viscous pair 308 -> 353 us, r12e)
       for (int k = 0; k < 6; ++k) a[1 + k] = (g * k3[k >> 1]) * (in[k] ? vs : fc.wsk[nb[k]]);
     } else {
       a[0] = c[lat::C_KD];
