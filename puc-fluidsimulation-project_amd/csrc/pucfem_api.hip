@@ -20,6 +20,7 @@
 #include <tuple>
 #include <utility>
 #include <vector>
+#include <future>
 #include <map>
 
 #include "pucfem.h"
@@ -485,7 +486,15 @@ struct Ctx {
   bool use_mg = false;
   std::vector<MgLevel> mg;
   double* dKp_raw = nullptr;        // unscaled finest pressure operator on sPp
-  double* dAinv = nullptr;          // dense pseudo-inverse of the coarsest operator (replicated)
+  double* dAinv = nullptr;          // dense pseudo-inverse of the coarse-solve level's operator (replicated)
+  float* dAinv32 = nullptr;         // its fp32 copy (the fp32 V-cycle, when that level is not the coarsest)
+  // The V-cycle's dense coarse solve runs on level mg_dense_l: 0 (the coarsest, mesh_fine's 1,067 nodes), or with
+  // PUCFEM_MG_DENSE_LEVEL=1 (measurement knob) on level 1: the ~3.6k-node level's 8 latency-bound launches per V-cycle
+  // and the coarsest's dense solve replaced by one fp32 dense product.  At L7: 238 -> 214 launches per step, the
+  // window +0.3 %, steady +0.6 % (within the spread), but the per-step parity margin at L7 5.7x / 7.5x -> 3.6x / 5.2x
+  // (the iterates take another path to the tolerance) and setup +1 s (r12f / r12g): off.
+  int mg_dense_l = 0;
+  std::future<std::vector<double>> dense_fut;  // level mg_dense_l > 0: its inverse, computed beside the rest of setup
   bool mg_single = false;                        // fp32 V-cycle
   double* z = nullptr;              // preconditioned residual (finest; the fp64 V-cycle's)
   // the fp32 V-cycle's z: its last smoothing step computes in fp32, so z is fp32-exact -- stored as such,
@@ -1533,13 +1542,18 @@ struct Ctx {
     const HFace& hf = finest ? fP : L.hA;
     T* xa = B.x;
     T* xb = B.x2;
-    if (l == 0) {
+    if (l == mg_dense_l) {
       if constexpr (std::is_same<T, TB>::value) {
-        // coarsest: dense pseudo-inverse (replicated on every rank of a multi-rank run)
+        // coarse solve: dense pseudo-inverse (replicated on every rank of a multi-rank run)
         const i64 N0 = (i64)L.ord.new2old.size();
-        algo_bytes += 8.0 * (double)N0 * (double)N0 + 2.0 * sizeof(T) * (double)N0;
-        hipLaunchKernelGGL(k_dense_mv<T>, dim3((unsigned)std::min<i64>(4096, (N0 + 3) / 4)), dim3(BS), 0, st, N0,
-                           dAinv, b, xa, ctl);
+        const dim3 g((unsigned)std::min<i64>(4096, (N0 + 3) / 4));
+        if (std::is_same<T, float>::value && dAinv32) {
+          algo_bytes += 4.0 * (double)N0 * (double)N0 + 2.0 * sizeof(T) * (double)N0;
+          hipLaunchKernelGGL((k_dense_mv<T, float>), g, dim3(BS), 0, st, N0, (const float*)dAinv32, b, xa, ctl);
+        } else {
+          algo_bytes += 8.0 * (double)N0 * (double)N0 + 2.0 * sizeof(T) * (double)N0;
+          hipLaunchKernelGGL(k_dense_mv<T>, g, dim3(BS), 0, st, N0, (const double*)dAinv, b, xa, ctl);
+        }
         KCHK();
         return xa;
       } else {
@@ -2749,6 +2763,31 @@ void mg_refine(Ctx& c) {
     }
   }
 }
+double diag_of(const Csr& A, const std::vector<double>& val, i64 g);
+// the dense pseudo-inverse of a coarse level's merged operator, constants regularised on the free dofs
+static std::vector<double> dense_coarse_inverse(const MgLevel& L0) {
+  const i64 n0 = L0.mesh.N;
+  require(n0 <= 8192, "multigrid coarse level too large for the dense coarse solve (<= 8192 nodes)");
+  std::vector<double> D(n0 * n0, 0.0);
+  const Csr& A = L0.Pp;
+  double dsum = 0.0;
+  i64 nf = 0;
+  for (i64 r = 0; r < n0; ++r) {
+    for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) D[r * n0 + A.col[k]] += A.val[k];
+    if (L0.master_of[r] < 0) {
+      dsum += diag_of(A, A.val, r);
+      ++nf;
+    }
+  }
+  const double cc = dsum / (double)nf / (double)nf;
+  for (i64 i = 0; i < n0; ++i)
+    if (L0.master_of[i] < 0)
+      for (i64 j = 0; j < n0; ++j)
+        if (L0.master_of[j] < 0) D[i * n0 + j] += cc;
+  require(spd_inverse(D, n0), "coarse operator is not SPD after regularisation");
+  return D;
+}
+
 void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
   const int Lv = c.mg_levels;
   for (int l = 0; l < Lv; ++l) {
@@ -2781,6 +2820,13 @@ void build_mg_host(Ctx& c, SetupClock& clk) {  // (after mg_refine)
     L.P = Csr();  // only the merged operator is needed on coarse levels
   }
   clk.mark("  mg: coarse level operators");
+  // the level of the dense coarse solve; level 1's inverse (~3.6k rows: ~1.5 s of host work) runs beside the rest of
+  // setup from here
+  c.mg_dense_l = 0;
+  if (const char* e = std::getenv("PUCFEM_MG_DENSE_LEVEL"))
+    c.mg_dense_l = std::max(0, std::min(std::min(1, Lv - 1), std::atoi(e)));
+  if (c.mg_dense_l > 0)
+    c.dense_fut = std::async(std::launch::async, [&c] { return dense_coarse_inverse(c.mg[c.mg_dense_l]); });
   MgLevel& F = c.mg[Lv];
   F.ord = c.ord;
   if (c.lattice) F.latl = std::move(c.lat_fine);
@@ -3523,29 +3569,12 @@ void build(Ctx& c) {
       }
     }
     clk.mark("  dev: lattice face tables");
-    // coarsest: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
+    // coarse solve: dense pseudo-inverse of the merged operator, constants regularised on the free dofs
     {
-      MgLevel& L0 = c.mg[0];
-      const i64 n0 = L0.mesh.N;
-      require(n0 <= 8192, "multigrid coarse level too large for the dense coarse solve (<= 8192 nodes)");
-      std::vector<double> D(n0 * n0, 0.0);
-      const Csr& A = L0.Pp;
-      double dsum = 0.0;
-      i64 nf = 0;
-      for (i64 r = 0; r < n0; ++r) {
-        for (i64 k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) D[r * n0 + A.col[k]] += A.val[k];
-        if (L0.master_of[r] < 0) {
-          dsum += diag_of(A, A.val, r);
-          ++nf;
-        }
-      }
-      const double cc = dsum / (double)nf / (double)nf;
-      for (i64 i = 0; i < n0; ++i)
-        if (L0.master_of[i] < 0)
-          for (i64 j = 0; j < n0; ++j)
-            if (L0.master_of[j] < 0) D[i * n0 + j] += cc;
-      require(spd_inverse(D, n0), "coarse operator is not SPD after regularisation");
+      const std::vector<double> D =
+          c.dense_fut.valid() ? c.dense_fut.get() : dense_coarse_inverse(c.mg[c.mg_dense_l]);
       c.dAinv = c.upload(D);
+      if (c.mg_dense_l > 0) c.dAinv32 = c.upload(std::vector<float>(D.begin(), D.end()));
     }
   }
   c.block_cg = c.prm.solver_path != 1;

@@ -3648,13 +3648,13 @@ __global__ __launch_bounds__(BS) void k_transfer(SellDev M, FaceDev fc, const T*
 }
 
 // coarse solve: y = Ainv x (dense, n x n row-major fp64, replicated); one wave per row
-template <typename T>
-__global__ __launch_bounds__(BS) void k_dense_mv(int64_t n, const double* __restrict__ Ainv, const T* __restrict__ x,
+template <typename T, typename MT = double>
+__global__ __launch_bounds__(BS) void k_dense_mv(int64_t n, const MT* __restrict__ Ainv, const T* __restrict__ x,
                                                  T* __restrict__ y, const int* ctl) {
   if (ctl && ctl[0]) return;
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
-    const double* a = Ainv + row * n;
+    const MT* a = Ainv + row * n;
     double acc = 0.0;
     for (int64_t j = lane; j < n; j += 64) acc += a[j] * (double)x[j];
     acc = wave_sum(acc);
