@@ -2023,19 +2023,26 @@ struct Ctx {
     KCHK();
   }
   // sb_fused: the preceding k_div reduced sum(braw) into redbuf slot 3 itself (div_rhs)
+  // PUCFEM_RHS_FUSE=0 (measurement knob): the pressure right-hand side always in its own pass (k_pres_rhs)
+  bool rhs_fuse = !(std::getenv("PUCFEM_RHS_FUSE") && std::atoi(std::getenv("PUCFEM_RHS_FUSE")) == 0);
   int pressure(double* yst, double* pout, int which, bool sb_fused = false) {  // StokesColor.py:554-555 (restated)
     const int nb = div_grid();
     Red sb{redbuf + 24, 1, 1};
     if (!sb_fused) sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
     const i64 n = lp.n_own;
     const double* sc = (use_mg || dense) ? nullptr : dsp;  // MG and dense paths solve the unscaled system
-    algo_bytes += 24.0 * (double)n;  // braw, slave_of, master_of read; bh written
-    hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
-                       sb.p, sb.nb, 1.0 / (double)n_free, bh);
-    KCHK();
-    if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
     const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
-    const bool projected = proj && project_guess(proj_slot(which), bh, yst);
+    // with a projected guess k_mdot2 (the first pass over the rows) forms the right-hand side itself
+    const bool rhs_in_mdot = proj && rhs_fuse && !sc && proj_pend[proj_slot(which)];
+    if (!rhs_in_mdot) {
+      algo_bytes += 24.0 * (double)n;  // braw, slave_of, master_of read; bh written
+      hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
+                         sb.p, sb.nb, 1.0 / (double)n_free, bh);
+      KCHK();
+    }
+    if (!prm.warm_start) HIPCHK(hipMemsetAsync(yst, 0, sizeof(double) * nloc, st));
+    const RhsIn rin{braw, dslave_of, sb.p, 1.0 / (double)n_free, bh};
+    const bool projected = proj && project_guess(proj_slot(which), bh, yst, rhs_in_mdot ? &rin : nullptr);
     const bool acc = projected && !proj_spmv;  // the CG accumulates v (k_pcomb cleared pv)
     int it;
     if (dense) {
@@ -2094,7 +2101,8 @@ struct Ctx {
   // 4m + 15.  A full basis is re-seeded first (proj_reseed).  With an empty basis the solve keeps
   // its warm start (x0 = 0).
   // returns whether a guess was projected (false: the first solve of the basis keeps its warm start)
-  bool project_guess(int which, const double* b, double* y) {
+  // rin: the right-hand side b is formed (and stored) by k_mdot2 from the divergence instead of read
+  bool project_guess(int which, const double* b, double* y, const RhsIn* rin = nullptr) {
     const i64 n = lp.n_own;
     const ProjOp op = proj_op(which);
     ProjHist& H = proj_hist[which];
@@ -2116,10 +2124,13 @@ struct Ctx {
     const PendDir pd = otf ? PendDir{vz0 ? nullptr : pend_y[which], (const double*)proj_x0[which], (const double*)cg_r[0],
                                      pend_acc[which] ? vp : nullptr}
                            : PendDir{nullptr, nullptr, nullptr, nullptr};
-    klaunch(14, (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0)) * (double)n,
+    // (rin: braw and slave_of read and b written instead of b read)
+    klaunch(14,
+            (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0) + (rin ? 12.0 : 0.0)) *
+                (double)n,
             mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], vp,
-            op.null_free, proj_part, rmd, pd);
+            op.null_free, proj_part, rmd, pd, rin ? *rin : RhsIn{});
     if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);

@@ -803,6 +803,16 @@ __global__ __launch_bounds__(BS) void k_reseed(int64_t n, const ProjT* __restric
 // from the residuals then does not match that v, the new direction is mis-normalised and the basis decays
 // (driver-window rtol 5e-8 runs went from 0-1 to 6 iterations per solve, profiles/r11_projection.txt).
 // Without D.v (the first direction, whose guess was 0): v = D.y - D.x0.
+// the pressure right-hand side formed in k_mdot2 from the divergence (k_pres_rhs's operations on the unscaled
+// multigrid path: slaves merged into their masters, zero at slave rows, the mean over the free rows removed) and
+// stored for the solve; braw null: k_mdot2 reads the stored b
+struct RhsIn {
+  const double* braw;
+  const int32_t* slave_of;
+  const double* sum;  // sum of braw (a reduced scalar)
+  double inv_nfree;
+  double* bh;
+};
 struct PendDir {
   const double* y;   // the last solve's solution (with x0; used when v is null)
   const double* x0;  // its guess
@@ -813,15 +823,28 @@ template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
                                               const double* __restrict__ v, const int32_t* __restrict__ master_of,
-                                              double* part, RedOut ro, PendDir D) {
+                                              double* part, RedOut ro, PendDir D, RhsIn R = RhsIn{}) {
   constexpr int NA = 2 * M + 4;
   __shared__ double sh[NA][4];
   double acc[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+  const double mean = R.braw ? R.sum[0] * R.inv_nfree : 0.0;
   const int64_t step = (int64_t)gridDim.x * BS;
   for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
-    const double br = b[r];
+    double br;
+    if (R.braw) {  // (k_pres_rhs's row)
+      if (master_of[r] >= 0) {
+        br = 0.0;
+      } else {
+        br = R.braw[r];
+        if (R.slave_of[r] >= 0) br += R.braw[R.slave_of[r]];
+        br = br - mean;
+      }
+      stnt(R.bh + r, br);
+    } else {
+      br = b[r];
+    }
     const double ar = D.rf ? av[r] - D.rf[r] : av[r];
     const double vr = D.v ? D.v[r] : (D.y ? D.y[r] - D.x0[r] : (v ? v[r] : 0.0));  // (all null: v = 0)
     ProjT x[M > 0 ? M : 1];
