@@ -474,6 +474,8 @@ struct Ctx {
   // PUCFEM_MG_PAIR=0 runs every step as its own k_cheb (a measurement knob); a third x buffer and a second
   // d buffer of the finest level are allocated on first use
   bool mg_pair = !(std::getenv("PUCFEM_MG_PAIR") && std::atoi(std::getenv("PUCFEM_MG_PAIR")) == 0);
+  // PUCFEM_MG_PAIR_LEVELS (measurement knob): the step pairs on the finest k levels (default 1: the finest only)
+  int mg_pair_levels = std::getenv("PUCFEM_MG_PAIR_LEVELS") ? std::max(1, std::atoi(std::getenv("PUCFEM_MG_PAIR_LEVELS"))) : 1;
   int64_t mg_pairs = 0;
   float* mgp_x = nullptr;
   float* mgp_d = nullptr;
@@ -1416,7 +1418,7 @@ struct Ctx {
     bool pairs = false;
     if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
       // (finest level only: pairs on L6 / L5 too measured neutral to -0.7 %, r10m)
-      pairs = mg_pair && finest && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
+      pairs = mg_pair && (int)(&mg.back() - &L) < mg_pair_levels && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
     if (pairs && !mgp_x) {  // (sized for the finest level: every pair level uses them in turn)
       mgp_x = dalloc<float>(mg.back().nloc);
       mgp_d = dalloc<float>(mg.back().nloc);
