@@ -409,6 +409,28 @@ def test_pending_pressure_directions_equal_stored(monkeypatch, refine, shared):
     b.close()
 
 
+@pytest.mark.parametrize("refine", [3, 5])
+def test_pressure_rhs_in_projection_pass_equals_separate(monkeypatch, refine):
+    """The pressure right-hand side (StokesColor.py:554, restated: slaves merged into masters, the mean over the free
+    rows removed) formed inside the projection's first pass (k_mdot2) on projected solves is bit-identical to the
+    separate k_pres_rhs pass, over step() calls of several sizes including solves that pass at their guess; the
+    pressure fields read back agree too."""
+    mesh = pf.load_mesh("fine", refine=refine)
+    a = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.setenv("PUCFEM_RHS_FUSE", "0")
+    b = stokes(mesh, tol=S.Tolerances.production())
+    sa, sb = [], []
+    for k in (1, 5, 14):
+        sa += a.step(k)
+        sb += b.step(k)
+    assert [(s.it_visc, s.it_p, s.it_p2) for s in sa] == [(s.it_visc, s.it_p, s.it_p2) for s in sb]
+    assert np.array_equal(a.u, b.u) and np.array_equal(a.c, b.c)
+    assert np.array_equal(a.field(L.F_P), b.field(L.F_P))
+    assert np.array_equal(a.field(L.F_P2), b.field(L.F_P2))
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("records", ["0", "1"])
 def test_knn_radii_device_equals_host(monkeypatch, records):
     """The semi-Lagrangian fast-accept radii (k-NN distances of every centroid and vertex) are built on
