@@ -144,13 +144,14 @@ def main():
             summary[key] = sum(res["kernels"][k]["hbm_bytes_per_launch"] * res["kernels"][k]["dispatches_fetch"]
                                for k in ks) / n
     # the projection passes' bytes depend on the basis size M (their template argument): the ratio of PMC to
-    # algorithmic bytes over the instances with M >= 16 ((4 M + 32) n for both with the production path's pending
-    # directions -- the CG's accumulated v and A v = r0 - r_final formed in k_mdot2; PUCFEM_P_FROM_Y=0 runs:
-    # 24 / 32), which bench.py applies to the algorithmic bytes of the launches it timed
+    # algorithmic bytes over the instances with M >= 16 ((4 M + 44) n for k_mdot2 -- b, the CG's accumulated v and
+    # A v = r0 - r_final, with the pressure right-hand side formed in the pass: braw and slave_of read, b written
+    # (+12) -- and (4 M + 24) n for k_pcomb with the production path's pending directions; PUCFEM_P_FROM_Y=0 runs:
+    # 36 / 32), which bench.py applies to the algorithmic bytes of the launches it timed
     ratios = {}
     pend = os.environ.get("PUCFEM_P_FROM_Y", "1") != "0"
     if nrows:
-        for key, extra in (("k_mdot2", 32.0 if pend else 24.0), ("k_pcomb", 32.0)):
+        for key, extra in (("k_mdot2", 44.0 if pend else 36.0), ("k_pcomb", 24.0 if pend else 32.0)):
             pmc = alg = 0.0
             for k, e in res["kernels"].items():
                 mm = re.match(r"^" + key + r"<(\d+)>", k)
