@@ -234,7 +234,8 @@ def main():
             "pressure_guess": (f"projection onto up to {a.proj_k} solution directions"
                                + (" per solve" if a.proj_separate else " shared by both solves")) if a.proj_k else "previous solution",
             "viscous_guess": f"projection onto up to {a.proj_k_visc} solution directions" if a.proj_k_visc else "u^n",
-            "parallelism": f"y-slab domain decomposition x{world} (RCCL)",
+            "parallelism": (f"y-slab domain decomposition x{world} (RCCL halo + all-reduce)" if world > 1
+                            else "single GPU (the y-slab partition has one part; no RCCL)"),
         },
         "cg_iters_per_s": cg_iters / elapsed,
         "cg_iters_counted": "pressure PCG iterations (both solves)" + ("" if visc_cheb else " + 2 x viscous CG iterations"),
@@ -429,9 +430,10 @@ def cpu_baseline(pf, level, stats, l5=None):
     Threads: the element loops (divergence, gradient), the semi-Lagrangian k-NN query and per-node tests
     run on `cores` threads (the box's CPU share, at most 16), the two viscous SuperLU solves on two; the
     pressure SuperLU solves are single-threaded (SuperLU).  The benchmarked mesh (L7) is too large for the
-    direct solves' fill-in, so the L5 rate is reported as measured -- beside the GPU's own L5 rate (same
-    configuration: `same_config_ratio`) -- and, for the headline, scaled linearly in the node count to L7
-    (a lower bound on the CPU cost: the sparse LU solves grow faster than linearly)."""
+    direct solves' fill-in, so `value` is the rate MEASURED at L5 (its mesh in `mesh`) -- not the
+    benchmarked mesh's: a ratio against the headline must use `same_config` (GPU and CPU both at L5) or
+    `extrapolated_to_benchmark_mesh` (the L5 rate scaled linearly in the node count to L7, a lower bound on
+    the CPU cost: the sparse LU solves grow faster than linearly), never value / cpu_baseline.value."""
     import oracle as O
 
     cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))

@@ -273,7 +273,8 @@ int pucfem_info(void* ctx, int64_t* out12);
    basis sizes of the two pressure solves, [5] extrapolation order of the viscous warm start in use,
    [6] projection basis capacity (0: off), [7] bit 0: the operators are lattice stencils on the face
    interiors (pucfem_params.assembled = 0 with a hierarchy; clear: every row is a stored SELL row),
-   bit 1: the semi-Lagrangian point location uses the lattice locator (else per-triangle records) */
+   bit 1: the semi-Lagrangian point location uses the lattice locator (else per-triangle records),
+   bit 7: pressure PCG iterations ran in the single-reduction (Chronopoulos-Gear) form */
 int pucfem_path_info(void* ctx, int64_t* out8);
 /* multi-rank data flow of the last step: out[0] dye values this rank received in the wide halo before
    the semi-Lagrangian step, out[1] the values a full all-gather of the dye would have received

@@ -804,11 +804,13 @@ struct Ctx {
       const double sl_bytes = (16.0 + 16.0 + 8.0 + 4.0 + 8.0 + 8.0 + (w ? 8.0 : 0.0) + 8.0) * (double)n;
       klaunch(4, sl_bytes, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
+      kl_lds = 0;  // (the knob's LDS is k_sl's alone: k_sl_slow has static LDS of its own)
       klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
     } else {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
+      kl_lds = 0;
       klaunch(8, 0.0, k_sl_slow<LocDev>, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt,
               cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
     }
@@ -1650,7 +1652,7 @@ struct Ctx {
   bool use_cgcg() const { return cgcg_env >= 0 ? cgcg_env != 0 : dist(); }
   double* part_cc = nullptr;  // CGCG_NV x MAXB partials
   double* cgcg_sc = nullptr;  // k_cgcg_coef's scalars (8)
-  int64_t cgcg_iters = 0;     // iterations run in the single-reduction form (pucfem_comm_info)
+  int64_t cgcg_iters = 0;     // iterations run in the single-reduction form (pucfem_path_info bit 7)
   // preconditioned CG on the unscaled merged pressure operator (finest level = dPp / dKp_raw)
   // prm.proj_shared: both pressure solves of a step project onto ONE basis (the same merged operator, so
   // one A-orthonormal basis serves both) that collects the solutions of both -- slot 1 for both; else a
@@ -4934,7 +4936,7 @@ int pucfem_path_info(void* ctx, int64_t* o) {
     o[6] = c.proj_k;
     o[7] = (c.lattice ? 1 : 0) | (c.lat_sl ? 2 : 0) |
            (!c.dense && !block && c.visc_solver == 0 && c.visc_R < 0.25 ? 4 : 0) | (c.visc_check_fail ? 8 : 0) |
-           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.p_from_y ? 64 : 0);
+           (c.visc_pairs ? 16 : 0) | (c.mg_pairs ? 32 : 0) | (c.p_from_y ? 64 : 0) | (c.cgcg_iters ? 128 : 0);
   });
 }
 

@@ -679,7 +679,11 @@ __global__ void k_cgcg_coef(const double* __restrict__ red8, const double* __res
   sc[1] = beta;
   sc[3] = alpha;
   sc[4] = gamma;
-  if (rho1 <= tol2 * b2) {
+  // the recurrence's estimate decides only when it is resolved: its rounding error is ~eps (rho + 2 |alpha rs| +
+  // alpha^2 ss), so a value within a few of those (or negative, from cancellation) says nothing about the accepted
+  // iterate -- the next iteration's exact lagged rho decides then
+  const double floor1 = 16.0 * 2.220446049250313e-16 * (rho + 2.0 * fabs(alpha * rs) + alpha * alpha * ss);
+  if (rho1 > floor1 && rho1 <= tol2 * b2) {
     ctl[0] = 1;
     ctl[1] = it + 1;
   }
@@ -762,9 +766,6 @@ constexpr int PROJ_KEEP_MAX = 16;
 struct QMat {
   double q[PROJ_KEEP_MAX][PROJ_MAX];
 };
-// The re-seed coefficients are staged in LDS once per block, and a row's m basis values are all loaded before the
-// sums (the j loop with one load per step waited one memory round trip per vector: 1.18 ms at L7, r10z); the per-row
-// operations and their order are unchanged (acc_i += q_ij x_j, j ascending)
 // The re-seed coefficients are staged in LDS once per block (uniform loads of all 16 x 32 of them per row from
 // device memory: 1.18 ms at L7 in-step, r10z; isolated 0.77 ms with LDS, r11q, where all 32 basis loads issued first
 // and then the sums took 1.93 ms); the per-row operations and their order are unchanged

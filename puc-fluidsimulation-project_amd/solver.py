@@ -238,7 +238,8 @@ class Context:
                     visc_check_failed=bool(o[7] & 8),
                     visc_step_pairs=bool(o[7] & 16),
                     mg_step_pairs=bool(o[7] & 32),
-                    pending_pressure_directions=bool(o[7] & 64))
+                    pending_pressure_directions=bool(o[7] & 64),
+                    single_reduction_pcg=bool(o[7] & 128))
 
     def visc_interval(self):
         """[lo, hi] of the viscous Chebyshev iteration (pucfem_visc_interval)."""
