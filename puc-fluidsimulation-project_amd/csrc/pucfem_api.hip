@@ -86,7 +86,23 @@ struct DevSell {
   int32_t wrap = 0;        // c16 modulus (local vector length)
   int32_t* rows = nullptr; // row list (lattice operators: the skeleton rows), else null
   int64_t n_own = 0;       // owned rows of the vector space (0: nrows)
+  // deep halos (Sell::gk0): slices [nslices, nslices_g) hold ghost rows one layer out, which the launches that
+  // compute them redundantly (step pairs, residuals, last smoothing steps on W > 1 ranks) include: with_ghosts()
+  int64_t nslices_g = 0;
   SellDev view() const { return SellDev{off, w, col, nslices, nrows, c16, wrap, rows, n_own ? n_own : nrows}; }
+  bool has_ghost_rows() const { return nslices_g > nslices; }
+  DevSell with_ghosts() const {
+    DevSell d = *this;
+    if (nslices_g > nslices) d.nslices = nslices_g;
+    return d;
+  }
+  // after a row-listed upload of S: the own rows' slices only by default, the ghost rows' ones behind with_ghosts()
+  void ghost_slices(const pucfem::Sell& S) {
+    if (S.gk0 < 0) return;
+    nslices_g = S.nslices;
+    nslices = S.nslices_own;
+    nrows = S.nrows - (int64_t)S.grow.size();
+  }
   double idx_bytes() const { return c16 ? 2.0 : 4.0; }  // per stored entry
   double row_bytes() const { return rows ? 4.0 : 0.0; }  // per row (the row list)
   int64_t own() const { return n_own ? n_own : nrows; }   // rows of the vector space
@@ -242,6 +258,16 @@ struct MgLevel {
   // smooths the whole level, no halos); the restriction into the finest replicated level computes
   // the rows of the strip partition (rs) and an all-gather (broadcast group) completes the vector
   bool rep = false;
+  // deep halos (W > 1, lattice, PUCFEM_DEEP_HALO): the plan's ghosts reach two layers out (make_local_plan2's G2) and
+  // the operator's SELL carries the ghost rows one layer out (g1, global ids) behind DevSell::with_ghosts().  Then
+  // - a step pair runs its first step on those rows too (one exchange of x for two steps; pairs at W > 1),
+  // - res_deep: the residual runs on them too, so the restriction reads no exchanged residual,
+  // - the post-smoothing's last step runs on them (x and d exchanged before it, as x alone was), so its output is
+  //   current at the ghosts the next consumer gathers: z for the PCG's A z (finest), x for the prolongation into
+  //   the finer level (xc_deep, on that finer level: its prolongation's coarse columns lie in own + G1).
+  // Every rank takes the same path (the flags are all-reduced at build).
+  std::vector<i32> g1;
+  bool deep = false, res_deep = false, xc_deep = false;
   i64 r_r0 = 0;  // first row of this level's restriction operator (rows live on level l-1)
   i64 own0(int rank) const { return rep ? 0 : rs[rank]; }
   // lattice face parts (Ctx::lattice): the faces whose interiors are this rank's rows of this level,
@@ -448,6 +474,10 @@ struct Ctx {
 
   // ---- lattice operators (pucfem_lattice.hpp): multigrid hierarchies with faces of interior nodes
   bool lattice = false;
+  // deep halos on W > 1 ranks (MgLevel::deep; PUCFEM_DEEP_HALO=0 keeps one-layer halos and single smoothing steps,
+  // a test / measurement knob)
+  bool deep_halo = !(std::getenv("PUCFEM_DEEP_HALO") && std::atoi(std::getenv("PUCFEM_DEEP_HALO")) == 0);
+  bool z_cur = false;  // the finest level's last smoothing step wrote z at the ghost rows one layer out too
   Macro macro;
   LatticeLevel lat_fine;  // the finest level's layout until build_mg_host moves it into mg.back()
   HFace fK, fVisc, fP;  // finest level: K / Gx / Gy (plain table), scaled A_visc (plain), pressure (merged)
@@ -599,6 +629,8 @@ struct Ctx {
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_coef) (void)hipHostFree(h_coef);
       if (h_pinned) (void)hipHostFree(h_pinned);
+      if (h_yr_pin) (void)hipHostFree(h_yr_pin);
+      if (ev_yr) (void)hipEventDestroy(ev_yr);
       for (int k = 0; k < 2; ++k) {
         if (stage[k]) (void)hipHostFree(stage[k]);
         if (stage_ev[k]) (void)hipEventDestroy(stage_ev[k]);
@@ -723,6 +755,7 @@ struct Ctx {
   // the k_sl blocks resident per CU (160 KB / bytes), leaving wave slots and registers to the main stream
   size_t sl_lds = std::getenv("PUCFEM_SL_LDS") ? (size_t)std::max(0, std::min(65536, std::atoi(std::getenv("PUCFEM_SL_LDS"))))
                                                : 0;
+  bool sl_wave = !(std::getenv("PUCFEM_SL_WAVE") && std::atoi(std::getenv("PUCFEM_SL_WAVE")) == 0);
   int nb_sl(i64 n) const {
     return (int)std::max<i64>(1, std::min<i64>(sl_cap, (n + 4 * 64 - 1) / (4 * 64)));
   }
@@ -805,8 +838,15 @@ struct Ctx {
       klaunch(4, sl_bytes, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
       kl_lds = 0;  // (the knob's LDS is k_sl's alone: k_sl_slow has static LDS of its own)
-      klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
-              dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
+      // the queued rows: one wave per point (k_sl_wave; 1,024 waves take k_sl's blocks in turn), or -- with the
+      // fused reductions (a measurement knob) or PUCFEM_SL_WAVE=0 -- k_sl_slow on k_sl's grid, one lane per point
+      if (sl_wave && !ro.out)
+        klaunch(8, 0.0, k_sl_wave, dim3(std::max(1, std::min(256, nb / 8))), dim3(BS), M, llgrid, cgrid, (int64_t)row0,
+                (int64_t)n, vx, vy, dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt,
+                (int32_t)nb);
+      else
+        klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
+                dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
     } else {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
@@ -890,29 +930,42 @@ struct Ctx {
     comm->group_end(st);
   }
   template <typename T>
-  void mg_halo(MgLevel& L, T* a) {
-    if (&L == &mg.back()) halo_lp(lp, dsend, bufs<T>(L).sendbuf, nsend, a);
-    else halo_lp(L.lp, L.dsend, bufs<T>(L).sendbuf, L.nsend, a);
+  void mg_halo(MgLevel& L, T* a, T* b = nullptr) {  // (two vectors: one grouped exchange; sendbuf holds 2 nsend)
+    if (&L == &mg.back()) halo_lp(lp, dsend, bufs<T>(L).sendbuf, nsend, a, b);
+    else halo_lp(L.lp, L.dsend, bufs<T>(L).sendbuf, L.nsend, a, b);
   }
   // Before the semi-Lagrangian step on W > 1 ranks: refresh the dye replica where this step's
   // back-traced points can reach -- the strips within dt max|u_y| + (largest triangle height) of each
   // rank's own y extent -- with point-to-point copies of contiguous internal-id ranges (every rank's
   // own segment is current: its SL wrote it).  Replaces the all-gather of the whole field (SURVEY.md
   // §8e: the departure distance bounds the gather).
-  void dye_halo(const double* vy, double dt) {
-    if (!dist()) return;
+  // The wide halo in two halves.  dye_range_start: every rank's range of back-traced y (StokesColor.py:361-372),
+  // all-gathered as a max-reduction of a 2 W vector holding (1 - min, max) in each rank's slot, copied to pinned
+  // host memory behind an event.  dye_halo_exchange: once that copy has landed, the point-to-point copies of the
+  // strip ranges each rank reads.  The step (stokes_step) queues the first half at its end and the second half at
+  // the next step, after that step's viscous solve, whose host round trip has seen the copy land -- no blocking
+  // read of its own (round 5 synchronised the stream here every step).
+  double* h_yr_pin = nullptr;  // 2 W (pinned)
+  hipEvent_t ev_yr = nullptr;
+  void dye_range_start(const double* vy, double dt) {
     const i64 n = lp.n_own;
     const int nb = nb_rows(n);
-    // every rank's range of back-traced y (StokesColor.py:361-372), all-gathered as a max-reduction
-    // of a 2 W vector holding (1 - min, max) in each rank's slot
+    if (!h_yr_pin) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_yr_pin), sizeof(double) * 2 * world));
+      HIPCHK(hipEventCreateWithFlags(&ev_yr, hipEventDisableTiming));
+    }
     hipLaunchKernelGGL(k_yrange, dim3(nb), dim3(BS), 0, st, n, my + lp.r0, vy, dt, part_u);
     KCHK();
     hipLaunchKernelGGL(k_reduce, dim3(2), dim3(RB), 0, st, part_u, nb, MAXB, 2, 1, yr_own);
     hipLaunchKernelGGL(k_place2, dim3(1), dim3(64), 0, st, world, rank, (const double*)yr_own, yr_all);
     KCHK();
     comm->allreduce(yr_all, 2 * (size_t)world, true, st);
-    HIPCHK(hipMemcpyAsync(h_yr.data(), yr_all, sizeof(double) * 2 * world, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyAsync(h_yr_pin, yr_all, sizeof(double) * 2 * world, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(ev_yr, st));
+  }
+  void dye_halo_exchange() {
+    wait_event(ev_yr);  // (at the step's use: long complete, a query)
+    std::copy(h_yr_pin, h_yr_pin + 2 * world, h_yr.begin());
     const i64 S = (i64)strip_ylo.size();
     auto need = [&](int j, i64& a, i64& b) {  // internal-id range rank j reads: the strips that meet
       // its back-traced y range widened by a triangle height (the located triangle's vertices)
@@ -1080,19 +1133,23 @@ struct Ctx {
   dbl2 *vx2[3] = {nullptr, nullptr, nullptr}, *vb2 = nullptr;
   flt2* vd2[2] = {nullptr, nullptr};
   // halo of an interleaved vector (both components of each ghost row)
-  void halo2(dbl2* a) {
+  void halo2(dbl2* a, dbl2* b = nullptr) {  // (b: a second interleaved vector in the same grouped exchange)
     const LocalPlan& P = lp;
     if (!dist() || (P.send_peer.empty() && P.recv_peer.empty())) return;
     if (nsend > 0) {
       hipLaunchKernelGGL(k_pack<dbl2>, dim3(grid_ew(nsend)), dim3(BS), 0, st, nsend, dsend, (const dbl2*)a,
-                         (const dbl2*)nullptr, reinterpret_cast<dbl2*>(dsendbuf));
+                         (const dbl2*)b, reinterpret_cast<dbl2*>(dsendbuf));
       KCHK();
     }
     comm->group_start();
-    for (size_t k = 0; k < P.send_peer.size(); ++k)
+    for (size_t k = 0; k < P.send_peer.size(); ++k) {
       comm->send(dsendbuf + 2 * P.send_off[k], 2 * P.send_cnt[k], P.send_peer[k], st);
-    for (size_t k = 0; k < P.recv_peer.size(); ++k)
+      if (b) comm->send(dsendbuf + 2 * (nsend + P.send_off[k]), 2 * P.send_cnt[k], P.send_peer[k], st);
+    }
+    for (size_t k = 0; k < P.recv_peer.size(); ++k) {
       comm->recv(reinterpret_cast<double*>(a + P.n_own + P.recv_off[k]), 2 * P.recv_cnt[k], P.recv_peer[k], st);
+      if (b) comm->recv(reinterpret_cast<double*>(b + P.n_own + P.recv_off[k]), 2 * P.recv_cnt[k], P.recv_peer[k], st);
+    }
     comm->group_end(st);
   }
   // PUCFEM_VISC_SPEC=0 (measurement knob): no speculative finish ahead of the |r_0| round trip (see vcheb)
@@ -1103,16 +1160,24 @@ struct Ctx {
     if (fin_done) *fin_done = false;
     const FaceDev fc = hf.part();
     const int nb = grid_part(fc, A);
-    // step pairs (k_vcheb_pair): one rank, a face part of lattice size <= VP_HALO
-    const bool pairs = visc_pair && !dist() && hf.items > 0 && fc.n <= VP_HALO &&
-                       nb_for(A.nslices) + hf.items <= MAXB;  // (the check's partials of both halves)
+    // step pairs (k_vcheb_pair): a face part of lattice size <= VP_HALO.  On W > 1 ranks only the solve's first pair
+    // (0, 1), whose first step also runs on the ghost rows one layer out (deep halos: x and b exchanged two layers
+    // out together, one exchange for the two steps); later pairs would need d exchanged too, so single steps
+    const bool deepv = dist() && A.has_ghost_rows() && use_mg && mg.back().deep;
+    const DevSell Ag = A.with_ghosts();  // (= A without ghost rows)
+    const int nbs = nb_for(Ag.nslices);  // a pair's SELL grids (its first launch covers the ghost rows)
+    const bool pairs_ok = visc_pair && hf.items > 0 && fc.n <= VP_HALO &&
+                          nbs + hf.items <= MAXB;  // (the check's partials of both halves)
+    const bool pairs = pairs_ok && !dist();
     dbl2* xa = y;
     dbl2* xb = vx2[1];
     dbl2* xc = vx2[2];  // step pairs: x_{a+2}
     flt2* dcur = vd2[0];  // the fp32 increments d (in place for single steps)
     flt2* dalt = vd2[1];  // step pairs: d_{a+2}
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st));
-    halo2(xa);
+    const bool pair0 = (pairs || (pairs_ok && deepv)) && !ro(redbuf, CNT_VCHEB, 2 * NR).out;
+    if (pair0 && deepv) halo2(xa, const_cast<dbl2*>(b));  // (b's ghosts: the first step on the ghost rows)
+    else halo2(xa);
     // the interval [visc_lo, 1 + visc_R]: theta its centre, delta its half-width
     const double hi = 1.0 + visc_R, lo = visc_lo;
     const double theta = 0.5 * (hi + lo), delta = 0.5 * (hi - lo), sigma = theta / delta, tol2 = tol * tol;
@@ -1155,7 +1220,6 @@ struct Ctx {
     // both steps on the face interiors (k_vcheb_pair: x_{a+1} in LDS), the skeleton rows' step a + 1.
     // check: the |r_{a+1}|^2 partials of both halves in part_c (SELL blocks first); fin: step a + 1 is
     // the solve's last and writes u* and the increment.
-    const int nbs = nb_for(A.nslices);
     const double bytes_sk = (8.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                             32.0 * NR * (double)(A.own() - hf.rows);
     // first: the pair is the solve's steps 0 and 1: step 0 reads no d and both halves write the |r_0|^2 /
@@ -1196,7 +1260,7 @@ struct Ctx {
       double* pc = check ? part_c : nullptr;
       with_c16(A, [&](auto c16) {
         klaunch(-1, bytes_sk - (first ? 4.0 * NR * (double)(A.own() - hf.rows) : 0.0), k_vcheb<decltype(c16)::value>,
-                dim3(nbs), dim3(BS), A.view(), fs, val, v1, c1a, c2a, first ? 1 : 0, (const int*)ctl,
+                dim3(nbs), dim3(BS), Ag.view(), fs, val, v1, c1a, c2a, first ? 1 : 0, (const int*)ctl,
                 first ? part_a : (double*)nullptr, first ? part_b : (double*)nullptr, RedOut{});
         KCHK();
         klaunch(12, bytes_f - (first ? 4.0 * NR * (double)hf.rows : 0.0), k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p,
@@ -1215,6 +1279,7 @@ struct Ctx {
       xc = xb;
       xb = t;
       std::swap(dcur, dalt);
+      if (dist()) halo2(xa);  // (W > 1: the next single step gathers x_{a+2}'s ghosts)
     };
     // Step 0 gives r_0 = b - A^ x_0.  The residual polynomial of the Chebyshev iteration on an interval
     // holding the spectrum is bounded by 1 / T_k(sigma) there, so |r_k| <= |r_0| / T_k(sigma): the step
@@ -1228,7 +1293,6 @@ struct Ctx {
     double rho_old = 1.0 / sigma;
     int done = 1;
     int nb0 = nb;  // the first step's partial count
-    const bool pair0 = pairs && !ro(redbuf, CNT_VCHEB, 2 * NR).out;
     if (pair0) {
       const double rho = 1.0 / (2.0 * sigma - rho_old);
       pair_step(0.0, 1.0 / theta, rho * rho_old, 2.0 * rho / delta, true, false, true);
@@ -1406,8 +1470,9 @@ struct Ctx {
 
   template <typename T, typename TB>
   // toz: the last step writes the preconditioned residual (z32 in the fp32 cycle, z in the fp64 one)
+  // last_g (deep halos): the last step also runs on the ghost rows one layer out (x and d exchanged before it)
   T* mg_smooth(MgLevel& L, const DevSell& A, const HFace& hf, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb,
-               bool tozr, const double* rdot, double* part, int deg) {
+               bool tozr, const double* rdot, double* part, int deg, bool last_g = false) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
@@ -1433,9 +1498,13 @@ struct Ctx {
     // step pairs (k_cheb_pair) on the finest level of the fp32 cycle, one rank: two steps per pass on the
     // face interiors; not the step that writes z / the <r, z> partials
     bool pairs = false;
+    // deep halos (W > 1): a pair's first step also runs on the ghost rows one layer out, so a pair needs one
+    // exchange (x, two layers) where two single steps needed two -- pairs on every partitioned level
+    const bool dg = dist() && L.deep;
     if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
-      // (finest level only: pairs on L6 / L5 too measured neutral to -0.7 %, r10m)
-      pairs = mg_pair && (int)(&mg.back() - &L) < mg_pair_levels && !dist() && hf.items > 0 && hf.d.n <= VP_HALO;
+      // (one rank: the finest level only; pairs on L6 / L5 too measured neutral to -0.7 %, r10m)
+      pairs = mg_pair && hf.items > 0 && hf.d.n <= VP_HALO &&
+              (dist() ? dg : (int)(&mg.back() - &L) < mg_pair_levels);
     if (pairs && !mgp_x) {  // (sized for the finest level: every pair level uses them in turn)
       mgp_x = dalloc<float>(mg.back().nloc);
       mgp_d = dalloc<float>(mg.back().nloc);
@@ -1454,7 +1523,10 @@ struct Ctx {
       const int mode = (cur == nullptr && k == 0) ? 0 : (cur == nullptr ? 2 : 1);
       if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value) {
         const bool next_last = k + 1 == deg - 1;
-        if (pairs && mode != 0 && k + 1 < deg && !(next_last && (tozr || rdot))) {
+        // (W > 1: a general-step pair only where d_a is not read, c1 = 0: d is not exchanged before it)
+        if (pairs && mode != 0 && k + 1 < deg && !(next_last && (tozr || rdot || last_g)) &&
+            (!dg || mode == 2 || c1 == 0.0)) {
+          if (dg && mode == 1) mg_halo(L, cur);  // x_a two layers out: the first step runs on the ghost rows
           // steps k, k + 1: x_a = cur (mode 1) -> x_{a+1} in p1 (skeleton rows, the face rows next to
           // them) -> x_{a+2} in p2; d_a = dcur -> d_{a+2} in the other d buffer
           float* p1 = mode == 2 ? xa : (cur == xa ? xb : xa);
@@ -1467,6 +1539,8 @@ struct Ctx {
           FaceDev fs = hf.full();
           fs.nb = 0;
           const int nbs = nb_mg(A.nslices);
+          const DevSell Ag = dg ? A.with_ghosts() : A;  // the first SELL launch: + the ghost rows one layer out
+          const int nbg = nb_mg(Ag.nslices);
           // skeleton rows: the SELL part of a k_cheb step (bytes as in the single step, SELL rows only)
           const double sk_row = (mode == 1 ? 3.0 * sizeof(T) : 1.0 * sizeof(T)) + sizeof(TB) + 2.0 * sizeof(T);
           const double bytes_sk = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz +
@@ -1482,7 +1556,7 @@ struct Ctx {
             using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
             with_c16(A, [&](auto c16) {
               constexpr bool C = decltype(c16)::value;
-              klaunch(-1, bytes_sk, k_cheb<T, TB, T, VT, C, 1>, dim3(nbs), dim3(BS), A.view(), fs, val,
+              klaunch(-1, bytes_sk, k_cheb<T, TB, T, VT, C, 1>, dim3(nbg), dim3(BS), Ag.view(), fs, val,
                       (const T*)B.dinv, b, (const T*)(mode == 1 ? cur : nullptr), p1, dcur, c1, c2, c20, mode,
                       (const int*)ctl, (const double*)nullptr, (double*)nullptr, RedOut{}, (T*)nullptr);
               KCHK();
@@ -1507,13 +1581,20 @@ struct Ctx {
         }
       }
       T* out = (cur == xa) ? xb : xa;
-      if (mode == 1) mg_halo(L, cur);
       const bool last = k == deg - 1;
+      // the last step on the ghost rows one layer out too (deep halos): x two layers out and d one layer out
+      const bool gl = last && last_g && dg;
+      if (mode == 1) {
+        if (gl) mg_halo(L, cur, dcur);
+        else mg_halo(L, cur);
+      }
+      const DevSell& As = gl ? A.with_ghosts() : A;
       const bool timed = finest && mode != 0;
       const double* rd = last ? rdot : nullptr;
       const bool toz = last && tozr;
+      if (toz) z_cur = gl;
       const FaceDev fc = rd ? hf.part() : hf.full();
-      const int nb = rd ? grid_part(fc, A) : grid_full(fc, A);
+      const int nb = rd ? grid_part(fc, As) : grid_full(fc, As);
       const T* xi = mode == 1 ? cur : nullptr;
       // algorithmic bytes: matrix (value + column) per entry; per row x_in (mode 1) or b and dinv
       // (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r; face rows
@@ -1531,15 +1612,15 @@ struct Ctx {
           if constexpr (std::is_same<T, float>::value) zo = z32;
           else zo = z;
           if (toz)
-            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), As.view(), fc, val,
                     (const T*)B.dinv, b, xi, zo, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part,
                     rd ? ro_rz : RedOut{}, (T*)nullptr);
           else if (finest)
-            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), A.view(), fc, val,
+            klaunch(timed ? 0 : -1, bytes, k_cheb<T, TB, T, VT, C, 1>, dim3(nb), dim3(BS), As.view(), fc, val,
                     (const T*)B.dinv, b, xi, out, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{},
                     (T*)nullptr);
           else
-            klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), A.view(), fc, val, (const T*)B.dinv, b,
+            klaunch(-1, bytes, k_cheb<T, TB, T, VT, C, 0>, dim3(nb), dim3(BS), As.view(), fc, val, (const T*)B.dinv, b,
                     xi, out, dcur, c1, c2, c20, mode, (const int*)ctl, rd, part, RedOut{}, (T*)nullptr);
         });
       });
@@ -1586,7 +1667,10 @@ struct Ctx {
     }
     T* x = mg_smooth<T, TB>(L, A, hf, B, b, nullptr, xa, xb, false, nullptr, nullptr, pre);
     mg_halo(L, x);
-    // residual: matrix entries, x gathered once, b read, res written
+    // residual: matrix entries, x gathered once, b read, res written; deep halos: also on the ghost rows one layer
+    // out, which the restriction gathers (no exchange of the residual)
+    const bool rg = dist() && L.res_deep;
+    const DevSell& Ar = rg ? A.with_ghosts() : A;
     const double bytes_res = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                              (double)A.own() * (2.0 * sizeof(T) + sizeof(TB));
     const FaceDev fr = hf.full();
@@ -1594,15 +1678,15 @@ struct Ctx {
       using VT = std::remove_const_t<std::remove_pointer_t<decltype(val)>>;
       with_c16(A, [&](auto c16) {
         if (finest)
-          klaunch(5, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 1>, dim3(grid_full(fr, A)), dim3(BS),
-                  A.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
+          klaunch(5, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 1>, dim3(grid_full(fr, Ar)), dim3(BS),
+                  Ar.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
         else
-          klaunch(-1, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 0>, dim3(grid_full(fr, A)), dim3(BS),
-                  A.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
+          klaunch(-1, bytes_res, k_resid<T, TB, VT, decltype(c16)::value, 0>, dim3(grid_full(fr, Ar)), dim3(BS),
+                  Ar.view(), fr, val, b, (const T*)x, B.res, (const int*)ctl);
       });
     });
     KCHK();
-    mg_halo(L, B.res);
+    if (!rg) mg_halo(L, B.res);
     MgLevel& C = mg[l - 1];
     MgBufs<T>& CB = bufs<T>(C);
     const bool gather = C.rep && !L.rep && dist();  // into the finest replicated level
@@ -1621,7 +1705,7 @@ struct Ctx {
       comm->group_end(st);
     }
     T* xc = vcycle<T, T>(l - 1, CB.b, nullptr, nullptr);
-    mg_halo(C, xc);
+    if (!(dist() && L.xc_deep)) mg_halo(C, xc);  // (xc_deep: level l - 1's last step wrote its ghosts one layer out)
     // prolongation: entries, coarse x read once, fine x read + written
     klaunch(finest ? 7 : -1,
             (double)(sizeof(T) + 4) * (double)L.dPr.nnz + L.dPr.row_bytes() * (double)L.dPr.nrows +
@@ -1631,13 +1715,16 @@ struct Ctx {
     KCHK();
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
-    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part,
-                            post);
+    // the last step on the ghost rows one layer out where its consumer gathers them: the PCG's A z on the finest
+    // level, the prolongation into level l + 1 (xc_deep) below it
+    const bool last_g = dist() && L.deep && (finest || mg[l + 1].xc_deep);
+    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part, post, last_g);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
   void precondition(double* rz_part = nullptr) {
     if (!rz_part) rz_part = part_d + 2 * MAXB;
+    z_cur = false;
     if (mg_single) {
       vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], rz_part);
     } else {
@@ -1819,8 +1906,10 @@ struct Ctx {
         if (cgcg) {  // single-reduction iteration (k_cgcg_*)
           ++cgcg_iters;
           precondition(part_cc + 3 * MAXB);
-          if (mg_single) mg_halo(mg.back(), z32);
-          else halo(z);
+          if (!z_cur) {  // (deep halos: the last smoothing step wrote z's ghosts one layer out)
+            if (mg_single) mg_halo(mg.back(), z32);
+            else halo(z);
+          }
           with_c16(dPp, [&](auto c16) {
             if (mg_single)
               klaunch(1, bytes_w, k_cgcg_w<decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -1858,8 +1947,10 @@ struct Ctx {
         Red rz{redbuf + 32, 1, 1};
         if (ro(redbuf + 32, CNT_RZ, 1).out) red_done(redbuf + 32, 1, false);
         else rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-        if (mg_single) mg_halo(mg.back(), z32);
-        else halo(z);
+        if (!z_cur) {
+          if (mg_single) mg_halo(mg.back(), z32);
+          else halo(z);
+        }
         with_c16(dPp, [&](auto c16) {
           if (mg_single)
             klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -2364,9 +2455,39 @@ struct Ctx {
     HIPCHK(hipEventRecord(ev_sl, st_sl));
     sl_pending = true;
   }
+  // W > 1, StokesColor: the second half of a step's dye tail (dye_range_start queued the first at its end): the
+  // wide halo, the semi-Lagrangian advection of the owned rows, the mixing sums and the rest of the step record.
+  // It reads the step's final u and c; the next step's viscous solve writes neither, and its first write to u (the
+  // gradient projection) follows in stream order.
+  bool tail_pend = false;
+  double* tail_rec = nullptr;
+  void dye_tail_dist() {
+    if (!tail_pend) return;
+    tail_pend = false;
+    dye_halo_exchange();
+    const int nb = nb_sl(lp.n_own);
+    sl_ro = ro(vals + 2, CNT_SL, 3, SLB);
+    sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, sl_ro);
+    KCHK();
+    // the replica keeps its (halo) values; only the owned segment is new
+    HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+    if (sl_ro.out) red_done(vals + 2, 3, false);
+    else reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+    sl_ro = RedOut{};
+    const int nbm = nb_rows(lp.n_own);
+    algo_bytes += 16.0 * (double)lp.n_own;
+    const RedOut rm = ro(vals + 5, CNT_MIX, 1);
+    hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx, rm);
+    KCHK();
+    if (rm.out) red_done(vals + 5, 1, false);
+    else reduce_into(part_mx, nbm, 1, false, 5);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, tail_rec, 4);
+    KCHK();
+  }
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
     viscous(itv);
+    dye_tail_dist();  // (W > 1: the previous step's dye tail)
     // max |div u*| -> vals[0]; the div u* field itself is computed when read (pucfem_get_field): nothing in the
     // step reads it, and its 8 B/row store is a quarter of the kernel's bytes
     const bool f1 = div_rhs(usx, usy, nullptr, vals);
@@ -2409,8 +2530,18 @@ struct Ctx {
         last_dye_it = dye_step(ux, uy, final_div, c_full, c_new);
         hipLaunchKernelGGL(k_wsum, dim3(nb), dim3(BS), 0, st, lp.r0, lp.n_own, (const double*)c_new,
                            (const double*)dwmix, part_sl);
+      } else if (dist()) {
+        // W > 1: the back-traced ranges now, the rest of the tail at the next step (dye_tail_dist)
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 3);  // max |div u*|, max |final div|
+        KCHK();
+        dye_range_start(uy, prm.dt);
+        tail_pend = true;
+        tail_rec = rec;
+        its[0] = itv;
+        its[1] = itp;
+        its[2] = itp2;
+        return;
       } else {
-        dye_halo(uy, prm.dt);
         sl_ro = ro(vals + 2, CNT_SL, 3, SLB);
         sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, sl_ro);
       }
@@ -3060,12 +3191,13 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
                      S.rows.empty() ? A.rowptr[r0 + n] - A.rowptr[r0] : S.nnz, S.padded, 0};
       if (!S.rows.empty()) L.dA.rows = c.upload(S.rows);
       L.dA.n_own = n;
+      L.dA.ghost_slices(S);
       c.attach_c16(S, L.nloc, L.dA);
       B.Aval = upload_as<T>(c, tmp);
       if constexpr (std::is_same<T, float>::value) B.Aval16 = upload_f16(c, tmp, false);
       L.nsend = (i64)L.lp.send_local.size();
       L.dsend = c.upload(L.lp.send_local);
-      B.sendbuf = c.dalloc<T>(std::max<i64>(1, L.nsend));
+      B.sendbuf = c.dalloc<T>(std::max<i64>(1, 2 * L.nsend));  // (two vectors per exchange: x and d)
     } else {
       if constexpr (std::is_same<T, double>::value) {
         B.Aval = c.dKp_raw;
@@ -3073,7 +3205,7 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
         B.Aval = upload_as<T>(c, kp_vals);
         B.Aval16 = upload_f16(c, kp_vals, true);
       }
-      B.sendbuf = c.dalloc<T>(std::max<i64>(1, (i64)c.lp.send_local.size()));
+      B.sendbuf = c.dalloc<T>(std::max<i64>(1, 2 * (i64)c.lp.send_local.size()));
     }
     if (l >= 1) {
       const Sell& S = L.sPr;
@@ -3329,7 +3461,15 @@ void build(Ctx& c) {
       if (l >= 1) pr.push_back({&L.R, &c.mg[l - 1].rs});
       if (l < Lv) pr.push_back({&c.mg[l + 1].Pr, &c.mg[l + 1].rs});
       if (l == Lv) pr.push_back({&c.P, &L.rs});
-      make_local_plan2(pr, L.rs, c.rank, L.lp);
+      // deep halos on the partitioned lattice levels (Ctx::deep_halo): the ghost rows one layer out of the level
+      // operator (the finest level: of the pressure and the K / A_visc patterns) and their columns
+      std::vector<const Csr*> deep;
+      if (c.deep_halo && c.lattice && c.world > 1) {
+        deep.push_back(l == Lv ? &c.Pp : &L.Pp);
+        if (l == Lv) deep.push_back(&c.P);
+      }
+      make_local_plan2(pr, L.rs, c.rank, L.lp, deep.empty() ? nullptr : &deep, deep.empty() ? nullptr : &L.g1);
+      L.deep = !deep.empty();
     }
     c.lp = c.mg[Lv].lp;
     // lattice operators: SELL rows for the skeleton (macro edge / vertex nodes) only
@@ -3345,6 +3485,7 @@ void build(Ctx& c) {
       if (l < Lv) {
         if (c.lattice) build_sell_rows(L.Pp, o0, skel(L.latl, o0, L.lp.n_own), L.lp, L.sA);
         else build_sell_x(L.Pp, o0, L.lp.n_own, L.lp, L.sA, true);
+        if (L.deep) sell_append_ghost_rows(L.Pp, L.g1, L.lp, L.sA);
       }
       if (l >= 1) {
         const MgLevel& C = c.mg[l - 1];
@@ -3358,6 +3499,40 @@ void build(Ctx& c) {
         if (c.lattice) build_sell_rows(L.R, L.r_r0, skel(C.latl, L.r_r0, nr), L.lp, L.sR);
         else build_sell_x(L.R, L.r_r0, nr, L.lp, L.sR);
       }
+    }
+    // deep halos: which consumers can read the ghost rows one layer out instead of an exchange (every column
+    // they gather outside the rank's rows must be one of them); all-reduced over the ranks at the upload
+    for (int l = 1; l <= Lv; ++l) {
+      MgLevel& L = c.mg[l];
+      MgLevel& C = c.mg[l - 1];
+      if (!L.deep) continue;
+      const i64 lo = L.own0(c.rank), hi = lo + L.lp.n_own;
+      auto in_g1 = [](const std::vector<i32>& g1, i32 g) { return std::binary_search(g1.begin(), g1.end(), g); };
+      // the restriction's rows (on level l - 1) gather this level's residual
+      const bool gather = C.rep && !L.rep;
+      const i64 nr = gather ? C.rs[c.rank + 1] - C.rs[c.rank] : C.lp.n_own;
+      bool ok = true;
+      for (i64 r = L.r_r0; r < L.r_r0 + nr && ok; ++r)
+        for (i64 k = L.R.rowptr[r]; k < L.R.rowptr[r + 1]; ++k) {
+          const i32 j = L.R.col[k];
+          if ((j < lo || j >= hi) && !in_g1(L.g1, j)) {
+            ok = false;
+            break;
+          }
+        }
+      L.res_deep = ok;
+      // the prolongation into this level gathers level l - 1's result: its ghosts one layer out suffice
+      ok = C.deep && !C.rep;
+      const i64 clo = C.own0(c.rank), chi = clo + C.lp.n_own;
+      for (i64 r = lo; r < hi && ok; ++r)
+        for (i64 k = L.Pr.rowptr[r]; k < L.Pr.rowptr[r + 1]; ++k) {
+          const i32 j = L.Pr.col[k];
+          if ((j < clo || j >= chi) && !in_g1(C.g1, j)) {
+            ok = false;
+            break;
+          }
+        }
+      L.xc_deep = ok;
     }
     if (c.lattice) {  // face tables and coefficient records of every level (pucfem_lattice.hpp)
       const double dtnu = prm.dt * prm.nu;
@@ -3413,6 +3588,10 @@ void build(Ctx& c) {
       if (LL.type[c.lp.r0 + i] != 0) rows.push_back((i32)i);
     build_sell_rows(c.P, c.lp.r0, rows, c.lp, c.sP);
     build_sell_rows(c.Pp, c.lp.r0, rows, c.lp, c.sPp);
+    if (c.use_mg && c.mg.back().deep) {  // deep halos: the finest level's ghost rows (pressure, A_visc / K)
+      sell_append_ghost_rows(c.Pp, c.mg.back().g1, c.lp, c.sPp);
+      sell_append_ghost_rows(c.P, c.mg.back().g1, c.lp, c.sP);
+    }
   } else {
     build_sell(c.P, c.lp, c.sP);
     if (stokes) build_sell(c.Pp, c.lp, c.sPp);
@@ -3455,6 +3634,7 @@ void build(Ctx& c) {
     D.nnz = S.rows.empty() ? A.rowptr[lp.r1] - A.rowptr[lp.r0] : S.nnz;
     if (!S.rows.empty()) D.rows = c.upload(S.rows);
     D.n_own = lp.n_own;
+    D.ghost_slices(S);
   };
   std::vector<double> tmp;
   dsell(c.sP, c.P, c.dP);
@@ -3605,6 +3785,25 @@ void build(Ctx& c) {
           c.dense_fut.valid() ? c.dense_fut.get() : dense_coarse_inverse(c.mg[c.mg_dense_l]);
       c.dAinv = c.upload(D);
       if (c.mg_dense_l > 0) c.dAinv32 = c.upload(std::vector<float>(D.begin(), D.end()));
+    }
+  }
+  if (c.dist() && c.use_mg) {  // deep-halo flags: every rank takes the same exchanges (a flag off anywhere is off)
+    const size_t nl = c.mg.size();
+    std::vector<double> off(3 * nl);
+    for (size_t l = 0; l < nl; ++l) {
+      off[3 * l] = c.mg[l].deep ? 0.0 : 1.0;
+      off[3 * l + 1] = c.mg[l].res_deep ? 0.0 : 1.0;
+      off[3 * l + 2] = c.mg[l].xc_deep ? 0.0 : 1.0;
+    }
+    DevTmp<double> t(off, c.st);
+    c.comm->allreduce(t.p, off.size(), true, c.st);
+    t.get(off, off.size(), c.st);
+    HIPCHK(hipStreamSynchronize(c.st));
+    for (size_t l = 0; l < nl; ++l) {
+      MgLevel& L = c.mg[l];
+      L.deep = L.deep && off[3 * l] == 0.0;
+      L.res_deep = L.deep && L.res_deep && off[3 * l + 1] == 0.0;
+      L.xc_deep = l > 0 && c.mg[l - 1].deep && L.xc_deep && off[3 * l + 2] == 0.0;
     }
   }
   c.block_cg = c.prm.solver_path != 1;
@@ -3806,7 +4005,7 @@ void build(Ctx& c) {
   // halo plan
   c.nsend = (i64)lp.send_local.size();
   c.dsend = c.upload(lp.send_local);
-  c.dsendbuf = c.dalloc<double>(2 * std::max<i64>(1, c.nsend));
+  c.dsendbuf = c.dalloc<double>(4 * std::max<i64>(1, c.nsend));  // (two interleaved vectors: halo2(x, b))
   // fields + workspace
   for (double** f : {&c.p, &c.p2, &c.yp, &c.yp2, &c.yvx, &c.yvy, &c.div_star, &c.div_u, &c.final_div, &c.braw,
                      &c.bh, &c.bvx, &c.bvy, &c.scalar})
@@ -4374,11 +4573,13 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.stokes_step(rec + 8 * s, its.data() + 3 * s);
           }
           c.proj_materialize();  // (no direction stays pending between API calls)
+          c.dye_tail_dist();     // (nor a dye tail: the last step's, now)
           c.sl_join();
         } catch (...) {
           c.dits = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
+          c.tail_pend = false;
           throw;
         }
         c.dits = nullptr;

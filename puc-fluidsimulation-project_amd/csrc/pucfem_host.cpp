@@ -1009,7 +1009,8 @@ bool spd_inverse(std::vector<double>& A, i64 n) {
   return true;
 }
 
-void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& row_start, int rank, LocalPlan& lp) {
+void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& row_start, int rank, LocalPlan& lp,
+                      const std::vector<const Csr*>* deep, std::vector<i32>* g1_out) {
   const int world = (int)row_start.size() - 1;
   lp.r0 = row_start[rank];
   lp.r1 = row_start[rank + 1];
@@ -1031,8 +1032,40 @@ void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& 
     std::sort(out.begin(), out.end());
     out.erase(std::unique(out.begin(), out.end()), out.end());
   };
+  // deep halos: rank q's ghost rows one layer out (G1) and their columns (G2)
+  auto deep_of = [&](int q, std::vector<i32>& g1, std::vector<i32>& g2) {
+    g1.clear();
+    g2.clear();
+    if (!deep) return;
+    const i64 lo = row_start[q], hi = row_start[q + 1];
+    for (const Csr* A : *deep)
+      for (i64 r = lo; r < hi; ++r)
+        for (i64 k = A->rowptr[r]; k < A->rowptr[r + 1]; ++k)
+          if (A->col[k] < lo || A->col[k] >= hi) g1.push_back(A->col[k]);
+    std::sort(g1.begin(), g1.end());
+    g1.erase(std::unique(g1.begin(), g1.end()), g1.end());
+    for (const Csr* A : *deep)
+      for (i32 r : g1)
+        for (i64 k = A->rowptr[r]; k < A->rowptr[r + 1]; ++k)
+          if (A->col[k] < lo || A->col[k] >= hi) g2.push_back(A->col[k]);
+  };
+  // every ghost of rank q: the patterns' off-range columns and (deep) G1 and G2
+  auto ghosts_of = [&](int q, std::vector<i32>& out) {
+    cols_of(q, out, row_start[q], row_start[q + 1], false);
+    if (!deep) return;
+    std::vector<i32> g1, g2;
+    deep_of(q, g1, g2);
+    out.insert(out.end(), g1.begin(), g1.end());
+    out.insert(out.end(), g2.begin(), g2.end());
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+  };
   std::vector<i32> gh;
-  cols_of(rank, gh, lp.r0, lp.r1, false);
+  ghosts_of(rank, gh);
+  if (g1_out) {
+    std::vector<i32> g2;
+    deep_of(rank, *g1_out, g2);
+  }
   lp.ghost_global = gh;
   lp.n_ghost = (i64)gh.size();
   lp.ghost_owner.resize(gh.size());
@@ -1055,7 +1088,14 @@ void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& 
   for (int q = 0; q < world; ++q) {
     if (q == rank) continue;
     std::vector<i32> need;
-    cols_of(q, need, lp.r0, lp.r1, true);
+    if (deep) {  // q's ghosts inside my range
+      std::vector<i32> gq;
+      ghosts_of(q, gq);
+      for (i32 g : gq)
+        if (g >= lp.r0 && g < lp.r1) need.push_back(g);
+    } else {
+      cols_of(q, need, lp.r0, lp.r1, true);
+    }
     // q only needs those of my rows that are not its own (q's rows are outside my range anyway)
     if (need.empty()) continue;
     lp.send_peer.push_back(q);
@@ -1152,10 +1192,49 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
     for (i64 l = 0; l < 64; ++l) {
       const i64 k = s * 64 + l;
       if (k >= S.nrows) continue;
-      const i64 r = r0 + S.rows[k];
+      const i64 r = S.global_row(r0, k);
       const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
       for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = val[b + e];
     }
+}
+
+void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S) {
+  if (S.gk0 >= 0) throw std::runtime_error("SELL already has ghost rows");
+  if (S.rows.empty() && S.nrows > 0) throw std::runtime_error("ghost rows need a row-listed SELL");
+  S.nslices_own = S.nslices;
+  S.gk0 = S.nslices * 64;
+  S.grow = grows;
+  const i64 n = (i64)grows.size(), ns = (n + 63) / 64;
+  S.rows.resize((S.nslices + ns) * 64, -1);
+  S.slice_w.resize(S.nslices + ns, 0);
+  S.slice_off.resize(S.nslices + ns + 1, S.slice_off[S.nslices]);
+  for (i64 s = 0; s < ns; ++s) {
+    i64 w = 0;
+    for (i64 l = 0; l < 64 && s * 64 + l < n; ++l) {
+      const i64 g = grows[s * 64 + l];
+      w = std::max(w, A.rowptr[g + 1] - A.rowptr[g]);
+      S.rows[S.gk0 + s * 64 + l] = to_local(cols, (i32)g);
+      if (S.rows[S.gk0 + s * 64 + l] < cols.n_own) throw std::runtime_error("ghost row list holds an owned row");
+    }
+    S.slice_w[S.nslices + s] = (i32)w;
+    S.slice_off[S.nslices + s + 1] = S.slice_off[S.nslices + s] + w * 64;
+  }
+  const i64 p0 = S.padded;
+  S.padded = S.slice_off[S.nslices + ns];
+  S.col.resize(S.padded, 0);
+  for (i64 s = 0; s < ns; ++s)
+    for (i64 l = 0; l < 64; ++l) {
+      const i64 k = s * 64 + l;
+      const i64 r = k < n ? grows[k] : -1;
+      const i64 len = k < n ? A.rowptr[r + 1] - A.rowptr[r] : 0;
+      const i32 first = len > 0 ? to_local(cols, A.col[A.rowptr[r]]) : 0;
+      for (i64 e = 0; e < S.slice_w[S.nslices + s]; ++e)
+        S.col[S.slice_off[S.nslices + s] + e * 64 + l] = e < len ? to_local(cols, A.col[A.rowptr[r] + e]) : first;
+      S.nnz += len;
+    }
+  (void)p0;
+  S.nslices += ns;
+  S.nrows += n;
 }
 
 

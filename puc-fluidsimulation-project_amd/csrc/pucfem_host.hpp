@@ -239,8 +239,12 @@ struct PatRows {
   const Csr* A;
   const std::vector<i64>* rows;  // owner ranges of A's rows
 };
+// deep (optional): operator patterns (rows partitioned by row_start) whose rows ONE layer out -- the ghost rows
+// adjacent to a rank's rows, "G1" -- the rank computes redundantly (Ctx: step pairs, residuals and last smoothing
+// steps on W > 1 ranks with one exchange where two were needed).  Their columns ("G2") join the ghost set of every
+// rank (and so the send lists), and g1_out receives this rank's G1 rows (sorted global ids).
 void make_local_plan2(const std::vector<PatRows>& pats, const std::vector<i64>& row_start, int rank,
-                      LocalPlan& lp);
+                      LocalPlan& lp, const std::vector<const Csr*>* deep = nullptr, std::vector<i32>* g1_out = nullptr);
 
 // SELL-64: slices of 64 rows, per-slice width = max row length, entries column-major
 // inside a slice (lane = row) so a wave's loads are contiguous.
@@ -253,11 +257,20 @@ struct Sell {
   // with -1; empty: slice s holds rows s*64 .. s*64+63
   std::vector<i32> rows;
   i64 nnz = 0;  // stored (unpadded) entries of the listed rows (build_sell_rows)
+  // ghost rows appended by sell_append_ghost_rows (deep halos): entries k >= gk0 of `rows` are ghost rows, whose
+  // operator rows are A's rows grow[k - gk0] (global ids; their `rows` entries are the local ghost indices);
+  // nslices_own slices hold the rank's own rows (-1: no ghost rows)
+  i64 gk0 = -1, nslices_own = -1;
+  std::vector<i32> grow;
+  i64 global_row(i64 r0, i64 k) const { return gk0 >= 0 && k >= gk0 ? (i64)grow[k - gk0] : r0 + (i64)rows[k]; }
 };
 // SELL of the rows `rows` (offsets from r0 into A's rows; they are also the local output indices),
 // columns resolved in `cols`; int32 columns only (rows are not contiguous)
 void build_sell_rows(const Csr& A, i64 r0, const std::vector<i32>& rows, const LocalPlan& cols, Sell& S);
 void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
+// append the rows `grows` (global ids, each a ghost of `cols`) to a row-listed SELL as whole slices of their own:
+// local output index = the ghost's local id, columns resolved in `cols`
+void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S);
 // the SELL image of A's rows in S (rows r0 + k, or r0 + S.rows[k]) with entry values f(r, e) computed in
 // place (r: the row's global index, e: its CSR entry) -- no full-length value array for a SELL that
 // holds only the lattice skeleton's rows
@@ -269,7 +282,7 @@ void sell_values_fn(const Csr& A, i64 r0, const Sell& S, F&& f, std::vector<doub
       for (i64 l = 0; l < 64; ++l) {
         const i64 k = s * 64 + l;
         if (k >= S.nrows) continue;
-        const i64 r = r0 + (S.rows.empty() ? k : (i64)S.rows[k]);
+        const i64 r = S.rows.empty() ? r0 + k : S.global_row(r0, k);
         const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
         for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = f(r, b + e);
       }

@@ -1177,7 +1177,8 @@ __global__ LB_GATHER void k_vcheb(SellDev A, FaceDev fc, const double* __restric
   const bool fin = v.us[0] != nullptr;
   flt2* dout = v.dout ? v.dout : const_cast<flt2*>(v.d);
   // row: r = b - A^ x (both components), d = c1 d + c2 r, x_out = x + d
-  auto finish = [&](int64_t row, dbl2 ax, dbl2 x0, dbl2 br, flt2 dr) {
+  // own: the row adds to the partials (not a ghost row one layer out, deep halos)
+  auto finish = [&](int64_t row, dbl2 ax, dbl2 x0, dbl2 br, flt2 dr, bool own = true) {
     const double r0 = br.x - ax.x, r1 = br.y - ax.y;
     const double dn0 = first ? c2 * r0 : c1 * (double)dr.x + c2 * r0;
     const double dn1 = first ? c2 * r1 : c1 * (double)dr.y + c2 * r1;
@@ -1193,6 +1194,7 @@ __global__ LB_GATHER void k_vcheb(SellDev A, FaceDev fc, const double* __restric
       stnt(dout + row, dn);
       stnt(v.xout + row, xo);
     }
+    if (!own) return;
     rr[0] += r0 * r0;
     rr[1] += r1 * r1;
     bb[0] += br.x * br.x;
@@ -1274,7 +1276,7 @@ __global__ LB_GATHER void k_vcheb(SellDev A, FaceDev fc, const double* __restric
           }
         }
       });
-      if (row >= 0) finish(row, dbl2{acc0, acc1}, x0, br, dr);
+      if (row >= 0) finish(row, dbl2{acc0, acc1}, x0, br, dr, row < A.n_own);
     }
   }
   if (!part_rr) return;  // steps after the first: no residual norms needed (the step count is known)
@@ -2403,9 +2405,10 @@ __device__ __forceinline__ bool sl_fast(const LOC& L, const SlTri& r, double qx,
 // nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
 // Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
 // Two passes.  k_sl finishes the points of the lattice fast path (q strictly inside a cell of its
-// row's home face, rank settled by a fast accept: ~95 % of the rows) with a small register
-// footprint; the rest are queued and k_sl_slow runs the general locate and the centroid rank count
-// on dense waves.  The record locator has no fast path: k_sl queues every row.
+// row's home face, rank settled by a fast accept: all but 796 of L7's 14.2M rows, 0.006 %, r12n) with a
+// small register footprint; the rest are queued, and k_sl_wave (lattice locator: one wave per queued
+// point) or k_sl_slow (record locator) runs the general locate and the centroid rank count.  The record
+// locator has no fast path: k_sl queues every row.
 // The queue is per wave and deterministic: wave w of block b writes its k-th entry into slot
 // k % 64 of the (k / 64)-th 64-row slice it processed (entries never outrun the rows they come from);
 // k_sl_slow block b runs the same waves' queues and adds its partial sums to block b's, so the
@@ -2586,6 +2589,167 @@ __global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int
     }
   }
   red_finish(ro, part, sh);
+}
+
+// ---- k_sl_wave: the second pass of the lattice locator with ONE WAVE PER QUEUED POINT.  k_sl_slow ran a queued
+// point's general locate (every candidate cell of every macro face listed in q's macro-grid cell, up to ~20 x 18
+// dependent coordinate loads) and its centroid rank count serially in one lane, on k_sl's full 8,192-block grid:
+// at L7 796 points (0.006 % of the rows, r12n) took 290 us per step, the latency of the slowest lane.  Here the
+// wave's 64 lanes test the candidates together (the answer is the passing triangle with the smallest (d^2, id)
+// key: a margin / inner pass is the only passing triangle, so the sequential scan's early exits never change it),
+// then count the centroids below it together (ballots; the sequential count's early exit only saves work), and
+// lane 0 writes the value -- the same arithmetic per candidate, so the same bits as k_sl_slow.
+// Work: a small grid whose wave g takes k_sl's blocks g, g + NW, ... (their four waves' queues in order), and adds
+// each origin block's slow contributions to that block's partials itself: no two waves share a partial, the sums'
+// order is fixed.
+__device__ __forceinline__ void rows_of_block(int64_t n, int64_t nb, int64_t b, int64_t& r0, int64_t& r1) {
+  const int64_t ns = (n + 63) / 64, s0 = (ns * b) / nb, s1 = (ns * (b + 1)) / nb;  // block_rows for block b of nb
+  r0 = s0 * 64;
+  r1 = s1 * 64 < n ? s1 * 64 : n;
+}
+// (d, id) key minimum over the wave (every lane gets it)
+__device__ __forceinline__ void wave_min_key(double& d, int32_t& id) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double od = __shfl_xor(d, o, 64);
+    const int32_t oi = __shfl_xor(id, o, 64);
+    if (knn_less(od, oi, d, id)) {
+      d = od;
+      id = oi;
+    }
+  }
+}
+// the general lattice locate of one point by a whole wave (sl_best with home = -1): false when no cell passes
+__device__ __forceinline__ bool sl_best_wave(const LatLocDev& L, double qx, double qy, SlTri& out, double& bestd,
+                                             float& rho2) {
+  const int lane = threadIdx.x & 63;
+  const double gx = floor((qx - L.x0) * L.ihx), gy = floor((qy - L.y0) * L.ihy);
+  const int32_t ci = !(gx >= 0.0) ? 0 : (gx >= (double)L.nx ? L.nx - 1 : (int32_t)gx);
+  const int32_t cj = !(gy >= 0.0) ? 0 : (gy >= (double)L.ny ? L.ny - 1 : (int32_t)gy);
+  const int64_t gc = (int64_t)cj * L.nx + ci;
+  const int32_t n = L.n;
+  const double dn = (double)n;
+  const int32_t e0 = L.start[gc], e1 = L.start[gc + 1];
+  double md = INFINITY;
+  int32_t mid = 0x7fffffff;
+  SlTri mine{};
+  // candidate k = (face e0 + k / 18, cell k % 18): 3 rows j x 3 columns i x 2 orientations s around (u, v), the
+  // sequential scan's cells; cell 0 of a face also reports its inner cell
+  for (int32_t k = lane; k < (e1 - e0) * 18; k += 64) {
+    const lat::SlFace& S = L.face[L.item[e0 + k / 18]];
+    const int32_t c = k % 18;
+    SlTri r;
+    double d, u, v;
+    if (sl_inner(L, S, qx, qy, r, d, u, v)) {
+      if (c == 0 && knn_less(d, r.id, md, mid)) {
+        md = d;
+        mid = r.id;
+        mine = r;
+      }
+      continue;
+    }
+    if (!(u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL)) continue;
+    const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
+    const int32_t j = max(j0 - 1, 0) + c / 6, i = max(i0 - 1, 0) + (c / 2) % 3, s = c & 1;
+    if (j > j0 + 1 || i > i0 + 1 || i + j > n - 1) continue;
+    const double a = u - i, b = v - j;
+    const bool near = s == 0 ? (a >= -SL_LDEL && b >= -SL_LDEL && a + b <= 1.0 + SL_LDEL)
+                             : (i + j <= n - 2 && a <= 1.0 + SL_LDEL && b <= 1.0 + SL_LDEL && a + b >= 1.0 - SL_LDEL);
+    if (!near) continue;
+    r = sl_cell(L, S, i, j, s);
+    bool margin;
+    if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, md, mid)) {
+      md = d;
+      mid = r.id;
+      mine = r;
+    }
+  }
+  double bd = md;
+  int32_t bid = mid;
+  wave_min_key(bd, bid);
+  if (bid == 0x7fffffff) return false;
+  const uint64_t own = __ballot(md == bd && mid == bid);
+  const int src = __ffsll((unsigned long long)own) - 1;  // (one lane holds the winning cell; ties are one triangle)
+  out.x1 = __shfl(mine.x1, src, 64);
+  out.y1 = __shfl(mine.y1, src, 64);
+  out.x2 = __shfl(mine.x2, src, 64);
+  out.y2 = __shfl(mine.y2, src, 64);
+  out.x3 = __shfl(mine.x3, src, 64);
+  out.y3 = __shfl(mine.y3, src, 64);
+  out.a = __shfl(mine.a, src, 64);
+  out.b = __shfl(mine.b, src, 64);
+  out.d = __shfl(mine.d, src, 64);
+  out.id = bid;
+  bestd = bd;
+  rho2 = L.rho2[bid];
+  return true;
+}
+// sl_rank_ok by a whole wave: the centroids below (bestd, best) counted over the lanes (same result)
+__device__ __forceinline__ bool sl_rank_ok_wave(const GridDev& G, double qx, double qy, double bestd, int32_t best) {
+  const int lane = threadIdx.x & 63;
+  const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
+  const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
+  const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
+  int cnt = 0;
+  for (int32_t j = j0; j <= j1; ++j) {
+    const int32_t f0 = G.start[(int64_t)j * G.nx + i0], f1 = G.start[(int64_t)j * G.nx + i1 + 1];
+    for (int32_t e = f0; e < f1; e += 64) {
+      bool below = false;
+      if (e + lane < f1) {
+        const double dx = G.px[e + lane] - qx, dy = G.py[e + lane] - qy;
+        below = knn_less(dx * dx + dy * dy, G.item[e + lane], bestd, best);
+      }
+      cnt += __popcll(__ballot(below));
+      if (cnt >= KNN) return false;
+    }
+  }
+  return true;
+}
+__global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev G, int64_t row0, int64_t n,
+                                                const double* __restrict__ ux, const double* __restrict__ uy, double dt,
+                                                const double* __restrict__ c, double* __restrict__ cout,
+                                                const double* __restrict__ wmix, int32_t* notfound, double* part,
+                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt,
+                                                int32_t nbq) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (BS / 64), gw = (int64_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
+  for (int64_t ob = gw; ob < nbq; ob += nw) {
+    int32_t cnt[BS / 64];
+    int32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < BS / 64; ++w) tot += (cnt[w] = qcnt[BS / 64 * ob + w]);
+    if (tot == 0) continue;  // (wave-uniform)
+    int64_t r0, r1;
+    rows_of_block(n, nbq, ob, r0, r1);
+    double swc = 0.0, nnf = 0.0;
+    for (int w = 0; w < BS / 64; ++w)
+      for (int32_t p = 0; p < cnt[w]; ++p) {
+        const int64_t i = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + w) * 64 + (p & 63)], g = row0 + i;
+        double xb, yb;
+        sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
+        SlTri r;
+        double bestd;
+        float rho2;
+        const bool cand = sl_best_wave(L, xb, yb, r, bestd, rho2);
+        const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok_wave(G, xb, yb, bestd, r.id));
+        double cn;
+        if (ok) {
+          cn = sl_value(r, xb, yb, c);
+        } else {
+          cn = c[g];
+          nnf += 1.0;
+        }
+        if (lane == 0) {
+          stnt(cout + g, cn);
+          if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;
+        }
+        swc += (wmix ? wmix[i] : 0.0) * cn;
+      }
+    if (lane == 0) {  // k_sl's partials of block ob plus this pass's (this wave alone writes them)
+      part[ob] += swc;
+      part[2 * SLB + ob] += nnf;
+    }
+  }
 }
 
 // the locator's answer for every row's own node (q = its node after the x wrap: zero velocity), once
@@ -3370,7 +3534,8 @@ __device__ __forceinline__ void cheb_body(const SellDev& A, const FaceDev& fc, c
       const int64_t rr = row >= 0 ? row : 0;
       const T brow = (T)b[rr], di = dinv[rr];
       const T xrow = MODE == 1 ? xin[rr] : (T)0, drow = MODE == 1 ? d[rr] : (T)0;
-      const double rrow = RD ? rdot[rr] : 0.0;
+      // (ghost rows one layer out -- deep halos, row >= n_own -- add nothing to <rdot, x_out>)
+      const double rrow = RD && row < A.n_own ? rdot[rr] : 0.0;
       T ax = 0;
       if constexpr (MODE == 1) ax = sell_row_dot<C16>(A, val, xin, s, lane);
       else if constexpr (MODE == 2)

@@ -157,6 +157,9 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
     N = mesh.N
     sim = stokes(mesh, tol=S.Tolerances.production())
     assert sim.ctx.path_info()["sl_locator"] == "lattice"
+    monkeypatch.setenv("PUCFEM_SL_WAVE", "0")  # the queued points one lane each (k_sl_slow) instead of one wave
+    lane = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.delenv("PUCFEM_SL_WAVE")
     monkeypatch.setenv("PUCFEM_SL_RECORDS", "1")
     rec = stokes(mesh, tol=S.Tolerances.production())
     assert rec.ctx.path_info()["sl_locator"] == "records"
@@ -183,8 +186,10 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
             u[np.all(q == X, axis=1)] = 0.0
         c, nf = sl_on(sim.ctx, c0, u, dt)
         c_rec, nf_rec = sl_on(rec.ctx, c0, u, dt)
+        c_lane, nf_lane = sl_on(lane.ctx, c0, u, dt)
         assert np.array_equal(nf, nf_rec), kind
         assert np.array_equal(c, c_rec), kind
+        assert np.array_equal(nf, nf_lane) and np.array_equal(c, c_lane), kind  # k_sl_wave = k_sl_slow, bit for bit
         ref, ref_nf = O.sl_advect(c0, u, dt, X, T, tree)
         assert np.array_equal(nf, ref_nf), kind
         if kind in ("random", "hole", "inside"):
@@ -193,6 +198,7 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
             assert np.abs(c - ref).max() < 1e-13, kind
     sim.close()
     rec.close()
+    lane.close()
 
 
 @pytest.mark.parametrize("m", ["mesh1", "fine"])
