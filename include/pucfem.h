@@ -287,6 +287,13 @@ int pucfem_comm_info(void* ctx, int64_t* out4);
    The replaced reference sites are the dot products inside the np.linalg.solve calls
    (StokesColor.py:544-545, 555, 569), which become all-reduced CG dots on multi-rank runs. */
 int pucfem_comm_selftest(void* ctx, double* out4);
+/* unit probe of the single-reduction PCG's scalar kernel (k_cgcg_coef, the multi-rank pressure solve of
+   StokesColor.py:555,569): one launch on the context's stream from the given 8 reduced values red8, <b, b> bb,
+   the state sc5 (alpha, beta, gamma of the last iteration, alpha_(it-1), gamma_(it-1)) and iteration `it`;
+   ctl_out[2] receives the control word ({0, 0} continue, {1, k} converged at iteration k, {2, it} maxit,
+   {3, it} not finite), sc_out5 the new state.  Test infrastructure (tests/test_gpu_parity.py). */
+int pucfem_cgcg_coef_probe(void* ctx, const double* red8, double bb, const double* sc5, double tol2, int32_t it,
+                           int32_t maxit, double rho0, int32_t* ctl_out, double* sc_out5);
 /* cumulative data-path traffic of this rank's communicator (zeros without one): out[0] all-reduce calls,
    [1] all-reduced values, [2] point-to-point sends, [3] bytes sent, [4] grouped launches (group_start),
    [5] broadcasts (DESIGN.md §7's per-step counts; measurement only) */

@@ -88,6 +88,8 @@ SIGNATURES = {
     "pucfem_mixing_index": ([_P, _D, _D], ct.c_int),
     "pucfem_mixing_index_w": ([_P, _D, _D, _D], ct.c_int),
     "pucfem_comm_selftest": ([_P, _D], ct.c_int),
+    "pucfem_cgcg_coef_probe": ([_P, _D, ct.c_double, _D, ct.c_double, ct.c_int32, ct.c_int32, ct.c_double, _I32, _D],
+                               ct.c_int),
     "pucfem_timing_enable": ([_P, ct.c_int32], ct.c_int),
     "pucfem_timing_get": ([_P, ct.c_int32, _D, _I64, _D], ct.c_int),
     "pucfem_counters": ([_P, _I64, _D], ct.c_int),

@@ -5246,6 +5246,32 @@ int pucfem_comm_selftest(void* ctx, double* out4) {
   });
 }
 
+int pucfem_cgcg_coef_probe(void* ctx, const double* red8, double bb, const double* sc5, double tol2, int32_t it,
+                           int32_t maxit, double rho0, int32_t* ctl_out, double* sc_out5) {
+  return guard(ctx, [&] {
+    Ctx& c = *C(ctx);
+    c.need_dev();
+    std::vector<double> h(24, 0.0);
+    for (int k = 0; k < 8; ++k) h[k] = red8[k];
+    h[8] = bb;
+    h[9] = rho0;
+    for (int k = 0; k < 5; ++k) h[16 + k] = sc5[k];
+    DevTmp<double> d(h, c.st);
+    DevTmp<int> ctl(std::vector<int>{0, 0}, c.st);
+    hipLaunchKernelGGL(k_cgcg_coef, dim3(1), dim3(64), 0, c.st, (const double*)d.p, (const double*)(d.p + 8), d.p + 16,
+                       tol2, ctl.p, (int)it, (int)maxit, (const double*)(d.p + 9));
+    KCHK();
+    std::vector<int> hc;
+    std::vector<double> out;
+    ctl.get(hc, 2, c.st);
+    d.get(out, 24, c.st);
+    HIPCHK(hipStreamSynchronize(c.st));
+    ctl_out[0] = hc[0];
+    ctl_out[1] = hc[1];
+    for (int k = 0; k < 5; ++k) sc_out5[k] = out[16 + k];
+  });
+}
+
 // ---- host-only
 int pucfem_refine(int64_t N, const double* xy, const int32_t* mk, int64_t T, const int32_t* tris, int32_t levels,
                   int64_t* N_out, int64_t* T_out, double* xy_out, int32_t* mk_out, int32_t* tris_out) {
@@ -5460,7 +5486,16 @@ int pucfem_host_partition(void* ctx, int32_t rank, int32_t world, int64_t* n_own
     LocalPlan lp;
     std::vector<const Csr*> pats = {&c.P};
     if (c.Pp.nrows) pats.push_back(&c.Pp);
-    make_local_plan(pats, rs, rank, lp);
+    // PUCFEM_HOST_PLAN_DEEP=1 (test knob): the deep-halo plan of the W > 1 multigrid runs (make_local_plan2 with the
+    // patterns' ghost rows one layer out and their columns), as Ctx builds it for the finest level
+    const char* deep_env = std::getenv("PUCFEM_HOST_PLAN_DEEP");
+    if (deep_env && std::atoi(deep_env) != 0) {
+      std::vector<PatRows> pr;
+      for (const Csr* A : pats) pr.push_back({A, &rs});
+      make_local_plan2(pr, rs, rank, lp, &pats);
+    } else {
+      make_local_plan(pats, rs, rank, lp);
+    }
     *n_own = lp.n_own;
     *n_ghost = lp.n_ghost;
     *n_send = (i64)lp.send_local.size();

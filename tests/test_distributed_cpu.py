@@ -62,6 +62,39 @@ def test_partition_plan_invariants(world):
             assert np.array_equal(sent, gq)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_deep_halo_plan_invariants(world, monkeypatch):
+    """The deep-halo plan of the W > 1 multigrid runs (make_local_plan2 with `deep`: pucfem_host.cpp): every rank's
+    ghosts are its rows' off-rank neighbours (G1) AND their off-rank neighbours (G2) over the stiffness and pressure
+    patterns -- what a step computed redundantly on the G1 rows gathers -- and the send lists still mirror the
+    receivers' ghost lists."""
+    mesh = pf.load_mesh("fine", refine=2)
+    ctx, pairs = host_stokes_ctx(mesh)
+    K = ctx.host_csr(L.OP_K)
+    Pp = ctx.host_csr(L.OP_PRES)
+    monkeypatch.setenv("PUCFEM_HOST_PLAN_DEEP", "1")
+    plans = [ctx.host_partition(r, world) for r in range(world)]
+    monkeypatch.delenv("PUCFEM_HOST_PLAN_DEEP")
+    shallow = [ctx.host_partition(r, world) for r in range(world)]
+    owner = -np.ones(mesh.N, dtype=int)
+    for r, p in enumerate(plans):
+        owner[p["owned"]] = r
+    assert (owner >= 0).all()
+    for r, p in enumerate(plans):
+        rows = p["owned"]
+        nb1 = np.unique(np.concatenate([K[rows].indices, Pp[rows].indices]))
+        g1 = nb1[owner[nb1] != r]
+        assert np.array_equal(np.sort(shallow[r]["ghosts"]), g1)  # the one-layer plan: G1 exactly
+        nb2 = np.unique(np.concatenate([K[g1].indices, Pp[g1].indices]))
+        g12 = np.union1d(g1, nb2[owner[nb2] != r])
+        assert np.array_equal(np.sort(p["ghosts"]), g12)
+        assert len(g12) > len(g1)  # the second layer is real
+        assert np.array_equal(p["ghost_owner"], owner[p["ghosts"]])
+        for q in range(world):
+            if q != r:
+                assert np.array_equal(p["send_ids"][p["send_peer"] == q], plans[q]["ghosts"][plans[q]["ghost_owner"] == r])
+
+
 # ------------------------------------------------------------------------------------------- gloo
 def _free_port():
     s = socket.socket()

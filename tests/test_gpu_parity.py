@@ -542,3 +542,32 @@ def test_single_reduction_pcg_matches_standard(monkeypatch, refine):
         assert abs(x.it_p - y.it_p) <= 1 and abs(x.it_p2 - y.it_p2) <= 1, (x.it_p, x.it_p2, y.it_p, y.it_p2)
     a.close()
     b.close()
+
+
+def test_single_reduction_recurrence_needs_a_resolved_estimate():
+    """k_cgcg_coef: the one-step recurrence rho_(it+1) = rho - 2 alpha rs + alpha^2 ss only ends a solve
+    when the estimate is resolved -- positive and above its rounding floor (~eps (rho + 2 |alpha rs| + alpha^2 ss));
+    a cancelled (zero, negative or rounding-level) estimate leaves the decision to the next iteration's exact rho.
+    State: alpha_(it-1) = gamma_(it-1) = 1, gamma = 1, delta = 2, so beta = 1 and alpha = 1."""
+    mesh = pf.load_mesh("fine")
+    sim = stokes(mesh)
+
+    def coef(rho, rw, ww, tol2, b2=1.0):
+        red8 = np.array([rho, 0.0, 0.0, 1.0, 2.0, rw, ww, 0.0])  # rho, rs_old, ss_old, gamma, delta, rw, ww, ws
+        sc = np.array([0.0, 0.0, 0.0, 1.0, 1.0])
+        ctl = np.zeros(2, dtype=np.int32)
+        out = np.zeros(5)
+        L.check(sim.ctx.L.pucfem_cgcg_coef_probe(sim.ctx.h, L.dptr(red8), float(b2), L.dptr(sc), float(tol2), 1, 100,
+                                                 1.0, L.iptr(ctl), L.dptr(out)), sim.ctx.h)
+        if not (ctl[0] == 1 and ctl[1] == 1):  # (an exact pass returns before the scalars)
+            assert out[0] == 1.0 and out[1] == 1.0  # alpha, beta
+        return tuple(int(v) for v in ctl)
+
+    # rho1 = rho - 2 rw + ww
+    assert coef(1.0, 0.5, 0.0, 1e-14) == (0, 0)        # cancels to exactly 0: not accepted
+    assert coef(1.0, 0.5, -1e-3, 1e-14) == (0, 0)      # negative: not accepted
+    assert coef(1.0, 0.5, 1e-15, 1e-14) == (0, 0)      # 1e-15, below the rounding floor of 1: not accepted
+    assert coef(2.0, 0.5, 0.0, 1.0) == (1, 2)          # 1.0 <= tol2 b2, resolved: the update of it = 1 completes
+    assert coef(2.0, 0.25, 0.0, 1.0) == (0, 0)         # 1.5 > tol2 b2: continue
+    assert coef(1e-15, 0.0, 0.0, 1e-14) == (1, 1)      # the exact rho passes: converged at it = 1
+    sim.close()

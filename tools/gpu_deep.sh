@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 T=${TAG:-deep}
-timeout -k 10 400 python -u -m pytest -x -v -s --timeout 380 --timeout-method thread tests/test_gpu_parity.py -k "semilagrange or knn or step_pairs" \
+timeout -k 10 400 python -u -m pytest -x -v -s --timeout 380 --timeout-method thread tests/test_gpu_parity.py -k "semilagrange or knn or step_pairs or single_reduction" \
   > gpurun_out/${T}_sl.out 2>&1
 rc=$?; echo "sl rc=$rc" >&2; grep -E "PASSED|FAILED|ERROR|passed|failed|Error" gpurun_out/${T}_sl.out | tail -20 >&2
 [ $rc -ne 0 ] && exit $rc
