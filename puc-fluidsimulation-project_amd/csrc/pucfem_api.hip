@@ -266,8 +266,11 @@ struct MgLevel {
   //   current at the ghosts the next consumer gathers: z for the PCG's A z (finest), x for the prolongation into
   //   the finer level (xc_deep, on that finer level: its prolongation's coarse columns lie in own + G1).
   // Every rank takes the same path (the flags are all-reduced at build).
+  // - pr_deep: the prolongation into this level also runs on its ghost rows (x there is current since the exchange
+  //   before the residual), its coarse columns in level l - 1's own + G1 rows: the post-smoothing's first pair needs
+  //   no exchange of x.
   std::vector<i32> g1;
-  bool deep = false, res_deep = false, xc_deep = false;
+  bool deep = false, res_deep = false, xc_deep = false, pr_deep = false;
   i64 r_r0 = 0;  // first row of this level's restriction operator (rows live on level l-1)
   i64 own0(int rank) const { return rep ? 0 : rs[rank]; }
   // lattice face parts (Ctx::lattice): the faces whose interiors are this rank's rows of this level,
@@ -757,8 +760,12 @@ struct Ctx {
                                                : 0;
   bool sl_wave = !(std::getenv("PUCFEM_SL_WAVE") && std::atoi(std::getenv("PUCFEM_SL_WAVE")) == 0);
   int nb_sl(i64 n) const {
+    if (sl_rec_wave(n)) return (int)((n + BS / 64 - 1) / (BS / 64));  // k_sl_rec_wave: a wave per row
     return (int)std::max<i64>(1, std::min<i64>(sl_cap, (n + 4 * 64 - 1) / (4 * 64)));
   }
+  // the record locator on a small mesh (mesh.1, mesh_fine): one wave per row in one launch instead of k_sl queueing
+  // every row for k_sl_slow's one lane per point (PUCFEM_SL_WAVE=0 keeps the two passes)
+  bool sl_rec_wave(i64 n) const { return !lat_sl && sl_wave && n <= SLB * (BS / 64); }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
 
   // ------------------------------------------------------------------ timing helpers
@@ -847,6 +854,10 @@ struct Ctx {
       else
         klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
                 dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
+    } else if (sl_rec_wave(n) && !ro.out) {
+      kl_lds = 0;
+      klaunch(4, 8.0 * 6 * (double)n, k_sl_rec_wave, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx,
+              vy, dt, cf, cn, w, nf, part_sl);
     } else {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
@@ -1471,8 +1482,9 @@ struct Ctx {
   template <typename T, typename TB>
   // toz: the last step writes the preconditioned residual (z32 in the fp32 cycle, z in the fp64 one)
   // last_g (deep halos): the last step also runs on the ghost rows one layer out (x and d exchanged before it)
+  // xin_cur (deep halos): xin's ghosts (two layers) are current, the first step needs no exchange
   T* mg_smooth(MgLevel& L, const DevSell& A, const HFace& hf, MgBufs<T>& B, const TB* b, T* xin, T* xa, T* xb,
-               bool tozr, const double* rdot, double* part, int deg, bool last_g = false) {
+               bool tozr, const double* rdot, double* part, int deg, bool last_g = false, bool xin_cur = false) {
     const double lmax = L.lmax, lmin = lmax / prm.mg_ratio;
     const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
     double rho_old = 1.0 / sigma;
@@ -1526,7 +1538,8 @@ struct Ctx {
         // (W > 1: a general-step pair only where d_a is not read, c1 = 0: d is not exchanged before it)
         if (pairs && mode != 0 && k + 1 < deg && !(next_last && (tozr || rdot || last_g)) &&
             (!dg || mode == 2 || c1 == 0.0)) {
-          if (dg && mode == 1) mg_halo(L, cur);  // x_a two layers out: the first step runs on the ghost rows
+          if (dg && mode == 1 && !(xin_cur && cur == xin)) mg_halo(L, cur);  // x_a two layers out: the first step
+                                                                              // runs on the ghost rows
           // steps k, k + 1: x_a = cur (mode 1) -> x_{a+1} in p1 (skeleton rows, the face rows next to
           // them) -> x_{a+2} in p2; d_a = dcur -> d_{a+2} in the other d buffer
           float* p1 = mode == 2 ? xa : (cur == xa ? xb : xa);
@@ -1586,7 +1599,7 @@ struct Ctx {
       const bool gl = last && last_g && dg;
       if (mode == 1) {
         if (gl) mg_halo(L, cur, dcur);
-        else mg_halo(L, cur);
+        else if (!(xin_cur && cur == xin && k == 0)) mg_halo(L, cur);
       }
       const DevSell& As = gl ? A.with_ghosts() : A;
       const bool timed = finest && mode != 0;
@@ -1594,7 +1607,9 @@ struct Ctx {
       const bool toz = last && tozr;
       if (toz) z_cur = gl;
       const FaceDev fc = rd ? hf.part() : hf.full();
-      const int nb = rd ? grid_part(fc, As) : grid_full(fc, As);
+      // (the grid of the own rows also with the ghost rows, whose slices its SELL blocks share: the <r, z> partials
+      // keep the block count the PCG's reduction reads)
+      const int nb = rd ? grid_part(fc, A) : grid_full(fc, A);
       const T* xi = mode == 1 ? cur : nullptr;
       // algorithmic bytes: matrix (value + column) per entry; per row x_in (mode 1) or b and dinv
       // (mode 2) gathered once, b, dinv, d read (mode 1), d and x_out written, <r, z>'s r; face rows
@@ -1706,11 +1721,14 @@ struct Ctx {
     }
     T* xc = vcycle<T, T>(l - 1, CB.b, nullptr, nullptr);
     if (!(dist() && L.xc_deep)) mg_halo(C, xc);  // (xc_deep: level l - 1's last step wrote its ghosts one layer out)
-    // prolongation: entries, coarse x read once, fine x read + written
+    // prolongation: entries, coarse x read once, fine x read + written; pr_deep: also on this level's ghost rows (x
+    // there is current since the exchange before the residual), so the post-smoothing starts without an exchange
+    const bool pg = dist() && L.pr_deep;
+    const DevSell& Apr = pg ? L.dPr.with_ghosts() : L.dPr;
     klaunch(finest ? 7 : -1,
             (double)(sizeof(T) + 4) * (double)L.dPr.nnz + L.dPr.row_bytes() * (double)L.dPr.nrows +
                 (double)sizeof(T) * (double)(2 * A.own() + L.dR.nrows + L.hR.rows),
-            k_transfer<T>, dim3(grid_full(fpr, L.dPr)), dim3(BS), L.dPr.view(), fpr, (const T*)B.Prval, (const T*)xc,
+            k_transfer<T>, dim3(grid_full(fpr, Apr)), dim3(BS), Apr.view(), fpr, (const T*)B.Prval, (const T*)xc,
             x, 1, (const int*)ctl);
     KCHK();
     T* other = (x == xa) ? xb : xa;
@@ -1718,7 +1736,7 @@ struct Ctx {
     // the last step on the ghost rows one layer out where its consumer gathers them: the PCG's A z on the finest
     // level, the prolongation into level l + 1 (xc_deep) below it
     const bool last_g = dist() && L.deep && (finest || mg[l + 1].xc_deep);
-    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part, post, last_g);
+    return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part, post, last_g, pg);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
@@ -3213,6 +3231,8 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
       L.dPr = DevSell{c.upload(S.slice_off), c.upload(S.slice_w), c.upload(S.col), nullptr, S.nslices, S.nrows,
                       S.rows.empty() ? L.Pr.rowptr[r0 + n] - L.Pr.rowptr[r0] : S.nnz, S.padded};
       if (!S.rows.empty()) L.dPr.rows = c.upload(S.rows);
+      L.dPr.n_own = n;
+      L.dPr.ghost_slices(S);
       B.Prval = upload_as<T>(c, tmp);
       const Sell& R = L.sR;
       sell_values_x(L.R, L.r_r0, R, L.R.val, tmp);
@@ -3533,6 +3553,21 @@ void build(Ctx& c) {
           }
         }
       L.xc_deep = ok;
+      // ... and on this level's ghost rows too (pr_deep): their coarse columns in level l - 1's own + G1 rows
+      ok = L.xc_deep;
+      for (size_t k = 0; k < L.lp.ghost_global.size() && ok; ++k) {
+        const i32 r = L.lp.ghost_global[k];
+        for (i64 e = L.Pr.rowptr[r]; e < L.Pr.rowptr[r + 1]; ++e) {
+          const i32 j = L.Pr.col[e];
+          if ((j < clo || j >= chi) && !in_g1(C.g1, j)) {
+            ok = false;
+            break;
+          }
+        }
+      }
+      L.pr_deep = ok;
+      if (L.pr_deep)  // the prolongation's SELL: + every ghost row of this level (rows in this level's plan)
+        sell_append_ghost_rows(L.Pr, L.lp.ghost_global, C.lp, L.sPr, &L.lp);
     }
     if (c.lattice) {  // face tables and coefficient records of every level (pucfem_lattice.hpp)
       const double dtnu = prm.dt * prm.nu;
@@ -3789,11 +3824,12 @@ void build(Ctx& c) {
   }
   if (c.dist() && c.use_mg) {  // deep-halo flags: every rank takes the same exchanges (a flag off anywhere is off)
     const size_t nl = c.mg.size();
-    std::vector<double> off(3 * nl);
+    std::vector<double> off(4 * nl);
     for (size_t l = 0; l < nl; ++l) {
-      off[3 * l] = c.mg[l].deep ? 0.0 : 1.0;
-      off[3 * l + 1] = c.mg[l].res_deep ? 0.0 : 1.0;
-      off[3 * l + 2] = c.mg[l].xc_deep ? 0.0 : 1.0;
+      off[4 * l] = c.mg[l].deep ? 0.0 : 1.0;
+      off[4 * l + 1] = c.mg[l].res_deep ? 0.0 : 1.0;
+      off[4 * l + 2] = c.mg[l].xc_deep ? 0.0 : 1.0;
+      off[4 * l + 3] = c.mg[l].pr_deep ? 0.0 : 1.0;
     }
     DevTmp<double> t(off, c.st);
     c.comm->allreduce(t.p, off.size(), true, c.st);
@@ -3801,9 +3837,10 @@ void build(Ctx& c) {
     HIPCHK(hipStreamSynchronize(c.st));
     for (size_t l = 0; l < nl; ++l) {
       MgLevel& L = c.mg[l];
-      L.deep = L.deep && off[3 * l] == 0.0;
-      L.res_deep = L.deep && L.res_deep && off[3 * l + 1] == 0.0;
-      L.xc_deep = l > 0 && c.mg[l - 1].deep && L.xc_deep && off[3 * l + 2] == 0.0;
+      L.deep = L.deep && off[4 * l] == 0.0;
+      L.res_deep = L.deep && L.res_deep && off[4 * l + 1] == 0.0;
+      L.xc_deep = l > 0 && c.mg[l - 1].deep && L.xc_deep && off[4 * l + 2] == 0.0;
+      L.pr_deep = L.deep && L.xc_deep && L.pr_deep && off[4 * l + 3] == 0.0;
     }
   }
   c.block_cg = c.prm.solver_path != 1;

@@ -1198,7 +1198,9 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
     }
 }
 
-void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S) {
+void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S,
+                            const LocalPlan* rows_plan) {
+  const LocalPlan& rp = rows_plan ? *rows_plan : cols;
   if (S.gk0 >= 0) throw std::runtime_error("SELL already has ghost rows");
   if (S.rows.empty() && S.nrows > 0) throw std::runtime_error("ghost rows need a row-listed SELL");
   S.nslices_own = S.nslices;
@@ -1213,8 +1215,8 @@ void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const L
     for (i64 l = 0; l < 64 && s * 64 + l < n; ++l) {
       const i64 g = grows[s * 64 + l];
       w = std::max(w, A.rowptr[g + 1] - A.rowptr[g]);
-      S.rows[S.gk0 + s * 64 + l] = to_local(cols, (i32)g);
-      if (S.rows[S.gk0 + s * 64 + l] < cols.n_own) throw std::runtime_error("ghost row list holds an owned row");
+      S.rows[S.gk0 + s * 64 + l] = to_local(rp, (i32)g);
+      if (S.rows[S.gk0 + s * 64 + l] < rp.n_own) throw std::runtime_error("ghost row list holds an owned row");
     }
     S.slice_w[S.nslices + s] = (i32)w;
     S.slice_off[S.nslices + s + 1] = S.slice_off[S.nslices + s] + w * 64;

@@ -270,7 +270,9 @@ void build_sell_rows(const Csr& A, i64 r0, const std::vector<i32>& rows, const L
 void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<double>& val, std::vector<double>& out);
 // append the rows `grows` (global ids, each a ghost of `cols`) to a row-listed SELL as whole slices of their own:
 // local output index = the ghost's local id, columns resolved in `cols`
-void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S);
+// (rows_plan: the plan holding the rows as ghosts, when it is not the columns' -- a transfer between two levels)
+void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S,
+                            const LocalPlan* rows_plan = nullptr);
 // the SELL image of A's rows in S (rows r0 + k, or r0 + S.rows[k]) with entry values f(r, e) computed in
 // place (r: the row's global index, e: its CSR entry) -- no full-length value array for a SELL that
 // holds only the lattice skeleton's rows

@@ -2752,6 +2752,100 @@ __global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev 
   }
 }
 
+// Record locator (meshes without a red-refinement hierarchy: mesh.1, mesh_fine), whose k_sl has no fast path and
+// queued every row for k_sl_slow's one lane per point: one wave per ROW instead, in one launch (k_sl_rec_wave), the
+// records of q's grid cell tested by the lanes together (the passing record with the smallest (d^2, id) key, as
+// sl_best's scan returns it) and the rank count as k_sl_wave's.  Same arithmetic per candidate: the same bits.
+__device__ __forceinline__ bool sl_best_wave(const LocDev& L, double qx, double qy, SlTri& out, double& bestd,
+                                             float& rho2) {
+  const int lane = threadIdx.x & 63;
+  const int32_t ci = gcell(qx, L.x0, L.hx, L.nx), cj = gcell(qy, L.y0, L.hy, L.ny);
+  const int64_t cell = (int64_t)cj * L.nx + ci;
+  const int32_t e0 = L.start[cell], e1 = L.start[cell + 1];
+  double md = INFINITY;
+  int32_t mid = 0x7fffffff, mpos = -1;
+  SlTri mine{};
+  for (int32_t e = e0 + lane; e < e1; e += 64) {
+    const int32_t pos = L.item[e];
+    const SlTri r = sl_tri(L, pos);
+    double d;
+    bool margin;
+    if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, md, mid)) {
+      md = d;
+      mid = r.id;
+      mpos = pos;
+      mine = r;
+    }
+  }
+  double bd = md;
+  int32_t bid = mid;
+  wave_min_key(bd, bid);
+  if (bid == 0x7fffffff) return false;
+  const int src = __ffsll((unsigned long long)__ballot(md == bd && mid == bid)) - 1;
+  out.x1 = __shfl(mine.x1, src, 64);
+  out.y1 = __shfl(mine.y1, src, 64);
+  out.x2 = __shfl(mine.x2, src, 64);
+  out.y2 = __shfl(mine.y2, src, 64);
+  out.x3 = __shfl(mine.x3, src, 64);
+  out.y3 = __shfl(mine.y3, src, 64);
+  out.a = __shfl(mine.a, src, 64);
+  out.b = __shfl(mine.b, src, 64);
+  out.d = __shfl(mine.d, src, 64);
+  out.id = bid;
+  bestd = bd;
+  rho2 = L.rho2[__shfl(mpos, src, 64)];
+  return true;
+}
+// one row per wave (row = 4 blockIdx + wave); partials of the block's rows (its four waves in order) at the block's
+// index, as k_sl + k_sl_slow leave them: [0] sum w c, [1] sum w, [2] not-found count
+__global__ __launch_bounds__(BS) void k_sl_rec_wave(MeshDev M, LocDev L, GridDev G, int64_t row0, int64_t n,
+                                                    const double* __restrict__ ux, const double* __restrict__ uy,
+                                                    double dt, const double* __restrict__ c, double* __restrict__ cout,
+                                                    const double* __restrict__ wmix, int32_t* notfound, double* part) {
+  __shared__ double sw_[3][BS / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * (BS / 64) + wv;
+  double swc = 0.0, sw = 0.0, nnf = 0.0;
+  if (i < n) {
+    const int64_t g = row0 + i;
+    double xb, yb;
+    sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
+    SlTri r;
+    double bestd;
+    float rho2;
+    const bool cand = sl_best_wave(L, xb, yb, r, bestd, rho2);
+    const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok_wave(G, xb, yb, bestd, r.id));
+    double cn;
+    if (ok) {
+      cn = sl_value(r, xb, yb, c);
+    } else {
+      cn = c[g];
+      nnf = 1.0;
+    }
+    if (lane == 0) {
+      stnt(cout + g, cn);
+      if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;
+    }
+    const double w = wmix ? wmix[i] : 0.0;
+    sw = w;
+    swc = w * cn;
+  }
+  if (lane == 0) {
+    sw_[0][wv] = swc;
+    sw_[1][wv] = sw;
+    sw_[2][wv] = nnf;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      double a = 0.0;
+      for (int k = 0; k < BS / 64; ++k) a += sw_[v][k];
+      part[(int64_t)v * SLB + blockIdx.x] = a;
+    }
+  }
+}
+
 // the locator's answer for every row's own node (q = its node after the x wrap: zero velocity), once
 // at build: the triangle id, or -1 when no triangle is accepted
 template <class LOC>

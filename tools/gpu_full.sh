@@ -1,12 +1,13 @@
 #!/bin/bash
-# the whole GPU suite, smoke(), then the driver command twice (no secondary legs)
+# The whole GPU suite (one process), then the W=8 exchange counts at L7
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${1:-full}; mkdir -p "$OUT"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1; rc=$?
-echo "pytest rc=$rc" >&2; tail -n 2 $OUT/pytest_gpu.txt >&2; [ $rc -ne 0 ] && { grep -B5 -A30 "^_____" $OUT/pytest_gpu.txt | head -80 >&2; exit $rc; }
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo smoke failed >&2; tail -20 $OUT/smoke.txt >&2; exit 1; }
-tail -n 2 $OUT/smoke.txt >&2
-for rep in 1 2; do
-  timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-secondary --warmup 5 --steps 20 > $OUT/bench_$rep.json 2> $OUT/bench_$rep.err || exit 1
-  python -c "import json; d=json.loads(open('$OUT/bench_$rep.json').read().strip().splitlines()[-1]); k=d['kernels']; print('bench', round(d['value'],2), 'steady', round(d['steady']['steps_per_s'],2), 'launches', round(d['launches_per_step'],1), d['roofline']['kernel'], round(d['roofline']['frac'],3), {n.split()[0]: round(v['avg_launch_ms']*1e3,1) for n, v in k.items()})" >&2
-done
+mkdir -p gpurun_out
+T=${TAG:-full}
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 900 --timeout-method thread --durations=25 \
+  > gpurun_out/${T}_pytest_gpu.txt 2>&1
+rc=$?; echo "pytest rc=$rc" >&2; grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/${T}_pytest_gpu.txt | tail -8 >&2
+grep -E "W=8|L6 W=8|L5 W=8" gpurun_out/${T}_pytest_gpu.txt | tail -20 >&2
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 150 python -u tools/comm_probe.py 7 8 5 > gpurun_out/${T}_comm_probe_l7_w8.txt 2>&1
+rc=$?; echo "probe rc=$rc" >&2; tail -4 gpurun_out/${T}_comm_probe_l7_w8.txt >&2
+exit $rc
