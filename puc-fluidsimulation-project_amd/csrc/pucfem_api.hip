@@ -480,7 +480,9 @@ struct Ctx {
   // deep halos on W > 1 ranks (MgLevel::deep; PUCFEM_DEEP_HALO=0 keeps one-layer halos and single smoothing steps,
   // a test / measurement knob)
   bool deep_halo = !(std::getenv("PUCFEM_DEEP_HALO") && std::atoi(std::getenv("PUCFEM_DEEP_HALO")) == 0);
-  bool z_cur = false;  // the finest level's last smoothing step wrote z at the ghost rows one layer out too
+  // PUCFEM_DEEP_MASK (diagnostic knob, default all): 1 multigrid step pairs, 2 residual rows, 4 last smoothing step
+  // (+ the skipped z / x exchanges), 8 prolongation rows, 16 the viscous first pair -- each use of the ghost rows
+  int deep_mask = std::getenv("PUCFEM_DEEP_MASK") ? std::atoi(std::getenv("PUCFEM_DEEP_MASK")) : 31;
   Macro macro;
   LatticeLevel lat_fine;  // the finest level's layout until build_mg_host moves it into mg.back()
   HFace fK, fVisc, fP;  // finest level: K / Gx / Gy (plain table), scaled A_visc (plain), pressure (merged)
@@ -1174,7 +1176,7 @@ struct Ctx {
     // step pairs (k_vcheb_pair): a face part of lattice size <= VP_HALO.  On W > 1 ranks only the solve's first pair
     // (0, 1), whose first step also runs on the ghost rows one layer out (deep halos: x and b exchanged two layers
     // out together, one exchange for the two steps); later pairs would need d exchanged too, so single steps
-    const bool deepv = dist() && A.has_ghost_rows() && use_mg && mg.back().deep;
+    const bool deepv = dist() && A.has_ghost_rows() && use_mg && mg.back().deep && (deep_mask & 16);
     const DevSell Ag = A.with_ghosts();  // (= A without ghost rows)
     const int nbs = nb_for(Ag.nslices);  // a pair's SELL grids (its first launch covers the ghost rows)
     const bool pairs_ok = visc_pair && hf.items > 0 && fc.n <= VP_HALO &&
@@ -1512,7 +1514,7 @@ struct Ctx {
     bool pairs = false;
     // deep halos (W > 1): a pair's first step also runs on the ghost rows one layer out, so a pair needs one
     // exchange (x, two layers) where two single steps needed two -- pairs on every partitioned level
-    const bool dg = dist() && L.deep;
+    const bool dg = dist() && L.deep && (deep_mask & 1);
     if constexpr (std::is_same<T, float>::value && std::is_same<TB, float>::value)
       // (one rank: the finest level only; pairs on L6 / L5 too measured neutral to -0.7 %, r10m)
       pairs = mg_pair && hf.items > 0 && hf.d.n <= VP_HALO &&
@@ -1596,7 +1598,7 @@ struct Ctx {
       T* out = (cur == xa) ? xb : xa;
       const bool last = k == deg - 1;
       // the last step on the ghost rows one layer out too (deep halos): x two layers out and d one layer out
-      const bool gl = last && last_g && dg;
+      const bool gl = last && last_g && dist() && L.deep;
       if (mode == 1) {
         if (gl) mg_halo(L, cur, dcur);
         else if (!(xin_cur && cur == xin && k == 0)) mg_halo(L, cur);
@@ -1605,7 +1607,6 @@ struct Ctx {
       const bool timed = finest && mode != 0;
       const double* rd = last ? rdot : nullptr;
       const bool toz = last && tozr;
-      if (toz) z_cur = gl;
       const FaceDev fc = rd ? hf.part() : hf.full();
       // (the grid of the own rows also with the ghost rows, whose slices its SELL blocks share: the <r, z> partials
       // keep the block count the PCG's reduction reads)
@@ -1684,7 +1685,7 @@ struct Ctx {
     mg_halo(L, x);
     // residual: matrix entries, x gathered once, b read, res written; deep halos: also on the ghost rows one layer
     // out, which the restriction gathers (no exchange of the residual)
-    const bool rg = dist() && L.res_deep;
+    const bool rg = dist() && L.res_deep && (deep_mask & 2);
     const DevSell& Ar = rg ? A.with_ghosts() : A;
     const double bytes_res = (B.val_bytes() + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows +
                              (double)A.own() * (2.0 * sizeof(T) + sizeof(TB));
@@ -1720,10 +1721,10 @@ struct Ctx {
       comm->group_end(st);
     }
     T* xc = vcycle<T, T>(l - 1, CB.b, nullptr, nullptr);
-    if (!(dist() && L.xc_deep)) mg_halo(C, xc);  // (xc_deep: level l - 1's last step wrote its ghosts one layer out)
+    if (!(dist() && L.xc_deep && (deep_mask & 4))) mg_halo(C, xc);  // (xc_deep: level l - 1's last step wrote its ghosts one layer out)
     // prolongation: entries, coarse x read once, fine x read + written; pr_deep: also on this level's ghost rows (x
     // there is current since the exchange before the residual), so the post-smoothing starts without an exchange
-    const bool pg = dist() && L.pr_deep;
+    const bool pg = dist() && L.pr_deep && (deep_mask & 8) && ((deep_mask & 4) || C.rep);
     const DevSell& Apr = pg ? L.dPr.with_ghosts() : L.dPr;
     klaunch(finest ? 7 : -1,
             (double)(sizeof(T) + 4) * (double)L.dPr.nnz + L.dPr.row_bytes() * (double)L.dPr.nrows +
@@ -1733,16 +1734,18 @@ struct Ctx {
     KCHK();
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
-    // the last step on the ghost rows one layer out where its consumer gathers them: the PCG's A z on the finest
-    // level, the prolongation into level l + 1 (xc_deep) below it
-    const bool last_g = dist() && L.deep && (finest || mg[l + 1].xc_deep);
+    // the last step on the ghost rows one layer out where its consumer gathers them: the prolongation into level
+    // l + 1 (xc_deep).  Not z on the finest level: the outer fp64 PCG needs w = A z of ONE vector z (its recurrences
+    // s = A p and r = b - A y hold only then), and a ghost row's fp32 step, computed through its stored row, rounds
+    // differently from the owner's face stencil -- z's ghosts are exchanged (the rest of the V-cycle is a
+    // preconditioner, where such rounding acts like the fp32 cycle's own; W = 2 at rtol 1e-12 stalled otherwise)
+    const bool last_g = dist() && L.deep && (deep_mask & 4) && !finest && mg[l + 1].xc_deep;
     return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part, post, last_g, pg);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
   void precondition(double* rz_part = nullptr) {
     if (!rz_part) rz_part = part_d + 2 * MAXB;
-    z_cur = false;
     if (mg_single) {
       vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], rz_part);
     } else {
@@ -1924,10 +1927,8 @@ struct Ctx {
         if (cgcg) {  // single-reduction iteration (k_cgcg_*)
           ++cgcg_iters;
           precondition(part_cc + 3 * MAXB);
-          if (!z_cur) {  // (deep halos: the last smoothing step wrote z's ghosts one layer out)
-            if (mg_single) mg_halo(mg.back(), z32);
-            else halo(z);
-          }
+          if (mg_single) mg_halo(mg.back(), z32);
+          else halo(z);
           with_c16(dPp, [&](auto c16) {
             if (mg_single)
               klaunch(1, bytes_w, k_cgcg_w<decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -1965,10 +1966,8 @@ struct Ctx {
         Red rz{redbuf + 32, 1, 1};
         if (ro(redbuf + 32, CNT_RZ, 1).out) red_done(redbuf + 32, 1, false);
         else rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-        if (!z_cur) {
-          if (mg_single) mg_halo(mg.back(), z32);
-          else halo(z);
-        }
+        if (mg_single) mg_halo(mg.back(), z32);
+        else halo(z);
         with_c16(dPp, [&](auto c16) {
           if (mg_single)
             klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -3553,13 +3552,14 @@ void build(Ctx& c) {
           }
         }
       L.xc_deep = ok;
-      // ... and on this level's ghost rows too (pr_deep): their coarse columns in level l - 1's own + G1 rows
-      ok = L.xc_deep;
+      // ... and on this level's ghost rows too (pr_deep): their coarse columns in level l - 1's own + G1 rows, or
+      // any, from a replicated level l - 1 (whose every value every rank holds)
+      ok = L.xc_deep || C.rep;
       for (size_t k = 0; k < L.lp.ghost_global.size() && ok; ++k) {
         const i32 r = L.lp.ghost_global[k];
         for (i64 e = L.Pr.rowptr[r]; e < L.Pr.rowptr[r + 1]; ++e) {
           const i32 j = L.Pr.col[e];
-          if ((j < clo || j >= chi) && !in_g1(C.g1, j)) {
+          if (!C.rep && (j < clo || j >= chi) && !in_g1(C.g1, j)) {
             ok = false;
             break;
           }
@@ -3840,7 +3840,7 @@ void build(Ctx& c) {
       L.deep = L.deep && off[4 * l] == 0.0;
       L.res_deep = L.deep && L.res_deep && off[4 * l + 1] == 0.0;
       L.xc_deep = l > 0 && c.mg[l - 1].deep && L.xc_deep && off[4 * l + 2] == 0.0;
-      L.pr_deep = L.deep && L.xc_deep && L.pr_deep && off[4 * l + 3] == 0.0;
+      L.pr_deep = l > 0 && L.deep && (L.xc_deep || c.mg[l - 1].rep) && L.pr_deep && off[4 * l + 3] == 0.0;
     }
   }
   c.block_cg = c.prm.solver_path != 1;

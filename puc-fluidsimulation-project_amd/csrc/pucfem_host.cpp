@@ -1191,7 +1191,7 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
   for (i64 s = 0; s < S.nslices; ++s)
     for (i64 l = 0; l < 64; ++l) {
       const i64 k = s * 64 + l;
-      if (k >= S.nrows) continue;
+      if (S.rows[k] < 0) continue;  // (a padding lane: the own rows' last slice is padded before any ghost rows)
       const i64 r = S.global_row(r0, k);
       const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
       for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = val[b + e];

@@ -283,7 +283,7 @@ void sell_values_fn(const Csr& A, i64 r0, const Sell& S, F&& f, std::vector<doub
     for (i64 s = s0; s < s1; ++s)
       for (i64 l = 0; l < 64; ++l) {
         const i64 k = s * 64 + l;
-        if (k >= S.nrows) continue;
+        if (S.rows.empty() ? k >= S.nrows : S.rows[k] < 0) continue;  // (row lists: padding lanes are -1)
         const i64 r = S.rows.empty() ? r0 + k : S.global_row(r0, k);
         const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
         for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = f(r, b + e);
