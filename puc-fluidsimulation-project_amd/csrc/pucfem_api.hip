@@ -474,6 +474,11 @@ struct Ctx {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   double* gstats = nullptr;
+  // the replayed step's records: a device ring of GRING steps (k_stats_ring), copied out per call / full ring
+  static constexpr int GRING = 1024;
+  double* gring = nullptr;
+  int* gcount = nullptr;
+  bool gcapture = false;  // (the step being captured)
 
   // ---- lattice operators (pucfem_lattice.hpp): multigrid hierarchies with faces of interior nodes
   bool lattice = false;
@@ -856,10 +861,10 @@ struct Ctx {
       else
         klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
                 dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);
-    } else if (sl_rec_wave(n) && !ro.out) {
+    } else if (sl_rec_wave(n)) {
       kl_lds = 0;
       klaunch(4, 8.0 * 6 * (double)n, k_sl_rec_wave, dim3(nb), dim3(BS), M, lgrid, cgrid, (int64_t)row0, (int64_t)n, vx,
-              vy, dt, cf, cn, w, nf, part_sl);
+              vy, dt, cf, cn, w, nf, part_sl, ro);
     } else {
       klaunch(4, 8.0 * 6 * (double)n, k_sl<LocDev>, dim3(nb), dim3(BS), M, lgrid, (int64_t)row0, (int64_t)n, vx, vy,
               dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
@@ -2161,6 +2166,15 @@ struct Ctx {
     const bool proj = use_mg && proj_k > 0 && (which == 1 || which == 2);
     // with a projected guess k_mdot2 (the first pass over the rows) forms the right-hand side itself
     const bool rhs_in_mdot = proj && rhs_fuse && !sc && proj_pend[proj_slot(which)];
+    if (dense) {  // small meshes: right-hand side, dense solve and p in one launch (k_dense_pres)
+      algo_bytes += 8.0 * (double)n * (double)n + 48.0 * (double)n;
+      hipLaunchKernelGGL(k_dense_pres, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n,
+                         (const double*)dPinv, (const double*)braw, (const int32_t*)dslave_of,
+                         (const int32_t*)dmaster_of, sb.p, sb.nb, 1.0 / (double)n_free, yst, pout);
+      KCHK();
+      halo(pout);
+      return 0;
+    }
     if (!rhs_in_mdot) {
       algo_bytes += 24.0 * (double)n;  // braw, slave_of, master_of read; bh written
       hipLaunchKernelGGL(k_pres_rhs, dim3(grid_ew(n)), dim3(BS), 0, st, n, braw, dslave_of, dmaster_of, sc,
@@ -2486,15 +2500,15 @@ struct Ctx {
     sl_ro = ro(vals + 2, CNT_SL, 3, SLB);
     sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, sl_ro);
     KCHK();
-    // the replica keeps its (halo) values; only the owned segment is new
-    HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
+    // (the replica keeps its halo values; k_mix2 copies the new owned segment into it)
     if (sl_ro.out) red_done(vals + 2, 3, false);
     else reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
     sl_ro = RedOut{};
     const int nbm = nb_rows(lp.n_own);
     algo_bytes += 16.0 * (double)lp.n_own;
     const RedOut rm = ro(vals + 5, CNT_MIX, 1);
-    hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx, rm);
+    hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, (const double*)c_new, dwmix, vals + 2, 1, 1,
+                       part_mx, rm, c_full);
     KCHK();
     if (rm.out) red_done(vals + 5, 1, false);
     else reduce_into(part_mx, nbm, 1, false, 5);
@@ -2563,11 +2577,11 @@ struct Ctx {
         sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, sl_ro);
       }
       KCHK();
-      if (graph_mode) {  // fixed buffers inside a captured graph: copy back instead of swapping
+      // fixed buffers inside a captured graph: k_mix2 copies the new values back instead of a swap
+      const bool mix_copy = graph_mode && !dye_impl;
+      if (graph_mode && dye_impl) {
         HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-      } else if (dist()) {  // the replica keeps its (halo) values; only the owned segment is new
-        HIPCHK(hipMemcpyAsync(c_full + lp.r0, c_new + lp.r0, sizeof(double) * lp.n_own, hipMemcpyDeviceToDevice, st));
-      } else {
+      } else if (!mix_copy) {
         std::swap(c_full, c_new);
       }
       if (sl_ro.out) red_done(vals + 2, 3, false);
@@ -2576,7 +2590,8 @@ struct Ctx {
       const int nbm = nb_rows(lp.n_own);
       algo_bytes += 16.0 * (double)lp.n_own;
       const RedOut rm = ro(vals + 5, CNT_MIX, 1);
-      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1, part_mx, rm);
+      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, mix_copy ? (const double*)c_new : c_full,
+                         dwmix, vals + 2, 1, 1, part_mx, rm, mix_copy ? c_full : (double*)nullptr);
       KCHK();
       if (rm.out) red_done(vals + 5, 1, false);
       else reduce_into(part_mx, nbm, 1, false, 5);
@@ -2584,7 +2599,8 @@ struct Ctx {
       tracer_advance(prm.dt);
     }
     if (!ovl) {
-      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 7);
+      if (gcapture) hipLaunchKernelGGL(k_stats_ring, dim3(1), dim3(64), 0, st, vals, gring, gcount, 7);
+      else hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 7);
       KCHK();
     }
     its[0] = itv;
@@ -3845,6 +3861,9 @@ void build(Ctx& c) {
   }
   c.block_cg = c.prm.solver_path != 1;
   c.dense = stokes && !c.dist() && N <= DENSE_MAX && c.prm.precond != 1 && c.prm.solver_path != 1;
+  // the small-mesh step is ~20 latency-bound launches replayed from a graph: its reductions finish inside their
+  // producers (RedOut, the last block reduces) instead of a k_reduce launch after each (PUCFEM_FUSED_RED=0 keeps them)
+  if (c.dense && !std::getenv("PUCFEM_FUSED_RED")) c.fused_red = true;
   clk.mark("device: A_visc, pressure, multigrid");
   // successive-RHS projections (multi-kernel CG paths only: the dense and one-workgroup solves of
   // small meshes need no better start)
@@ -4582,13 +4601,18 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
         // host synchronisation -> capture it once, replay it per step
         if (!c.gexec) {
           c.gstats = c.dalloc<double>(8);
+          c.gring = c.dalloc<double>(8 * (i64)Ctx::GRING);
+          c.gcount = c.dalloc<int>(1);
           HIPCHK(hipStreamSynchronize(c.st));
           c.graph_mode = true;
           int32_t tmp[3];
           HIPCHK(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
           try {
+            c.gcapture = true;
             c.stokes_step(c.gstats, tmp);
+            c.gcapture = false;
           } catch (...) {
+            c.gcapture = false;
             hipGraph_t g;
             (void)hipStreamEndCapture(c.st, &g);
             c.graph_mode = false;
@@ -4597,9 +4621,14 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
           HIPCHK(hipStreamEndCapture(c.st, &c.graph));
           HIPCHK(hipGraphInstantiate(&c.gexec, c.graph, nullptr, nullptr, 0));
         }
-        for (int s = 0; s < nsteps; ++s) {
+        HIPCHK(hipMemsetAsync(c.gcount, 0, sizeof(int), c.st));
+        for (int s = 0, k = 0; s < nsteps; ++s) {
           HIPCHK(hipGraphLaunch(c.gexec, c.st));
-          HIPCHK(hipMemcpyAsync(rec + 8 * s, c.gstats, 8 * sizeof(double), hipMemcpyDeviceToDevice, c.st));
+          if (++k == Ctx::GRING || s == nsteps - 1) {  // the ring's records -> this call's records
+            HIPCHK(hipMemcpyAsync(rec + 8 * (s + 1 - k), c.gring, sizeof(double) * 8 * k, hipMemcpyDeviceToDevice, c.st));
+            if (s < nsteps - 1) HIPCHK(hipMemsetAsync(c.gcount, 0, sizeof(int), c.st));
+            k = 0;
+          }
         }
       } else {
         c.graph_mode = c.gexec != nullptr;  // once captured, keep c in its fixed buffer

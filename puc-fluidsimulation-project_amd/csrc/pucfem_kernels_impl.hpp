@@ -2801,8 +2801,10 @@ __device__ __forceinline__ bool sl_best_wave(const LocDev& L, double qx, double 
 __global__ __launch_bounds__(BS) void k_sl_rec_wave(MeshDev M, LocDev L, GridDev G, int64_t row0, int64_t n,
                                                     const double* __restrict__ ux, const double* __restrict__ uy,
                                                     double dt, const double* __restrict__ c, double* __restrict__ cout,
-                                                    const double* __restrict__ wmix, int32_t* notfound, double* part) {
+                                                    const double* __restrict__ wmix, int32_t* notfound, double* part,
+                                                    RedOut ro = RedOut{}) {
   __shared__ double sw_[3][BS / 64];
+  __shared__ double sh[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * (BS / 64) + wv;
   double swc = 0.0, sw = 0.0, nnf = 0.0;
@@ -2841,9 +2843,11 @@ __global__ __launch_bounds__(BS) void k_sl_rec_wave(MeshDev M, LocDev L, GridDev
     for (int v = 0; v < 3; ++v) {
       double a = 0.0;
       for (int k = 0; k < BS / 64; ++k) a += sw_[v][k];
-      part[(int64_t)v * SLB + blockIdx.x] = a;
+      if (ro.out) red_part(ro, part, v, a);
+      else part[(int64_t)v * SLB + blockIdx.x] = a;
     }
   }
+  red_finish(ro, part, sh);
 }
 
 // the locator's answer for every row's own node (q = its node after the x wrap: zero velocity), once
@@ -2980,9 +2984,12 @@ __global__ __launch_bounds__(BS) void k_wsum(int64_t row0, int64_t n, const doub
 }
 
 // mixing_index second pass (StokesColor.py:399-401): partial sum w (c - mu)^2, mu from pass 1.
+// copy_to (non-null): also copies the owned segment of c there (the new dye into the replica: one launch less than
+// a separate device copy before the sums)
 __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const double* __restrict__ c,
                                              const double* __restrict__ wmix, const double* part1, int nb1,
-                                             int stride1, double* part, RedOut ro = RedOut{}) {
+                                             int stride1, double* part, RedOut ro = RedOut{},
+                                             double* __restrict__ copy_to = nullptr) {
   __shared__ double sh[4];
   const double swc = reduce_partials(part1, nb1, sh);
   const double sw = reduce_partials(part1 + stride1, nb1, sh);
@@ -2991,7 +2998,9 @@ __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const doub
   int64_t r0, r1;
   block_rows(n, r0, r1);
   for (int64_t i = r0 + threadIdx.x; i < r1; i += BS) {
-    const double d = c[row0 + i] - mu;
+    const double ci = c[row0 + i];
+    if (copy_to) copy_to[row0 + i] = ci;
+    const double d = ci - mu;
     acc += wmix[i] * (d * d);
   }
   const double t = block_sum(acc, sh);
@@ -3325,8 +3334,8 @@ __global__ void k_pack(int64_t n, const int32_t* __restrict__ idx, const T* __re
 // out : [0] max|div*| [1] max|final div| [2] I [3] mu [4] var [5] eaten [6] not-found
 // parts & 1: max |div u*| out[0]; & 2: max |final div| out[1]; & 4: the dye records out[2..6]
 // (2 and 4 are written by the side stream when the dye advection overlaps the next step)
-__global__ void k_stats(const double* vals, double* out, int parts) {
-  if (threadIdx.x == 0) {
+__device__ __forceinline__ void stats_body(const double* vals, double* out, int parts) {
+  {
     if (parts & 1) out[0] = vals[0];
     if (parts & 2) out[1] = vals[1];
     if (parts & 4) {
@@ -3338,6 +3347,18 @@ __global__ void k_stats(const double* vals, double* out, int parts) {
       out[5] = vals[6];
       out[6] = vals[4];
     }
+  }
+}
+__global__ void k_stats(const double* vals, double* out, int parts) {
+  if (threadIdx.x == 0) stats_body(vals, out, parts);
+}
+// a replayed small-mesh step (Ctx::graph_mode): the record goes to slot *count of a device ring and the count moves
+// on (one copy of the ring per pucfem_step call instead of a device copy per step)
+__global__ void k_stats_ring(const double* vals, double* ring, int* count, int parts) {
+  if (threadIdx.x == 0) {
+    const int k = count[0];
+    stats_body(vals, ring + 8 * (int64_t)k, parts);
+    count[0] = k + 1;
   }
 }
 
@@ -4131,6 +4152,43 @@ __global__ __launch_bounds__(CGB_THREADS) void k_cg_block(SellDev A, const doubl
 
 // dense 2-RHS matvec (small-mesh direct viscous solve): y0 = A x0, y1 = A x1; one wave per row
 // (x0 / x1 and y0 / y1: the interleaved velocity's components, stride VS)
+// small meshes (Ctx::dense): a pressure solve of StokesColor.py:554-555 in ONE launch -- the restated right-hand side
+// (k_pres_rhs: each master row takes its slave's entry, the free rows' mean is removed, slave rows are 0) formed at
+// every column from braw and the reduced sum, the dense pseudo-inverse product (k_dense_mv), and p = y with every
+// slave taking its master's value (k_cg_fin) -- the same operations in the same order as the three launches it
+// replaces, so the same bits
+__global__ __launch_bounds__(BS) void k_dense_pres(int64_t n, const double* __restrict__ Pinv,
+                                                   const double* __restrict__ braw, const int32_t* __restrict__ slave_of,
+                                                   const int32_t* __restrict__ master_of, const double* part_sum, int nb,
+                                                   double inv_nfree, double* __restrict__ y, double* __restrict__ p) {
+  __shared__ double sh[4];
+  const double mean = reduce_partials(part_sum, nb, sh) * inv_nfree;
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    const double* a = Pinv + row * n;
+    double acc = 0.0;
+    for (int64_t j = lane; j < n; j += 64) {
+      double b;
+      if (master_of[j] >= 0) {
+        b = 0.0;
+      } else {
+        b = braw[j];
+        if (slave_of[j] >= 0) b += braw[slave_of[j]];
+        b = b - mean;
+      }
+      acc += a[j] * b;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      y[row] = acc;
+      if (master_of[row] < 0) {
+        p[row] = 1.0 * acc;
+        if (slave_of[row] >= 0) p[slave_of[row]] = 1.0 * acc;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x0,
                                                   const double* __restrict__ x1, double* __restrict__ y0,
                                                   double* __restrict__ y1) {
