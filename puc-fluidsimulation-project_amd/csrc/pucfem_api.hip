@@ -3857,6 +3857,10 @@ void build(Ctx& c) {
       L.res_deep = L.deep && L.res_deep && off[4 * l + 1] == 0.0;
       L.xc_deep = l > 0 && c.mg[l - 1].deep && L.xc_deep && off[4 * l + 2] == 0.0;
       L.pr_deep = l > 0 && L.deep && (L.xc_deep || c.mg[l - 1].rep) && L.pr_deep && off[4 * l + 3] == 0.0;
+      if (std::getenv("PUCFEM_DEEP_REPORT") && c.rank == 0)  // (diagnostic: tools/comm_probe.py)
+        std::fprintf(stderr, "[deep] level %zu: rep %d deep %d res %d xc %d pr %d  own %lld ghosts %lld g1 %zu\n", l,
+                     (int)L.rep, (int)L.deep, (int)L.res_deep, (int)L.xc_deep, (int)L.pr_deep, (long long)L.lp.n_own,
+                     (long long)L.lp.n_ghost, L.g1.size());
     }
   }
   c.block_cg = c.prm.solver_path != 1;

@@ -15,3 +15,6 @@ python "$ROOT/tools/trace_replay.py" "$f" 3 > "$OUT/fine_replay_trace.txt"
 find /tmp/fine_$TAG -name "*kernel_stats.csv" -exec cp {} "$OUT/fine_kernel_stats.csv" \;
 tail -3 "$OUT/fine_replay_trace.txt" >&2
 timeout -k 10 120 python "$ROOT/tools/fine_probe.py" 2000 >&2
+cd "$ROOT"
+PUCFEM_DEEP_REPORT=1 timeout -k 10 240 python -u tools/comm_probe.py 7 8 2 > "$OUT/comm_probe_report.txt" 2>&1
+rc=$?; grep -E "\[deep\]|per pressure" "$OUT/comm_probe_report.txt" >&2; exit $rc
