@@ -852,12 +852,11 @@ struct Ctx {
       klaunch(4, sl_bytes, k_sl<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, (int64_t)row0, (int64_t)n, vx,
               vy, dt, cf, cn, w, nf, part_sl, sl_queue, sl_qcnt);
       kl_lds = 0;  // (the knob's LDS is k_sl's alone: k_sl_slow has static LDS of its own)
-      // the queued rows: one wave per point (k_sl_wave; 1,024 waves take k_sl's blocks in turn), or -- with the
-      // fused reductions (a measurement knob) or PUCFEM_SL_WAVE=0 -- k_sl_slow on k_sl's grid, one lane per point
+      // the queued rows: one wave per point (k_sl_wave, on k_sl's grid), or -- with the fused reductions (a
+      // measurement knob) or PUCFEM_SL_WAVE=0 -- k_sl_slow on k_sl's grid, one lane per point
       if (sl_wave && !ro.out)
-        klaunch(8, 0.0, k_sl_wave, dim3(std::max(1, std::min(256, nb / 8))), dim3(BS), M, llgrid, cgrid, (int64_t)row0,
-                (int64_t)n, vx, vy, dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt,
-                (int32_t)nb);
+        klaunch(8, 0.0, k_sl_wave, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt, cf, cn,
+                w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
       else
         klaunch(8, 0.0, k_sl_slow<LatLocDev>, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy,
                 dt, cf, cn, w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt, ro);

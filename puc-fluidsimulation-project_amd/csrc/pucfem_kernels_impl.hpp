@@ -2599,14 +2599,7 @@ __global__ __launch_bounds__(BS) void k_sl_slow(MeshDev M, LOC L, GridDev G, int
 // key: a margin / inner pass is the only passing triangle, so the sequential scan's early exits never change it),
 // then count the centroids below it together (ballots; the sequential count's early exit only saves work), and
 // lane 0 writes the value -- the same arithmetic per candidate, so the same bits as k_sl_slow.
-// Work: a small grid whose wave g takes k_sl's blocks g, g + NW, ... (their four waves' queues in order), and adds
-// each origin block's slow contributions to that block's partials itself: no two waves share a partial, the sums'
-// order is fixed.
-__device__ __forceinline__ void rows_of_block(int64_t n, int64_t nb, int64_t b, int64_t& r0, int64_t& r1) {
-  const int64_t ns = (n + 63) / 64, s0 = (ns * b) / nb, s1 = (ns * (b + 1)) / nb;  // block_rows for block b of nb
-  r0 = s0 * 64;
-  r1 = s1 * 64 < n ? s1 * 64 : n;
-}
+// Work: k_sl's grid, block b adding its points' contributions to block b's partials (the sums' order is fixed).
 // (d, id) key minimum over the wave (every lane gets it)
 __device__ __forceinline__ void wave_min_key(double& d, int32_t& id) {
 #pragma unroll
@@ -2684,24 +2677,58 @@ __device__ __forceinline__ bool sl_best_wave(const LatLocDev& L, double qx, doub
   rho2 = L.rho2[bid];
   return true;
 }
-// sl_rank_ok by a whole wave: the centroids below (bestd, best) counted over the lanes (same result)
+// sl_rank_ok by a whole wave: the centroids below (bestd, best) counted over the lanes (same result).  The grid rows
+// of the box [q - R, q + R] are flattened into one entry range (each row's cells are one contiguous entry range; a
+// wave scan of their lengths), so the lanes load entries of every row at once instead of one row after another
 __device__ __forceinline__ bool sl_rank_ok_wave(const GridDev& G, double qx, double qy, double bestd, int32_t best) {
   const int lane = threadIdx.x & 63;
   const double R = sqrt(bestd) * (1.0 + 1e-9) + 1e-300;
   const int32_t i0 = gcell(qx - R, G.x0, G.hx, G.nx), i1 = gcell(qx + R, G.x0, G.hx, G.nx);
   const int32_t j0 = gcell(qy - R, G.y0, G.hy, G.ny), j1 = gcell(qy + R, G.y0, G.hy, G.ny);
+  const int32_t nrow = j1 - j0 + 1;
   int cnt = 0;
-  for (int32_t j = j0; j <= j1; ++j) {
-    const int32_t f0 = G.start[(int64_t)j * G.nx + i0], f1 = G.start[(int64_t)j * G.nx + i1 + 1];
-    for (int32_t e = f0; e < f1; e += 64) {
-      bool below = false;
-      if (e + lane < f1) {
-        const double dx = G.px[e + lane] - qx, dy = G.py[e + lane] - qy;
-        below = knn_less(dx * dx + dy * dy, G.item[e + lane], bestd, best);
+  if (nrow > 64) {  // (a box taller than a wave: row after row)
+    for (int32_t j = j0; j <= j1; ++j) {
+      const int32_t f0 = G.start[(int64_t)j * G.nx + i0], f1 = G.start[(int64_t)j * G.nx + i1 + 1];
+      for (int32_t e = f0; e < f1; e += 64) {
+        bool below = false;
+        if (e + lane < f1) {
+          const double dx = G.px[e + lane] - qx, dy = G.py[e + lane] - qy;
+          below = knn_less(dx * dx + dy * dy, G.item[e + lane], bestd, best);
+        }
+        cnt += __popcll(__ballot(below));
+        if (cnt >= KNN) return false;
       }
-      cnt += __popcll(__ballot(below));
-      if (cnt >= KNN) return false;
     }
+    return true;
+  }
+  int32_t f0 = 0, len = 0;
+  if (lane < nrow) {
+    const int64_t rb = (int64_t)(j0 + lane) * G.nx;
+    f0 = G.start[rb + i0];
+    len = G.start[rb + i1 + 1] - f0;
+  }
+  int32_t incl = len;  // inclusive scan of the row lengths
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const int32_t total = __shfl(incl, 63, 64), excl = incl - len;
+  for (int32_t base = 0; base < total; base += 64) {
+    const int32_t t = base + lane;
+    int32_t e = -1;
+    for (int32_t r = 0; r < nrow; ++r) {  // (uniform loop: every lane shuffles)
+      const int32_t ex = __shfl(excl, r, 64), ln = __shfl(len, r, 64), st = __shfl(f0, r, 64);
+      if (t >= ex && t < ex + ln) e = st + (t - ex);
+    }
+    bool below = false;
+    if (e >= 0) {
+      const double dx = G.px[e] - qx, dy = G.py[e] - qy;
+      below = knn_less(dx * dx + dy * dy, G.item[e], bestd, best);
+    }
+    cnt += __popcll(__ballot(below));
+    if (cnt >= KNN) return false;
   }
   return true;
 }
@@ -2709,46 +2736,43 @@ __global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev 
                                                 const double* __restrict__ ux, const double* __restrict__ uy, double dt,
                                                 const double* __restrict__ c, double* __restrict__ cout,
                                                 const double* __restrict__ wmix, int32_t* notfound, double* part,
-                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt,
-                                                int32_t nbq) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (BS / 64), gw = (int64_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
-  for (int64_t ob = gw; ob < nbq; ob += nw) {
-    int32_t cnt[BS / 64];
-    int32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < BS / 64; ++w) tot += (cnt[w] = qcnt[BS / 64 * ob + w]);
-    if (tot == 0) continue;  // (wave-uniform)
-    int64_t r0, r1;
-    rows_of_block(n, nbq, ob, r0, r1);
-    double swc = 0.0, nnf = 0.0;
-    for (int w = 0; w < BS / 64; ++w)
-      for (int32_t p = 0; p < cnt[w]; ++p) {
-        const int64_t i = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + w) * 64 + (p & 63)], g = row0 + i;
-        double xb, yb;
-        sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
-        SlTri r;
-        double bestd;
-        float rho2;
-        const bool cand = sl_best_wave(L, xb, yb, r, bestd, rho2);
-        const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok_wave(G, xb, yb, bestd, r.id));
-        double cn;
-        if (ok) {
-          cn = sl_value(r, xb, yb, c);
-        } else {
-          cn = c[g];
-          nnf += 1.0;
-        }
-        if (lane == 0) {
-          stnt(cout + g, cn);
-          if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;
-        }
-        swc += (wmix ? wmix[i] : 0.0) * cn;
-      }
-    if (lane == 0) {  // k_sl's partials of block ob plus this pass's (this wave alone writes them)
-      part[ob] += swc;
-      part[2 * SLB + ob] += nnf;
+                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt) {
+  // k_sl's grid: block b runs the queues of k_sl's block b, wave w that of its wave w, one point at a time with the
+  // whole wave (the in-step trace of a 1,024-wave grid taking k_sl's blocks in turn: 2.0 ms, r13d -- its few
+  // long-lived blocks waited for wave slots beside the main stream)
+  __shared__ double sh[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  const int32_t cnt = qcnt[BS / 64 * blockIdx.x + wv];
+  double swc = 0.0, nnf = 0.0;
+  for (int32_t p = 0; p < cnt; ++p) {
+    const int64_t i = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)], g = row0 + i;
+    double xb, yb;
+    sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
+    SlTri r;
+    double bestd;
+    float rho2;
+    const bool cand = sl_best_wave(L, xb, yb, r, bestd, rho2);
+    const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok_wave(G, xb, yb, bestd, r.id));
+    double cn;
+    if (ok) {
+      cn = sl_value(r, xb, yb, c);
+    } else {
+      cn = c[g];
+      nnf += 1.0;
     }
+    if (lane == 0) {
+      stnt(cout + g, cn);
+      if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;
+    }
+    swc += (wmix ? wmix[i] : 0.0) * cn;
+  }
+  // k_sl's partials of this block plus this pass's (lane 0 of each wave carries its wave's sums)
+  const double a = block_sum(lane == 0 ? swc : 0.0, sh), d = block_sum(lane == 0 ? nnf : 0.0, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] += a;
+    part[2 * SLB + blockIdx.x] += d;
   }
 }
 
