@@ -234,6 +234,56 @@ struct MgBufs {
   double val_bytes() const { return Aval16 ? 2.0 : (double)sizeof(T); }
 };
 
+// face-interior node -> its macro face (the deep halos' face-stencil ghost rows, face_ghost_rows)
+struct FaceLookup {
+  std::vector<std::pair<i64, i32>> starts;  // (first interior node, face), ascending
+  LocalPlan full;                           // the level's whole range: to_local = the global id
+  void init(const Macro& M, const LatticeLevel& LL) {
+    starts.clear();
+    for (i64 f = 0; f < M.nf; ++f)
+      if (LL.face_start[f] >= 0) starts.push_back({LL.face_start[f], (i32)f});
+    std::sort(starts.begin(), starts.end());
+    full.r0 = 0;
+    full.r1 = (i64)LL.type.size();
+    full.n_own = full.r1;
+  }
+  // face-interior node g -> (face, offset t)
+  void find(i64 g, i32& f, i32& t) const {
+    auto it = std::upper_bound(starts.begin(), starts.end(), std::make_pair(g, (i32)INT32_MAX));
+    --it;
+    f = it->second;
+    t = (i32)(g - it->first);
+  }
+};
+GhostRowFn face_ghost_rows(const Macro& M, const LatticeLevel& LL, const FaceLookup& FL, const std::vector<i32>* dof,
+                           int l, double dtnu) {
+  return [&M, &LL, &FL, dof, l, dtnu](i32 g, std::vector<i32>& cols, std::vector<double>& vals) -> bool {
+    if (LL.F == 0 || LL.type[g] != 0) return false;
+    i32 f, t;
+    FL.find(g, f, t);
+    std::vector<lat::FaceTab> tab;
+    lattice_tabs(M, LL, {f}, 0, FL.full, dof, tab);
+    std::vector<double> rec;
+    lattice_coefs(M, {f}, l, dtnu, rec);
+    const i32 n = LL.n;
+    i32 i, j, nb[6];
+    bool in[6];
+    lat::coords(t, n, 1.0f / (float)(n - 1), i, j);
+    lat::neighbours(tab[0], n, t, i, j, nb, in);
+    cols.assign({g, nb[0], nb[1], nb[2], nb[3], nb[4], nb[5]});
+    const double kab = rec[lat::C_KAB], kac = rec[lat::C_KAC], kbc = rec[lat::C_KBC];
+    vals.assign({rec[lat::C_KD], kab, kab, kac, kac, kbc, kbc});
+    return true;
+  };
+}
+double face_dinv(const Macro& M, const LatticeLevel& LL, const FaceLookup& FL, int l, i64 g) {
+  i32 f, t;
+  FL.find(g, f, t);
+  std::vector<double> rec;
+  lattice_coefs(M, {f}, l, 0.0, rec);
+  return rec[lat::C_DINV];
+}
+
 // One level of the geometric multigrid hierarchy (pressure preconditioner).  Level 0 is the
 // coarsest (the caller's base mesh, solved densely), the last level is the simulation mesh.
 struct MgLevel {
@@ -271,6 +321,7 @@ struct MgLevel {
   //   no exchange of x.
   std::vector<i32> g1;
   bool deep = false, res_deep = false, xc_deep = false, pr_deep = false;
+  FaceLookup flook;  // (deep lattice levels) face-interior node -> face
   i64 r_r0 = 0;  // first row of this level's restriction operator (rows live on level l-1)
   i64 own0(int rank) const { return rep ? 0 : rs[rank]; }
   // lattice face parts (Ctx::lattice): the faces whose interiors are this rank's rows of this level,
@@ -485,6 +536,7 @@ struct Ctx {
   // deep halos on W > 1 ranks (MgLevel::deep; PUCFEM_DEEP_HALO=0 keeps one-layer halos and single smoothing steps,
   // a test / measurement knob)
   bool deep_halo = !(std::getenv("PUCFEM_DEEP_HALO") && std::atoi(std::getenv("PUCFEM_DEEP_HALO")) == 0);
+  bool z_cur = false;  // the finest level's last smoothing step wrote z at the ghost rows one layer out too
   // PUCFEM_DEEP_MASK (diagnostic knob, default all): 1 multigrid step pairs, 2 residual rows, 4 last smoothing step
   // (+ the skipped z / x exchanges), 8 prolongation rows, 16 the viscous first pair -- each use of the ghost rows
   int deep_mask = std::getenv("PUCFEM_DEEP_MASK") ? std::atoi(std::getenv("PUCFEM_DEEP_MASK")) : 31;
@@ -1611,6 +1663,7 @@ struct Ctx {
       const bool timed = finest && mode != 0;
       const double* rd = last ? rdot : nullptr;
       const bool toz = last && tozr;
+      if (toz) z_cur = gl;
       const FaceDev fc = rd ? hf.part() : hf.full();
       // (the grid of the own rows also with the ghost rows, whose slices its SELL blocks share: the <r, z> partials
       // keep the block count the PCG's reduction reads)
@@ -1739,17 +1792,17 @@ struct Ctx {
     T* other = (x == xa) ? xb : xa;
     const int post = prm.mg_post > 0 ? prm.mg_post : prm.mg_degree;
     // the last step on the ghost rows one layer out where its consumer gathers them: the prolongation into level
-    // l + 1 (xc_deep).  Not z on the finest level: the outer fp64 PCG needs w = A z of ONE vector z (its recurrences
-    // s = A p and r = b - A y hold only then), and a ghost row's fp32 step, computed through its stored row, rounds
-    // differently from the owner's face stencil -- z's ghosts are exchanged (the rest of the V-cycle is a
-    // preconditioner, where such rounding acts like the fp32 cycle's own; W = 2 at rtol 1e-12 stalled otherwise)
-    const bool last_g = dist() && L.deep && (deep_mask & 4) && !finest && mg[l + 1].xc_deep;
+    // l + 1 (xc_deep), and z for the PCG's A z on the finest level -- there the ghost rows must repeat the owners'
+    // arithmetic bit for bit (the outer fp64 PCG needs w = A z of ONE vector z: its recurrences s = A p and
+    // r = b - A y hold only then), which face_ghost_rows ensures: face-interior ghost rows are their face stencils
+    const bool last_g = dist() && L.deep && (deep_mask & 4) && (finest || mg[l + 1].xc_deep);
     return mg_smooth<T, TB>(L, A, hf, B, b, x, x, other, finest, rdot, part, post, last_g, pg);
   }
   // z = M^-1 r (finest level), <r, z> partials in part_d + 2 MAXB.  The fp32 cycle reads r32 (owned
   // rows written by k_cg_init / k_cg_upd; its ghosts are exchanged by the cycle); the fp64 one r itself
   void precondition(double* rz_part = nullptr) {
     if (!rz_part) rz_part = part_d + 2 * MAXB;
+    z_cur = false;
     if (mg_single) {
       vcycle<float, float>((int)mg.size() - 1, r32, cg_r[0], rz_part);
     } else {
@@ -1931,8 +1984,10 @@ struct Ctx {
         if (cgcg) {  // single-reduction iteration (k_cgcg_*)
           ++cgcg_iters;
           precondition(part_cc + 3 * MAXB);
-          if (mg_single) mg_halo(mg.back(), z32);
-          else halo(z);
+          if (!z_cur) {  // (deep halos: the last smoothing step wrote z's ghosts one layer out, bit for bit)
+            if (mg_single) mg_halo(mg.back(), z32);
+            else halo(z);
+          }
           with_c16(dPp, [&](auto c16) {
             if (mg_single)
               klaunch(1, bytes_w, k_cgcg_w<decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -1970,8 +2025,10 @@ struct Ctx {
         Red rz{redbuf + 32, 1, 1};
         if (ro(redbuf + 32, CNT_RZ, 1).out) red_done(redbuf + 32, 1, false);
         else rz = reduce_global(part_d + 2 * MAXB, nb, 1, false, 4);
-        if (mg_single) mg_halo(mg.back(), z32);
-        else halo(z);
+        if (!z_cur) {
+          if (mg_single) mg_halo(mg.back(), z32);
+          else halo(z);
+        }
         with_c16(dPp, [&](auto c16) {
           if (mg_single)
             klaunch(1, bytes_dir, k_cg_dir<1, 8, true, decltype(c16)::value, true>, dim3(nb), dim3(BS), dPp.view(), fc,
@@ -3215,6 +3272,19 @@ void mg_alloc(Ctx& c, const std::vector<double>& kp_vals) {
       for (i64 i = i0; i < i1; ++i) dv[i] = 1.0 / diag_of(A, A.val, r0 + i);
     });
     for (i64 k = 0; k < L.lp.n_ghost; ++k) dv[n + k] = 1.0 / diag_of(A, A.val, L.lp.ghost_global[k]);
+    if (L.deep && c.lattice && L.latl.F > 0 && !L.flook.starts.empty()) {
+      // deep halos: every face-interior row's 1 / diag is its face record's (the face kernels' value), so the ghost
+      // rows' steps repeat the owners' arithmetic (face_ghost_rows)
+      for (size_t q = 0; q < L.lf_faces.size(); ++q) {
+        const double di = L.lf_coef[q * lat::NCOEF + lat::C_DINV];
+        const i64 b0 = L.latl.face_start[L.lf_faces[q]] - r0;
+        for (i64 t = 0; t < L.latl.F; ++t) dv[b0 + t] = di;
+      }
+      for (i64 k = 0; k < L.lp.n_ghost; ++k) {
+        const i32 g = L.lp.ghost_global[k];
+        if (L.latl.type[g] == 0) dv[n + k] = face_dinv(c.macro, L.latl, L.flook, l, g);
+      }
+    }
     B.dinv = upload_as<T>(c, dv);
     if (l < Lv) {
       const Sell& S = L.sA;
@@ -3340,6 +3410,12 @@ void sl_prep(const Ctx& c, bool food, SlPrep& P) {
   ck.mark("  sl: home faces, initial dye");
 }
 
+// Deep halos: a ghost row one layer out that is a macro-face interior node goes into the SELL as its face stencil --
+// the node, then its six neighbours in lat::neighbours' order (the merged table's: slave columns are their masters),
+// with the face record's coefficients -- so that a launch computing it does the owner's face-kernel arithmetic bit
+// for bit (the stored row would sum the same terms in column order, and the assembled values agree with the
+// records only to rounding); its 1 / diag is the record's too (face_dinv, mg_alloc).  This is what lets a rank use
+// the ghost rows' results in place of exchanged values where the outer PCG needs one vector (z).
 void build(Ctx& c) {
   SetupClock clk;
   require(c.has_mesh, "mesh not uploaded");
@@ -3351,6 +3427,18 @@ void build(Ctx& c) {
   require(!(literal && c.dist()), "heat / Poisson literal operators run on one rank");
   require(!stokes || prm.sl_k == KNN, "sl_k must be 10 (PointLocator.find default)");
   HostMesh& m = c.mesh;
+  // PUCFEM_PLAN_EMULATE="rank,world" (diagnostic, host-only contexts): build rank `rank`'s plans and deep-halo
+  // flags of a `world`-rank run on the host (no communicator: nothing steps); with PUCFEM_DEEP_REPORT=1 the flags'
+  // checks are reported
+  if (const char* e = std::getenv("PUCFEM_PLAN_EMULATE")) {
+    if (c.host_only && !c.dist()) {
+      int r = 0, w = 1;
+      if (std::sscanf(e, "%d,%d", &r, &w) == 2 && w > 1 && r >= 0 && r < w) {
+        c.rank = r;
+        c.world = w;
+      }
+    }
+  }
   // lattice operators: a multigrid hierarchy of >= 2 red refinements (face interiors exist)
   c.lattice = stokes && prm.precond == 1 && c.mg_levels >= 2 && prm.assembled == 0;
   c.dye_impl = prm.scheme == PUCFEM_STOKES_COLOR && prm.dye_scheme == 1;
@@ -3519,7 +3607,11 @@ void build(Ctx& c) {
       if (l < Lv) {
         if (c.lattice) build_sell_rows(L.Pp, o0, skel(L.latl, o0, L.lp.n_own), L.lp, L.sA);
         else build_sell_x(L.Pp, o0, L.lp.n_own, L.lp, L.sA, true);
-        if (L.deep) sell_append_ghost_rows(L.Pp, L.g1, L.lp, L.sA);
+        if (L.deep) {
+          L.flook.init(c.macro, L.latl);
+          const GhostRowFn fn = face_ghost_rows(c.macro, L.latl, L.flook, &L.dof, l, prm.dt * prm.nu);
+          sell_append_ghost_rows(L.Pp, L.g1, L.lp, L.sA, nullptr, c.lattice ? &fn : nullptr);
+        }
       }
       if (l >= 1) {
         const MgLevel& C = c.mg[l - 1];
@@ -3581,6 +3673,29 @@ void build(Ctx& c) {
         }
       }
       L.pr_deep = ok;
+      if (std::getenv("PUCFEM_DEEP_REPORT") && c.rank == 0) {  // (diagnostic: which rows fail the prolongation check)
+        i64 bad_rows = 0, bad_g1 = 0;
+        i32 ex = -1, exc = -1;
+        for (const i32 r : L.lp.ghost_global) {
+          bool bad = false;
+          for (i64 e = L.Pr.rowptr[r]; e < L.Pr.rowptr[r + 1]; ++e) {
+            const i32 j = L.Pr.col[e];
+            if (!C.rep && (j < clo || j >= chi) && !in_g1(C.g1, j)) {
+              bad = true;
+              exc = j;
+            }
+          }
+          if (bad) {
+            ++bad_rows;
+            bad_g1 += in_g1(L.g1, r) ? 1 : 0;
+            ex = r;
+          }
+        }
+        std::fprintf(stderr, "[deep] level %d: res %d xc %d pr %d; ghost rows failing the prolongation check %lld "
+                     "(%lld of them G1), e.g. row %d (type %d) -> coarse %d (type %d)\n", l, (int)L.res_deep,
+                     (int)L.xc_deep, (int)L.pr_deep, (long long)bad_rows, (long long)bad_g1, ex,
+                     ex >= 0 ? (int)L.latl.type[ex] : -1, exc, exc >= 0 ? (int)C.latl.type[exc] : -1);
+      }
       if (L.pr_deep)  // the prolongation's SELL: + every ghost row of this level (rows in this level's plan)
         sell_append_ghost_rows(L.Pr, L.lp.ghost_global, C.lp, L.sPr, &L.lp);
     }
@@ -3639,8 +3754,11 @@ void build(Ctx& c) {
     build_sell_rows(c.P, c.lp.r0, rows, c.lp, c.sP);
     build_sell_rows(c.Pp, c.lp.r0, rows, c.lp, c.sPp);
     if (c.use_mg && c.mg.back().deep) {  // deep halos: the finest level's ghost rows (pressure, A_visc / K)
-      sell_append_ghost_rows(c.Pp, c.mg.back().g1, c.lp, c.sPp);
-      sell_append_ghost_rows(c.P, c.mg.back().g1, c.lp, c.sP);
+      MgLevel& F = c.mg.back();
+      F.flook.init(c.macro, F.latl);
+      const GhostRowFn fn = face_ghost_rows(c.macro, F.latl, F.flook, &F.dof, c.mg_levels, prm.dt * prm.nu);
+      sell_append_ghost_rows(c.Pp, F.g1, c.lp, c.sPp, nullptr, &fn);
+      sell_append_ghost_rows(c.P, F.g1, c.lp, c.sP);
     }
   } else {
     build_sell(c.P, c.lp, c.sP);

@@ -1192,6 +1192,14 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
     for (i64 l = 0; l < 64; ++l) {
       const i64 k = s * 64 + l;
       if (S.rows[k] < 0) continue;  // (a padding lane: the own rows' last slice is padded before any ghost rows)
+      if (!S.gval.empty() && k >= S.gk0) {  // (ghost rows with their own entries: the values stored with them)
+        const i64 p0 = S.slice_off[S.nslices_own];
+        for (i64 e = 0; e < S.slice_w[s]; ++e) {
+          const i64 q = S.slice_off[s] + e * 64 + l;
+          out[q] = S.gval[q - p0];
+        }
+        continue;
+      }
       const i64 r = S.global_row(r0, k);
       const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
       for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = val[b + e];
@@ -1199,8 +1207,22 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
 }
 
 void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S,
-                            const LocalPlan* rows_plan) {
+                            const LocalPlan* rows_plan, const GhostRowFn* custom) {
   const LocalPlan& rp = rows_plan ? *rows_plan : cols;
+  // every ghost row's entries: A's row, or the custom one
+  const i64 ng = (i64)grows.size();
+  std::vector<std::vector<i32>> ccols(custom ? ng : 0);
+  std::vector<std::vector<double>> cvals(custom ? ng : 0);
+  std::vector<char> is_custom(ng, 0);
+  if (custom)
+    for (i64 k = 0; k < ng; ++k) is_custom[k] = (*custom)(grows[k], ccols[k], cvals[k]) ? 1 : 0;
+  auto row_len = [&](i64 k) -> i64 {
+    return is_custom[k] ? (i64)ccols[k].size() : A.rowptr[grows[k] + 1] - A.rowptr[grows[k]];
+  };
+  auto row_col = [&](i64 k, i64 e) -> i32 { return is_custom[k] ? ccols[k][e] : A.col[A.rowptr[grows[k]] + e]; };
+  auto row_val = [&](i64 k, i64 e) -> double { return is_custom[k] ? cvals[k][e] : A.val[A.rowptr[grows[k]] + e]; };
+  bool any_custom = false;
+  for (char c : is_custom) any_custom = any_custom || c;
   if (S.gk0 >= 0) throw std::runtime_error("SELL already has ghost rows");
   if (S.rows.empty() && S.nrows > 0) throw std::runtime_error("ghost rows need a row-listed SELL");
   S.nslices_own = S.nslices;
@@ -1214,7 +1236,7 @@ void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const L
     i64 w = 0;
     for (i64 l = 0; l < 64 && s * 64 + l < n; ++l) {
       const i64 g = grows[s * 64 + l];
-      w = std::max(w, A.rowptr[g + 1] - A.rowptr[g]);
+      w = std::max(w, row_len(s * 64 + l));
       S.rows[S.gk0 + s * 64 + l] = to_local(rp, (i32)g);
       if (S.rows[S.gk0 + s * 64 + l] < rp.n_own) throw std::runtime_error("ghost row list holds an owned row");
     }
@@ -1224,17 +1246,19 @@ void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const L
   const i64 p0 = S.padded;
   S.padded = S.slice_off[S.nslices + ns];
   S.col.resize(S.padded, 0);
+  if (any_custom) S.gval.assign(S.padded - p0, 0.0);
   for (i64 s = 0; s < ns; ++s)
     for (i64 l = 0; l < 64; ++l) {
       const i64 k = s * 64 + l;
-      const i64 r = k < n ? grows[k] : -1;
-      const i64 len = k < n ? A.rowptr[r + 1] - A.rowptr[r] : 0;
-      const i32 first = len > 0 ? to_local(cols, A.col[A.rowptr[r]]) : 0;
-      for (i64 e = 0; e < S.slice_w[S.nslices + s]; ++e)
-        S.col[S.slice_off[S.nslices + s] + e * 64 + l] = e < len ? to_local(cols, A.col[A.rowptr[r] + e]) : first;
+      const i64 len = k < n ? row_len(k) : 0;
+      const i32 first = len > 0 ? to_local(cols, row_col(k, 0)) : 0;
+      for (i64 e = 0; e < S.slice_w[S.nslices + s]; ++e) {
+        const i64 q = S.slice_off[S.nslices + s] + e * 64 + l;
+        S.col[q] = e < len ? to_local(cols, row_col(k, e)) : first;
+        if (any_custom && e < len) S.gval[q - p0] = row_val(k, e);
+      }
       S.nnz += len;
     }
-  (void)p0;
   S.nslices += ns;
   S.nrows += n;
 }

@@ -7,11 +7,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <stdexcept>
 #include <memory>
 #include <string>
 #include <algorithm>
 #include <thread>
 #include <utility>
+#include <functional>
 #include <vector>
 
 #include <sys/mman.h>
@@ -262,6 +264,10 @@ struct Sell {
   // nslices_own slices hold the rank's own rows (-1: no ghost rows)
   i64 gk0 = -1, nslices_own = -1;
   std::vector<i32> grow;
+  // values of the ghost slices' entries when some ghost rows are not A's rows as stored (a face-interior row in its
+  // face stencil's order and coefficients: the owner's arithmetic, bit for bit), laid out like col from
+  // slice_off[nslices_own]; empty: every ghost row is A's row
+  std::vector<double> gval;
   i64 global_row(i64 r0, i64 k) const { return gk0 >= 0 && k >= gk0 ? (i64)grow[k - gk0] : r0 + (i64)rows[k]; }
 };
 // SELL of the rows `rows` (offsets from r0 into A's rows; they are also the local output indices),
@@ -271,8 +277,10 @@ void sell_values_rows(const Csr& A, i64 r0, const Sell& S, const std::vector<dou
 // append the rows `grows` (global ids, each a ghost of `cols`) to a row-listed SELL as whole slices of their own:
 // local output index = the ghost's local id, columns resolved in `cols`
 // (rows_plan: the plan holding the rows as ghosts, when it is not the columns' -- a transfer between two levels)
+// custom (optional): a ghost row's entries (global columns, values) in place of A's row when it returns true
+using GhostRowFn = std::function<bool(i32 g, std::vector<i32>& cols, std::vector<double>& vals)>;
 void sell_append_ghost_rows(const Csr& A, const std::vector<i32>& grows, const LocalPlan& cols, Sell& S,
-                            const LocalPlan* rows_plan = nullptr);
+                            const LocalPlan* rows_plan = nullptr, const GhostRowFn* custom = nullptr);
 // the SELL image of A's rows in S (rows r0 + k, or r0 + S.rows[k]) with entry values f(r, e) computed in
 // place (r: the row's global index, e: its CSR entry) -- no full-length value array for a SELL that
 // holds only the lattice skeleton's rows
@@ -284,6 +292,8 @@ void sell_values_fn(const Csr& A, i64 r0, const Sell& S, F&& f, std::vector<doub
       for (i64 l = 0; l < 64; ++l) {
         const i64 k = s * 64 + l;
         if (S.rows.empty() ? k >= S.nrows : S.rows[k] < 0) continue;  // (row lists: padding lanes are -1)
+        if (!S.gval.empty() && S.gk0 >= 0 && k >= S.gk0)
+          throw std::runtime_error("sell_values_fn: ghost rows with their own values (use sell_values_rows)");
         const i64 r = S.rows.empty() ? r0 + k : S.global_row(r0, k);
         const i64 b = A.rowptr[r], len = A.rowptr[r + 1] - b;
         for (i64 e = 0; e < len; ++e) out[S.slice_off[s] + e * 64 + l] = f(r, b + e);
