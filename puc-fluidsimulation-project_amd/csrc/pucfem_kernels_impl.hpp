@@ -2627,35 +2627,46 @@ __device__ __forceinline__ bool sl_best_wave(const LatLocDev& L, double qx, doub
   int32_t mid = 0x7fffffff;
   SlTri mine{};
   // candidate k = (face e0 + k / 18, cell k % 18): 3 rows j x 3 columns i x 2 orientations s around (u, v), the
-  // sequential scan's cells; cell 0 of a face also reports its inner cell
-  for (int32_t k = lane; k < (e1 - e0) * 18; k += 64) {
-    const lat::SlFace& S = L.face[L.item[e0 + k / 18]];
-    const int32_t c = k % 18;
-    SlTri r;
-    double d, u, v;
-    if (sl_inner(L, S, qx, qy, r, d, u, v)) {
-      if (c == 0 && knn_less(d, r.id, md, mid)) {
-        md = d;
-        mid = r.id;
-        mine = r;
+  // sequential scan's cells; cell 0 of a face also reports its inner cell.  Chunks of 64 candidates, in the scan's
+  // order, until one holds an inner cell or a margin pass (the only passing triangle then: the scan stops there too)
+  const int32_t total = (e1 - e0) * 18;
+  for (int32_t base = 0; base < total; base += 64) {
+    const int32_t k = base + lane;
+    bool hit = false;
+    if (k < total) {
+      const lat::SlFace& S = L.face[L.item[e0 + k / 18]];
+      const int32_t c = k % 18;
+      SlTri r;
+      double d, u, v;
+      if (sl_inner(L, S, qx, qy, r, d, u, v)) {
+        hit = true;
+        if (c == 0 && knn_less(d, r.id, md, mid)) {
+          md = d;
+          mid = r.id;
+          mine = r;
+        }
+      } else if (u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL) {
+        const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
+        const int32_t j = max(j0 - 1, 0) + c / 6, i = max(i0 - 1, 0) + (c / 2) % 3, s = c & 1;
+        const double a = u - i, b = v - j;
+        const bool near = !(j > j0 + 1 || i > i0 + 1 || i + j > n - 1) &&
+                          (s == 0 ? (a >= -SL_LDEL && b >= -SL_LDEL && a + b <= 1.0 + SL_LDEL)
+                                  : (i + j <= n - 2 && a <= 1.0 + SL_LDEL && b <= 1.0 + SL_LDEL && a + b >= 1.0 - SL_LDEL));
+        if (near) {
+          r = sl_cell(L, S, i, j, s);
+          bool margin;
+          if (sl_test(r, qx, qy, d, margin)) {
+            hit = margin;
+            if (knn_less(d, r.id, md, mid)) {
+              md = d;
+              mid = r.id;
+              mine = r;
+            }
+          }
+        }
       }
-      continue;
     }
-    if (!(u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL)) continue;
-    const int32_t i0 = min(max((int32_t)floor(u), 0), n - 1), j0 = min(max((int32_t)floor(v), 0), n - 1);
-    const int32_t j = max(j0 - 1, 0) + c / 6, i = max(i0 - 1, 0) + (c / 2) % 3, s = c & 1;
-    if (j > j0 + 1 || i > i0 + 1 || i + j > n - 1) continue;
-    const double a = u - i, b = v - j;
-    const bool near = s == 0 ? (a >= -SL_LDEL && b >= -SL_LDEL && a + b <= 1.0 + SL_LDEL)
-                             : (i + j <= n - 2 && a <= 1.0 + SL_LDEL && b <= 1.0 + SL_LDEL && a + b >= 1.0 - SL_LDEL);
-    if (!near) continue;
-    r = sl_cell(L, S, i, j, s);
-    bool margin;
-    if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, md, mid)) {
-      md = d;
-      mid = r.id;
-      mine = r;
-    }
+    if (__ballot(hit)) break;
   }
   double bd = md;
   int32_t bid = mid;
@@ -2789,17 +2800,25 @@ __device__ __forceinline__ bool sl_best_wave(const LocDev& L, double qx, double 
   double md = INFINITY;
   int32_t mid = 0x7fffffff, mpos = -1;
   SlTri mine{};
-  for (int32_t e = e0 + lane; e < e1; e += 64) {
-    const int32_t pos = L.item[e];
-    const SlTri r = sl_tri(L, pos);
-    double d;
-    bool margin;
-    if (sl_test(r, qx, qy, d, margin) && knn_less(d, r.id, md, mid)) {
-      md = d;
-      mid = r.id;
-      mpos = pos;
-      mine = r;
+  for (int32_t base = e0; base < e1; base += 64) {  // (chunks until a margin pass, the only passing record then)
+    const int32_t e = base + lane;
+    bool hit = false;
+    if (e < e1) {
+      const int32_t pos = L.item[e];
+      const SlTri r = sl_tri(L, pos);
+      double d;
+      bool margin;
+      if (sl_test(r, qx, qy, d, margin)) {
+        hit = margin;
+        if (knn_less(d, r.id, md, mid)) {
+          md = d;
+          mid = r.id;
+          mpos = pos;
+          mine = r;
+        }
+      }
     }
+    if (__ballot(hit)) break;
   }
   double bd = md;
   int32_t bid = mid;
