@@ -496,6 +496,7 @@ struct Ctx {
   double* part_sl = nullptr;  // k_sl partials, 3 x SLB
   int32_t* sl_queue = nullptr; // k_sl -> k_sl_slow: rows off the lattice fast path (mesh.N)
   int32_t* sl_qcnt = nullptr; // per wave of k_sl: queued entries (SLB * BS / 64)
+  int32_t* sl_qoff = nullptr; // k_sl_qscan: the queues' first entry numbers (SLB * BS / 64 + 1)
   bool has_cgrid = false, has_tgrid = false;
   double *c_full = nullptr, *c_new = nullptr, *ufx = nullptr, *ufy = nullptr;
   int32_t* dnotfound = nullptr;
@@ -817,7 +818,10 @@ struct Ctx {
   // the k_sl blocks resident per CU (160 KB / bytes), leaving wave slots and registers to the main stream
   size_t sl_lds = std::getenv("PUCFEM_SL_LDS") ? (size_t)std::max(0, std::min(65536, std::atoi(std::getenv("PUCFEM_SL_LDS"))))
                                                : 0;
-  bool sl_wave = !(std::getenv("PUCFEM_SL_WAVE") && std::atoi(std::getenv("PUCFEM_SL_WAVE")) == 0);
+  // PUCFEM_SL_WAVE (measurement knob): the lattice locator's second pass -- 2 (default) the numbered list
+  // (k_sl_qscan + k_sl_wq + k_sl_qsum), 1 k_sl_wave (each wave its own queue), 0 k_sl_slow (one lane per point)
+  int sl_wave_mode = std::getenv("PUCFEM_SL_WAVE") ? std::atoi(std::getenv("PUCFEM_SL_WAVE")) : 2;
+  bool sl_wave = sl_wave_mode != 0;
   int nb_sl(i64 n) const {
     if (sl_rec_wave(n)) return (int)((n + BS / 64 - 1) / (BS / 64));  // k_sl_rec_wave: a wave per row
     return (int)std::max<i64>(1, std::min<i64>(sl_cap, (n + 4 * 64 - 1) / (4 * 64)));
@@ -906,7 +910,16 @@ struct Ctx {
       kl_lds = 0;  // (the knob's LDS is k_sl's alone: k_sl_slow has static LDS of its own)
       // the queued rows: one wave per point (k_sl_wave, on k_sl's grid), or -- with the fused reductions (a
       // measurement knob) or PUCFEM_SL_WAVE=0 -- k_sl_slow on k_sl's grid, one lane per point
-      if (sl_wave && !ro.out)
+      if (sl_wave_mode == 2 && !ro.out) {
+        const int32_t nq = nb * (BS / 64);
+        hipLaunchKernelGGL(k_sl_qscan, dim3(1), dim3(QSCAN_BS), 0, st, (const int32_t*)sl_qcnt, nq, sl_qoff);
+        KCHK();
+        klaunch(8, 0.0, k_sl_wq, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, (int32_t)nb, vx, vy,
+                dt, cf, cn, nf, sl_queue, (const int32_t*)sl_qoff, nq);
+        KCHK();
+        hipLaunchKernelGGL(k_sl_qsum, dim3(nb), dim3(BS), 0, st, (int64_t)row0, (int64_t)n, (const double*)cn, w,
+                           part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
+      } else if (sl_wave && !ro.out)
         klaunch(8, 0.0, k_sl_wave, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, vx, vy, dt, cf, cn,
                 w, nf, part_sl, (const int32_t*)sl_queue, (const int32_t*)sl_qcnt);
       else
@@ -4216,6 +4229,7 @@ void build(Ctx& c) {
   if (stokes) {
     c.sl_queue = c.dalloc<int32_t>(m.N);
     c.sl_qcnt = c.dalloc<int32_t>(SLB * BS / 64);
+    c.sl_qoff = c.dalloc<int32_t>(SLB * BS / 64 + 1);
   }
   c.scal = c.dalloc<double>(32);
   c.part_cc = c.dalloc<double>(CGCG_NV * MAXB);

@@ -2787,6 +2787,208 @@ __global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev 
   }
 }
 
+// ---- The second pass over ONE numbered list (round 6).  k_sl_wave on k_sl's grid runs each wave's own queue one
+// point after another, and the queued points cluster: at L7 ~35k departure points inside the squirmer (not found)
+// plus ~800 rank counts (r12n) come from the few row blocks around the body, so a handful of waves ran hundreds of
+// points each: 981 us per step in the window (r13g; k_sl_slow's one lane per point: 290 us, r12t).  Here
+//   k_sl_qscan  numbers the entries of every per-wave queue (an exclusive scan of k_sl's wave counts, one block),
+//   k_sl_wq     lets wave w of a large grid take the entries p = w, w + (number of waves), ... of that numbering:
+//               the queue holding p by a 64-ary search of the offsets, the locate faces first (sl_best_wave2) and
+//               the rank count by the whole wave; lane 0 writes c_new and marks a not-found entry by complementing
+//               its row index in the queue,
+//   k_sl_qsum   adds the queued rows' contributions to k_sl's block partials in k_sl_slow's order (lane p % 64 of
+//               the wave that queued entry p), so the sums are k_sl_slow's, bit for bit.
+constexpr int QSCAN_BS = 1024;
+__global__ __launch_bounds__(QSCAN_BS) void k_sl_qscan(const int32_t* __restrict__ qcnt, int32_t nq,
+                                                       int32_t* __restrict__ qoff) {
+  __shared__ int32_t ws[QSCAN_BS / 64];
+  const int32_t per = (nq + QSCAN_BS - 1) / QSCAN_BS;
+  const int32_t a = (int32_t)threadIdx.x * per, b = min(a + per, nq);
+  int32_t s = 0;
+  for (int32_t q = a; q < b; ++q) s += qcnt[q];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) ws[wv] = incl;
+  __syncthreads();
+  int32_t off = incl - s;
+  for (int k = 0; k < wv; ++k) off += ws[k];
+  for (int32_t q = a; q < b; ++q) {
+    qoff[q] = off;
+    off += qcnt[q];
+  }
+  if (threadIdx.x == QSCAN_BS - 1) qoff[nq] = off;  // (the last thread's running offset is the total)
+}
+// the general lattice locate of one point by a whole wave, faces first: the lanes take the candidate faces of q's
+// macro-grid cell (sl_inner: an inner cell is the only passing triangle), then the cells around (u, v) of every face
+// whose closure holds q up to SL_LDEL -- the candidates the sequential scan tests, with the same arithmetic each (it
+// stops early only at a pass that is the only passing triangle): two rounds of dependent loads per 64 faces where
+// sl_best_wave's 64-candidate chunks (3.6 faces each) took one round per chunk
+__device__ __forceinline__ bool sl_best_wave2(const LatLocDev& L, double qx, double qy, SlTri& out, double& bestd,
+                                              float& rho2) {
+  const int lane = threadIdx.x & 63;
+  const double gx = floor((qx - L.x0) * L.ihx), gy = floor((qy - L.y0) * L.ihy);
+  const int32_t ci = !(gx >= 0.0) ? 0 : (gx >= (double)L.nx ? L.nx - 1 : (int32_t)gx);
+  const int32_t cj = !(gy >= 0.0) ? 0 : (gy >= (double)L.ny ? L.ny - 1 : (int32_t)gy);
+  const int64_t gc = (int64_t)cj * L.nx + ci;
+  const int32_t n = L.n;
+  const double dn = (double)n;
+  const int32_t e0 = L.start[gc], e1 = L.start[gc + 1];
+  double md = INFINITY;
+  int32_t mid = 0x7fffffff;
+  SlTri mine{};
+  for (int32_t base = e0; base < e1; base += 64) {
+    const int32_t e = base + lane;
+    bool inner = false, near = false;
+    double u = 0.0, v = 0.0;
+    int32_t fi = 0;
+    if (e < e1) {
+      fi = L.item[e];
+      SlTri r;
+      double d;
+      if (sl_inner(L, L.face[fi], qx, qy, r, d, u, v)) {
+        inner = true;
+        if (knn_less(d, r.id, md, mid)) {
+          md = d;
+          mid = r.id;
+          mine = r;
+        }
+      } else {
+        near = u >= -SL_LDEL && v >= -SL_LDEL && u + v <= dn + SL_LDEL;
+      }
+    }
+    if (__ballot(inner)) break;
+    const uint64_t nm = __ballot(near);
+    const int32_t ncand = 18 * __popcll(nm);
+    bool stop = false;
+    for (int32_t t0 = 0; t0 < ncand; t0 += 64) {
+      const int32_t t = t0 + lane;
+      int32_t fl = 0;  // the lane that holds candidate t's face: the (t / 18)-th near face
+      if (t < ncand) {
+        uint64_t m = nm;
+        for (int32_t k = t / 18; k > 0; --k) m &= m - 1;
+        fl = __ffsll((unsigned long long)m) - 1;
+      }
+      const double fu = __shfl(u, fl, 64), fv = __shfl(v, fl, 64);
+      const int32_t ff = __shfl(fi, fl, 64);
+      bool hit = false;
+      if (t < ncand) {
+        const int32_t c = t % 18;
+        const int32_t i0 = min(max((int32_t)floor(fu), 0), n - 1), j0 = min(max((int32_t)floor(fv), 0), n - 1);
+        const int32_t j = max(j0 - 1, 0) + c / 6, i = max(i0 - 1, 0) + (c / 2) % 3, s = c & 1;
+        const double a = fu - i, b = fv - j;
+        const bool cnear = !(j > j0 + 1 || i > i0 + 1 || i + j > n - 1) &&
+                           (s == 0 ? (a >= -SL_LDEL && b >= -SL_LDEL && a + b <= 1.0 + SL_LDEL)
+                                   : (i + j <= n - 2 && a <= 1.0 + SL_LDEL && b <= 1.0 + SL_LDEL && a + b >= 1.0 - SL_LDEL));
+        if (cnear) {
+          const SlTri r = sl_cell(L, L.face[ff], i, j, s);
+          double d;
+          bool margin;
+          if (sl_test(r, qx, qy, d, margin)) {
+            hit = margin;
+            if (knn_less(d, r.id, md, mid)) {
+              md = d;
+              mid = r.id;
+              mine = r;
+            }
+          }
+        }
+      }
+      if (__ballot(hit)) {
+        stop = true;
+        break;
+      }
+    }
+    if (stop) break;
+  }
+  double bd = md;
+  int32_t bid = mid;
+  wave_min_key(bd, bid);
+  if (bid == 0x7fffffff) return false;
+  const int src = __ffsll((unsigned long long)__ballot(md == bd && mid == bid)) - 1;
+  out.x1 = __shfl(mine.x1, src, 64);
+  out.y1 = __shfl(mine.y1, src, 64);
+  out.x2 = __shfl(mine.x2, src, 64);
+  out.y2 = __shfl(mine.y2, src, 64);
+  out.x3 = __shfl(mine.x3, src, 64);
+  out.y3 = __shfl(mine.y3, src, 64);
+  out.a = __shfl(mine.a, src, 64);
+  out.b = __shfl(mine.b, src, 64);
+  out.d = __shfl(mine.d, src, 64);
+  out.id = bid;
+  bestd = bd;
+  rho2 = L.rho2[bid];
+  return true;
+}
+__global__ __launch_bounds__(BS) void k_sl_wq(MeshDev M, LatLocDev L, GridDev G, int64_t row0, int64_t n, int32_t nb_sl,
+                                              const double* __restrict__ ux, const double* __restrict__ uy, double dt,
+                                              const double* __restrict__ c, double* __restrict__ cout,
+                                              int32_t* notfound, int32_t* __restrict__ queue,
+                                              const int32_t* __restrict__ qoff, int32_t nq) {
+  const int lane = threadIdx.x & 63;
+  const int32_t nw = (int32_t)gridDim.x * (BS / 64);
+  const int32_t total = qoff[nq];
+  const int64_t nsl = (n + 63) / 64;
+  for (int32_t p = (int32_t)blockIdx.x * (BS / 64) + (int32_t)(threadIdx.x >> 6); p < total; p += nw) {
+    // the queue holding entry p: the last q < nq with qoff[q] <= p (qoff[0] = 0), 64 offsets per round
+    int32_t lo = 0, hi = nq, qlo = 0;
+    while (hi - lo > 1) {
+      const int32_t step = (hi - lo + 63) / 64, idx = lo + lane * step;
+      const int32_t qv = idx < hi ? qoff[idx] : 0x7fffffff;
+      const uint64_t m = __ballot(qv <= p);  // (lane 0: qoff[lo] <= p)
+      const int last = 63 - __clzll((long long)m);
+      qlo = __shfl(qv, last, 64);
+      lo += last * step;
+      hi = min(lo + step, hi);
+    }
+    const int32_t bq = lo / (BS / 64), wq = lo % (BS / 64), k = p - qlo;
+    const int64_t r0 = ((nsl * bq) / nb_sl) * 64;  // block_rows of k_sl's block bq
+    const int64_t e = r0 + (int64_t)((BS / 64) * (k >> 6) + wq) * 64 + (k & 63);
+    const int32_t i = queue[e];
+    const int64_t g = row0 + i;
+    double xb, yb;
+    sl_point(M, g, ux[VS * i], uy[VS * i], dt, xb, yb);
+    SlTri r;
+    double bestd;
+    float rho2;
+    const bool cand = sl_best_wave2(L, xb, yb, r, bestd, rho2);
+    const bool ok = cand && (sl_fast(L, r, xb, yb, bestd, rho2) || sl_rank_ok_wave(G, xb, yb, bestd, r.id));
+    const double cn = ok ? sl_value(r, xb, yb, c) : c[g];
+    if (lane == 0) {
+      stnt(cout + g, cn);
+      if (notfound) notfound[i] = ok ? ((L.probe & 2) ? 2 : 0) : 1;
+      if (!ok) queue[e] = ~i;
+    }
+  }
+}
+__global__ __launch_bounds__(BS) void k_sl_qsum(int64_t row0, int64_t n, const double* __restrict__ cout,
+                                                const double* __restrict__ wmix, double* part,
+                                                const int32_t* __restrict__ queue, const int32_t* __restrict__ qcnt) {
+  __shared__ double sh[4];
+  double swc = 0.0, nnf = 0.0;
+  int64_t r0, r1;
+  block_rows(n, r0, r1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t cnt = qcnt[BS / 64 * blockIdx.x + wv];
+  for (int32_t p = lane; p < cnt; p += 64) {
+    const int32_t e = queue[r0 + (int64_t)(BS / 64 * (p >> 6) + wv) * 64 + (p & 63)];
+    const bool nf = e < 0;
+    const int32_t i = nf ? ~e : e;
+    const double cn = cout[row0 + i];
+    if (nf) nnf += 1.0;
+    swc += (wmix ? wmix[i] : 0.0) * cn;
+  }
+  const double a = block_sum(swc, sh), d = block_sum(nnf, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] += a;
+    part[2 * SLB + blockIdx.x] += d;
+  }
+}
+
 // Record locator (meshes without a red-refinement hierarchy: mesh.1, mesh_fine), whose k_sl has no fast path and
 // queued every row for k_sl_slow's one lane per point: one wave per ROW instead, in one launch (k_sl_rec_wave), the
 // records of q's grid cell tested by the lanes together (the passing record with the smallest (d^2, id) key, as

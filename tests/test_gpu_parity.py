@@ -157,8 +157,12 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
     N = mesh.N
     sim = stokes(mesh, tol=S.Tolerances.production())
     assert sim.ctx.path_info()["sl_locator"] == "lattice"
-    monkeypatch.setenv("PUCFEM_SL_WAVE", "0")  # the queued points one lane each (k_sl_slow) instead of one wave
+    # the second pass's three forms: the numbered list (default, k_sl_wq), each wave its own queue (k_sl_wave), one
+    # lane per point (k_sl_slow)
+    monkeypatch.setenv("PUCFEM_SL_WAVE", "0")
     lane = stokes(mesh, tol=S.Tolerances.production())
+    monkeypatch.setenv("PUCFEM_SL_WAVE", "1")
+    wave = stokes(mesh, tol=S.Tolerances.production())
     monkeypatch.delenv("PUCFEM_SL_WAVE")
     monkeypatch.setenv("PUCFEM_SL_RECORDS", "1")
     rec = stokes(mesh, tol=S.Tolerances.production())
@@ -189,7 +193,9 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
         c_lane, nf_lane = sl_on(lane.ctx, c0, u, dt)
         assert np.array_equal(nf, nf_rec), kind
         assert np.array_equal(c, c_rec), kind
-        assert np.array_equal(nf, nf_lane) and np.array_equal(c, c_lane), kind  # k_sl_wave = k_sl_slow, bit for bit
+        c_wave, nf_wave = sl_on(wave.ctx, c0, u, dt)
+        assert np.array_equal(nf, nf_lane) and np.array_equal(c, c_lane), kind  # k_sl_wq = k_sl_slow, bit for bit
+        assert np.array_equal(nf, nf_wave) and np.array_equal(c, c_wave), kind  # = k_sl_wave
         ref, ref_nf = O.sl_advect(c0, u, dt, X, T, tree)
         assert np.array_equal(nf, ref_nf), kind
         if kind in ("random", "hole", "inside"):
@@ -199,6 +205,7 @@ def test_semilagrange_lattice_locator(refine, monkeypatch):
     sim.close()
     rec.close()
     lane.close()
+    wave.close()
 
 
 @pytest.mark.parametrize("m", ["mesh1", "fine"])
