@@ -525,6 +525,11 @@ struct Ctx {
   bool graph_mode = false;
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
+  // and GK consecutive steps in one graph (one host launch per GK steps: a replay of the one-step graph costs
+  // the host about as long as the GPU takes for the step); PUCFEM_GRAPH_STEPS (measurement knob, 1 = off)
+  int gk = std::getenv("PUCFEM_GRAPH_STEPS") ? std::max(1, std::min(64, std::atoi(std::getenv("PUCFEM_GRAPH_STEPS")))) : 8;
+  hipGraphExec_t gexec_k = nullptr;
+  hipGraph_t graph_k = nullptr;
   double* gstats = nullptr;
   // the replayed step's records: a device ring of GRING steps (k_stats_ring), copied out per call / full ring
   static constexpr int GRING = 1024;
@@ -688,6 +693,8 @@ struct Ctx {
       if (st) (void)hipStreamSynchronize(st);
       if (gexec) (void)hipGraphExecDestroy(gexec);
       if (graph) (void)hipGraphDestroy(graph);
+      if (gexec_k) (void)hipGraphExecDestroy(gexec_k);
+      if (graph_k) (void)hipGraphDestroy(graph_k);
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_coef) (void)hipHostFree(h_coef);
@@ -2032,6 +2039,7 @@ struct Ctx {
           if (pcg_trace) trace_pcg(which, it + 1);
           continue;
         }
+        if (dye_gate == 1 && which == 1) dye_tail_release();
         ro_rz = ro(redbuf + 32, CNT_RZ, 1);
         precondition();
         ro_rz = RedOut{};
@@ -2227,6 +2235,7 @@ struct Ctx {
   // PUCFEM_RHS_FUSE=0 (measurement knob): the pressure right-hand side always in its own pass (k_pres_rhs)
   bool rhs_fuse = !(std::getenv("PUCFEM_RHS_FUSE") && std::atoi(std::getenv("PUCFEM_RHS_FUSE")) == 0);
   int pressure(double* yst, double* pout, int which, bool sb_fused = false) {  // StokesColor.py:554-555 (restated)
+    if (dye_gate == 2 && which == 1) dye_tail_release();
     const int nb = div_grid();
     Red sb{redbuf + 24, 1, 1};
     if (!sb_fused) sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
@@ -2509,6 +2518,7 @@ struct Ctx {
   };
   // order the main stream after the pending dye advection
   void sl_join() {
+    dye_tail_release();
     if (!sl_pending) return;
     HIPCHK(hipStreamWaitEvent(st, ev_sl, 0));
     sl_pending = false;
@@ -2523,34 +2533,65 @@ struct Ctx {
   // (round 4 measured the tail released after the next step's first viscous step and after its viscous
   // solve: neutral, r10f; it is released at the end of the step)
   hipEvent_t ev_gate = nullptr;
+  // PUCFEM_DYE_GATE (measurement knob): where the semi-Lagrangian part of the tail (advection, mixing sums, the
+  // record) is released -- 0 with the final-divergence record at the end of the step (default), 1 at the first
+  // V-cycle of the next step's first pressure solve (beside its latency-bound coarse levels), 2 at the start of that
+  // pressure solve
+  int dye_gate = std::getenv("PUCFEM_DYE_GATE") ? std::atoi(std::getenv("PUCFEM_DYE_GATE")) : 0;
+  bool slb_pend = false;     // the semi-Lagrangian part waits for its release (dye_gate > 0)
+  double* slb_rec = nullptr;
+  struct SmallRed {  // (reset on unwind)
+    bool& f;
+    explicit SmallRed(bool& x) : f(x) { f = true; }
+    ~SmallRed() { f = false; }
+  };
   void dye_tail(double* rec) {
     HIPCHK(hipEventRecord(ev_gate, st));
     HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
     {
       StreamSwap sw(st, st_sl);
-      struct SmallRed {  // (reset on unwind)
-        bool& f;
-        explicit SmallRed(bool& x) : f(x) { f = true; }
-        ~SmallRed() { f = false; }
-      } small_red(red_small);
+      SmallRed small_red(red_small);
       const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
       div(ux, uy, nullptr, false, part_fd, rf);  // (the final div field is computed when read)
       if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
-      const int nb = nb_sl(lp.n_own);
-      const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
-      sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
-      KCHK();
-      std::swap(c_full, c_new);
-      if (!rs.out) reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
-      const int nbm = nb_rows(lp.n_own);
-      algo_bytes += 16.0 * (double)lp.n_own;  // c, w
-      const RedOut rm = ro(vals + 5, CNT_DYE_MIX, 1);
-      hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
-                         part_mx, rm);
-      KCHK();
-      if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
-      hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
-      KCHK();
+      if (dye_gate == 0) dye_tail_sl(rec);
+    }
+    if (dye_gate == 0) {
+      HIPCHK(hipEventRecord(ev_sl, st_sl));
+      sl_pending = true;
+    } else {
+      slb_pend = true;
+      slb_rec = rec;
+    }
+  }
+  // the semi-Lagrangian part of the tail (launched on st_sl: the caller swapped the streams)
+  void dye_tail_sl(double* rec) {
+    const int nb = nb_sl(lp.n_own);
+    const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
+    sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
+    KCHK();
+    std::swap(c_full, c_new);
+    if (!rs.out) reduce_into(part_sl, nb, 3, false, 2, SLB);  // sum wc, sum w, not-found
+    const int nbm = nb_rows(lp.n_own);
+    algo_bytes += 16.0 * (double)lp.n_own;  // c, w
+    const RedOut rm = ro(vals + 5, CNT_DYE_MIX, 1);
+    hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, c_full, dwmix, vals + 2, 1, 1,
+                       part_mx, rm);
+    KCHK();
+    if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
+    KCHK();
+  }
+  // release a deferred semi-Lagrangian part (dye_gate > 0): behind the main stream's work so far
+  void dye_tail_release() {
+    if (!slb_pend) return;
+    slb_pend = false;
+    HIPCHK(hipEventRecord(ev_gate, st));
+    HIPCHK(hipStreamWaitEvent(st_sl, ev_gate, 0));
+    {
+      StreamSwap sw(st, st_sl);
+      SmallRed small_red(red_small);
+      dye_tail_sl(slb_rec);
     }
     HIPCHK(hipEventRecord(ev_sl, st_sl));
     sl_pending = true;
@@ -4563,6 +4604,12 @@ int pucfem_build_operators(void* ctx, const pucfem_params* prm) {
       c.graph = nullptr;
       c.graph_mode = false;
     }
+    if (c.gexec_k) {
+      (void)hipGraphExecDestroy(c.gexec_k);
+      (void)hipGraphDestroy(c.graph_k);
+      c.gexec_k = nullptr;
+      c.graph_k = nullptr;
+    }
     build(c);
   });
 }
@@ -4733,35 +4780,48 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       std::vector<int32_t> its(3 * (size_t)nsteps);
       if (c.dense && !c.timer.on && !c.dye_impl) {
         // direct-solve small-mesh path: every step is the same sequence of ~25 launches with no
-        // host synchronisation -> capture it once, replay it per step
+        // host synchronisation -> capture it once (and GK steps of it once), replay them
+        // capture `count` consecutive steps into one graph (the steps' buffers are fixed in graph mode)
+        auto capture = [&](int count, hipGraph_t& gr, hipGraphExec_t& ex) {
+          int32_t tmp[3];
+          HIPCHK(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
+          try {
+            c.gcapture = true;
+            for (int k = 0; k < count; ++k) c.stokes_step(c.gstats, tmp);
+            c.gcapture = false;
+          } catch (...) {
+            c.gcapture = false;
+            hipGraph_t g;
+            (void)hipStreamEndCapture(c.st, &g);
+            c.graph_mode = c.gexec != nullptr;
+            throw;
+          }
+          HIPCHK(hipStreamEndCapture(c.st, &gr));
+          HIPCHK(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0));
+        };
         if (!c.gexec) {
           c.gstats = c.dalloc<double>(8);
           c.gring = c.dalloc<double>(8 * (i64)Ctx::GRING);
           c.gcount = c.dalloc<int>(1);
           HIPCHK(hipStreamSynchronize(c.st));
           c.graph_mode = true;
-          int32_t tmp[3];
-          HIPCHK(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
-          try {
-            c.gcapture = true;
-            c.stokes_step(c.gstats, tmp);
-            c.gcapture = false;
-          } catch (...) {
-            c.gcapture = false;
-            hipGraph_t g;
-            (void)hipStreamEndCapture(c.st, &g);
-            c.graph_mode = false;
-            throw;
-          }
-          HIPCHK(hipStreamEndCapture(c.st, &c.graph));
-          HIPCHK(hipGraphInstantiate(&c.gexec, c.graph, nullptr, nullptr, 0));
+          capture(1, c.graph, c.gexec);
         }
+        if (!c.gexec_k && c.gk > 1 && nsteps >= c.gk) capture(c.gk, c.graph_k, c.gexec_k);
         HIPCHK(hipMemsetAsync(c.gcount, 0, sizeof(int), c.st));
-        for (int s = 0, k = 0; s < nsteps; ++s) {
-          HIPCHK(hipGraphLaunch(c.gexec, c.st));
-          if (++k == Ctx::GRING || s == nsteps - 1) {  // the ring's records -> this call's records
-            HIPCHK(hipMemcpyAsync(rec + 8 * (s + 1 - k), c.gring, sizeof(double) * 8 * k, hipMemcpyDeviceToDevice, c.st));
-            if (s < nsteps - 1) HIPCHK(hipMemsetAsync(c.gcount, 0, sizeof(int), c.st));
+        for (int s = 0, k = 0; s < nsteps;) {
+          int d = 1;
+          if (c.gexec_k && nsteps - s >= c.gk && k + c.gk <= Ctx::GRING) {
+            HIPCHK(hipGraphLaunch(c.gexec_k, c.st));
+            d = c.gk;
+          } else {
+            HIPCHK(hipGraphLaunch(c.gexec, c.st));
+          }
+          s += d;
+          k += d;
+          if (k == Ctx::GRING || s == nsteps) {  // the ring's records -> this call's records
+            HIPCHK(hipMemcpyAsync(rec + 8 * (s - k), c.gring, sizeof(double) * 8 * k, hipMemcpyDeviceToDevice, c.st));
+            if (s < nsteps) HIPCHK(hipMemsetAsync(c.gcount, 0, sizeof(int), c.st));
             k = 0;
           }
         }
@@ -4780,6 +4840,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
           c.dits = nullptr;
           if (c.sl_pending) (void)hipStreamSynchronize(c.st_sl);
           c.sl_pending = false;
+          c.slb_pend = false;
           c.tail_pend = false;
           throw;
         }

@@ -84,3 +84,21 @@ def test_color_mesh_fine_5000_steps_config2():
     # the printed max|div u*| and max|final div| of the last step (11.5 and 11.6)
     assert abs(st[-1].max_div_star - 11.5) < 0.05 * 11.5
     assert abs(st[-1].max_final_div - 11.6) < 0.05 * 11.6
+
+
+@pytest.mark.parametrize("m", ["mesh1", "fine"])
+def test_graph_of_k_steps_equals_single_step_graph(m, monkeypatch):
+    """The small-mesh path replays GK steps per graph launch (PUCFEM_GRAPH_STEPS, default 8) and the one-step
+    graph for the rest of a call and at a full record ring: the same fields and per-step records, bit for bit, as
+    one-step replays (a call of 1, one of 37 = 4 x 8 + 5, one of 1030 across the 1024-step ring)."""
+    mesh = pf.load_mesh(m)
+    out = {}
+    for gk in ("1", "8"):
+        monkeypatch.setenv("PUCFEM_GRAPH_STEPS", gk)
+        sim = S.StokesSimulation(mesh, S.SquirmerBC(), 0.05, "color", 0, S.Tolerances())
+        st = sim.step(1) + sim.step(37) + sim.step(1030)
+        out[gk] = (sim.u.copy(), sim.c.copy(), [(s.max_div_star, s.max_final_div, s.mix_var) for s in st])
+        sim.close()
+    assert np.array_equal(out["1"][0], out["8"][0])
+    assert np.array_equal(out["1"][1], out["8"][1])
+    assert out["1"][2] == out["8"][2]
