@@ -145,7 +145,7 @@ struct Timer {
   bool on = false;
   uint32_t mask = ~0u;  // timed kernel classes
   std::vector<hipEvent_t> pool;
-  struct Pend { int cls; hipEvent_t a, b; double bytes; };
+  struct Pend { int cls; hipEvent_t a, b; double bytes; bool keep = false; };  // (cls < 0: not accounted)
   std::vector<Pend> pend;
   // classes: 0 k_cheb (finest), 1 k_cg_dir, 2 k_cg_upd, 3 k_grad_proj, 4 k_sl, 5 k_resid (finest), 6 / 7 the
   // finest level's restriction / prolongation, 8 k_sl_slow, 9 k_vcheb (whole-grid steps), 10 k_cheb_pair,
@@ -168,11 +168,13 @@ struct Timer {
   size_t done = 0;  // samples accounted so far (the absolute index of pend[0])
   size_t mark() const { return done + pend.size(); }
   void account(const Pend& p) {
-    float t = 0;
-    HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
-    ms[p.cls] += t;
-    bytes[p.cls] += p.bytes;
-    n[p.cls]++;
+    if (p.cls >= 0) {
+      float t = 0;
+      HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
+      ms[p.cls] += t;
+      bytes[p.cls] += p.bytes;
+      n[p.cls]++;
+    }
     pool.push_back(p.a);
     pool.push_back(p.b);
   }
@@ -197,13 +199,18 @@ struct Timer {
   }
   // drop the pending samples from absolute index k on (launches that found the solve converged and returned
   // without work: counting them would credit their bytes to a near-zero duration)
+  // (samples marked `keep` stay: a gated gradient projection behind the read that found the solve converged)
   void drop_from(size_t k) {
-    const size_t r = k > done ? k - done : 0;
-    for (size_t i = r; i < pend.size(); ++i) {
+    size_t w = k > done ? k - done : 0;
+    for (size_t i = w; i < pend.size(); ++i) {
+      if (pend[i].keep) {
+        pend[w++] = pend[i];
+        continue;
+      }
       pool.push_back(pend[i].a);
       pool.push_back(pend[i].b);
     }
-    if (r < pend.size()) pend.resize(r);
+    if (w < pend.size()) pend.resize(w);
   }
   ~Timer() {
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -1991,8 +1998,7 @@ struct Ctx {
     bool done0 = false;
     const bool eligible = seen && last_it[which] <= 1;
     if (eligible && __builtin_popcount(zero_hist[which] & 0xffu) >= 2) {
-      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
-      sync_st();
+      read_ctl();
       done0 = h_ctl[0] != 0;
     }
     for (bool first = true; !done0; first = false) {
@@ -2083,10 +2089,9 @@ struct Ctx {
         std::swap(v.po[0], v.pn[0]);
         if (pcg_trace) trace_pcg(which, it + 1);
       }
-      HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
       // the samples before this chunk, while the GPU runs it (this chunk's stay pending until its test is read)
       if (timer.on && !marks.empty()) timer.flush_ready(marks.front().second);
-      sync_st();
+      read_ctl();
       if (timer.on && h_ctl[0])  // iterations from the converged one on launched kernels that did no work
         for (auto& mk : marks)
           if (mk.first >= h_ctl[1]) {
@@ -2493,16 +2498,69 @@ struct Ctx {
     return true;
   }
   // pp: p, or with p_from_y the pressure solve's y (gathered through the merged tables and columns)
-  void grad_proj(const double* pp, int mode) {
+  // gate (optional): the PCG's control word -- the projection runs only if the solve has finished by then
+  double grad_proj(const double* pp, int mode, const int* gate = nullptr) {
     const FaceDev fc = p_from_y ? fP.full() : fK.full();
     const DevSell& A = p_from_y ? dPm : dP;
+    const double bytes = (16.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 40.0 * (double)lp.n_own;
     with_c16(A, [&](auto c16) {
-      klaunch(3, (16.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 40.0 * (double)lp.n_own,
-              k_grad_proj<decltype(c16)::value>, dim3(grid_full(fc, A)), dim3(BS), A.view(), fc, (const double*)dGx,
-              (const double*)dGy, pp, (const double*)das1, prm.dt, mode, (const uint8_t*)ddir, (const double*)usx,
-              (const double*)usy, ux, uy);
+      klaunch(3, bytes, k_grad_proj<decltype(c16)::value>, dim3(grid_full(fc, A)), dim3(BS), A.view(), fc,
+              (const double*)dGx, (const double*)dGy, pp, (const double*)das1, prm.dt, mode, (const uint8_t*)ddir,
+              (const double*)usx, (const double*)usy, ux, uy, gate);
     });
     KCHK();
+    return bytes;
+  }
+  // The gradient projection after a pressure solve, enqueued behind the solve's convergence reads and gated on its
+  // control word (PUCFEM_GP_GATE, default on): when the read finds the solve converged the GPU has been running the
+  // projection during the host's round trip (the r13g trace: ~50 us idle before each k_grad_proj), and when it finds
+  // it not converged the launch did nothing and the next read enqueues it again.  Single rank, multigrid path with
+  // p kept in y (nothing is launched between the solve's last read and the projection there).
+  struct GpGate {
+    bool on = false, done = false;
+    const double* pp = nullptr;
+    int mode = 0;
+    double bytes = 0.0;
+  } gp_gate;
+  // after the solve: whether the gated projection ran (then its bytes are counted here)
+  bool gp_gate_end() {
+    const bool d = gp_gate.done;
+    if (d) {
+      algo_bytes += gp_gate.bytes;
+      cls_bytes[3] += gp_gate.bytes;
+      ++cls_n[3];
+    }
+    gp_gate = GpGate{};
+    return d;
+  }
+  bool gp_gate_env = !(std::getenv("PUCFEM_GP_GATE") && std::atoi(std::getenv("PUCFEM_GP_GATE")) == 0);
+  // the PCG's control-word read (h_ctl), with the gated projection behind it
+  void read_ctl() {
+    HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
+    if (!gp_gate.on) {
+      sync_st();
+      return;
+    }
+    if (!ev_wait) HIPCHK(hipEventCreateWithFlags(&ev_wait, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev_wait, st));
+    sl_join();  // (the dye tail reads u)
+    const size_t np = timer.pend.size();
+    const double b = grad_proj(gp_gate.pp, gp_gate.mode, ctl);
+    const bool timed = timer.on && timer.pend.size() == np + 1;
+    if (timed) timer.pend.back().keep = true;
+    // its bytes are counted by the caller once the solve has returned (the solve takes back the counts of launches
+    // behind its converged iteration)
+    algo_bytes -= b;
+    cls_bytes[3] -= b;
+    --cls_n[3];
+    gp_gate.bytes = b;
+    wait_event(ev_wait);
+    if (h_ctl[0]) {
+      gp_gate.done = true;
+      gp_gate.on = false;
+    } else if (timed) {
+      timer.pend[np].cls = -1;  // (the launch found the solve unfinished: no sample)
+    }
   }
 
   // side stream of the overlapped dye advection (stokes_step)
@@ -2633,14 +2691,19 @@ struct Ctx {
     // step reads it, and its 8 B/row store is a quarter of the kernel's bytes
     const bool f1 = div_rhs(usx, usy, nullptr, vals);
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
+    const bool gpg = gp_gate_env && use_mg && proj_k > 0 && p_from_y && !dist() && !proj_spmv;
+    gp_gate = GpGate{gpg, false, yp, 0, 0.0};
     const int itp = pressure(yp, p, 1, f1);
+    const bool gp1 = gp_gate_end();
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
-    grad_proj(p_from_y ? yp : p, 0);
+    if (!gp1) grad_proj(p_from_y ? yp : p, 0);
     bc(ux, uy);
     halo_v(ux);
     const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
+    gp_gate = GpGate{gpg, false, yp2, 1, 0.0};
     const int itp2 = pressure(yp2, p2, 2, f2);
-    grad_proj(p_from_y ? yp2 : p2, 1);
+    const bool gp2 = gp_gate_end();
+    if (!gp2) grad_proj(p_from_y ? yp2 : p2, 1);
     halo_v(ux);
     // single-rank explicit dye: the final-divergence record and the advection of this step (they read
     // the final u and c, write final_div, c_new and their own partials) run on a side stream,

@@ -1881,7 +1881,9 @@ __global__ LB_GATHER void k_grad_proj(SellDev A, FaceDev fc, const double* __res
                                                   const double* __restrict__ gy, const double* __restrict__ p,
                                                   const double* __restrict__ as1, double dt, int mode,
                                                   const uint8_t* __restrict__ dirflag, const double* usx,
-                                                  const double* usy, double* ux, double* uy) {
+                                                  const double* usy, double* ux, double* uy,
+                                                  const int* gate = nullptr) {
+  if (gate && gate[0] == 0) return;  // (gated on the PCG's control word: the solve has not finished)
   if (mode == 0) grad_proj_body<0, C16>(A, fc, gx, gy, p, as1, dt, dirflag, usx, usy, ux, uy);
   else grad_proj_body<1, C16>(A, fc, gx, gy, p, as1, dt, dirflag, usx, usy, ux, uy);
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6: the K-step small-mesh graph (bit identity, mesh_fine rate) and the dye tail's release point
-# (PUCFEM_DYE_GATE 0 / 1 / 2; bit identity, then alternating driver-command benches).
+# (PUCFEM_DYE_GATE 0 / 1 / 2) and the gated gradient projection (PUCFEM_GP_GATE): bit identity, then alternating
+# driver-command benches.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-gate}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
@@ -22,7 +23,11 @@ for rep in range(3):
 sim.close()
 PY
 done
-for g in 0 1; do
-  PUCFEM_DYE_GATE=$g timeout -k 10 300 python tools/bitcmp.py 7 30 || exit 1
+for e in "PUCFEM_DYE_GATE=0" "PUCFEM_DYE_GATE=1" "PUCFEM_GP_GATE=0"; do
+  echo "$e"; env $e timeout -k 10 300 python tools/bitcmp.py 7 30 || exit 1
 done
-tools/gpu_env_ab.sh "$TAG" "" "PUCFEM_DYE_GATE=1" "PUCFEM_DYE_GATE=2" "" "PUCFEM_DYE_GATE=1" "PUCFEM_DYE_GATE=1 PUCFEM_SL_BLOCKS=2048"
+for e in "PUCFEM_GP_GATE=1" "PUCFEM_GP_GATE=0"; do
+  echo "$e"; env $e timeout -k 10 300 python tools/bitcmp.py 5 60 || exit 1
+done
+tools/gpu_env_ab.sh "$TAG" "" "PUCFEM_GP_GATE=0" "PUCFEM_DYE_GATE=1" "PUCFEM_DYE_GATE=2" "" "PUCFEM_GP_GATE=0" \
+  "PUCFEM_DYE_GATE=1" "PUCFEM_DYE_GATE=1 PUCFEM_SL_BLOCKS=2048"
