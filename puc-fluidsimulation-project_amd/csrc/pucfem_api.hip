@@ -532,9 +532,10 @@ struct Ctx {
   bool graph_mode = false;
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
-  // and GK consecutive steps in one graph (one host launch per GK steps: a replay of the one-step graph costs
-  // the host about as long as the GPU takes for the step); PUCFEM_GRAPH_STEPS (measurement knob, 1 = off)
-  int gk = std::getenv("PUCFEM_GRAPH_STEPS") ? std::max(1, std::min(64, std::atoi(std::getenv("PUCFEM_GRAPH_STEPS")))) : 8;
+  // and, with PUCFEM_GRAPH_STEPS = GK > 1 (measurement knob), GK consecutive steps in one graph: one host launch per
+  // GK steps, the same bits (test_graph_of_k_steps_equals_single_step_graph), but slower -- mesh_fine 9.7k steps/s
+  // with 8 steps per graph against 10.5k with one (r14b): the host's replay is not what bounds the small step
+  int gk = std::getenv("PUCFEM_GRAPH_STEPS") ? std::max(1, std::min(64, std::atoi(std::getenv("PUCFEM_GRAPH_STEPS")))) : 1;
   hipGraphExec_t gexec_k = nullptr;
   hipGraph_t graph_k = nullptr;
   double* gstats = nullptr;
