@@ -845,6 +845,28 @@ struct Ctx {
   // every row for k_sl_slow's one lane per point (PUCFEM_SL_WAVE=0 keeps the two passes)
   bool sl_rec_wave(i64 n) const { return !lat_sl && sl_wave && n <= SLB * (BS / 64); }
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
+  // A grid-stride kernel whose grid holds more blocks than the chip keeps resident runs its work in two rounds of
+  // equal blocks, the second on part of the chip (k_mdot2 at 96 VGPRs: 5 blocks per CU resident, 1,280 of its 2,048);
+  // fit_grid caps such a grid at the resident count (hipOccupancy..., cached per kernel).  PUCFEM_FIT_GRID=0
+  // (measurement knob) keeps the full grids.
+  bool fit_grid_on = !(std::getenv("PUCFEM_FIT_GRID") && std::atoi(std::getenv("PUCFEM_FIT_GRID")) == 0);
+  std::map<const void*, int> resident_blocks;
+  int n_cu = 0;
+  int fit_grid(const void* kern, int nb) {
+    if (!fit_grid_on) return nb;
+    auto it = resident_blocks.find(kern);
+    if (it == resident_blocks.end()) {
+      if (n_cu == 0) {
+        int d = 0;
+        HIPCHK(hipGetDevice(&d));
+        HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, d));
+      }
+      int per = 0;
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, BS, 0));
+      it = resident_blocks.emplace(kern, std::max(1, per) * std::max(1, n_cu)).first;
+    }
+    return std::max(1, std::min(nb, it->second));
+  }
 
   // ------------------------------------------------------------------ timing helpers
   // Launch on the library stream.  When timing (cls >= 0), the start / stop events are taken by the
@@ -2338,7 +2360,7 @@ struct Ctx {
       H.gamma.clear();
       return false;
     }
-    const int nb = grid_ew(n);
+    const int nb = grid_ew(n), nbd = fit_grid((const void*)mdot2_kernel(m), nb);
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
     // k_mdot2: X (fp32), b, A v, v read
     const bool otf = pend_otf[which];
@@ -2353,10 +2375,10 @@ struct Ctx {
     klaunch(14,
             (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0) + (rin ? 12.0 : 0.0)) *
                 (double)n,
-            mdot2_kernel(m), dim3(nb), dim3(BS), (int64_t)n,
+            mdot2_kernel(m), dim3(nbd), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], vp,
             op.null_free, proj_part, rmd, pd, rin ? *rin : RhsIn{});
-    if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
+    if (!rmd.out) launch_reduce(proj_part, nbd, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
     QMat qm{};
@@ -2610,10 +2632,15 @@ struct Ctx {
     {
       StreamSwap sw(st, st_sl);
       SmallRed small_red(red_small);
+      if (dye_gate == 0 && dye_sl_first) dye_tail_sl(rec, false);
       const RedOut rf = ro(vals + 1, CNT_DYE_DIV, 1, MAXB, 1u);
       div(ux, uy, nullptr, false, part_fd, rf);  // (the final div field is computed when read)
       if (!rf.out) reduce_into(part_fd, div_grid(), 1, true, 1);  // max |final div|
-      if (dye_gate == 0) dye_tail_sl(rec);
+      if (dye_gate == 0 && !dye_sl_first) dye_tail_sl(rec);
+      if (dye_gate == 0 && dye_sl_first) {
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
+        KCHK();
+      }
     }
     if (dye_gate == 0) {
       HIPCHK(hipEventRecord(ev_sl, st_sl));
@@ -2623,8 +2650,11 @@ struct Ctx {
       slb_rec = rec;
     }
   }
-  // the semi-Lagrangian part of the tail (launched on st_sl: the caller swapped the streams)
-  void dye_tail_sl(double* rec) {
+  // PUCFEM_DYE_SL_FIRST=1 (measurement knob): the tail's semi-Lagrangian part before its final-divergence record
+  bool dye_sl_first = std::getenv("PUCFEM_DYE_SL_FIRST") && std::atoi(std::getenv("PUCFEM_DYE_SL_FIRST")) != 0;
+  // the semi-Lagrangian part of the tail (launched on st_sl: the caller swapped the streams); stats: the step
+  // record after it (else the caller writes it)
+  void dye_tail_sl(double* rec, bool stats = true) {
     const int nb = nb_sl(lp.n_own);
     const RedOut rs = ro(vals + 2, CNT_DYE_SL, 3, SLB);
     sl_launch(nb, lp.r0, lp.n_own, ux, uy, prm.dt, c_full, c_new, dwmix, nullptr, rs);
@@ -2638,6 +2668,7 @@ struct Ctx {
                        part_mx, rm);
     KCHK();
     if (!rm.out) reduce_into(part_mx, nbm, 1, false, 5);
+    if (!stats) return;
     hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 6);
     KCHK();
   }
