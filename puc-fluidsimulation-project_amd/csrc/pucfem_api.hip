@@ -847,9 +847,12 @@ struct Ctx {
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
   // A grid-stride kernel whose grid holds more blocks than the chip keeps resident runs its work in two rounds of
   // equal blocks, the second on part of the chip (k_mdot2 at 96 VGPRs: 5 blocks per CU resident, 1,280 of its 2,048);
-  // fit_grid caps such a grid at the resident count (hipOccupancy..., cached per kernel).  PUCFEM_FIT_GRID=0
-  // (measurement knob) keeps the full grids.
-  bool fit_grid_on = !(std::getenv("PUCFEM_FIT_GRID") && std::atoi(std::getenv("PUCFEM_FIT_GRID")) == 0);
+  // fit_grid caps such a grid at the resident count (hipOccupancy..., cached per kernel).  PUCFEM_FIT_GRID=1
+  // (measurement knob, off by default): k_mdot2 442 -> 397 us, the step +0.6 % (r14d), but the dots' partials
+  // group other rows, so the projection's guesses differ in their last bits and with them where each production
+  // solve stops below rtol: the L7 per-step margins went 5.7x / 7.5x -> 2.8x / 2.6x (r14e; asserted at 2x).  The
+  // default keeps the validated bits.
+  bool fit_grid_on = std::getenv("PUCFEM_FIT_GRID") && std::atoi(std::getenv("PUCFEM_FIT_GRID")) != 0;
   std::map<const void*, int> resident_blocks;
   int n_cu = 0;
   int fit_grid(const void* kern, int nb) {
