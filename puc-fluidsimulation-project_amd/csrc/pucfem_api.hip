@@ -56,6 +56,7 @@ __global__ void pucfem::k_comm_reduce(int world, int is_max, size_t n, const dou
 namespace {
 
 constexpr int64_t DENSE_MAX = 1500;  // small-mesh direct-solve threshold (mesh_fine: 1,067 nodes)
+static_assert(DENSE_MAX <= dev::DENSE_LDS, "the dense solves stage their vectors in LDS");
 
 struct Error : std::runtime_error {
   int code;
@@ -444,6 +445,7 @@ struct Ctx {
   int32_t *dslave_of = nullptr, *dmaster_of = nullptr;
   int32_t *dcdst = nullptr, *dcsrc = nullptr, *ddnode = nullptr;
   double *ddval = nullptr, *dbctmp = nullptr;
+  int32_t *dbcsrc = nullptr, *dbcdir = nullptr;  // dense path: k_dense_mv2_bc's row maps
   int ncopy = 0, ndir = 0;
   bool bc_gather = true;  // some copy source is also written: k_bc_gather saves the sources first
   int32_t* dsend = nullptr;
@@ -2160,14 +2162,23 @@ struct Ctx {
   void halo_v(double* vx) { halo2(reinterpret_cast<dbl2*>(vx)); }
   // PUCFEM_VISC_FUSE_FIN=0 (measurement knob): k_visc_fin as its own launch after the solve
   bool visc_fuse_fin = !(std::getenv("PUCFEM_VISC_FUSE_FIN") && std::atoi(std::getenv("PUCFEM_VISC_FUSE_FIN")) == 0);
+  bool dense_bc = !(std::getenv("PUCFEM_DENSE_BC") && std::atoi(std::getenv("PUCFEM_DENSE_BC")) == 0);
   int viscous(int& iters) {  // StokesColor.py:540-547
     const i64 n = lp.n_own;
     if (dense) {  // u* = A_visc^-1 (u + DT * 0)
-      hipLaunchKernelGGL(k_dense_mv2, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dVinv, ux, uy,
-                         usx, usy);
-      KCHK();
+      // (PUCFEM_DENSE_BC=0, measurement knob: the BCs in their own launch)
+      if (dbcsrc && dense_bc && dir_ncomp == 2) {  // (velocity BCs: both components copied / set)
+        hipLaunchKernelGGL(k_dense_mv2_bc, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dVinv, ux,
+                           uy, usx, usy, (const int32_t*)dbcsrc, (const int32_t*)dbcdir, (const double*)ddval,
+                           dir_ncomp);
+        KCHK();
+      } else {
+        hipLaunchKernelGGL(k_dense_mv2, dim3((int)std::min<i64>(2048, (n + 3) / 4)), dim3(BS), 0, st, n, dVinv, ux, uy,
+                           usx, usy);
+        KCHK();
+        bc(usx, usy);
+      }
       iters = 0;
-      bc(usx, usy);
       return 0;
     }
     const bool ext = dvinc[0] != nullptr && !proj_k_visc;
@@ -4329,6 +4340,14 @@ void build(Ctx& c) {
     c.ddnode = c.upload(dn);
     c.ddval = c.upload(dv);
     c.dbctmp = c.dalloc<double>(2 * std::max(1, c.ncopy));
+    if (c.dense) {  // k_dense_mv2_bc's per-row maps
+      std::vector<i32> bsrc(no), bdir(no, -1);
+      for (i64 i = 0; i < no; ++i) bsrc[i] = (i32)i;
+      for (size_t k = 0; k < cd.size(); ++k) bsrc[cd[k]] = cs[k];
+      for (size_t k = 0; k < dn.size(); ++k) bdir[dn[k]] = (i32)k;
+      c.dbcsrc = c.upload(bsrc);
+      c.dbcdir = c.upload(bdir);
+    }
   }
   clk.mark("  dev: BC lists");
   // halo plan

@@ -4404,27 +4404,34 @@ __global__ __launch_bounds__(CGB_THREADS) void k_cg_block(SellDev A, const doubl
 // every column from braw and the reduced sum, the dense pseudo-inverse product (k_dense_mv), and p = y with every
 // slave taking its master's value (k_cg_fin) -- the same operations in the same order as the three launches it
 // replaces, so the same bits
+// The right-hand side is formed once per block into LDS (n <= DENSE_LDS), so a row's loop issues only its
+// independent matrix loads (the column-wise formation took three dependent loads per column and row: 13 us per
+// solve on mesh_fine, r14c)
+constexpr int DENSE_LDS = 1536;
 __global__ __launch_bounds__(BS) void k_dense_pres(int64_t n, const double* __restrict__ Pinv,
                                                    const double* __restrict__ braw, const int32_t* __restrict__ slave_of,
                                                    const int32_t* __restrict__ master_of, const double* part_sum, int nb,
                                                    double inv_nfree, double* __restrict__ y, double* __restrict__ p) {
   __shared__ double sh[4];
+  __shared__ double bl[DENSE_LDS];
   const double mean = reduce_partials(part_sum, nb, sh) * inv_nfree;
+  for (int64_t j = threadIdx.x; j < n; j += BS) {
+    double b;
+    if (master_of[j] >= 0) {
+      b = 0.0;
+    } else {
+      b = braw[j];
+      if (slave_of[j] >= 0) b += braw[slave_of[j]];
+      b = b - mean;
+    }
+    bl[j] = b;
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
     const double* a = Pinv + row * n;
     double acc = 0.0;
-    for (int64_t j = lane; j < n; j += 64) {
-      double b;
-      if (master_of[j] >= 0) {
-        b = 0.0;
-      } else {
-        b = braw[j];
-        if (slave_of[j] >= 0) b += braw[slave_of[j]];
-        b = b - mean;
-      }
-      acc += a[j] * b;
-    }
+    for (int64_t j = lane; j < n; j += 64) acc += a[j] * bl[j];
     acc = wave_sum(acc);
     if (lane == 0) {
       y[row] = acc;
@@ -4436,17 +4443,67 @@ __global__ __launch_bounds__(BS) void k_dense_pres(int64_t n, const double* __re
   }
 }
 
+// (x0, x1 staged in LDS once per block, n <= DENSE_LDS)
 __global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __restrict__ Ainv, const double* __restrict__ x0,
                                                   const double* __restrict__ x1, double* __restrict__ y0,
                                                   double* __restrict__ y1) {
+  __shared__ double xl[2 * DENSE_LDS];
+  for (int64_t j = threadIdx.x; j < n; j += BS) {
+    xl[2 * j] = x0[VS * j];
+    xl[2 * j + 1] = x1[VS * j];
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
     const double* a = Ainv + row * n;
     double s0 = 0.0, s1 = 0.0;
     for (int64_t j = lane; j < n; j += 64) {
       const double v = a[j];
-      s0 += v * x0[VS * j];
-      s1 += v * x1[VS * j];
+      s0 += v * xl[2 * j];
+      s1 += v * xl[2 * j + 1];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+      y0[VS * row] = s0;
+      y1[VS * row] = s1;
+    }
+  }
+}
+
+// k_dense_mv2 with the velocity BCs of the solve's result (Ctx::bc) in the same launch: a Dirichlet row takes its
+// value, a periodic copy row the product of its source's matrix row (the source's value before the BCs, which is what
+// k_bc_apply copies: write sets are disjoint, chained sources are read before the writes), every other row its own
+// product -- the same values bit for bit without k_bc_apply's launch (bsrc: the row whose product the row takes,
+// bdir: the Dirichlet entry or -1)
+__global__ __launch_bounds__(BS) void k_dense_mv2_bc(int64_t n, const double* __restrict__ Ainv,
+                                                     const double* __restrict__ x0, const double* __restrict__ x1,
+                                                     double* __restrict__ y0, double* __restrict__ y1,
+                                                     const int32_t* __restrict__ bsrc, const int32_t* __restrict__ bdir,
+                                                     const double* __restrict__ dval, int ncomp) {
+  // (ncomp = 2: the velocity BCs set and copy both components)
+  __shared__ double xl[2 * DENSE_LDS];
+  for (int64_t j = threadIdx.x; j < n; j += BS) {
+    xl[2 * j] = x0[VS * j];
+    xl[2 * j + 1] = x1[VS * j];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    const int32_t d = bdir[row];
+    if (d >= 0) {
+      if (lane == 0) {
+        y0[VS * row] = dval[ncomp * d];
+        y1[VS * row] = dval[ncomp * d + 1];
+      }
+      continue;
+    }
+    const double* a = Ainv + (int64_t)bsrc[row] * n;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t j = lane; j < n; j += 64) {
+      const double v = a[j];
+      s0 += v * xl[2 * j];
+      s1 += v * xl[2 * j + 1];
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
