@@ -849,11 +849,12 @@ struct Ctx {
   static int grid_ew(i64 n) { return (int)std::max<i64>(1, std::min<i64>(2048, (n + BS - 1) / BS)); }
   // A grid-stride kernel whose grid holds more blocks than the chip keeps resident runs its work in two rounds of
   // equal blocks, the second on part of the chip (k_mdot2 at 96 VGPRs: 5 blocks per CU resident, 1,280 of its 2,048);
-  // fit_grid caps such a grid at the resident count (hipOccupancy..., cached per kernel).  PUCFEM_FIT_GRID=1
-  // (measurement knob, off by default): k_mdot2 442 -> 397 us, the step +0.6 % (r14d), but the dots' partials
-  // group other rows, so the projection's guesses differ in their last bits and with them where each production
-  // solve stops below rtol: the L7 per-step margins went 5.7x / 7.5x -> 2.8x / 2.6x (r14e; asserted at 2x).  The
-  // default keeps the validated bits.
+  // fit_grid gives the resident count (hipOccupancy..., cached per kernel) for such a grid.  With PUCFEM_FIT_GRID=1
+  // (measurement knob, off) k_mdot2 keeps its 2,048 blocks' rows and partials as virtual blocks run by a grid of
+  // nb / ceil(nb / resident) blocks: the same bits, and no faster (461 vs 465 us, r14g: 1,024 blocks of two units at
+  // 4 blocks per CU).  Capping the grid itself made k_mdot2 442 -> 397 us, but its partials then group other rows, the
+  // projection's guesses differ in their last bits and with them where each production solve stops below rtol: the
+  // L7 per-step margins went 5.7x / 7.5x -> 2.8x / 2.6x (r14d / r14e), so the plain grid stays.
   bool fit_grid_on = std::getenv("PUCFEM_FIT_GRID") && std::atoi(std::getenv("PUCFEM_FIT_GRID")) != 0;
   std::map<const void*, int> resident_blocks;
   int n_cu = 0;
@@ -2374,8 +2375,18 @@ struct Ctx {
       H.gamma.clear();
       return false;
     }
-    const int nb = grid_ew(n), nbd = fit_grid((const void*)mdot2_kernel(m), nb);
+    const int nb = grid_ew(n);
     const RedOut rmd = ro(proj_d, CNT_MDOT, 2 * m + 4);
+    // virtual blocks: nb blocks' rows and partials on a grid the chip holds at once (not with the fused reduction)
+    int nbp = nb, nvb = 0;
+    if (!rmd.out) {
+      const int res = fit_grid((const void*)mdot2_kernel(m), nb);
+      if (res < nb) {
+        const int per = (nb + res - 1) / res;
+        nbp = (nb + per - 1) / per;
+        nvb = nb;
+      }
+    }
     // k_mdot2: X (fp32), b, A v, v read
     const bool otf = pend_otf[which];
     // a pending direction: A v from the residuals; v accumulated (pend_acc) or y - x0 (the first direction)
@@ -2389,10 +2400,10 @@ struct Ctx {
     klaunch(14,
             (4.0 * m + 24.0 + (otf ? 8.0 : 0.0) + (vdiff ? 8.0 : 0.0) - (vz0 ? 8.0 : 0.0) + (rin ? 12.0 : 0.0)) *
                 (double)n,
-            mdot2_kernel(m), dim3(nbd), dim3(BS), (int64_t)n,
+            mdot2_kernel(m), dim3(nbp), dim3(BS), (int64_t)n,
             (const ProjT*)projX[which], (int64_t)pld(which), b, (const double*)pav[which], vp,
-            op.null_free, proj_part, rmd, pd, rin ? *rin : RhsIn{});
-    if (!rmd.out) launch_reduce(proj_part, nbd, MAXB, 2 * m + 4, false, proj_d);
+            op.null_free, proj_part, rmd, pd, rin ? *rin : RhsIn{}, nvb);
+    if (!rmd.out) launch_reduce(proj_part, nb, MAXB, 2 * m + 4, false, proj_d);
     KCHK();
     if (dist()) comm->allreduce(proj_d, 2 * m + 4, false, st);
     QMat qm{};

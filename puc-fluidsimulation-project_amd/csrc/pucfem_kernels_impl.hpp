@@ -820,19 +820,25 @@ struct PendDir {
   const double* rf;  // its final residual (null: A v was stored in av)
   const double* v;   // its accumulated correction (null: y - x0, or the stored v)
 };
+// Virtual blocks (nvb > 0): the rows and partials are those of a grid of nvb blocks (virtual block vb: rows
+// vb BS + t + k nvb BS, its partials at index vb), run by a smaller grid whose blocks take virtual blocks vb =
+// blockIdx.x, + gridDim.x, ... one after another -- the same sums in the same order, so the same bits, on a grid the
+// chip holds at once (at 96 VGPRs 1,280 of the 2,048 blocks are resident: the rest ran as a second, partial round)
 template <int M>
 __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict__ X, int64_t ld,
                                               const double* __restrict__ b, const double* __restrict__ av,
                                               const double* __restrict__ v, const int32_t* __restrict__ master_of,
-                                              double* part, RedOut ro, PendDir D, RhsIn R = RhsIn{}) {
+                                              double* part, RedOut ro, PendDir D, RhsIn R = RhsIn{}, int nvb = 0) {
   constexpr int NA = 2 * M + 4;
   __shared__ double sh[NA][4];
+  const double mean = R.braw ? R.sum[0] * R.inv_nfree : 0.0;
+  const int V = nvb > 0 ? nvb : (int)gridDim.x;
+  const int64_t step = (int64_t)V * BS;
+  for (int vb = blockIdx.x; vb < V; vb += gridDim.x) {
   double acc[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) acc[i] = 0.0;
-  const double mean = R.braw ? R.sum[0] * R.inv_nfree : 0.0;
-  const int64_t step = (int64_t)gridDim.x * BS;
-  for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < n; r += step) {
+  for (int64_t r = (int64_t)vb * BS + threadIdx.x; r < n; r += step) {
     double br;
     if (R.braw) {  // (k_pres_rhs's row)
       if (master_of[r] >= 0) {
@@ -869,7 +875,13 @@ __global__ __launch_bounds__(BS) void k_mdot2(int64_t n, const ProjT* __restrict
     if ((threadIdx.x & 63) == 0) sh[i][threadIdx.x >> 6] = t;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NA; i += BS) red_part(ro, part, i, (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]));
+  for (int i = threadIdx.x; i < NA; i += BS) {
+    const double t = (sh[i][0] + sh[i][1]) + (sh[i][2] + sh[i][3]);
+    if (nvb > 0) part[(int64_t)i * MAXB + vb] = t;  // (virtual blocks: the plain partials, no fused reduction)
+    else red_part(ro, part, i, t);
+  }
+  __syncthreads();  // (sh is reused by the next virtual block)
+  }
   red_finish(ro, part, sh[0], true);  // (several waves stored partials)
 }
 
@@ -2407,10 +2419,12 @@ __device__ __forceinline__ bool sl_fast(const LOC& L, const SlTri& r, double qx,
 // nodes; c is the full replica, cout receives the owned segment [row0, row0 + n).
 // Partials (stride SLB): [0] sum w c, [1] sum w (mixing, marker==0 nodes), [2] not-found count.
 // Two passes.  k_sl finishes the points of the lattice fast path (q strictly inside a cell of its
-// row's home face, rank settled by a fast accept: all but 796 of L7's 14.2M rows, 0.006 %, r12n) with a
-// small register footprint; the rest are queued, and k_sl_wave (lattice locator: one wave per queued
-// point) or k_sl_slow (record locator) runs the general locate and the centroid rank count.  The record
-// locator has no fast path: k_sl queues every row.
+// row's home face, rank settled by a fast accept: all but ~36k of L7's 14.2M rows, ~0.25 % -- ~35k
+// departure points inside the squirmer, which no triangle holds, and ~800 rank counts, r12n) with a
+// small register footprint; the rest are queued, and the second pass runs the general locate and the
+// centroid rank count: lattice locator k_sl_qscan + k_sl_wq + k_sl_qsum (one numbered list, a wave per
+// point; k_sl_wave / k_sl_slow by PUCFEM_SL_WAVE), record locator k_sl_slow.  The record locator has no
+// fast path: k_sl queues every row (or k_sl_rec_wave runs both passes on small meshes).
 // The queue is per wave and deterministic: wave w of block b writes its k-th entry into slot
 // k % 64 of the (k / 64)-th 64-row slice it processed (entries never outrun the rows they come from);
 // k_sl_slow block b runs the same waves' queues and adds its partial sums to block b's, so the
