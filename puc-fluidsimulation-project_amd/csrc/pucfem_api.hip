@@ -1388,10 +1388,12 @@ struct Ctx {
                 dim3(nbs), dim3(BS), Ag.view(), fs, val, v1, c1a, c2a, first ? 1 : 0, (const int*)ctl,
                 first ? part_a : (double*)nullptr, first ? part_b : (double*)nullptr, RedOut{});
         KCHK();
+        if (first && dye_gate == 3) dye_tail_release();
         klaunch(12, bytes_f - (first ? 4.0 * NR * (double)hf.rows : 0.0), k_vcheb_pair, dim3(hf.items), dim3(BS), fc, p,
                 c1a, c2a, c1b, c2b, (const int*)ctl, pc, (int32_t)nbs, first ? 1 : 0,
                 first ? part_a : (double*)nullptr, first ? part_b : (double*)nullptr);
         KCHK();
+        if (first && dye_gate == 4) dye_tail_release();
         klaunch(-1, bytes_sk + fin_sk, k_vcheb<decltype(c16)::value>, dim3(nbs), dim3(BS), A.view(), fs, val, v2,
                 c1b, c2b, 0, (const int*)ctl, pc, (double*)nullptr, RedOut{});
         KCHK();
@@ -2278,7 +2280,7 @@ struct Ctx {
   // PUCFEM_RHS_FUSE=0 (measurement knob): the pressure right-hand side always in its own pass (k_pres_rhs)
   bool rhs_fuse = !(std::getenv("PUCFEM_RHS_FUSE") && std::atoi(std::getenv("PUCFEM_RHS_FUSE")) == 0);
   int pressure(double* yst, double* pout, int which, bool sb_fused = false) {  // StokesColor.py:554-555 (restated)
-    if (dye_gate == 2 && which == 1) dye_tail_release();
+    if (dye_gate >= 2 && which == 1) dye_tail_release();  // (gates 3 / 4 when the viscous solve ran no pair)
     const int nb = div_grid();
     Red sb{redbuf + 24, 1, 1};
     if (!sb_fused) sb = reduce_global(part_d + MAXB, nb, 1, false, 3);
@@ -2642,7 +2644,7 @@ struct Ctx {
   // PUCFEM_DYE_GATE (measurement knob): where the semi-Lagrangian part of the tail (advection, mixing sums, the
   // record) is released -- 0 with the final-divergence record at the end of the step (default), 1 at the first
   // V-cycle of the next step's first pressure solve (beside its latency-bound coarse levels), 2 at the start of that
-  // pressure solve
+  // pressure solve, 3 / 4 after the first SELL launch / the face kernel of the next viscous solve's first pair
   int dye_gate = std::getenv("PUCFEM_DYE_GATE") ? std::atoi(std::getenv("PUCFEM_DYE_GATE")) : 0;
   bool slb_pend = false;     // the semi-Lagrangian part waits for its release (dye_gate > 0)
   double* slb_rec = nullptr;
