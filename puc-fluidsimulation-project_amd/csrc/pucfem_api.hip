@@ -2779,7 +2779,20 @@ struct Ctx {
       if (!st_sl) {
         // (stream priorities and CU masks for the side stream were measured and changed nothing or lost,
         // rounds 2-3: r4d, r6c)
-        HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
+        // PUCFEM_SL_CUMASK=k (measurement knob, 1..7): the side stream on k of every 8 CUs (mask bits i with
+        // i % 8 < k), the rest left to the main stream's small launches
+        const int cuk = std::getenv("PUCFEM_SL_CUMASK") ? std::atoi(std::getenv("PUCFEM_SL_CUMASK")) : 0;
+        if (cuk > 0 && cuk < 8) {
+          int d = 0, ncu = 0;
+          HIPCHK(hipGetDevice(&d));
+          HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d));
+          std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+          for (int i = 0; i < ncu; ++i)
+            if (i % 8 < cuk) mask[(size_t)i / 32] |= 1u << (i % 32);
+          HIPCHK(hipExtStreamCreateWithCUMask(&st_sl, (uint32_t)mask.size(), mask.data()));
+        } else {
+          HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
+        }
         HIPCHK(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_sl, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
