@@ -162,7 +162,7 @@ def main():
     log(f"[bench] timed {a.steps} steps in {elapsed:.2f}s")
     names = ["k_cheb (MG smoother, finest level)", "k_cg_dir", "k_cg_upd", "k_grad_proj", "k_sl",
              "k_resid (MG residual, finest level)", "k_transfer (restriction from finest)",
-             "k_transfer (prolongation to finest)", "k_sl_slow (general locate + rank count)",
+             "k_transfer (prolongation to finest)", "k_sl_wq (SL second pass: general locate + rank count)",
              "k_vcheb (viscous Chebyshev step, whole grid)", "k_cheb_pair (two MG smoothing steps, finest level)",
              "k_div (divergence + pressure rhs)", "k_vcheb_pair (two viscous Chebyshev steps, face rows)",
              "k_visc_prep (viscous rhs + extrapolated start)", "k_mdot2 (projection multi-dot)",

@@ -11,5 +11,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-secondary "$@" > "$OUT/pmc_$c.out" 2> "$OUT/pmc_$c.err" \
     || { echo "pmc $c failed" >&2; tail -5 "$OUT/pmc_$c.err" >&2; exit 1; }
 done
-cp "$OUT/pmc_FETCH_SIZE.out" "$OUT/bench.out"
+cp "$OUT/pmc_FETCH_SIZE.out" "$OUT/pmc_bench.out"  # (not bench.out: gpu_check_head.sh keeps the driver line there)
 cd "$ROOT" && timeout -k 10 300 python tools/pmc_traffic.py /tmp/prof_$TAG/fetch /tmp/prof_$TAG/write "$OUT/pmc_traffic.json"
