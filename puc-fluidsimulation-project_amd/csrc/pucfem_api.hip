@@ -546,6 +546,9 @@ struct Ctx {
   double* gring = nullptr;
   int* gcount = nullptr;
   bool gcapture = false;  // (the step being captured)
+  // the captured step's record appended by k_mix2's reducing block (PUCFEM_RING_FOLD=0, measurement knob: k_stats_ring)
+  bool ring_fold = !(std::getenv("PUCFEM_RING_FOLD") && std::atoi(std::getenv("PUCFEM_RING_FOLD")) == 0);
+  bool ring_in_mix = false;
 
   // ---- lattice operators (pucfem_lattice.hpp): multigrid hierarchies with faces of interior nodes
   bool lattice = false;
@@ -955,6 +958,7 @@ struct Ctx {
       // measurement knob) or PUCFEM_SL_WAVE=0 -- k_sl_slow on k_sl's grid, one lane per point
       if (sl_wave_mode == 2 && !ro.out) {
         const int32_t nq = nb * (BS / 64);
+        if (nq > QSCAN_BS * QSCAN_PER) throw Error(PUCFEM_ESTATE, "k_sl grid larger than k_sl_qscan covers");
         hipLaunchKernelGGL(k_sl_qscan, dim3(1), dim3(QSCAN_BS), 0, st, (const int32_t*)sl_qcnt, nq, sl_qoff);
         KCHK();
         klaunch(8, 0.0, k_sl_wq, dim3(nb), dim3(BS), M, llgrid, cgrid, (int64_t)row0, (int64_t)n, (int32_t)nb, vx, vy,
@@ -2744,6 +2748,7 @@ struct Ctx {
   }
   void stokes_step(double* rec, int32_t* its) {
     int itv = 0;
+    ring_in_mix = false;
     viscous(itv);
     dye_tail_dist();  // (W > 1: the previous step's dye tail)
     // max |div u*| -> vals[0]; the div u* field itself is computed when read (pucfem_get_field): nothing in the
@@ -2835,8 +2840,11 @@ struct Ctx {
       const int nbm = nb_rows(lp.n_own);
       algo_bytes += 16.0 * (double)lp.n_own;
       const RedOut rm = ro(vals + 5, CNT_MIX, 1);
+      // (captured small-mesh step with the fused reduction: k_mix2's reducing block appends the step record)
+      ring_in_mix = gcapture && rm.out && !ovl && ring_fold;
       hipLaunchKernelGGL(k_mix2, dim3(nbm), dim3(BS), 0, st, lp.r0, lp.n_own, mix_copy ? (const double*)c_new : c_full,
-                         dwmix, vals + 2, 1, 1, part_mx, rm, mix_copy ? c_full : (double*)nullptr);
+                         dwmix, vals + 2, 1, 1, part_mx, rm, mix_copy ? c_full : (double*)nullptr, (const double*)vals,
+                         ring_in_mix ? gring : (double*)nullptr, ring_in_mix ? gcount : (int*)nullptr, 7);
       KCHK();
       if (rm.out) red_done(vals + 5, 1, false);
       else reduce_into(part_mx, nbm, 1, false, 5);
@@ -2844,8 +2852,11 @@ struct Ctx {
       tracer_advance(prm.dt);
     }
     if (!ovl) {
-      if (gcapture) hipLaunchKernelGGL(k_stats_ring, dim3(1), dim3(64), 0, st, vals, gring, gcount, 7);
-      else hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 7);
+      if (gcapture) {
+        if (!ring_in_mix) hipLaunchKernelGGL(k_stats_ring, dim3(1), dim3(64), 0, st, vals, gring, gcount, 7);
+      } else {
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(64), 0, st, vals, rec, 7);
+      }
       KCHK();
     }
     its[0] = itv;

@@ -174,8 +174,9 @@ __device__ __forceinline__ double red_load(const double* p) {
 // Called by every thread of every block after thread 0 stored the block's partials with red_store
 // (and, as every block must, with no early return before it).  sh: >= 4 doubles of LDS.
 // all_waves: partials were stored by several waves (each drains its stores before the barrier).
-__device__ __forceinline__ void red_finish(const RedOut& R, const double* part, double* sh, bool all_waves = false) {
-  if (!R.out) return;
+// returns true in the block that reduced (the last one to finish), after its thread 0 stored the values
+__device__ __forceinline__ bool red_finish(const RedOut& R, const double* part, double* sh, bool all_waves = false) {
+  if (!R.out) return false;
   __shared__ int last;
   if (all_waves) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -189,7 +190,7 @@ __device__ __forceinline__ void red_finish(const RedOut& R, const double* part, 
     last = t == gridDim.x - 1;
   }
   __syncthreads();
-  if (!last) return;
+  if (!last) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the last block reads after the ticket
   const int nb = gridDim.x;
   for (int v = 0; v < R.nv; ++v) {
@@ -207,6 +208,7 @@ __device__ __forceinline__ void red_finish(const RedOut& R, const double* part, 
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(R.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 // thread 0: partial of value v of this block (stride R.stride when fused, else MAXB: the k_reduce layout)
 __device__ __forceinline__ void red_part(const RedOut& R, double* part, int v, double x) {

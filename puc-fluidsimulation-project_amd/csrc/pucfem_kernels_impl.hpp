@@ -2815,29 +2815,47 @@ __global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev 
 //   k_sl_qsum   adds the queued rows' contributions to k_sl's block partials in k_sl_slow's order (lane p % 64 of
 //               the wave that queued entry p), so the sums are k_sl_slow's, bit for bit.
 constexpr int QSCAN_BS = 1024;
+constexpr int QSCAN_PER = (SLB * (BS / 64) + QSCAN_BS - 1) / QSCAN_BS;  // entries per thread (32 at SLB = 8192)
+// one block: wave w scans entries [w 64 QSCAN_PER, (w + 1) 64 QSCAN_PER) in chunks of 64 consecutive entries (one per
+// lane), every chunk's load issued first (a loop of dependent loads per thread took 79 us, r14z trace)
 __global__ __launch_bounds__(QSCAN_BS) void k_sl_qscan(const int32_t* __restrict__ qcnt, int32_t nq,
                                                        int32_t* __restrict__ qoff) {
   __shared__ int32_t ws[QSCAN_BS / 64];
-  const int32_t per = (nq + QSCAN_BS - 1) / QSCAN_BS;
-  const int32_t a = (int32_t)threadIdx.x * per, b = min(a + per, nq);
-  int32_t s = 0;
-  for (int32_t q = a; q < b; ++q) s += qcnt[q];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int32_t incl = s;
+  const int32_t base = wv * 64 * QSCAN_PER;
+  int32_t v[QSCAN_PER];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
+  for (int k = 0; k < QSCAN_PER; ++k) {
+    const int32_t e = base + k * 64 + lane;
+    v[k] = e < nq ? qcnt[e] : 0;
   }
-  if (lane == 63) ws[wv] = incl;
+  int32_t run = 0;  // this wave's total before chunk k
+#pragma unroll
+  for (int k = 0; k < QSCAN_PER; ++k) {
+    int32_t incl = v[k];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const int32_t tot = __shfl(incl, 63, 64);
+    v[k] = run + incl - v[k];  // (exclusive, within the wave)
+    run += tot;
+  }
+  if (lane == 0) ws[wv] = run;
   __syncthreads();
-  int32_t off = incl - s;
-  for (int k = 0; k < wv; ++k) off += ws[k];
-  for (int32_t q = a; q < b; ++q) {
-    qoff[q] = off;
-    off += qcnt[q];
+  int32_t wb = 0;
+  for (int k = 0; k < wv; ++k) wb += ws[k];
+#pragma unroll
+  for (int k = 0; k < QSCAN_PER; ++k) {
+    const int32_t e = base + k * 64 + lane;
+    if (e < nq) qoff[e] = wb + v[k];
   }
-  if (threadIdx.x == QSCAN_BS - 1) qoff[nq] = off;  // (the last thread's running offset is the total)
+  if (threadIdx.x == 0) {
+    int32_t t = 0;
+    for (int k = 0; k < QSCAN_BS / 64; ++k) t += ws[k];
+    qoff[nq] = t;
+  }
 }
 // the general lattice locate of one point by a whole wave, faces first: the lanes take the candidate faces of q's
 // macro-grid cell (sl_inner: an inner cell is the only passing triangle), then the cells around (u, v) of every face
@@ -3247,10 +3265,14 @@ __global__ __launch_bounds__(BS) void k_wsum(int64_t row0, int64_t n, const doub
 // mixing_index second pass (StokesColor.py:399-401): partial sum w (c - mu)^2, mu from pass 1.
 // copy_to (non-null): also copies the owned segment of c there (the new dye into the replica: one launch less than
 // a separate device copy before the sums)
+// (small-mesh graph: with the fused reduction, the block that reduced also appends the step record to the ring --
+// k_stats_ring's work, after the value it reduced -- when ring is given; vals: the step's values)
+__device__ __forceinline__ void stats_body(const double* vals, double* out, int parts);
 __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const double* __restrict__ c,
                                              const double* __restrict__ wmix, const double* part1, int nb1,
                                              int stride1, double* part, RedOut ro = RedOut{},
-                                             double* __restrict__ copy_to = nullptr) {
+                                             double* __restrict__ copy_to = nullptr, const double* vals = nullptr,
+                                             double* ring = nullptr, int* count = nullptr, int parts = 0) {
   __shared__ double sh[4];
   const double swc = reduce_partials(part1, nb1, sh);
   const double sw = reduce_partials(part1 + stride1, nb1, sh);
@@ -3266,7 +3288,11 @@ __global__ __launch_bounds__(BS) void k_mix2(int64_t row0, int64_t n, const doub
   }
   const double t = block_sum(acc, sh);
   if (threadIdx.x == 0) red_part(ro, part, 0, t);
-  red_finish(ro, part, sh);
+  if (red_finish(ro, part, sh) && ring && threadIdx.x == 0) {  // (thread 0 stored the reduced value itself)
+    const int k = count[0];
+    stats_body(vals, ring + 8 * (int64_t)k, parts);
+    count[0] = k + 1;
+  }
 }
 
 // ----------------------------------------------------------------------------- tracers
