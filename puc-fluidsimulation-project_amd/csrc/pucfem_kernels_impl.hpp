@@ -2814,10 +2814,11 @@ __global__ __launch_bounds__(BS) void k_sl_wave(MeshDev M, LatLocDev L, GridDev 
 //               its row index in the queue,
 //   k_sl_qsum   adds the queued rows' contributions to k_sl's block partials in k_sl_slow's order (lane p % 64 of
 //               the wave that queued entry p), so the sums are k_sl_slow's, bit for bit.
-constexpr int QSCAN_BS = 1024;
-constexpr int QSCAN_PER = (SLB * (BS / 64) + QSCAN_BS - 1) / QSCAN_BS;  // entries per thread (32 at SLB = 8192)
-// one block: wave w scans entries [w 64 QSCAN_PER, (w + 1) 64 QSCAN_PER) in chunks of 64 consecutive entries (one per
-// lane), every chunk's load issued first (a loop of dependent loads per thread took 79 us, r14z trace)
+constexpr int QSCAN_BS = 256;
+constexpr int QSCAN_PER = (SLB * (BS / 64) + QSCAN_BS - 1) / QSCAN_BS;  // entries per thread (128 at SLB = 8192)
+// one block of 256 threads (a 1,024-thread block waited for a whole CU's wave slots beside the main stream: 79 us with
+// a loop of dependent loads per thread, r14z; 168 us with them issued together, r14k): wave w scans entries
+// [w 64 QSCAN_PER, (w + 1) 64 QSCAN_PER) in chunks of 64 consecutive entries (one per lane), every load issued first
 __global__ __launch_bounds__(QSCAN_BS) void k_sl_qscan(const int32_t* __restrict__ qcnt, int32_t nq,
                                                        int32_t* __restrict__ qoff) {
   __shared__ int32_t ws[QSCAN_BS / 64];
