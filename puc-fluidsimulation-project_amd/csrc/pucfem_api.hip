@@ -2576,6 +2576,16 @@ struct Ctx {
     int mode = 0;
     double bytes = 0.0;
   } gp_gate;
+  // a pressure solve with the gated projection armed (disarmed if the solve throws)
+  int gated_pressure(const GpGate& g, double* yst, double* pout, int which, bool sb_fused) {
+    gp_gate = g;
+    try {
+      return pressure(yst, pout, which, sb_fused);
+    } catch (...) {
+      gp_gate = GpGate{};
+      throw;
+    }
+  }
   // after the solve: whether the gated projection ran (then its bytes are counted here)
   bool gp_gate_end() {
     const bool d = gp_gate.done;
@@ -2619,6 +2629,8 @@ struct Ctx {
 
   // side stream of the overlapped dye advection (stokes_step)
   hipStream_t st_sl = nullptr;
+  int sl_prio = 0;  // (PUCFEM_STREAM_PRIO: the side stream's priority)
+  bool sl_prio_on = false;
   hipEvent_t ev_u = nullptr, ev_sl = nullptr;
   bool sl_overlap = true, sl_pending = false;
   double* part_mx = nullptr;  // k_mix2 partials (part_b belongs to the solvers of the main stream)
@@ -2756,16 +2768,15 @@ struct Ctx {
     const bool f1 = div_rhs(usx, usy, nullptr, vals);
     if (!f1) reduce_into(part_d, div_grid(), 1, true, 0);
     const bool gpg = gp_gate_env && use_mg && proj_k > 0 && p_from_y && !dist() && !proj_spmv;
-    gp_gate = GpGate{gpg, false, yp, 0, 0.0};
-    const int itp = pressure(yp, p, 1, f1);
+    // (a solve that throws leaves no gated projection armed for later calls: gated_pressure resets it on unwind)
+    const int itp = gated_pressure(GpGate{gpg, false, yp, 0, 0.0}, yp, p, 1, f1);
     const bool gp1 = gp_gate_end();
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
     if (!gp1) grad_proj(p_from_y ? yp : p, 0);
     bc(ux, uy);
     halo_v(ux);
     const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
-    gp_gate = GpGate{gpg, false, yp2, 1, 0.0};
-    const int itp2 = pressure(yp2, p2, 2, f2);
+    const int itp2 = gated_pressure(GpGate{gpg, false, yp2, 1, 0.0}, yp2, p2, 2, f2);
     const bool gp2 = gp_gate_end();
     if (!gp2) grad_proj(p_from_y ? yp2 : p2, 1);
     halo_v(ux);
@@ -2795,6 +2806,8 @@ struct Ctx {
           for (int i = 0; i < ncu; ++i)
             if (i % 8 < cuk) mask[(size_t)i / 32] |= 1u << (i % 32);
           HIPCHK(hipExtStreamCreateWithCUMask(&st_sl, (uint32_t)mask.size(), mask.data()));
+        } else if (sl_prio_on) {
+          HIPCHK(hipStreamCreateWithPriority(&st_sl, hipStreamNonBlocking, sl_prio));
         } else {
           HIPCHK(hipStreamCreateWithFlags(&st_sl, hipStreamNonBlocking));
         }
@@ -4604,7 +4617,17 @@ int pucfem_ctx_create(int32_t device, void** out) {
     if (const char* e = std::getenv("PUCFEM_MG_BLOCKS")) c->mg_nb_max = std::max(1, std::atoi(e));  // tuning knob
     if (!c->host_only) {
       HIPCHK(hipSetDevice(device));
-      HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      // PUCFEM_STREAM_PRIO=1 (measurement knob): the main stream at the highest priority, the dye side stream at the
+      // lowest (the dispatcher then hands freed slots to the main stream's blocks first)
+      if (std::getenv("PUCFEM_STREAM_PRIO") && std::atoi(std::getenv("PUCFEM_STREAM_PRIO")) != 0) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, hi));
+        c->sl_prio = lo;
+        c->sl_prio_on = true;
+      } else {
+        HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+      }
       HIPCHK(hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_coef, 5 * Ctx::NCOEF * sizeof(double), hipHostMallocDefault));
       HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64 * sizeof(double), hipHostMallocDefault));
