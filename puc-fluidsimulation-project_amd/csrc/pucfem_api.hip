@@ -2126,7 +2126,7 @@ struct Ctx {
       }
       // the samples before this chunk, while the GPU runs it (this chunk's stay pending until its test is read)
       if (timer.on && !marks.empty()) timer.flush_ready(marks.front().second);
-      read_ctl();
+      read_ctl(it >= last_it[which]);
       if (timer.on && h_ctl[0])  // iterations from the converged one on launched kernels that did no work
         for (auto& mk : marks)
           if (mk.first >= h_ctl[1]) {
@@ -2565,6 +2565,25 @@ struct Ctx {
     KCHK();
     return bytes;
   }
+  // small meshes: the first projection with the velocity BCs (k_grad_proj_bc; the faces are empty there)
+  int32_t* dspos = nullptr;  // the projection operator's (slice, lane) position of each row
+  void grad_proj_bc(const double* pp) {
+    const DevSell& A = p_from_y ? dPm : dP;
+    const int nb = (int)std::max<i64>(1, std::min<i64>(1024, (A.nslices * 64 + BS - 1) / BS));
+    if (!dspos) {
+      dspos = dalloc<int32_t>(std::max<i64>(1, lp.n_own));
+      hipLaunchKernelGGL(k_sell_pos, dim3(nb), dim3(BS), 0, st, A.view(), dspos);
+      KCHK();
+    }
+    algo_bytes += (16.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 40.0 * (double)lp.n_own;
+    with_c16(A, [&](auto c16) {
+      hipLaunchKernelGGL(k_grad_proj_bc<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, A.view(), (const double*)dGx,
+                         (const double*)dGy, pp, (const double*)das1, prm.dt, (const double*)usx, ux,
+                         (const int32_t*)dbcsrc, (const int32_t*)dbcdir, (const int32_t*)dspos, (const double*)ddval,
+                         dir_ncomp);
+    });
+    KCHK();
+  }
   // The gradient projection after a pressure solve, enqueued behind the solve's convergence reads and gated on its
   // control word (PUCFEM_GP_GATE, default on): when the read finds the solve converged the GPU has been running the
   // projection during the host's round trip (the r13g trace: ~50 us idle before each k_grad_proj), and when it finds
@@ -2599,9 +2618,11 @@ struct Ctx {
   }
   bool gp_gate_env = !(std::getenv("PUCFEM_GP_GATE") && std::atoi(std::getenv("PUCFEM_GP_GATE")) == 0);
   // the PCG's control-word read (h_ctl), with the gated projection behind it
-  void read_ctl() {
+  // arm: enqueue the gated projection behind this read (pcg_mg: when the solve has reached the last solve's count, so
+  // that a read unlikely to find it converged adds no launch that does nothing)
+  void read_ctl(bool arm = true) {
     HIPCHK(hipMemcpyAsync(h_ctl, ctl, 6 * sizeof(int), hipMemcpyDeviceToHost, st));  // (+ the note)
-    if (!gp_gate.on) {
+    if (!gp_gate.on || !arm) {
       sync_st();
       return;
     }
@@ -2772,8 +2793,12 @@ struct Ctx {
     const int itp = gated_pressure(GpGate{gpg, false, yp, 0, 0.0}, yp, p, 1, f1);
     const bool gp1 = gp_gate_end();
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
-    if (!gp1) grad_proj(p_from_y ? yp : p, 0);
-    bc(ux, uy);
+    if (dense && dbcsrc && dense_bc && dir_ncomp == 2 && !gp1 && (p_from_y ? fP : fK).rows == 0) {
+      grad_proj_bc(p_from_y ? yp : p);  // (the BCs inside the projection: small meshes)
+    } else {
+      if (!gp1) grad_proj(p_from_y ? yp : p, 0);
+      bc(ux, uy);
+    }
     halo_v(ux);
     const bool f2 = div_rhs(ux, uy, div_u, redbuf + 40);  // (its max is not recorded: scratch slot 5)
     const int itp2 = gated_pressure(GpGate{gpg, false, yp2, 1, 0.0}, yp2, p2, 2, f2);

@@ -4512,6 +4512,51 @@ __global__ __launch_bounds__(BS) void k_dense_mv2(int64_t n, const double* __res
   }
 }
 
+// Small meshes (Ctx::dense): the first gradient projection (grad_proj_body, mode 0, SELL rows) and the velocity BCs
+// after it (Ctx::bc) in one launch -- a Dirichlet row takes its value, a periodic copy row the projection of its
+// source row (from the source's SELL entries at its slice position spos[src]: the same operations in the same order,
+// so the value k_bc_apply copies), every other row its own.  One thread per (slice, lane).
+__global__ __launch_bounds__(BS) void k_sell_pos(SellDev A, int32_t* __restrict__ spos) {
+  for (int64_t t = (int64_t)blockIdx.x * BS + threadIdx.x; t < A.nslices * 64; t += (int64_t)gridDim.x * BS) {
+    const int64_t row = sell_row(A, t >> 6, (int)(t & 63));
+    if (row >= 0) spos[row] = (int32_t)t;
+  }
+}
+template <bool C16>
+__global__ __launch_bounds__(BS) void k_grad_proj_bc(SellDev A, const double* __restrict__ gx,
+                                                     const double* __restrict__ gy, const double* __restrict__ p,
+                                                     const double* __restrict__ as1, double dt, const double* usx,
+                                                     double* ux, const int32_t* __restrict__ bsrc,
+                                                     const int32_t* __restrict__ bdir, const int32_t* __restrict__ spos,
+                                                     const double* __restrict__ dval, int ncomp) {
+  for (int64_t t = (int64_t)blockIdx.x * BS + threadIdx.x; t < A.nslices * 64; t += (int64_t)gridDim.x * BS) {
+    const int64_t row = sell_row(A, t >> 6, (int)(t & 63));
+    if (row < 0) continue;
+    const int32_t dj = bdir[row];
+    if (dj >= 0) {
+      reinterpret_cast<dbl2*>(ux)[row] = dbl2{dval[ncomp * dj], dval[ncomp * dj + 1]};
+      continue;
+    }
+    const int32_t src = bsrc[row];
+    const int64_t pos = src == row ? t : (int64_t)spos[src];
+    const int64_t ss = pos >> 6;
+    const int lane = (int)(pos & 63);
+    const int64_t off = A.off[ss];
+    const int w = A.w[ss];
+    const int32_t base = (int32_t)(ss * 64);
+    const dbl2 o = reinterpret_cast<const dbl2*>(usx)[src];
+    const double d = as1[src];
+    double ax = 0.0, ay = 0.0;
+    for (int k = 0; k < w; ++k) {
+      const int64_t e = off + (int64_t)k * 64 + lane;
+      const double pj = p[sell_col<C16>(A, e, base)];
+      ax += ldnt(gx + e) * pj;
+      ay += ldnt(gy + e) * pj;
+    }
+    reinterpret_cast<dbl2*>(ux)[row] = dbl2{o.x - dt * (ax / d), o.y - dt * (ay / d)};
+  }
+}
+
 // k_dense_mv2 with the velocity BCs of the solve's result (Ctx::bc) in the same launch: a Dirichlet row takes its
 // value, a periodic copy row the product of its source's matrix row (the source's value before the BCs, which is what
 // k_bc_apply copies: write sets are disjoint, chained sources are read before the writes), every other row its own
