@@ -2567,14 +2567,18 @@ struct Ctx {
   }
   // small meshes: the first projection with the velocity BCs (k_grad_proj_bc; the faces are empty there)
   int32_t* dspos = nullptr;  // the projection operator's (slice, lane) position of each row
+  // (the position map is built before any graph capture: an allocation inside a captured step is not allowed)
+  void prep_grad_proj_bc() {
+    if (!dense || !dbcsrc || dspos) return;
+    const DevSell& A = p_from_y ? dPm : dP;
+    const int nb = (int)std::max<i64>(1, std::min<i64>(1024, (A.nslices * 64 + BS - 1) / BS));
+    dspos = dalloc<int32_t>(std::max<i64>(1, lp.n_own));
+    hipLaunchKernelGGL(k_sell_pos, dim3(nb), dim3(BS), 0, st, A.view(), dspos);
+    KCHK();
+  }
   void grad_proj_bc(const double* pp) {
     const DevSell& A = p_from_y ? dPm : dP;
     const int nb = (int)std::max<i64>(1, std::min<i64>(1024, (A.nslices * 64 + BS - 1) / BS));
-    if (!dspos) {
-      dspos = dalloc<int32_t>(std::max<i64>(1, lp.n_own));
-      hipLaunchKernelGGL(k_sell_pos, dim3(nb), dim3(BS), 0, st, A.view(), dspos);
-      KCHK();
-    }
     algo_bytes += (16.0 + A.idx_bytes()) * (double)A.nnz + A.row_bytes() * (double)A.nrows + 40.0 * (double)lp.n_own;
     with_c16(A, [&](auto c16) {
       hipLaunchKernelGGL(k_grad_proj_bc<decltype(c16)::value>, dim3(nb), dim3(BS), 0, st, A.view(), (const double*)dGx,
@@ -2793,7 +2797,7 @@ struct Ctx {
     const int itp = gated_pressure(GpGate{gpg, false, yp, 0, 0.0}, yp, p, 1, f1);
     const bool gp1 = gp_gate_end();
     sl_join();  // the previous step's dye advection still reads u: it must finish before u is rewritten
-    if (dense && dbcsrc && dense_bc && dir_ncomp == 2 && !gp1 && (p_from_y ? fP : fK).rows == 0) {
+    if (dense && dspos && dense_bc && dir_ncomp == 2 && !gp1 && (p_from_y ? fP : fK).rows == 0) {
       grad_proj_bc(p_from_y ? yp : p);  // (the BCs inside the projection: small meshes)
     } else {
       if (!gp1) grad_proj(p_from_y ? yp : p, 0);
@@ -5001,6 +5005,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
           HIPCHK(hipStreamEndCapture(c.st, &gr));
           HIPCHK(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0));
         };
+        c.prep_grad_proj_bc();
         if (!c.gexec) {
           c.gstats = c.dalloc<double>(8);
           c.gring = c.dalloc<double>(8 * (i64)Ctx::GRING);
@@ -5030,6 +5035,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
       } else {
         c.graph_mode = c.gexec != nullptr;  // once captured, keep c in its fixed buffer
         c.dits = dits;
+        c.prep_grad_proj_bc();
         try {
           for (int s = 0; s < nsteps; ++s) {
             c.cur_step = s;
