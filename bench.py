@@ -63,7 +63,7 @@ def parse():
                     help="per-launch kernel events on the last N of the timed steps (each timed launch costs a few "
                          "us of dispatch: events on all 20 steps slowed the step by ~2 %%, r10i)")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--fine-steps", type=int, default=200)
+    ap.add_argument("--fine-steps", type=int, default=2000)  # (~0.2 s of replays: 200 steps timed ~18 ms, +-10 %)
     ap.add_argument("--steady-after", type=int, default=100,
                     help="steady-state leg: the same run continued to this step, then --steady-steps timed (0: off)")
     ap.add_argument("--steady-steps", type=int, default=20)
