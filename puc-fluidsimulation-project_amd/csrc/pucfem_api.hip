@@ -549,6 +549,23 @@ struct Ctx {
   // the captured step's record appended by k_mix2's reducing block (PUCFEM_RING_FOLD=0, measurement knob: k_stats_ring)
   bool ring_fold = !(std::getenv("PUCFEM_RING_FOLD") && std::atoi(std::getenv("PUCFEM_RING_FOLD")) == 0);
   bool ring_in_mix = false;
+  // the captured step's fork (PUCFEM_GRAPH_FORK=1, measurement knob, off): a side stream and its events, made before
+  // the capture (prep_fork).  The same bits, but the graph's cross-stream edges cost more than the overlap gains:
+  // mesh_fine 10.0k steps/s forked against 12.5k in one chain (r14q)
+  hipStream_t st_fk = nullptr;
+  hipEvent_t ev_fk = nullptr, ev_fj = nullptr;
+  bool fork_pend = false;
+  void prep_fork() {
+    if (st_fk || !(std::getenv("PUCFEM_GRAPH_FORK") && std::atoi(std::getenv("PUCFEM_GRAPH_FORK")) != 0)) return;
+    HIPCHK(hipStreamCreateWithFlags(&st_fk, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev_fk, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_fj, hipEventDisableTiming));
+  }
+  void fork_join() {
+    if (!fork_pend) return;
+    HIPCHK(hipStreamWaitEvent(st, ev_fj, 0));
+    fork_pend = false;
+  }
 
   // ---- lattice operators (pucfem_lattice.hpp): multigrid hierarchies with faces of interior nodes
   bool lattice = false;
@@ -708,6 +725,9 @@ struct Ctx {
       if (graph) (void)hipGraphDestroy(graph);
       if (gexec_k) (void)hipGraphExecDestroy(gexec_k);
       if (graph_k) (void)hipGraphDestroy(graph_k);
+      if (st_fk) (void)hipStreamDestroy(st_fk);
+      if (ev_fk) (void)hipEventDestroy(ev_fk);
+      if (ev_fj) (void)hipEventDestroy(ev_fj);
       for (void* a : allocs) (void)hipFree(a);
       if (h_ctl) (void)hipHostFree(h_ctl);
       if (h_coef) (void)hipHostFree(h_coef);
@@ -2816,7 +2836,21 @@ struct Ctx {
     const bool ovl = sl_overlap && scheme == PUCFEM_STOKES_COLOR && !dye_impl && !graph_mode && !dist();
     if (!ovl) {
       const RedOut r = ro(vals + 1, CNT_DIV, 1, MAXB, 1u);
-      div(ux, uy, dye_impl ? final_div : nullptr, false, nullptr, r);  // (the implicit dye reads it)
+      // captured small-mesh step (fused reductions): the final-divergence record on a forked branch of the graph, beside
+      // the semi-Lagrangian advection (both read u and write their own partials); joined before the step record
+      const bool fork = gcapture && r.out && !dye_impl && st_fk != nullptr && scheme == PUCFEM_STOKES_COLOR;
+      if (fork) {
+        HIPCHK(hipEventRecord(ev_fk, st));
+        HIPCHK(hipStreamWaitEvent(st_fk, ev_fk, 0));
+        {
+          StreamSwap sw(st, st_fk);
+          div(ux, uy, nullptr, false, nullptr, r);
+        }
+        HIPCHK(hipEventRecord(ev_fj, st_fk));
+        fork_pend = true;
+      } else {
+        div(ux, uy, dye_impl ? final_div : nullptr, false, nullptr, r);  // (the implicit dye reads it)
+      }
       if (r.out) red_done(vals + 1, 1, true);
       else reduce_into(part_d, div_grid(), 1, true, 1);  // max |final div|
     }
@@ -2881,6 +2915,7 @@ struct Ctx {
       sl_ro = RedOut{};
       const int nbm = nb_rows(lp.n_own);
       algo_bytes += 16.0 * (double)lp.n_own;
+      fork_join();  // (k_mix2's reducing block writes the step record, which holds the final divergence)
       const RedOut rm = ro(vals + 5, CNT_MIX, 1);
       // (captured small-mesh step with the fused reduction: k_mix2's reducing block appends the step record)
       ring_in_mix = gcapture && rm.out && !ovl && ring_fold;
@@ -2893,6 +2928,7 @@ struct Ctx {
     } else {
       tracer_advance(prm.dt);
     }
+    fork_join();
     if (!ovl) {
       if (gcapture) {
         if (!ring_in_mix) hipLaunchKernelGGL(k_stats_ring, dim3(1), dim3(64), 0, st, vals, gring, gcount, 7);
@@ -4997,6 +5033,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
             c.gcapture = false;
           } catch (...) {
             c.gcapture = false;
+            c.fork_pend = false;
             hipGraph_t g;
             (void)hipStreamEndCapture(c.st, &g);
             c.graph_mode = c.gexec != nullptr;
@@ -5006,6 +5043,7 @@ int pucfem_step(void* ctx, int32_t nsteps, pucfem_step_stats* stats) {
           HIPCHK(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0));
         };
         c.prep_grad_proj_bc();
+        c.prep_fork();
         if (!c.gexec) {
           c.gstats = c.dalloc<double>(8);
           c.gring = c.dalloc<double>(8 * (i64)Ctx::GRING);
