@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch listing of the last hipGraph replays of the small-mesh step (tools/fine_probe.py under rocprofv3
---kernel-trace): every kernel of the last REPLAYS steps (a step ends with k_stats and the record's copy) with its
+--kernel-trace): every kernel of the last REPLAYS steps (a step ends with k_stats, or with k_mix2 when that kernel
+appends the step record, and the record's copy) with its
 start offset, duration and the gap before it, then the per-step totals.
 Usage: trace_replay.py KERNEL_TRACE_CSV [REPLAYS]"""
 import csv
@@ -20,8 +21,10 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
     ends = [i for i, r in enumerate(rows) if r[2].startswith("k_stats")]
+    if len(ends) < k + 1:  # (the record appended by k_mix2: the step ends there)
+        ends = [i for i, r in enumerate(rows) if r[2].startswith("k_mix2")]
     if len(ends) < k + 1:
-        print("not enough k_stats launches")
+        print("not enough k_stats / k_mix2 launches")
         return
     a, b = ends[-k - 1] + 1, len(rows)
     # the record copy after the last k_stats belongs to that step
