@@ -4455,6 +4455,8 @@ void build(Ctx& c) {
     c.ddnode = c.upload(dn);
     c.ddval = c.upload(dv);
     c.dbctmp = c.dalloc<double>(2 * std::max(1, c.ncopy));
+    c.dspos = nullptr;  // (k_grad_proj_bc's position map follows the operators: rebuilt at the next step call)
+    c.dbcsrc = c.dbcdir = nullptr;
     if (c.dense) {  // k_dense_mv2_bc's per-row maps
       std::vector<i32> bsrc(no), bdir(no, -1);
       for (i64 i = 0; i < no; ++i) bsrc[i] = (i32)i;
