@@ -534,10 +534,11 @@ struct Ctx {
   bool graph_mode = false;
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
-  // and, with PUCFEM_GRAPH_STEPS = GK > 1 (measurement knob), GK consecutive steps in one graph: one host launch per
-  // GK steps, the same bits (test_graph_of_k_steps_equals_single_step_graph), but slower -- mesh_fine 9.7k steps/s
-  // with 8 steps per graph against 10.5k with one (r14b): the host's replay is not what bounds the small step
-  int gk = std::getenv("PUCFEM_GRAPH_STEPS") ? std::max(1, std::min(64, std::atoi(std::getenv("PUCFEM_GRAPH_STEPS")))) : 1;
+  // and GK = 8 consecutive steps in one graph (PUCFEM_GRAPH_STEPS, measurement knob; 1 = one step per replay): one
+  // launch per 8 steps, whose ~8 us between replays (r14u trace) the steps inside a graph do not pay; the same bits
+  // (test_graph_of_k_steps_equals_single_step_graph).  mesh_fine 12.3-12.6k -> 13.1-13.5k steps/s (r14x; with the
+  // step's earlier 13 launches, 8-step graphs measured slower, r14b)
+  int gk = std::getenv("PUCFEM_GRAPH_STEPS") ? std::max(1, std::min(64, std::atoi(std::getenv("PUCFEM_GRAPH_STEPS")))) : 8;
   hipGraphExec_t gexec_k = nullptr;
   hipGraph_t graph_k = nullptr;
   double* gstats = nullptr;

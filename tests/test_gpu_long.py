@@ -88,7 +88,7 @@ def test_color_mesh_fine_5000_steps_config2():
 
 @pytest.mark.parametrize("m", ["mesh1", "fine"])
 def test_graph_of_k_steps_equals_single_step_graph(m, monkeypatch):
-    """The small-mesh path replays GK steps per graph launch (PUCFEM_GRAPH_STEPS=8, a measurement knob) and the one-step
+    """The small-mesh path replays GK steps per graph launch (PUCFEM_GRAPH_STEPS, default 8) and the one-step
     graph for the rest of a call and at a full record ring: the same fields and per-step records, bit for bit, as
     one-step replays (a call of 1, one of 37 = 4 x 8 + 5, one of 1030 across the 1024-step ring)."""
     mesh = pf.load_mesh(m)
